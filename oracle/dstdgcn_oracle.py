@@ -1,0 +1,141 @@
+"""CPU oracle for the DSTDGC hot path -- TEST INFRASTRUCTURE ONLY.
+
+A functional restatement of the reference forward (``/root/reference/model/
+dstdgcn.py``) written against a plain ``{name: array}`` state dict, in torch on
+the CPU, in fp64 (default) or fp32.  It exists to *check* the MI355X path and to
+give ``bench.py`` its ``cpu_baseline`` leg; the product never imports it
+(only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s baseline may).
+
+Parity status: PINNED.  ``tests/test_oracle_golden.py`` checks this restatement
+against fixtures produced by running the reference itself in the build
+container (``tests/golden/make_golden.py``): per op, per block and whole model
+for the h36m / cmu / 3dpw / h36m-T75 configs.
+
+Every function cites the reference lines it restates.
+"""
+import torch
+
+BN_EPS = 1e-5  # nn.BatchNorm1d default, model/dstdgcn.py:42
+
+
+def _t(a, dtype):
+    if torch.is_tensor(a):
+        return a.detach().to("cpu", dtype)
+    return torch.as_tensor(a, dtype=dtype)
+
+
+def conv1x1(x, w, b):
+    """nn.Conv2d(cin, cout, 1) on NCTV (model/dstdgcn.py:66-71)."""
+    y = torch.einsum("oc,nctv->notv", w.reshape(w.shape[0], w.shape[1]), x)
+    return y + b.view(1, -1, 1, 1)
+
+
+def dstdgc(x, p, A, alpha, mode):
+    """DSTDGC.forward (model/dstdgcn.py:80-94).
+
+    x: [N, Cin, T, V]; p: dict with conv_{f,m1,m2,rm}.{weight,bias};
+    A: [1, V, V] (spatial) or [1, T, T] (temporal); alpha: scalar tensor.
+    """
+    xf = conv1x1(x, p["conv_f.weight"], p["conv_f.bias"])            # :81
+    p1 = conv1x1(x, p["conv_m1.weight"], p["conv_m1.bias"])          # :82
+    q1 = conv1x1(x, p["conv_m2.weight"], p["conv_m2.bias"])
+    n, r, t, v = p1.shape
+    wrm = p["conv_rm.weight"].reshape(p["conv_rm.weight"].shape[0], -1)
+    brm = p["conv_rm.bias"]
+    if mode == "spatial":                                             # :83-87
+        pk = p1.reshape(n, r * t, v)                                  # k = r*T + t'
+        qk = q1.reshape(n, r * t, v)
+        m = torch.tanh(pk[:, :, :, None] - qk[:, :, None, :])         # [n, 2T, V, V]
+        d = torch.einsum("tk,nkvw->ntvw", wrm, m) + brm.view(1, -1, 1, 1)
+        adj = d * alpha + A                                           # [n, T, V, V]
+        return torch.einsum("nctv,ntvw->nctw", xf, adj)
+    if mode == "temporal":                                            # :88-93
+        pk = p1.permute(0, 1, 3, 2).reshape(n, r * v, t)              # k = r*V + v'
+        qk = q1.permute(0, 1, 3, 2).reshape(n, r * v, t)
+        m = torch.tanh(pk[:, :, :, None] - qk[:, :, None, :])         # [n, 2V, T, T]
+        d = torch.einsum("vk,nktu->nvtu", wrm, m) + brm.view(1, -1, 1, 1)
+        adj = d * alpha + A                                           # [n, V, T, T]
+        return torch.einsum("nctv,nvtu->ncuv", xf, adj)
+    raise ValueError(mode)
+
+
+def batchnorm(x, p, training=False, eps=BN_EPS):
+    """BatchNorm wrapper (model/dstdgcn.py:35-50): BN1d over channel c*V+v,
+    statistics over (n, t).  Eval uses running stats; train uses batch stats
+    (biased variance for normalisation)."""
+    n, c, t, v = x.shape
+    xc = x.permute(0, 1, 3, 2).reshape(n, c * v, t)
+    if training:
+        mean = xc.mean(dim=(0, 2))
+        var = xc.var(dim=(0, 2), unbiased=False)
+    else:
+        mean, var = p["running_mean"], p["running_var"]
+    y = (xc - mean.view(1, -1, 1)) / torch.sqrt(var.view(1, -1, 1) + eps)
+    y = y * p["weight"].view(1, -1, 1) + p["bias"].view(1, -1, 1)
+    return y.reshape(n, c, v, t).permute(0, 1, 3, 2)
+
+
+def prelu(x, w):
+    """nn.PReLU with a single slope (model/dstdgcn.py:132, 284, 291)."""
+    return torch.where(x >= 0, x, w.reshape(()) * x)
+
+
+def sub(sd, prefix):
+    return {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}
+
+
+def dstdgcb(x, p, training=False):
+    """DSTDGCB.forward (model/dstdgcn.py:141-163).  ``p`` holds the block's
+    state-dict entries without prefix.  R_s aliases A_s in the reference
+    (:107-109); the formula below uses whatever the dict holds for both."""
+    cin = x.shape[1]
+    cout = p["conv_s.0.conv_f.weight"].shape[0]
+    if cin != cout:                                                   # :117-121
+        r = conv1x1(x, p["residual.0.weight"], p["residual.0.bias"])
+        r = batchnorm(r, sub(p, "residual.1.bn."), training)
+    else:
+        r = x
+    y = None
+    for i in range(p["A_s"].shape[0]):                                # :145-150
+        a = p["A_s"][i:i + 1] * p["W_s"][i:i + 1] + p["R_s"][i:i + 1]
+        z = dstdgc(x, sub(p, f"conv_s.{i}."), a, p["alpha_sm"], "spatial")
+        y = z if y is None else y + z
+    h = prelu(batchnorm(y, sub(p, "bn.bn."), training) + r, p["prelu.weight"])   # :151-154
+    a_t = p["A_t"][0:1] + p["R_t"][0:1]                               # :157-162
+    return dstdgc(h, sub(p, "conv_t.0."), a_t, p["alpha_tm"], "temporal")
+
+
+def dstdgcn(x, sd, num_layers, dtype=torch.float64, training=False):
+    """DSTDGCN.forward (model/dstdgcn.py:293-317), dropout treated as eval.
+
+    x: [N, T, V, 3]; sd: reference state dict (numpy or tensors)."""
+    sd = {k: _t(v, dtype) for k, v in sd.items() if not k.endswith("num_batches_tracked")}
+    x = _t(x, dtype)
+    residual = x[:, -1:]                                              # :299
+    h = torch.cat((x, x - residual), dim=-1).permute(0, 3, 1, 2)      # :298-303
+    h = dstdgcb(h, sub(sd, "conv_st_in.stgcn.0.0."), training)        # :305 (residual=None)
+    h = prelu(batchnorm(h, sub(sd, "bn_in.bn."), training), sd["prelu.weight"])   # :306-308
+    for i in range(num_layers):                                       # :310-311, 278-285
+        e = f"encoders.{i}."
+        y = dstdgcb(h, sub(sd, e + "0.stgcn.0.0."), training) + h     # Identity residual :247-248
+        h = prelu(batchnorm(y, sub(sd, e + "1.bn."), training), sd[e + "2.weight"])
+    y = dstdgcb(h, sub(sd, "conv_st_out.stgcn.0.0."), training)       # :313
+    return y.permute(0, 2, 3, 1) + residual                           # :314-315
+
+
+def dstdgcb_forward(x, sd, dtype=torch.float64):
+    sd = {k: _t(v, dtype) for k, v in sd.items() if not k.endswith("num_batches_tracked")}
+    return dstdgcb(_t(x, dtype), sd)
+
+
+def dstdgc_forward(x, sd, A, alpha, mode, dtype=torch.float64):
+    sd = {k: _t(v, dtype) for k, v in sd.items()}
+    return dstdgc(_t(x, dtype), sd, _t(A, dtype), _t(alpha, dtype).reshape(()), mode)
+
+
+def mpjpe_error_3d(outputs, targets):
+    """engine/utils/loss.py:52-65 with joint_weights=None (all-ones weights:
+    the broadcast makes it a plain mean of per-joint L2)."""
+    n, t, vc = outputs.shape
+    d = (outputs.reshape(-1, 3) - targets.reshape(-1, 3)).norm(dim=1)
+    return d.mean()

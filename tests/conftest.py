@@ -1,0 +1,36 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "dstd-gcn_amd")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+
+
+def load_npz(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def group(d, prefix):
+    """Sub-dict of an npz keyed '<prefix>/<rest>' -> {rest: array}."""
+    return {k[len(prefix):]: d[k] for k in d.files if k.startswith(prefix)}
+
+
+def rel_err(y, ref):
+    y = np.asarray(y, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    return float(np.abs(y - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return load_npz

@@ -1,0 +1,304 @@
+#!/usr/bin/env python
+"""Generate the golden parity fixtures by running the REFERENCE implementation.
+
+This script is the only place that executes reference code, and it runs only in
+the build container (``/root/reference`` does not exist on the GPU box).  It
+imports ``model/`` and ``engine/`` from the reference checkout, builds the ops,
+blocks and whole models named in SURVEY.md §8(c), randomises the parameters that
+are zero at init (``alpha_sm``, ``alpha_tm``, ``W_s``, ``R_t`` -- SURVEY §0.6),
+calibrates BatchNorm running statistics with train-mode passes, and records the
+inputs, the full ``state_dict`` and the outputs in fp32 and fp64 as ``.npz``
+files next to this script.  Nothing is pickled: every array is plain numpy.
+
+Usage:  python tests/golden/make_golden.py            (writes tests/golden/*.npz)
+
+Fixture list (all committed):
+  graphs.npz          Graph(layout).get_all_adjacency(), Time(T).get_all_adjacency()
+  dstdgc_ops.npz      single DSTDGC ops (spatial/temporal), random A, random alpha
+  dstdgcb.npz         DSTDGCB blocks 64->64, 6->64, 64->3 with calibrated BN
+  model_<cfg>.npz     whole DSTDGCN (h36m, cmu, 3dpw, h36m75) at B=4
+  engine.npz          mpjpe_error_3d + PredictionEngine.test metric + 3DPW loss curve
+"""
+import copy
+import os
+import sys
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+sys.dont_write_bytecode = True
+sys.path.insert(0, REF)
+
+from model import get_model  # noqa: E402  (reference)
+from model.dstdgcn import DSTDGC, DSTDGCB  # noqa: E402  (reference)
+from model.layers.graph import Graph  # noqa: E402  (reference)
+from model.layers.time import Time  # noqa: E402  (reference)
+
+# shapes per BASELINE.json / SURVEY §0.3
+CONFIGS = {
+    "h36m": dict(layout="h36m", V=22, Tin=10, Tout=25),
+    "cmu": dict(layout="cmu", V=25, Tin=10, Tout=25),
+    "3dpw": dict(layout="3dpw", V=23, Tin=10, Tout=30),
+    "h36m75": dict(layout="h36m", V=22, Tin=50, Tout=25),
+}
+
+
+def synth_input(gen, B, T, V, Tin, C=3):
+    """N(0,1) poses; future frames padded with the last observed one
+    (dataset/h36m.py:53-64 convention)."""
+    x = torch.randn(B, T, V, C, generator=gen, dtype=torch.float32)
+    x[:, Tin:] = x[:, Tin - 1:Tin]
+    return x
+
+
+def randomise_dynamic(block, gen):
+    """Make the dynamic terms of a DSTDGCB non-trivial."""
+    with torch.no_grad():
+        block.alpha_sm.copy_(torch.empty(1).uniform_(0.3, 1.0, generator=gen) *
+                             (1 if torch.rand(1, generator=gen) > 0.3 else -1))
+        block.alpha_tm.copy_(torch.empty(1).uniform_(0.3, 1.0, generator=gen))
+        block.W_s.copy_(0.3 * torch.randn(block.W_s.shape, generator=gen))
+        # R_s aliases A_s (model/dstdgcn.py:107-109): perturbing it moves both
+        block.R_s.add_(0.1 * torch.randn(block.R_s.shape, generator=gen))
+        T = block.R_t.shape[-1]
+        block.R_t.copy_(torch.empty(block.R_t.shape).uniform_(-1 / T**0.5, 1 / T**0.5, generator=gen))
+        block.prelu.weight.copy_(torch.empty(1).uniform_(0.1, 0.4, generator=gen))
+
+
+def perturb_bn(module, gen):
+    with torch.no_grad():
+        for m in module.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.weight.copy_(torch.empty(m.weight.shape).uniform_(0.8, 1.2, generator=gen))
+                m.bias.copy_(0.1 * torch.randn(m.bias.shape, generator=gen))
+            if isinstance(m, torch.nn.PReLU):
+                m.weight.copy_(torch.empty(1).uniform_(0.1, 0.4, generator=gen))
+
+
+def calibrate(module, make_x, passes=20):
+    module.train()
+    with torch.no_grad():
+        for _ in range(passes):
+            module(make_x())
+    module.eval()
+
+
+def sd_numpy(module, prefix=""):
+    out = {}
+    for k, v in module.state_dict().items():
+        out[prefix + k] = v.detach().cpu().numpy().copy()
+    return out
+
+
+def run64(module, *args):
+    m64 = copy.deepcopy(module).double().eval()
+    with torch.no_grad():
+        return m64(*[a.double() if torch.is_tensor(a) else a for a in args]).numpy()
+
+
+def put_outputs(out, prefix, y32, y64):
+    """Store the fp64 reference output rounded to fp32 (6e-8 relative, far
+    below the 1e-4 parity bar) plus the reference's own fp32-vs-fp64 error
+     so tests can scale tolerances without storing y32."""
+    out[prefix + "y64"] = y64.astype(np.float32)
+    out[prefix + "ref32_err"] = np.array(np.abs(y32 - y64).max() / np.abs(y64).max())
+
+
+def gen_graphs():
+    out = {}
+    for layout in ("h36m", "cmu", "3dpw"):
+        out[f"graph_{layout}"] = Graph(layout).get_all_adjacency()
+    for T in (6, 35, 40, 75):
+        out[f"time_{T}"] = Time(T).get_all_adjacency()
+    np.savez_compressed(os.path.join(HERE, "graphs.npz"), **out)
+
+
+def gen_ops(gen):
+    cases = [
+        # name, mode, cin, cout, T, V
+        ("s_64_64_h36m", "spatial", 64, 64, 35, 22),
+        ("s_6_64_h36m", "spatial", 6, 64, 35, 22),
+        ("s_64_3_h36m", "spatial", 64, 3, 35, 22),
+        ("s_64_64_cmu", "spatial", 64, 64, 35, 25),
+        ("t_64_64_h36m", "temporal", 64, 64, 35, 22),
+        ("t_3_3_h36m", "temporal", 3, 3, 35, 22),
+        ("t_64_64_3dpw", "temporal", 64, 64, 40, 23),
+        ("t_64_64_h36m75", "temporal", 64, 64, 75, 22),
+    ]
+    out = {}
+    B = 1
+    for name, mode, cin, cout, T, V in cases:
+        ref, kpt = (T, V) if mode == "spatial" else (V, T)
+        op = DSTDGC(cin, cout, ref, kpt, mode=mode).eval()
+        with torch.no_grad():
+            for p in op.parameters():  # biases are 0 at init: make them matter
+                if p.dim() == 1:
+                    p.copy_(0.1 * torch.randn(p.shape, generator=gen))
+        Ad = V if mode == "spatial" else T
+        A = torch.randn(1, Ad, Ad, generator=gen) * 0.3
+        alpha = torch.empty(1).uniform_(0.5, 1.5, generator=gen)
+        x = torch.randn(B, cin, T, V, generator=gen)
+        with torch.no_grad():
+            y32 = op(x, A, alpha).numpy()
+        y64 = run64(op, x, A, alpha)
+        out[f"{name}/x"] = x.numpy()
+        out[f"{name}/A"] = A.numpy()
+        out[f"{name}/alpha"] = alpha.numpy()
+        put_outputs(out, f"{name}/", y32, y64)
+        for k, v in sd_numpy(op).items():
+            out[f"{name}/sd/{k}"] = v
+    np.savez_compressed(os.path.join(HERE, "dstdgc_ops.npz"), **out)
+
+
+def gen_blocks(gen):
+    cases = [("b_64_64_h36m", 64, 64, "h36m", 35, 22), ("b_6_64_h36m", 6, 64, "h36m", 35, 22),
+             ("b_64_3_h36m", 64, 3, "h36m", 35, 22), ("b_64_64_cmu", 64, 64, "cmu", 35, 25)]
+    out = {}
+    B = 1
+    for name, cin, cout, layout, T, V in cases:
+        blk = DSTDGCB(cin, cout, T, V, layout)
+        randomise_dynamic(blk, gen)
+        perturb_bn(blk, gen)
+        with torch.no_grad():
+            for m in blk.modules():
+                if isinstance(m, torch.nn.Conv2d):
+                    m.bias.copy_(0.1 * torch.randn(m.bias.shape, generator=gen))
+        calibrate(blk, lambda: torch.randn(8, cin, T, V, generator=gen))
+        x = torch.randn(B, cin, T, V, generator=gen)
+        with torch.no_grad():
+            y32 = blk(x).numpy()
+        y64 = run64(blk, x)
+        out[f"{name}/x"] = x.numpy()
+        put_outputs(out, f"{name}/", y32, y64)
+        for k, v in sd_numpy(blk).items():
+            out[f"{name}/sd/{k}"] = v
+    np.savez_compressed(os.path.join(HERE, "dstdgcb.npz"), **out)
+
+
+def build_model(cfg, gen, dropout=0.1):
+    opts = dict(input_channels=6, input_time_frame=cfg["Tin"], output_time_frame=cfg["Tout"],
+                st_gcnn_dropout=dropout, joints_to_consider=cfg["V"], num_feature=64, num_layers=5,
+                layout=cfg["layout"])
+    model = get_model("dstdgcn", dstdgcn=opts)
+    for m in model.modules():
+        if isinstance(m, DSTDGCB):
+            randomise_dynamic(m, gen)
+    perturb_bn(model, gen)
+    return model, opts
+
+
+def gen_models(gen):
+    for tag, cfg in CONFIGS.items():
+        model, opts = build_model(cfg, gen)
+        T = cfg["Tin"] + cfg["Tout"]
+        calibrate(model, lambda: synth_input(gen, 16, T, cfg["V"], cfg["Tin"]))
+        x = synth_input(gen, 4, T, cfg["V"], cfg["Tin"])
+        with torch.no_grad():
+            y32 = model(x).numpy()
+        y64 = run64(model, x)
+        out = {"x": x.numpy()}
+        put_outputs(out, "", y32, y64)
+        for k, v in opts.items():
+            out[f"opt/{k}"] = np.array(v)
+        for k, v in sd_numpy(model).items():
+            out[f"sd/{k}"] = v
+        np.savez_compressed(os.path.join(HERE, f"model_{tag}.npz"), **out)
+
+
+def gen_engine(gen):
+    """mpjpe_error_3d, the PredictionEngine.test metric and a short 3DPW
+    config-5 training curve (engine/prediction.py:198-317, 319-430)."""
+    from engine.utils.loss import mpjpe_error_3d  # reference
+    from engine.prediction import PredictionEngine  # reference
+
+    out = {}
+    pred = torch.randn(3, 7, 22 * 3, generator=gen)
+    targ = torch.randn(3, 7, 22 * 3, generator=gen)
+    out["mpjpe/pred"] = pred.numpy()
+    out["mpjpe/targ"] = targ.numpy()
+    out["mpjpe/value"] = np.array(mpjpe_error_3d(pred, targ).item())
+
+    class _Log:
+        def info(self, *a, **k):
+            pass
+
+    # reference engine moves batches with .cuda(); identity on this CPU-only box
+    torch.Tensor.cuda = lambda self, *a, **k: self
+
+    cfg = CONFIGS["h36m"]
+    T = cfg["Tin"] + cfg["Tout"]
+    model, _ = build_model(cfg, gen)
+    calibrate(model, lambda: synth_input(gen, 16, T, cfg["V"], cfg["Tin"]))
+    eng_cfg = dict(learn=dict(opt="adam", lr=3e-3, weight_decay=0, gamma=0.9, step_size=5),
+                   loss=dict(joint=["jl2", 1]), n_out=1, transform="tsc", use_weight=False, inverse=True)
+    engine = PredictionEngine(eng_cfg, model, _Log())
+    # one synthetic test batch: 32 H36M joints x 3 = 96 dims, 22 used
+    n = 4
+    all_seqs = torch.randn(n, T, 96, generator=gen)
+    dim_used = np.array([6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32,
+                         36, 37, 38, 39, 40, 41, 42, 43, 44, 45, 46, 47, 51, 52, 53, 54, 55, 56, 57, 58, 59, 63, 64,
+                         65, 66, 67, 68, 75, 76, 77, 78, 79, 80, 81, 82, 83, 87, 88, 89, 90, 91, 92])
+    inputs = all_seqs[:, :, dim_used].clone()
+    inputs[:, cfg["Tin"]:] = inputs[:, cfg["Tin"] - 1:cfg["Tin"]]
+    j_ign = np.array([16, 20, 23, 24, 28, 31])
+    j_eq = np.array([13, 19, 22, 13, 27, 30])
+    eval_frame = [1, 3, 7, 9, 13, 24]
+    loader = [(inputs, None, None, all_seqs)]
+    avg, metric = engine.test(loader, input_n=cfg["Tin"], eval_frame=eval_frame, dim_used=dim_used,
+                              joint_to_ignore=j_ign, joint_equal=j_eq)
+    out["test/all_seqs"] = all_seqs.numpy()
+    out["test/inputs"] = inputs.numpy()
+    out["test/dim_used"] = dim_used
+    out["test/joint_to_ignore"] = j_ign
+    out["test/joint_equal"] = j_eq
+    out["test/eval_frame"] = np.array(eval_frame)
+    out["test/avg"] = np.array(avg)
+    out["test/metric"] = metric
+    for k, v in sd_numpy(model).items():
+        out[f"test/sd/{k}"] = v
+
+    # 3DPW config-5 style loss curve: dropout 0 (dstdgcn_3dpw.yaml:137), inverse=True
+    cfg = CONFIGS["3dpw"]
+    T = cfg["Tin"] + cfg["Tout"]
+    torch.manual_seed(0)
+    model, _ = build_model(cfg, gen, dropout=0.0)
+    out.update({f"train/sd0/{k}": v for k, v in sd_numpy(model).items()})
+    engine = PredictionEngine(eng_cfg, model, _Log())
+    batches = []
+    for _ in range(4):
+        seq = torch.randn(8, T, cfg["V"] * 3, generator=gen)
+        inp = seq.clone()
+        inp[:, cfg["Tin"]:] = inp[:, cfg["Tin"] - 1:cfg["Tin"]]
+        inv = seq.flip(1).clone()
+        inv[:, cfg["Tin"]:] = inv[:, cfg["Tin"] - 1:cfg["Tin"]]
+        batches.append((inp, inv, seq, seq))
+    losses = []
+    for step in range(5):
+        losses.append(engine.train([batches[step % 4]], step, max_iter=1))
+    for i, (inp, inv, seq, _) in enumerate(batches):
+        out[f"train/inp{i}"] = inp.numpy()
+        out[f"train/inv{i}"] = inv.numpy()
+        out[f"train/seq{i}"] = seq.numpy()
+    out["train/losses"] = np.array(losses)
+    np.savez_compressed(os.path.join(HERE, "engine.npz"), **out)
+
+
+def main():
+    torch.set_num_threads(8)
+    gen = torch.Generator().manual_seed(20250725)
+    torch.manual_seed(1234)
+    gen_graphs()
+    gen_ops(gen)
+    gen_blocks(gen)
+    gen_models(gen)
+    gen_engine(gen)
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main()
