@@ -1,0 +1,280 @@
+#!/usr/bin/env python
+"""Throughput of the MI355X DSTDGC hot path (BASELINE.json metric).
+
+A "step" is one eval-mode DSTDGCN forward over one synthetic H36M-shape batch
+(B=256 per GPU, T = 10 + 25 = 35 frames, V = 22 joints), inputs
+already resident in HBM.  Weights are the committed H36M fixture state dict
+(tests/golden/model_h36m.npz: random init, dynamic terms randomised, BN
+calibrated), so activations stay finite; values do not change the work.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+         (weak scaling: every rank runs its own B=256 shard, no data-path
+          collective; the per-rank elapsed time is MAX-reduced over RCCL)
+
+One JSON line on rank 0.  Besides the driver's fields it carries
+  roofline     : the dominant kernel family, timed with HIP events around its
+                 launches inside the timed region; achieved = its algorithmic
+                 FLOPs / its summed launch time, against the
+                 fp32 MFMA peak.  traffic = HBM bytes per launch from
+                 profiles/pmc_traffic.json (rocprofv3 PMC run) when present.
+  cpu_baseline : the CPU oracle (op-for-op restatement of the reference
+                 forward, torch fp32) timed on this host's cores, N=1 only.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dstd-gcn_amd"))
+sys.path.insert(0, ROOT)
+
+import dstd_native as native  # noqa: E402
+from model import get_model  # noqa: E402
+
+METRIC = "pose-sequences/sec forward (H36M 22J×50T, B=256) at 1/2/4/8 GPUs; % HBM roofline"
+PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 MFMA / vector peak (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+CONFIGS = {
+    "h36m": ("model_h36m.npz", "H36M-shape synthetic, T=10+25=35, V=22"),
+    "h36m75": ("model_h36m75.npz", "H36M-shape synthetic '50 in / 25 out', T=75, V=22"),
+    "cmu": ("model_cmu.npz", "CMU-shape synthetic, T=35, V=25"),
+    "3dpw": ("model_3dpw.npz", "3DPW-shape synthetic, T=40, V=23"),
+}
+
+
+def load_model(cfg, device):
+    d = np.load(os.path.join(ROOT, "tests", "golden", CONFIGS[cfg][0]), allow_pickle=False)
+    opts = {k[4:]: d[k].item() for k in d.files if k.startswith("opt/")}
+    sd = {k[3:]: d[k] for k in d.files if k.startswith("sd/")}
+    m = get_model("dstdgcn", dstdgcn=opts)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return m.to(device).eval(), opts, sd
+
+
+def synth_input(B, T, V, Tin, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, T, V, 3, generator=g)
+    x[:, Tin:] = x[:, Tin - 1:Tin]  # future frames = last observed (dataset/h36m.py:53-64)
+    return x
+
+
+# ---------------------------------------------------------------------------
+# algorithmic FLOPs per sample of each kernel family
+# ---------------------------------------------------------------------------
+def block_flops(cin, cout, T, V, tail):
+    TV, R = T * V, 2
+    adj_s = 2 * (2 * R * T * V * V + 2 * T * (R * T) * V * V + T * V * V + 2 * T * V * V)
+    spatial = 2 * (2 * cout * cin * TV + cout * TV) + 2 * (2 * cout * TV * V) + cout * TV + 4 * cout * TV
+    if cin != cout:
+        spatial += 2 * cout * cin * TV + cout * TV + 2 * cout * TV
+    spatial += 2 * R * (2 * cout * TV + TV)  # P_t, Q_t of h (conv_m1/m2 of the temporal DSTDGC)
+    adj_t = 2 * R * V * T * T + 2 * V * (R * V) * T * T + V * T * T + 2 * V * T * T
+    temporal = 2 * cout * cout * TV + cout * TV + 2 * cout * T * T * V
+    temporal += {"enc": 4, "in": 3, "out": 1}[tail] * cout * TV
+    if tail != "out":
+        temporal += 2 * 2 * R * (2 * cout * TV + TV)  # next block's P_s, Q_s
+    return {native.KIND_ADJ_S: adj_s, native.KIND_SPATIAL: spatial, native.KIND_ADJ_T: adj_t,
+            native.KIND_TEMPORAL: temporal}
+
+
+def model_block_flops(opts):
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    V, C, L = opts["joints_to_consider"], opts["num_feature"], opts["num_layers"]
+    blocks = [block_flops(opts["input_channels"], C, T, V, "in")]
+    blocks += [block_flops(C, C, T, V, "enc") for _ in range(L)]
+    blocks.append(block_flops(C, opts["input_channels"] // 2, T, V, "out"))
+    return blocks
+
+
+class Profiler:
+    """Event pairs around the launches of chosen kernel families."""
+
+    def __init__(self, L, pairs, kind_mask):
+        self.L = L
+        self.n = 2 * pairs
+        self.events = (ctypes.c_void_p * self.n)()
+        native.check(L.dstd_events_create(self.n, self.events), "dstd_events_create")
+        self.kinds = (ctypes.c_int * pairs)()
+        self.block = (ctypes.c_int * pairs)()
+        self.prof = native.Profile(kind_mask, pairs, 0, self.events, self.kinds, self.block)
+
+    def elapsed(self):
+        out = []
+        ms = ctypes.c_float()
+        for i in range(self.prof.count):
+            native.check(self.L.dstd_event_elapsed_ms(self.events[2 * i], self.events[2 * i + 1], ctypes.byref(ms)),
+                         "dstd_event_elapsed_ms")
+            out.append((self.kinds[i], self.block[i], ms.value))
+        return out
+
+    def close(self):
+        self.L.dstd_events_destroy(self.n, self.events)
+
+
+def forward_profiled(model, x, y, prof):
+    L = native.lib()
+    p = model._native_params()
+    B, T, V = x.shape[0], x.shape[1], x.shape[2]
+    nbytes = L.dstd_model_workspace_bytes(B, T, V, model.num_feature, model.num_layers)
+    ws = native.workspace(x.device, nbytes)
+    code = L.dstd_model_fwd_profiled(p, x.data_ptr(), B, y.data_ptr(), ws.data_ptr(), ws.numel(),
+                                     native.stream_handle(x.device), ctypes.byref(prof.prof))
+    native.check(code, "dstd_model_fwd_profiled")
+
+
+def load_traffic(kernel):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(opts, sd, x_cpu, min_s, max_s):
+    from oracle import dstdgcn_oracle as O  # baseline leg only
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd32 = {k: torch.from_numpy(v).float() for k, v in sd.items()}
+    with torch.no_grad():
+        O.dstdgcn(x_cpu, sd32, opts["num_layers"], dtype=torch.float32)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            O.dstdgcn(x_cpu, sd32, opts["num_layers"], dtype=torch.float32)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= min_s or el >= max_s:
+                break
+    return {"value": n * x_cpu.shape[0] / el, "unit": "seq/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} x B={x_cpu.shape[0]} forwards of the fp32 CPU oracle (oracle/dstdgcn_oracle.py, "
+                      f"op-for-op restatement of model/dstdgcn.py:293-317), {el:.1f} s, "
+                      f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--config", default="h36m", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    model, opts, sd = load_model(args.config, device)
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    V = opts["joints_to_consider"]
+    B = args.batch
+    x_cpu = synth_input(B, T, V, opts["input_time_frame"], 1234 + rank)
+    x = x_cpu.to(device)
+    y = torch.empty_like(x)
+    L = native.lib()
+    fl = model_block_flops(opts)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            model(x)
+        torch.cuda.synchronize()
+
+        # untimed pass: per-family launch times -> dominant family
+        nb = len(fl)
+        prof = Profiler(L, args.steps * (2 + 4 * nb), (1 << len(native.KIND_NAMES)) - 1)
+        for _ in range(args.steps):
+            forward_profiled(model, x, y, prof)
+        torch.cuda.synchronize()
+        per_kind = {}
+        for kind, _, ms in prof.elapsed():
+            per_kind[kind] = per_kind.get(kind, 0.0) + ms
+        prof.close()
+        dominant = max((k for k in per_kind if k in fl[0]), key=lambda k: per_kind[k])
+
+        # timed region: exactly K steps, events only around the dominant family
+        prof = Profiler(L, args.steps * nb, 1 << dominant)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            forward_profiled(model, x, y, prof)
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        launches = prof.elapsed()
+        prof.close()
+
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        # metric exchange over RCCL (the only collective): per-rank checksum
+        cs = torch.tensor([float(y.double().abs().sum())], device=device, dtype=torch.float64)
+        gathered = [torch.zeros_like(cs) for _ in range(world)]
+        dist.all_gather(gathered, cs)
+
+    kernel_ms = sum(ms for _, _, ms in launches)
+    kernel_flop = sum(fl[blk][dominant] for _, blk, _ in launches) * B
+    achieved = kernel_flop / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+    kname = native.KIND_NAMES[dominant]
+    traffic = load_traffic(kname)
+    total_flop_per_seq = sum(sum(b.values()) for b in fl)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(B * world * args.steps / elapsed, 2),
+            "unit": "seq/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (N(0,1) poses, future frames padded with the last observed; fixture weights)",
+            "config": {"workload": CONFIGS[args.config][1] + f", B={B}/GPU, eval forward", "global_batch": B * world,
+                       "seq_len": T, "joints": V, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3),
+                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         "traffic": traffic, "launches": len(launches),
+                         "avg_launch_us": round(kernel_ms / max(len(launches), 1) * 1e3, 2),
+                         "whole_forward_tflops": round(total_flop_per_seq * B * args.steps / elapsed / 1e12, 3)},
+            "kernel_ms_per_step": {native.KIND_NAMES[k]: round(v / args.steps, 4) for k, v in sorted(per_kind.items())},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(opts, sd, x_cpu, args.cpu_seconds, 30.0)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,639 @@
+// C ABI (include/dstd_gcn.h): argument checking, workspace carving and the
+// launch sequence of one DSTDGC / DSTDGCB / DSTDGCN forward.
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/dstd_gcn.h"
+#include "dstd_common.h"
+#include "dstd_kernels.h"
+
+using namespace dstd;
+
+namespace {
+
+constexpr int kMaxT = 96;
+constexpr int kMaxV = 32;
+constexpr int kMaxC = 64;
+
+// Bump allocator over the caller's workspace.  With base == nullptr it only
+// measures, so *_workspace_bytes and the forward share one layout.
+struct Carver {
+  char* base;
+  size_t off = 0;
+  float* take(size_t nfloats) {
+    off = (off + 255) & ~size_t(255);
+    float* p = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += nfloats * sizeof(float);
+    return p;
+  }
+};
+
+#define DSTD_TRY(expr)                         \
+  do {                                         \
+    hipError_t _e = (expr);                    \
+    if (_e != hipSuccess) return (int)_e;      \
+  } while (0)
+
+bool shape_ok(int B, int T, int V) { return B > 0 && T > 1 && V > 0; }
+bool limits_ok(int T, int V, int cin, int cout) {
+  return T <= kMaxT && V <= kMaxV && cin >= 1 && cin <= kMaxC && cout >= 1 && cout <= kMaxC;
+}
+bool gc_ok(const dstd_gc_weights* w) {
+  return w && w->wf && w->bf && w->wm1 && w->bm1 && w->wm2 && w->bm2 && w->wrm && w->brm;
+}
+bool bn_ok(const dstd_bn& b) { return b.weight && b.bias && b.running_mean && b.running_var; }
+bool block_ok(const dstd_block_params* p) {
+  if (!p || !p->A_s || !p->W_s || !p->R_s || !p->A_t || !p->R_t || !p->alpha_sm || !p->alpha_tm || !p->prelu)
+    return false;
+  if (!gc_ok(&p->conv_s[0]) || !gc_ok(&p->conv_s[1]) || !gc_ok(&p->conv_t) || !bn_ok(p->bn)) return false;
+  if (p->cin != p->cout && (!p->res_w || !p->res_b || !bn_ok(p->res_bn))) return false;
+  return true;
+}
+
+// Optional per-launch event brackets (dstd_model_fwd_profiled).
+struct Prof {
+  dstd_profile* p = nullptr;
+  int block = -1;
+  int open = -1;
+  void begin(int kind, hipStream_t s) {
+    open = -1;
+    if (!p || !(p->kind_mask & (1u << kind)) || p->count >= p->capacity) return;
+    open = p->count++;
+    p->kinds[open] = kind;
+    if (p->block) p->block[open] = block;
+    (void)hipEventRecord((hipEvent_t)p->events[2 * open], s);
+  }
+  void end(hipStream_t s) {
+    if (open >= 0) (void)hipEventRecord((hipEvent_t)p->events[2 * open + 1], s);
+    open = -1;
+  }
+};
+
+// Folded per-block constants (filled by k_fold).
+struct BlockFold {
+  float* bn_s;
+  float* bn_h;
+  float* rbn_s;
+  float* rbn_h;
+  float* astat_s;  // [2][V][V]
+  float* astat_t;  // [T][T]
+};
+
+struct BlockScratch {
+  float* adj_s;  // [B][2][T][V][V]
+  float* adj_t;  // [B][V][T][T]
+  float* pq_s;   // [B][8][T][V]
+  float* pq_t;   // [B][4][T][V]
+};
+
+void carve_fold(Carver& cv, BlockFold& f, int T, int V, int cout, bool res) {
+  f.bn_s = cv.take((size_t)cout * V);
+  f.bn_h = cv.take((size_t)cout * V);
+  f.rbn_s = res ? cv.take((size_t)cout * V) : nullptr;
+  f.rbn_h = res ? cv.take((size_t)cout * V) : nullptr;
+  f.astat_s = cv.take((size_t)2 * V * V);
+  f.astat_t = cv.take((size_t)T * T);
+}
+
+void carve_scratch(Carver& cv, BlockScratch& s, int B, int T, int V) {
+  s.adj_s = cv.take((size_t)B * 2 * T * V * V);
+  s.adj_t = cv.take((size_t)B * V * T * T);
+  s.pq_s = cv.take((size_t)B * 8 * T * V);
+  s.pq_t = cv.take((size_t)B * 4 * T * V);
+}
+
+using FoldList = std::vector<FoldJob>;
+
+void add_bn_job(FoldList& fa, const dstd_bn& bn, int n, float* s, float* h) {
+  fa.emplace_back();
+  FoldJob& j = fa.back();
+  j.kind = FOLD_BN;
+  j.n = n;
+  j.p0 = bn.weight;
+  j.p1 = bn.bias;
+  j.p2 = bn.running_mean;
+  j.p3 = bn.running_var;
+  j.eps = bn.eps;
+  j.o0 = s;
+  j.o1 = h;
+}
+
+void add_block_jobs(FoldList& fa, const dstd_block_params* p, const BlockFold& f, int T, int V) {
+  add_bn_job(fa, p->bn, p->cout * V, f.bn_s, f.bn_h);
+  if (p->cin != p->cout) add_bn_job(fa, p->res_bn, p->cout * V, f.rbn_s, f.rbn_h);
+  fa.emplace_back();
+  FoldJob& a = fa.back();
+  a.kind = FOLD_AWR;  // A_s*W_s + R_s for both graphs (model/dstdgcn.py:146-149)
+  a.n = 2 * V * V;
+  a.p0 = p->A_s;
+  a.p1 = p->W_s;
+  a.p2 = p->R_s;
+  a.o0 = f.astat_s;
+  fa.emplace_back();
+  FoldJob& t = fa.back();
+  t.kind = FOLD_AR;  // A_t + R_t (:158-160)
+  t.n = T * T;
+  t.p0 = p->A_t;
+  t.p1 = p->R_t;
+  t.o0 = f.astat_t;
+}
+
+hipError_t run_fold(const FoldList& jobs, hipStream_t s) {
+  for (size_t i = 0; i < jobs.size(); i += kMaxFoldJobs) {
+    FoldArgs fa{};
+    for (size_t j = i; j < jobs.size() && j < i + kMaxFoldJobs; ++j) fa.jobs[fa.njobs++] = jobs[j];
+    hipError_t e = launch_fold(fa, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// What the temporal kernel does after the block (see TemporalEpi).
+struct BlockTail {
+  int epi;
+  const float* xres;
+  const float* bn_s;
+  const float* bn_h;
+  const float* prelu;
+  const dstd_block_params* next;  // next block: its spatial P/Q are produced here
+};
+
+// One DSTDGCB on NTVC activations.  pq_s must already hold P/Q of x for the
+// block's two spatial DSTDGCs.
+hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const BlockScratch& sc, int B, int T, int V,
+                     const float* x, float* h, float* y, const BlockTail& tail, hipStream_t s, Prof& pf) {
+  const int TV = T * V;
+  const bool res = p->cin != p->cout;
+  // (1) spatial adjacency for both graphs
+  AdjArgs aa{};
+  aa.pq = sc.pq_s;
+  aa.pq_sN = 8L * TV;
+  for (int g = 0; g < 2; ++g) {
+    aa.p_off[g] = 4 * g * TV;
+    aa.q_off[g] = (4 * g + 2) * TV;
+    aa.W[g] = p->conv_s[g].wrm;
+    aa.bias[g] = p->conv_s[g].brm;
+    aa.astat[g] = f.astat_s + g * V * V;
+  }
+  aa.mode = 0;
+  aa.B = B;
+  aa.T = T;
+  aa.V = V;
+  aa.nrow = T;
+  aa.K = 2 * T;
+  aa.NA = V;
+  aa.ncol = V * V;
+  aa.ngroups = 2;
+  aa.alpha = p->alpha_sm;
+  aa.out = sc.adj_s;
+  aa.out_sN = 2L * T * V * V;
+  aa.out_sG = (long)T * V * V;
+  pf.begin(DSTD_KIND_ADJ_S, s);
+  hipError_t e = launch_adj(aa, s);
+  pf.end(s);
+  if (e != hipSuccess) return e;
+
+  // (2) spatial GC + bn + residual + prelu, P_t/Q_t of h
+  SpatialArgs sa{};
+  sa.x = x;
+  sa.B = B;
+  sa.T = T;
+  sa.V = V;
+  sa.Cin = p->cin;
+  sa.Cout = p->cout;
+  sa.NI = 2;
+  sa.G = res ? 3 : 2;
+  sa.adj = sc.adj_s;
+  for (int g = 0; g < 2; ++g) {
+    sa.wf[g] = p->conv_s[g].wf;
+    sa.bf[g] = p->conv_s[g].bf;
+  }
+  sa.wf[2] = res ? p->res_w : nullptr;
+  sa.bf[2] = res ? p->res_b : nullptr;
+  sa.epi = 1;
+  sa.bn_s = f.bn_s;
+  sa.bn_h = f.bn_h;
+  sa.rbn_s = f.rbn_s;
+  sa.rbn_h = f.rbn_h;
+  sa.prelu = p->prelu;
+  sa.y = h;
+  sa.pqw[0] = p->conv_t.wm1;
+  sa.pqw[1] = p->conv_t.wm2;
+  sa.pqb[0] = p->conv_t.bm1;
+  sa.pqb[1] = p->conv_t.bm2;
+  sa.npqw = 2;
+  sa.pq = sc.pq_t;
+  sa.Tt = 0;
+  pf.begin(DSTD_KIND_SPATIAL, s);
+  e = launch_spatial(sa, s);
+  pf.end(s);
+  if (e != hipSuccess) return e;
+
+  // (3) temporal adjacency
+  AdjArgs ta{};
+  ta.pq = sc.pq_t;
+  ta.pq_sN = 4L * TV;
+  ta.p_off[0] = 0;
+  ta.q_off[0] = 2 * TV;
+  ta.W[0] = p->conv_t.wrm;
+  ta.bias[0] = p->conv_t.brm;
+  ta.astat[0] = f.astat_t;
+  ta.mode = 1;
+  ta.B = B;
+  ta.T = T;
+  ta.V = V;
+  ta.nrow = V;
+  ta.K = 2 * V;
+  ta.NA = T;
+  ta.ncol = T * T;
+  ta.ngroups = 1;
+  ta.alpha = p->alpha_tm;
+  ta.out = sc.adj_t;
+  ta.out_sN = (long)V * T * T;
+  ta.out_sG = 0;
+  pf.begin(DSTD_KIND_ADJ_T, s);
+  e = launch_adj(ta, s);
+  pf.end(s);
+  if (e != hipSuccess) return e;
+
+  // (4) temporal GC + tail epilogue (+ next block's spatial P/Q)
+  TemporalArgs tt{};
+  tt.h = h;
+  tt.B = B;
+  tt.T = T;
+  tt.V = V;
+  tt.Cin = p->cout;
+  tt.Cout = p->cout;
+  tt.adj = sc.adj_t;
+  tt.wf = p->conv_t.wf;
+  tt.bf = p->conv_t.bf;
+  tt.epi = tail.epi;
+  tt.xres = tail.xres;
+  tt.bn_s = tail.bn_s;
+  tt.bn_h = tail.bn_h;
+  tt.prelu = tail.prelu;
+  tt.y = y;
+  if (tail.next) {
+    const dstd_block_params* q = tail.next;
+    tt.pqw[0] = q->conv_s[0].wm1;
+    tt.pqw[1] = q->conv_s[0].wm2;
+    tt.pqw[2] = q->conv_s[1].wm1;
+    tt.pqw[3] = q->conv_s[1].wm2;
+    tt.pqb[0] = q->conv_s[0].bm1;
+    tt.pqb[1] = q->conv_s[0].bm2;
+    tt.pqb[2] = q->conv_s[1].bm1;
+    tt.pqb[3] = q->conv_s[1].bm2;
+    tt.npqw = 4;
+    tt.pq = sc.pq_s;
+  }
+  tt.Vt = 0;
+  pf.begin(DSTD_KIND_TEMPORAL, s);
+  e = launch_temporal(tt, s);
+  pf.end(s);
+  return e;
+}
+
+hipError_t spatial_pq(const dstd_block_params* p, const float* x_ntvc, int B, int T, int V, float* pq_s,
+                      hipStream_t s) {
+  PQArgs pa{};
+  pa.x = x_ntvc;
+  pa.B = B;
+  pa.T = T;
+  pa.V = V;
+  pa.Cin = p->cin;
+  pa.w[0] = p->conv_s[0].wm1;
+  pa.w[1] = p->conv_s[0].wm2;
+  pa.w[2] = p->conv_s[1].wm1;
+  pa.w[3] = p->conv_s[1].wm2;
+  pa.b[0] = p->conv_s[0].bm1;
+  pa.b[1] = p->conv_s[0].bm2;
+  pa.b[2] = p->conv_s[1].bm1;
+  pa.b[3] = p->conv_s[1].bm2;
+  pa.nw = 4;
+  pa.pq = pq_s;
+  return launch_pq(pa, s);
+}
+
+// ---- layouts ---------------------------------------------------------------
+struct OpLayout {
+  float* xin;
+  float* yout;
+  float* pq;
+  float* adj;
+};
+void carve_op(Carver& cv, OpLayout& L, int mode, int B, int cin, int cout, int T, int V) {
+  L.xin = cv.take((size_t)B * T * V * cin);
+  L.yout = cv.take((size_t)B * T * V * cout);
+  L.pq = cv.take((size_t)B * 4 * T * V);
+  L.adj = cv.take(mode == DSTD_MODE_SPATIAL ? (size_t)B * T * V * V : (size_t)B * V * T * T);
+}
+
+struct BlockLayout {
+  float* xin;
+  float* h;
+  float* yout;
+  BlockFold f;
+  BlockScratch sc;
+};
+void carve_block(Carver& cv, BlockLayout& L, int B, int cin, int cout, int T, int V) {
+  L.xin = cv.take((size_t)B * T * V * cin);
+  L.h = cv.take((size_t)B * T * V * cout);
+  L.yout = cv.take((size_t)B * T * V * cout);
+  carve_fold(cv, L.f, T, V, cout, cin != cout);
+  carve_scratch(cv, L.sc, B, T, V);
+}
+
+struct ModelLayout {
+  float* act[3];
+  BlockFold f_in, f_out, f_enc[DSTD_MAX_LAYERS];
+  float* bnin_s;
+  float* bnin_h;
+  float* ebn_s[DSTD_MAX_LAYERS];
+  float* ebn_h[DSTD_MAX_LAYERS];
+  BlockScratch sc;
+};
+void carve_model(Carver& cv, ModelLayout& L, int B, int T, int V, int C, int layers, int cin_model,
+                 int cout_model) {
+  for (int i = 0; i < 3; ++i) L.act[i] = cv.take((size_t)B * T * V * C);
+  carve_fold(cv, L.f_in, T, V, C, cin_model != C);
+  carve_fold(cv, L.f_out, T, V, cout_model, C != cout_model);
+  for (int i = 0; i < layers; ++i) {
+    carve_fold(cv, L.f_enc[i], T, V, C, false);
+    L.ebn_s[i] = cv.take((size_t)C * V);
+    L.ebn_h[i] = cv.take((size_t)C * V);
+  }
+  L.bnin_s = cv.take((size_t)C * V);
+  L.bnin_h = cv.take((size_t)C * V);
+  carve_scratch(cv, L.sc, B, T, V);
+}
+
+hipError_t to_layout(const float* src, float* dst, int B, int C, int TV, int to_ntvc, hipStream_t s) {
+  TransposeArgs t{src, dst, B, C, TV, to_ntvc};
+  return launch_transpose(t, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dstd_version(void) { return "dstd-gcn-mi355x 0.1 (gfx950, fp32 MFMA 16x16x4)"; }
+
+const char* dstd_error_string(int code) {
+  switch (code) {
+    case DSTD_OK: return "ok";
+    case DSTD_EINVAL: return "invalid argument (null pointer or bad shape)";
+    case DSTD_EWORKSPACE: return "workspace too small";
+    case DSTD_ELIMIT: return "shape outside the supported envelope (T<=96, V<=32, C<=64)";
+    default: return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
+  }
+}
+
+size_t dstd_dstdgc_workspace_bytes(int mode, int B, int cin, int cout, int T, int V) {
+  Carver cv{nullptr};
+  OpLayout L;
+  carve_op(cv, L, mode, B, cin, cout, T, V);
+  return cv.off + 256;
+}
+
+size_t dstd_block_workspace_bytes(int B, int cin, int cout, int T, int V) {
+  Carver cv{nullptr};
+  BlockLayout L;
+  carve_block(cv, L, B, cin, cout, T, V);
+  return cv.off + 256;
+}
+
+size_t dstd_model_workspace_bytes(int B, int T, int V, int num_feature, int num_layers) {
+  Carver cv{nullptr};
+  ModelLayout L;
+  carve_model(cv, L, B, T, V, num_feature, num_layers, 6, 3);
+  return cv.off + 256;
+}
+
+int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, int V, const dstd_gc_weights* w,
+                    const float* A, const float* alpha, float* y, void* workspace, size_t workspace_bytes,
+                    void* stream) {
+  if (!x || !y || !A || !alpha || !gc_ok(w) || !workspace || !shape_ok(B, T, V)) return DSTD_EINVAL;
+  if (mode != DSTD_MODE_SPATIAL && mode != DSTD_MODE_TEMPORAL) return DSTD_EINVAL;
+  if (!limits_ok(T, V, cin, cout)) return DSTD_ELIMIT;
+  if (workspace_bytes < dstd_dstdgc_workspace_bytes(mode, B, cin, cout, T, V)) return DSTD_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  Carver cv{(char*)workspace};
+  OpLayout L;
+  carve_op(cv, L, mode, B, cin, cout, T, V);
+  const int TV = T * V;
+  DSTD_TRY(to_layout(x, L.xin, B, cin, TV, 1, s));
+  PQArgs pa{};
+  pa.x = L.xin;
+  pa.B = B;
+  pa.T = T;
+  pa.V = V;
+  pa.Cin = cin;
+  pa.w[0] = w->wm1;
+  pa.w[1] = w->wm2;
+  pa.b[0] = w->bm1;
+  pa.b[1] = w->bm2;
+  pa.nw = 2;
+  pa.pq = L.pq;
+  DSTD_TRY(launch_pq(pa, s));
+  AdjArgs aa{};
+  aa.pq = L.pq;
+  aa.pq_sN = 4L * TV;
+  aa.p_off[0] = 0;
+  aa.q_off[0] = 2 * TV;
+  aa.W[0] = w->wrm;
+  aa.bias[0] = w->brm;
+  aa.astat[0] = A;  // the caller's combined adjacency is row independent
+  aa.mode = mode;
+  aa.B = B;
+  aa.T = T;
+  aa.V = V;
+  aa.ngroups = 1;
+  aa.alpha = alpha;
+  aa.out = L.adj;
+  aa.out_sG = 0;
+  if (mode == DSTD_MODE_SPATIAL) {
+    aa.nrow = T;
+    aa.K = 2 * T;
+    aa.NA = V;
+    aa.ncol = V * V;
+    aa.out_sN = (long)T * V * V;
+  } else {
+    aa.nrow = V;
+    aa.K = 2 * V;
+    aa.NA = T;
+    aa.ncol = T * T;
+    aa.out_sN = (long)V * T * T;
+  }
+  DSTD_TRY(launch_adj(aa, s));
+  if (mode == DSTD_MODE_SPATIAL) {
+    SpatialArgs sa{};
+    sa.x = L.xin;
+    sa.B = B;
+    sa.T = T;
+    sa.V = V;
+    sa.Cin = cin;
+    sa.Cout = cout;
+    sa.NI = 1;
+    sa.G = 1;
+    sa.adj = L.adj;
+    sa.wf[0] = w->wf;
+    sa.bf[0] = w->bf;
+    sa.epi = 0;
+    sa.y = L.yout;
+    DSTD_TRY(launch_spatial(sa, s));
+  } else {
+    TemporalArgs ta{};
+    ta.h = L.xin;
+    ta.B = B;
+    ta.T = T;
+    ta.V = V;
+    ta.Cin = cin;
+    ta.Cout = cout;
+    ta.adj = L.adj;
+    ta.wf = w->wf;
+    ta.bf = w->bf;
+    ta.epi = TEPI_RAW;
+    ta.y = L.yout;
+    DSTD_TRY(launch_temporal(ta, s));
+  }
+  DSTD_TRY(to_layout(L.yout, y, B, cout, TV, 0, s));
+  return DSTD_OK;
+}
+
+int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float* y, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  if (!x || !y || !workspace || !block_ok(p) || !shape_ok(B, T, V)) return DSTD_EINVAL;
+  if (!limits_ok(T, V, p->cin, p->cout)) return DSTD_ELIMIT;
+  if (workspace_bytes < dstd_block_workspace_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  Carver cv{(char*)workspace};
+  BlockLayout L;
+  carve_block(cv, L, B, p->cin, p->cout, T, V);
+  FoldList fa;
+  add_block_jobs(fa, p, L.f, T, V);
+  DSTD_TRY(run_fold(fa, s));
+  DSTD_TRY(to_layout(x, L.xin, B, p->cin, T * V, 1, s));
+  DSTD_TRY(spatial_pq(p, L.xin, B, T, V, L.sc.pq_s, s));
+  BlockTail tail{TEPI_RAW, nullptr, nullptr, nullptr, nullptr, nullptr};
+  Prof pf;
+  DSTD_TRY(run_block(p, L.f, L.sc, B, T, V, L.xin, L.h, L.yout, tail, s, pf));
+  DSTD_TRY(to_layout(L.yout, y, B, p->cout, T * V, 0, s));
+  return DSTD_OK;
+}
+
+int dstd_model_fwd(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  return dstd_model_fwd_profiled(p, x, B, y, workspace, workspace_bytes, stream, nullptr);
+}
+
+int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
+                            size_t workspace_bytes, void* stream, dstd_profile* prof) {
+  if (!p || !x || !y || !workspace) return DSTD_EINVAL;
+  if (prof && (prof->capacity < 0 || (prof->capacity > 0 && (!prof->events || !prof->kinds)))) return DSTD_EINVAL;
+  Prof pf;
+  pf.p = prof;
+  const int T = p->T, V = p->V, C = p->num_feature, L_ = p->num_layers;
+  if (!shape_ok(B, T, V) || L_ < 0 || L_ > DSTD_MAX_LAYERS || p->in_channels != 6) return DSTD_EINVAL;
+  if (!limits_ok(T, V, p->in_channels, C)) return DSTD_ELIMIT;
+  if (!block_ok(&p->st_in) || !block_ok(&p->st_out) || !bn_ok(p->bn_in) || !p->prelu) return DSTD_EINVAL;
+  if (p->st_in.cin != 6 || p->st_in.cout != C || p->st_out.cin != C || p->st_out.cout != 3) return DSTD_EINVAL;
+  for (int i = 0; i < L_; ++i) {
+    if (!block_ok(&p->enc[i]) || !bn_ok(p->enc_bn[i]) || !p->enc_prelu[i]) return DSTD_EINVAL;
+    if (p->enc[i].cin != C || p->enc[i].cout != C) return DSTD_EINVAL;
+  }
+  if (workspace_bytes < dstd_model_workspace_bytes(B, T, V, C, L_)) return DSTD_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  Carver cv{(char*)workspace};
+  ModelLayout L;
+  carve_model(cv, L, B, T, V, C, L_, 6, 3);
+
+  FoldList fa;
+  add_block_jobs(fa, &p->st_in, L.f_in, T, V);
+  add_block_jobs(fa, &p->st_out, L.f_out, T, V);
+  add_bn_job(fa, p->bn_in, C * V, L.bnin_s, L.bnin_h);
+  for (int i = 0; i < L_; ++i) {
+    add_block_jobs(fa, &p->enc[i], L.f_enc[i], T, V);
+    add_bn_job(fa, p->enc_bn[i], C * V, L.ebn_s[i], L.ebn_h[i]);
+  }
+  pf.begin(DSTD_KIND_FOLD, s);
+  DSTD_TRY(run_fold(fa, s));
+  pf.end(s);
+
+  // input prep: x6 = cat(x, x - x[:, -1]) and block-0 spatial P/Q (:298-305)
+  PQArgs pa{};
+  pa.x = x;
+  pa.B = B;
+  pa.T = T;
+  pa.V = V;
+  pa.Cin = 6;
+  pa.make_x6 = 1;
+  pa.x6 = L.act[0];
+  const dstd_block_params* b0 = &p->st_in;
+  pa.w[0] = b0->conv_s[0].wm1;
+  pa.w[1] = b0->conv_s[0].wm2;
+  pa.w[2] = b0->conv_s[1].wm1;
+  pa.w[3] = b0->conv_s[1].wm2;
+  pa.b[0] = b0->conv_s[0].bm1;
+  pa.b[1] = b0->conv_s[0].bm2;
+  pa.b[2] = b0->conv_s[1].bm1;
+  pa.b[3] = b0->conv_s[1].bm2;
+  pa.nw = 4;
+  pa.pq = L.sc.pq_s;
+  pf.begin(DSTD_KIND_PREP, s);
+  DSTD_TRY(launch_pq(pa, s));
+  pf.end(s);
+
+  // conv_st_in -> bn_in -> prelu (dropout is identity in eval)
+  float* cur = L.act[0];
+  float* h = L.act[1];
+  float* out = L.act[2];
+  {
+    BlockTail tail{TEPI_IN, nullptr, L.bnin_s, L.bnin_h, p->prelu, L_ > 0 ? &p->enc[0] : &p->st_out};
+    pf.block = 0;
+    DSTD_TRY(run_block(&p->st_in, L.f_in, L.sc, B, T, V, cur, h, out, tail, s, pf));
+  }
+  // encoders: x = prelu_e(bn_e(DSTDGCB(x) + x))
+  for (int i = 0; i < L_; ++i) {
+    float* xin = out;
+    float* hh = cur;
+    float* yy = h;
+    BlockTail tail{TEPI_ENC, xin, L.ebn_s[i], L.ebn_h[i], p->enc_prelu[i], i + 1 < L_ ? &p->enc[i + 1] : &p->st_out};
+    pf.block = 1 + i;
+    DSTD_TRY(run_block(&p->enc[i], L.f_enc[i], L.sc, B, T, V, xin, hh, yy, tail, s, pf));
+    cur = xin;
+    h = hh;
+    out = yy;
+  }
+  // conv_st_out + output residual, written straight into y [B][T][V][3]
+  {
+    BlockTail tail{TEPI_OUT, x, nullptr, nullptr, nullptr, nullptr};
+    pf.block = 1 + L_;
+    DSTD_TRY(run_block(&p->st_out, L.f_out, L.sc, B, T, V, out, h, y, tail, s, pf));
+  }
+  return DSTD_OK;
+}
+
+int dstd_events_create(int n, void** events) {
+  if (n < 0 || (n > 0 && !events)) return DSTD_EINVAL;
+  for (int i = 0; i < n; ++i) {
+    hipEvent_t e;
+    DSTD_TRY(hipEventCreate(&e));
+    events[i] = (void*)e;
+  }
+  return DSTD_OK;
+}
+
+int dstd_events_destroy(int n, void** events) {
+  if (n < 0 || (n > 0 && !events)) return DSTD_EINVAL;
+  for (int i = 0; i < n; ++i)
+    if (events[i]) DSTD_TRY(hipEventDestroy((hipEvent_t)events[i]));
+  return DSTD_OK;
+}
+
+int dstd_event_elapsed_ms(void* start, void* stop, float* ms) {
+  if (!start || !stop || !ms) return DSTD_EINVAL;
+  return (int)hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop);
+}
+
+}  // extern "C"

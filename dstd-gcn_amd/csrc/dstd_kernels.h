@@ -1,0 +1,130 @@
+// Internal kernel interface (argument blocks + host launchers).  The public
+// C ABI is include/dstd_gcn.h; dstd_capi.hip sequences these launches.
+//
+// Internal activation layout is NTVC ([B][T][V][C], channels innermost): a
+// frame tile (spatial kernel) and a joint tile (temporal kernel) are then
+// both runs of contiguous channel vectors, and the MFMA accumulator (4
+// consecutive channels per lane) stores as one 16-byte write.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace dstd {
+
+// ---- parameter folding (one launch per forward) --------------------------
+enum FoldKind { FOLD_BN = 0, FOLD_AWR = 1, FOLD_AR = 2 };
+struct FoldJob {
+  int kind;   // FOLD_BN: o0 = w/sqrt(v+eps), o1 = b - m*o0
+              // FOLD_AWR: o0 = p0*p1 + p2   (A_s*W_s + R_s, model/dstdgcn.py:146-149)
+              // FOLD_AR:  o0 = p0 + p1      (A_t + R_t, :158-160)
+  int n;
+  const float* p0;
+  const float* p1;
+  const float* p2;
+  const float* p3;
+  float eps;
+  float* o0;
+  float* o1;
+};
+constexpr int kMaxFoldJobs = 32;  // per launch; longer lists are split
+struct FoldArgs {
+  FoldJob jobs[kMaxFoldJobs];
+  int njobs;
+};
+
+// ---- reduced embeddings P,Q (conv_m1 / conv_m2) ---------------------------
+// pq[n][2j+r][t][v] = sum_c w[j][r*Cin + c] * x[n][t][v][c] + b[j][r]
+// (j indexes up to 4 two-row weight blocks).  With make_x6 the input is the
+// model input [B][T][V][3] and the kernel also writes x6 = cat(x, x - x[:, -1])
+// (model/dstdgcn.py:298-303) in NTVC.
+struct PQArgs {
+  const float* x;
+  int B, T, V, Cin;
+  int make_x6;
+  float* x6;
+  const float* w[4];
+  const float* b[4];
+  int nw;
+  float* pq;
+};
+
+// ---- dynamic adjacency: Adj = alpha * (W_rm . tanh(P - Q) + b_rm) + Astat -
+struct AdjArgs {
+  const float* pq;
+  long pq_sN;          // floats per sample in pq
+  int p_off[2], q_off[2];
+  int mode;            // 0 spatial, 1 temporal (P/Q gather differs)
+  int B, T, V;
+  int nrow, K, NA, ncol;
+  int ngroups;
+  const float* W[2];
+  const float* bias[2];
+  const float* alpha;
+  const float* astat[2];  // [ncol], row independent
+  float* out;
+  long out_sN, out_sG;
+  int ctiles_per_wg, nchunks;
+};
+
+// ---- spatial GC (both graphs) + DSTDGCB mid epilogue ----------------------
+struct SpatialArgs {
+  const float* x;       // NTVC [B][T][V][Cin]
+  int B, T, V, Cin, Cout;
+  int NI, G;            // NI graphs (1 or 2); G = NI + has residual conv
+  const float* adj;     // [B][NI][T][V][V]
+  const float* wf[3];
+  const float* bf[3];
+  int epi;              // 0 raw sum; 1 prelu(bn(y) + r)
+  const float* bn_s;
+  const float* bn_h;
+  const float* rbn_s;
+  const float* rbn_h;
+  const float* prelu;
+  float* y;             // NTVC [B][T][V][Cout]
+  const float* pqw[4];
+  const float* pqb[4];
+  int npqw;
+  float* pq;            // [B][2*npqw][T][V] or null
+  int Tt;
+};
+
+// ---- temporal GC + inter-block epilogue ----------------------------------
+enum TemporalEpi { TEPI_RAW = 0, TEPI_ENC = 1, TEPI_IN = 2, TEPI_OUT = 3 };
+struct TemporalArgs {
+  const float* h;       // NTVC [B][T][V][Cin]
+  int B, T, V, Cin, Cout;
+  const float* adj;     // [B][V][T][T]
+  const float* wf;
+  const float* bf;
+  int epi;
+  const float* xres;
+  const float* bn_s;
+  const float* bn_h;
+  const float* prelu;
+  float* y;             // NTVC [B][T][V][Cout]
+  const float* pqw[4];
+  const float* pqb[4];
+  int npqw;
+  float* pq;
+  int Vt;
+};
+
+struct TransposeArgs {
+  const float* src;
+  float* dst;
+  int B, C, TV;
+  int to_ntvc;  // 1: [B][C][TV] -> [B][TV][C]; 0: inverse
+};
+
+hipError_t launch_fold(const FoldArgs& a, hipStream_t s);
+hipError_t launch_pq(const PQArgs& a, hipStream_t s);
+hipError_t launch_adj(AdjArgs a, hipStream_t s);
+hipError_t launch_spatial(SpatialArgs a, hipStream_t s);
+hipError_t launch_temporal(TemporalArgs a, hipStream_t s);
+hipError_t launch_transpose(const TransposeArgs& a, hipStream_t s);
+
+// tiling choices (host side, also used for workspace-free validation)
+int spatial_frames_per_wg(int T, int V, int Cin, int Cout, int G);
+int temporal_joints_per_wg(int T, int V, int Cin, int Cout);
+
+}  // namespace dstd

@@ -1,0 +1,174 @@
+"""ctypes binding of the MI355X C ABI (include/dstd_gcn.h).
+
+The shared library ``libdstd_gcn.so`` is built in-tree (``make -C dstd-gcn_amd``
+or ``__graft_entry__.build()``).  There is no fallback: if the library is
+missing or a tensor is not on a ROCm device, the call raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libdstd_gcn.so")
+
+MODE_SPATIAL = 0
+MODE_TEMPORAL = 1
+MAX_LAYERS = 16
+
+_fp = ctypes.POINTER(ctypes.c_float)
+
+
+class GCWeights(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wf", "bf", "wm1", "bm1", "wm2", "bm2", "wrm", "brm")]
+
+
+class BN(ctypes.Structure):
+    _fields_ = [("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p), ("running_mean", ctypes.c_void_p),
+                ("running_var", ctypes.c_void_p), ("eps", ctypes.c_float)]
+
+
+class BlockParams(ctypes.Structure):
+    _fields_ = [("cin", ctypes.c_int), ("cout", ctypes.c_int),
+                ("A_s", ctypes.c_void_p), ("W_s", ctypes.c_void_p), ("R_s", ctypes.c_void_p),
+                ("A_t", ctypes.c_void_p), ("R_t", ctypes.c_void_p),
+                ("alpha_sm", ctypes.c_void_p), ("alpha_tm", ctypes.c_void_p),
+                ("conv_s", GCWeights * 2), ("conv_t", GCWeights), ("bn", BN), ("prelu", ctypes.c_void_p),
+                ("res_w", ctypes.c_void_p), ("res_b", ctypes.c_void_p), ("res_bn", BN)]
+
+
+class ModelParams(ctypes.Structure):
+    _fields_ = [("T", ctypes.c_int), ("V", ctypes.c_int), ("num_layers", ctypes.c_int),
+                ("num_feature", ctypes.c_int), ("in_channels", ctypes.c_int),
+                ("st_in", BlockParams), ("bn_in", BN), ("prelu", ctypes.c_void_p),
+                ("enc", BlockParams * MAX_LAYERS), ("enc_bn", BN * MAX_LAYERS),
+                ("enc_prelu", ctypes.c_void_p * MAX_LAYERS), ("st_out", BlockParams)]
+
+
+class Profile(ctypes.Structure):
+    _fields_ = [("kind_mask", ctypes.c_uint), ("capacity", ctypes.c_int), ("count", ctypes.c_int),
+                ("events", ctypes.POINTER(ctypes.c_void_p)), ("kinds", ctypes.POINTER(ctypes.c_int)),
+                ("block", ctypes.POINTER(ctypes.c_int))]
+
+
+KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL = range(6)
+KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temporal_gc")
+
+_lib = None
+
+
+def lib():
+    """Load libdstd_gcn.so once; raise loudly if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"DSTD native library not built: {LIB_PATH} (run `make -C dstd-gcn_amd`)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.dstd_version.restype = ctypes.c_char_p
+        L.dstd_error_string.restype = ctypes.c_char_p
+        L.dstd_error_string.argtypes = [ci]
+        L.dstd_dstdgc_workspace_bytes.restype = sz
+        L.dstd_dstdgc_workspace_bytes.argtypes = [ci] * 6
+        L.dstd_block_workspace_bytes.restype = sz
+        L.dstd_block_workspace_bytes.argtypes = [ci] * 5
+        L.dstd_model_workspace_bytes.restype = sz
+        L.dstd_model_workspace_bytes.argtypes = [ci] * 5
+        L.dstd_dstdgc_fwd.restype = ci
+        L.dstd_dstdgc_fwd.argtypes = [ci, vp, ci, ci, ci, ci, ci, ctypes.POINTER(GCWeights), vp, vp, vp, vp, sz, vp]
+        L.dstd_block_fwd.restype = ci
+        L.dstd_block_fwd.argtypes = [ctypes.POINTER(BlockParams), vp, ci, ci, ci, vp, vp, sz, vp]
+        L.dstd_model_fwd.restype = ci
+        L.dstd_model_fwd.argtypes = [ctypes.POINTER(ModelParams), vp, ci, vp, vp, sz, vp]
+        L.dstd_model_fwd_profiled.restype = ci
+        L.dstd_model_fwd_profiled.argtypes = [ctypes.POINTER(ModelParams), vp, ci, vp, vp, sz, vp,
+                                              ctypes.POINTER(Profile)]
+        L.dstd_events_create.restype = ci
+        L.dstd_events_create.argtypes = [ci, ctypes.POINTER(ctypes.c_void_p)]
+        L.dstd_events_destroy.restype = ci
+        L.dstd_events_destroy.argtypes = [ci, ctypes.POINTER(ctypes.c_void_p)]
+        L.dstd_event_elapsed_ms.restype = ci
+        L.dstd_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_float)]
+        _lib = L
+    return _lib
+
+
+EXPORTS = ("dstd_version", "dstd_error_string", "dstd_dstdgc_workspace_bytes", "dstd_block_workspace_bytes",
+           "dstd_model_workspace_bytes", "dstd_dstdgc_fwd", "dstd_block_fwd", "dstd_model_fwd",
+           "dstd_model_fwd_profiled", "dstd_events_create", "dstd_events_destroy", "dstd_event_elapsed_ms")
+
+
+def check(code, what):
+    if code != 0:
+        msg = lib().dstd_error_string(code).decode()
+        raise RuntimeError(f"{what} failed ({code}): {msg}")
+
+
+# ---------------------------------------------------------------------------
+# tensor helpers
+# ---------------------------------------------------------------------------
+def require_device(t, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: the DSTD path runs on the MI355X only (tensor is on {t.device}); "
+                           "there is no CPU fallback")
+    if t.dtype != torch.float32:
+        raise ValueError(f"{name}: expected float32, got {t.dtype}")
+
+
+def ptr(t, name="tensor"):
+    require_device(t, name)
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+_ws_cache = {}
+
+
+def workspace(device, nbytes):
+    """Caller-owned scratch (torch caching allocator), grown on demand and kept
+    per (device, stream) so graph capture and steady state reuse one buffer."""
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf
+
+
+def gc_weights(dstdgc):
+    """GCWeights from a DSTDGC module (conv weights [O, I, 1, 1] are read as [O, I])."""
+    w = GCWeights()
+    for f, conv in (("f", dstdgc.conv_f), ("m1", dstdgc.conv_m1), ("m2", dstdgc.conv_m2), ("rm", dstdgc.conv_rm)):
+        setattr(w, "w" + f, ptr(conv.weight, f"conv_{f}.weight"))
+        setattr(w, "b" + f, ptr(conv.bias, f"conv_{f}.bias"))
+    return w
+
+
+def bn_struct(bnw):
+    """BN from the reference BatchNorm wrapper (.bn = BatchNorm1d(C*V))."""
+    b = bnw.bn
+    return BN(ptr(b.weight, "bn.weight"), ptr(b.bias, "bn.bias"), ptr(b.running_mean, "bn.running_mean"),
+              ptr(b.running_var, "bn.running_var"), float(b.eps))
+
+
+def block_struct(blk):
+    p = BlockParams()
+    p.cin, p.cout = blk.in_channels, blk.out_channels
+    p.A_s, p.W_s, p.R_s = ptr(blk.A_s, "A_s"), ptr(blk.W_s, "W_s"), ptr(blk.R_s, "R_s")
+    p.A_t, p.R_t = ptr(blk.A_t, "A_t"), ptr(blk.R_t, "R_t")
+    p.alpha_sm, p.alpha_tm = ptr(blk.alpha_sm, "alpha_sm"), ptr(blk.alpha_tm, "alpha_tm")
+    p.conv_s[0] = gc_weights(blk.conv_s[0])
+    p.conv_s[1] = gc_weights(blk.conv_s[1])
+    p.conv_t = gc_weights(blk.conv_t[0])
+    p.bn = bn_struct(blk.bn)
+    p.prelu = ptr(blk.prelu.weight, "prelu.weight")
+    if blk.in_channels != blk.out_channels:
+        conv, bnw = blk.residual[0], blk.residual[1]
+        p.res_w, p.res_b = ptr(conv.weight, "residual.0.weight"), ptr(conv.bias, "residual.0.bias")
+        p.res_bn = bn_struct(bnw)
+    return p

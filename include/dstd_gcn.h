@@ -1,0 +1,161 @@
+/*
+ * dstd_gcn.h -- C ABI of the MI355X-native DSTDGC hot path.
+ *
+ * The reference (Jaakk0F/DSTD-GCN) is pure PyTorch: its "FFI" for this path is
+ * the nn.Module API in /root/reference/model/dstdgcn.py.  Each entry point
+ * below replaces one forward of that API; the Python host layer
+ * (dstd-gcn_amd/model/dstdgcn.py) binds them with ctypes exactly as
+ * INTEGRATION.md shows.
+ *
+ *   dstd_dstdgc_fwd   <- DSTDGC.forward      model/dstdgcn.py:80-94
+ *   dstd_block_fwd    <- DSTDGCB.forward     model/dstdgcn.py:141-163
+ *   dstd_model_fwd    <- DSTDGCN.forward     model/dstdgcn.py:293-317 (eval)
+ *
+ * Conventions
+ *   - All tensors are device pointers to contiguous fp32.  Activations at the
+ *     op / block boundary are NCTV ([B][C][T][V], the reference layout); the
+ *     model boundary is [B][T][V][3] in and out (model/dstdgcn.py:295, 314).
+ *   - Weights are passed per call, in the reference's shapes: conv weights
+ *     [O][I] (the trailing 1x1 of Conv2d is dropped), BN vectors [C*V].
+ *   - Scalars that are nn.Parameters (alpha_sm, alpha_tm, PReLU slopes) are
+ *     device pointers to one float so a call never synchronises.
+ *   - Scratch comes from a caller-owned workspace of at least
+ *     dstd_*_workspace_bytes(...) bytes; the library allocates nothing and
+ *     keeps no state, so calls may be captured into a HIP graph.
+ *   - Every call is enqueued on `stream` (hipStream_t passed as void*).
+ *   - Return 0 on success, a positive hipError_t from a failed launch, or a
+ *     negative DSTD_E* code for bad arguments.  dstd_error_string() names it.
+ *   - Limits: T <= 96, V <= 32, channels <= 64, red_channels == 2.
+ */
+#ifndef DSTD_GCN_H
+#define DSTD_GCN_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSTD_OK 0
+#define DSTD_EINVAL -1      /* bad shape / null pointer */
+#define DSTD_EWORKSPACE -2  /* workspace too small */
+#define DSTD_ELIMIT -3      /* shape outside the supported envelope */
+
+#define DSTD_MODE_SPATIAL 0
+#define DSTD_MODE_TEMPORAL 1
+#define DSTD_MAX_LAYERS 16
+
+/* One DSTDGC (model/dstdgcn.py:53-94).  Shapes: wf [cout][cin], bf [cout],
+ * wm1/wm2 [2][cin], bm1/bm2 [2], wrm [ref][2*ref], brm [ref]
+ * (ref = T for spatial, V for temporal). */
+typedef struct dstd_gc_weights {
+  const float* wf;
+  const float* bf;
+  const float* wm1;
+  const float* bm1;
+  const float* wm2;
+  const float* bm2;
+  const float* wrm;
+  const float* brm;
+} dstd_gc_weights;
+
+/* BatchNorm wrapper (model/dstdgcn.py:35-50): nn.BatchNorm1d(C*V), eval mode.
+ * All four vectors are [C*V] with channel index c*V + v. */
+typedef struct dstd_bn {
+  const float* weight;
+  const float* bias;
+  const float* running_mean;
+  const float* running_var;
+  float eps;
+} dstd_bn;
+
+/* DSTDGCB (model/dstdgcn.py:97-163).  A_s may alias R_s (it does in the
+ * reference, :107-109); the runtime adjacency is A_s*W_s + R_s per graph. */
+typedef struct dstd_block_params {
+  int cin, cout;
+  const float* A_s;      /* [2][V][V] */
+  const float* W_s;      /* [2][V][V] */
+  const float* R_s;      /* [2][V][V] */
+  const float* A_t;      /* [1][T][T] */
+  const float* R_t;      /* [1][T][T] */
+  const float* alpha_sm; /* [1] */
+  const float* alpha_tm; /* [1] */
+  dstd_gc_weights conv_s[2];
+  dstd_gc_weights conv_t;
+  dstd_bn bn;
+  const float* prelu;    /* [1] */
+  const float* res_w;    /* [cout][cin] or NULL when cin == cout */
+  const float* res_b;    /* [cout] */
+  dstd_bn res_bn;
+} dstd_block_params;
+
+/* DSTDGCN (model/dstdgcn.py:252-317). */
+typedef struct dstd_model_params {
+  int T, V, num_layers, num_feature, in_channels;
+  dstd_block_params st_in;                  /* conv_st_in.stgcn.0.0 */
+  dstd_bn bn_in;                            /* bn_in.bn */
+  const float* prelu;                       /* prelu.weight */
+  dstd_block_params enc[DSTD_MAX_LAYERS];   /* encoders.<i>.0.stgcn.0.0 */
+  dstd_bn enc_bn[DSTD_MAX_LAYERS];          /* encoders.<i>.1.bn */
+  const float* enc_prelu[DSTD_MAX_LAYERS];  /* encoders.<i>.2.weight */
+  dstd_block_params st_out;                 /* conv_st_out.stgcn.0.0 */
+} dstd_model_params;
+
+const char* dstd_version(void);
+const char* dstd_error_string(int code);
+
+size_t dstd_dstdgc_workspace_bytes(int mode, int B, int cin, int cout, int T, int V);
+size_t dstd_block_workspace_bytes(int B, int cin, int cout, int T, int V);
+size_t dstd_model_workspace_bytes(int B, int T, int V, int num_feature, int num_layers);
+
+/* y = DSTDGC(x, A, alpha); x [B][cin][T][V] -> y [B][cout][T][V].
+ * A: [V][V] (spatial) or [T][T] (temporal), already combined by the caller
+ * (DSTDGCB passes A_s*W_s+R_s or A_t+R_t). */
+int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, int V,
+                    const dstd_gc_weights* w, const float* A, const float* alpha, float* y,
+                    void* workspace, size_t workspace_bytes, void* stream);
+
+/* y = DSTDGCB(x) in eval mode; x [B][cin][T][V] -> y [B][cout][T][V]. */
+int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float* y,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* y = DSTDGCN(x) in eval mode; x, y [B][T][V][in_channels/2]. */
+int dstd_model_fwd(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
+                   size_t workspace_bytes, void* stream);
+
+/* ---- measurement hooks (bench.py) ---------------------------------------
+ * Kernel families of one forward, in launch order per DSTDGCB:
+ *   ADJ_S (tanh GEMM, both graphs), SPATIAL (spatial GC + mid epilogue),
+ *   ADJ_T (tanh GEMM), TEMPORAL (temporal GC + tail epilogue). */
+#define DSTD_KIND_FOLD 0
+#define DSTD_KIND_PREP 1
+#define DSTD_KIND_ADJ_S 2
+#define DSTD_KIND_SPATIAL 3
+#define DSTD_KIND_ADJ_T 4
+#define DSTD_KIND_TEMPORAL 5
+#define DSTD_KIND_COUNT 6
+
+/* Every launch whose family bit is set in kind_mask is bracketed by a
+ * (start, stop) pair of hipEvents taken from events[2*i], events[2*i+1];
+ * kinds[i] and block[i] record the family and the DSTDGCB index (-1 outside
+ * blocks).  The call appends at `count` (pairs) and stops recording when
+ * `capacity` pairs are used.  Events come from dstd_events_create. */
+typedef struct dstd_profile {
+  unsigned kind_mask;
+  int capacity;
+  int count;
+  void** events;
+  int* kinds;
+  int* block;
+} dstd_profile;
+
+int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
+                            size_t workspace_bytes, void* stream, dstd_profile* prof);
+int dstd_events_create(int n, void** events);
+int dstd_events_destroy(int n, void** events);
+int dstd_event_elapsed_ms(void* start, void* stop, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSTD_GCN_H */

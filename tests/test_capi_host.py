@@ -1,0 +1,98 @@
+"""Host-side checks of the C ABI and the drop-in modules (no GPU needed)."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, group, load_npz
+import dstd_native as native
+from model import DSTDGC, DSTDGCB, DSTDGCN, get_model
+
+H36M = dict(input_channels=6, input_time_frame=10, output_time_frame=25, st_gcnn_dropout=0.1,
+            joints_to_consider=22, num_feature=64, num_layers=5, layout="h36m")
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "dstd_gcn.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(dstd_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    L = native.lib()
+    syms = header_symbols()
+    assert len(syms) == 12, syms
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(native.EXPORTS)
+
+
+def test_version_and_errors():
+    L = native.lib()
+    assert b"gfx950" in L.dstd_version()
+    assert L.dstd_error_string(-2) == b"workspace too small"
+    assert b"envelope" in L.dstd_error_string(-3)
+
+
+def test_workspace_sizes_scale_with_batch():
+    L = native.lib()
+    a = L.dstd_model_workspace_bytes(1, 35, 22, 64, 5)
+    b = L.dstd_model_workspace_bytes(256, 35, 22, 64, 5)
+    assert 0 < a < b
+    # three NTVC activations + adjacency scratch per sample dominate
+    per = 3 * 35 * 22 * 64 * 4 + (2 * 35 * 22 * 22 + 22 * 35 * 35) * 4
+    assert b >= 256 * per
+    assert L.dstd_dstdgc_workspace_bytes(0, 4, 64, 64, 35, 22) > 0
+    assert L.dstd_block_workspace_bytes(4, 6, 64, 35, 22) > 0
+
+
+def test_capi_rejects_bad_arguments_without_gpu():
+    L = native.lib()
+    # null pointers are rejected before any device work
+    assert L.dstd_model_fwd(None, None, 4, None, None, 0, None) == -1
+    assert L.dstd_block_fwd(None, None, 4, 35, 22, None, None, 0, None) == -1
+    w = native.GCWeights()
+    assert L.dstd_dstdgc_fwd(0, None, 4, 64, 64, 35, 22, w, None, None, None, None, 0, None) == -1
+
+
+def test_state_dict_schema_matches_reference():
+    m = get_model("dstdgcn", dstdgcn=H36M)
+    d = load_npz("model_h36m.npz")
+    ref = [k[3:] for k in d.files if k.startswith("sd/")]
+    assert list(m.state_dict().keys()) == ref
+    for k in ref:
+        assert tuple(m.state_dict()[k].shape) == d["sd/" + k].shape, k
+    assert sum(p.numel() for p in m.parameters() if p.requires_grad) == 173999
+    assert sum(p.numel() for p in m.parameters()) == 189350
+    m.load_state_dict({k: torch.from_numpy(d["sd/" + k]) for k in ref})
+
+
+def test_registry_keyerror():
+    with pytest.raises(KeyError):
+        get_model("stsgcn", stsgcn={})
+
+
+def test_A_s_R_s_alias_like_reference():
+    blk = DSTDGCB(64, 64, 35, 22, "h36m")
+    assert blk.A_s.data_ptr() == blk.R_s.data_ptr()
+    sd = blk.state_dict()
+    sd["A_s"] = torch.zeros_like(sd["A_s"])
+    sd["R_s"] = torch.full_like(sd["R_s"], 3.0)
+    blk.load_state_dict(sd)
+    assert torch.all(blk.A_s == 3.0) and torch.all(blk.R_s == 3.0)
+
+
+def test_cpu_forward_fails_loudly():
+    m = get_model("dstdgcn", dstdgcn=H36M).eval()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(torch.zeros(2, 35, 22, 3))
+    op = DSTDGC(64, 64, 35, 22, mode="spatial")
+    with pytest.raises(RuntimeError):
+        op(torch.zeros(1, 64, 35, 22), torch.zeros(1, 22, 22), 1.0)
+
+
+def test_train_mode_not_built_yet():
+    m = get_model("dstdgcn", dstdgcn=H36M)
+    with pytest.raises(NotImplementedError):
+        m(torch.zeros(2, 35, 22, 3))

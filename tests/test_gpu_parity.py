@@ -1,0 +1,145 @@
+"""MI355X parity: the HIP path vs the reference's own outputs (golden fixtures,
+fp64) and vs the CPU oracle.  Tolerance:
+  per op / block : max|y - y64| / max|y64| <= 1e-4
+  whole model    : <= max(1e-4, 2 * ref32_err) where ref32_err is the
+                   reference's own fp32-vs-fp64 error on that fixture.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import group, load_npz, rel_err
+from model import DSTDGC, DSTDGCB, DSTDGCN, get_model
+from oracle import dstdgcn_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+OPS = {  # name: (mode, cin, cout, T, V)
+    "s_64_64_h36m": ("spatial", 64, 64, 35, 22),
+    "s_6_64_h36m": ("spatial", 6, 64, 35, 22),
+    "s_64_3_h36m": ("spatial", 64, 3, 35, 22),
+    "s_64_64_cmu": ("spatial", 64, 64, 35, 25),
+    "t_64_64_h36m": ("temporal", 64, 64, 35, 22),
+    "t_3_3_h36m": ("temporal", 3, 3, 35, 22),
+    "t_64_64_3dpw": ("temporal", 64, 64, 40, 23),
+    "t_64_64_h36m75": ("temporal", 64, 64, 75, 22),
+}
+BLOCKS = {  # name: (cin, cout, layout, T, V)
+    "b_64_64_h36m": (64, 64, "h36m", 35, 22),
+    "b_6_64_h36m": (6, 64, "h36m", 35, 22),
+    "b_64_3_h36m": (64, 3, "h36m", 35, 22),
+    "b_64_64_cmu": (64, 64, "cmu", 35, 25),
+}
+MODELS = ["h36m", "cmu", "3dpw", "h36m75"]
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def load_model(tag):
+    d = load_npz(f"model_{tag}.npz")
+    opts = {k[4:]: d[k].item() for k in d.files if k.startswith("opt/")}
+    m = get_model("dstdgcn", dstdgcn=opts)
+    sd = group(d, "sd/")
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return m.to(DEV).eval(), d, sd, opts
+
+
+@pytest.mark.parametrize("name", list(OPS))
+def test_dstdgc_op(name):
+    mode, cin, cout, T, V = OPS[name]
+    d = load_npz("dstdgc_ops.npz")
+    ref, kpt = (T, V) if mode == "spatial" else (V, T)
+    op = DSTDGC(cin, cout, ref, kpt, mode=mode)
+    op.load_state_dict({k: torch.from_numpy(v) for k, v in group(d, f"{name}/sd/").items()})
+    op = op.to(DEV).eval()
+    with torch.no_grad():
+        y = op(t(d[f"{name}/x"]), t(d[f"{name}/A"]), t(d[f"{name}/alpha"]))
+    torch.cuda.synchronize()
+    assert rel_err(y.cpu().numpy(), d[f"{name}/y64"]) <= 1e-4
+
+
+@pytest.mark.parametrize("name", list(BLOCKS))
+def test_dstdgcb_block(name):
+    cin, cout, layout, T, V = BLOCKS[name]
+    d = load_npz("dstdgcb.npz")
+    blk = DSTDGCB(cin, cout, T, V, layout)
+    blk.load_state_dict({k: torch.from_numpy(v) for k, v in group(d, f"{name}/sd/").items()})
+    blk = blk.to(DEV).eval()
+    with torch.no_grad():
+        y = blk(t(d[f"{name}/x"]))
+    assert rel_err(y.cpu().numpy(), d[f"{name}/y64"]) <= 1e-4
+
+
+@pytest.mark.parametrize("tag", MODELS)
+def test_dstdgcn_model(tag):
+    m, d, _, _ = load_model(tag)
+    with torch.no_grad():
+        y = m(t(d["x"]))
+    tol = max(1e-4, 2 * float(d["ref32_err"]))
+    err = rel_err(y.cpu().numpy(), d["y64"])
+    assert err <= tol, (err, tol)
+
+
+def synth(B, T, V, Tin, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(B, T, V, 3, generator=g)
+    x[:, Tin:] = x[:, Tin - 1:Tin]
+    return x
+
+
+def test_large_batch_vs_oracle_and_sample_independence():
+    """B=256 (the bench workload): samples checked against the fp64 oracle,
+    and every sample equals its own B=1 run bit for bit (no cross-sample
+    coupling in eval; the property behind data-parallel sharding)."""
+    m, d, sd, opts = load_model("h36m")
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    x = synth(256, T, 22, opts["input_time_frame"], 7)
+    with torch.no_grad():
+        y = m(x.to(DEV)).cpu()
+        picks = [0, 1, 77, 255]
+        for i in picks:
+            yi = m(x[i:i + 1].to(DEV)).cpu()
+            assert torch.equal(yi[0], y[i]), i
+    y64 = O.dstdgcn(x[picks], sd, opts["num_layers"]).numpy()
+    tol = max(1e-4, 2 * float(d["ref32_err"]))
+    assert rel_err(y[picks].numpy(), y64) <= tol
+
+
+@pytest.mark.parametrize("B", [1, 3, 257])
+def test_ragged_batches(B):
+    m, d, sd, opts = load_model("3dpw")
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    x = synth(B, T, 23, opts["input_time_frame"], B)
+    with torch.no_grad():
+        y = m(x.to(DEV)).cpu()
+    assert torch.isfinite(y).all()
+    k = min(B, 3)
+    y64 = O.dstdgcn(x[:k], sd, opts["num_layers"]).numpy()
+    assert rel_err(y[:k].numpy(), y64) <= max(1e-4, 2 * float(d["ref32_err"]))
+
+
+def test_deterministic_repeat():
+    m, d, _, _ = load_model("cmu")
+    x = t(d["x"])
+    with torch.no_grad():
+        a = m(x)
+        b = m(x)
+    assert torch.equal(a, b)
+
+
+def test_bad_shape_raises():
+    m, d, _, _ = load_model("h36m")
+    with pytest.raises(AssertionError):
+        m(torch.zeros(2, 34, 22, 3, device=DEV))
+    with pytest.raises(ValueError):
+        m(torch.zeros(2, 35, 21, 3, device=DEV))
+
+
+def test_backward_refuses_loudly():
+    m, d, _, _ = load_model("h36m")
+    y = m(t(d["x"]))
+    with pytest.raises(NotImplementedError):
+        y.sum().backward()
