@@ -105,11 +105,13 @@ void carve_scratch(Carver& cv, BlockScratch& s, int B, int T, int V) {
 
 using FoldList = std::vector<FoldJob>;
 
-void add_bn_job(FoldList& fa, const dstd_bn& bn, int n, float* s, float* h) {
+void add_bn_job(FoldList& fa, const dstd_bn& bn, int C, int V, float* s, float* h) {
   fa.emplace_back();
   FoldJob& j = fa.back();
   j.kind = FOLD_BN;
-  j.n = n;
+  j.n = C * V;
+  j.C = C;
+  j.V = V;
   j.p0 = bn.weight;
   j.p1 = bn.bias;
   j.p2 = bn.running_mean;
@@ -120,8 +122,8 @@ void add_bn_job(FoldList& fa, const dstd_bn& bn, int n, float* s, float* h) {
 }
 
 void add_block_jobs(FoldList& fa, const dstd_block_params* p, const BlockFold& f, int T, int V) {
-  add_bn_job(fa, p->bn, p->cout * V, f.bn_s, f.bn_h);
-  if (p->cin != p->cout) add_bn_job(fa, p->res_bn, p->cout * V, f.rbn_s, f.rbn_h);
+  add_bn_job(fa, p->bn, p->cout, V, f.bn_s, f.bn_h);
+  if (p->cin != p->cout) add_bn_job(fa, p->res_bn, p->cout, V, f.rbn_s, f.rbn_h);
   fa.emplace_back();
   FoldJob& a = fa.back();
   a.kind = FOLD_AWR;  // A_s*W_s + R_s for both graphs (model/dstdgcn.py:146-149)
@@ -551,10 +553,10 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
   FoldList fa;
   add_block_jobs(fa, &p->st_in, L.f_in, T, V);
   add_block_jobs(fa, &p->st_out, L.f_out, T, V);
-  add_bn_job(fa, p->bn_in, C * V, L.bnin_s, L.bnin_h);
+  add_bn_job(fa, p->bn_in, C, V, L.bnin_s, L.bnin_h);
   for (int i = 0; i < L_; ++i) {
     add_block_jobs(fa, &p->enc[i], L.f_enc[i], T, V);
-    add_bn_job(fa, p->enc_bn[i], C * V, L.ebn_s[i], L.ebn_h[i]);
+    add_bn_job(fa, p->enc_bn[i], C, V, L.ebn_s[i], L.ebn_h[i]);
   }
   pf.begin(DSTD_KIND_FOLD, s);
   DSTD_TRY(run_fold(fa, s));

@@ -31,12 +31,12 @@ __device__ __forceinline__ float fast_tanh(float x) {
 
 __device__ __forceinline__ float prelu_f(float x, float w) { return x >= 0.f ? x : w * x; }
 
-__host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
-__host__ __device__ __forceinline__ int rup(int a, int b) { return cdiv(a, b) * b; }
+__host__ __device__ constexpr inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ constexpr inline int rup(int a, int b) { return cdiv(a, b) * b; }
 
 // Smallest stride >= n with stride % 32 == want (bank placement for LDS tiles
 // read with ds_read_b32 by 16-lane row groups).
-__host__ __device__ __forceinline__ int stride_mod32(int n, int want) {
+__host__ __device__ constexpr inline int stride_mod32(int n, int want) {
   int s = n;
   while ((s & 31) != want) ++s;
   return s;
@@ -46,7 +46,7 @@ __host__ __device__ __forceinline__ int stride_mod32(int n, int want) {
 // as an MFMA operand (lanes 0-15: 16 rows at column k, lanes 16-31: the same
 // rows at column k+1) then hits 32 distinct banks: 16 rows * (stride/2 odd)
 // cover the 16 even residues mod 32 and k+1 the odd ones.
-__host__ __device__ __forceinline__ int stride_2mod4(int n) {
+__host__ __device__ constexpr inline int stride_2mod4(int n) {
   int s = n;
   while ((s & 3) != 2) ++s;
   return s;
@@ -55,7 +55,7 @@ __host__ __device__ __forceinline__ int stride_2mod4(int n) {
 // K steps (4 input channels each) of a 1x1-conv GEMM, rounded up to a power
 // of two so the GEMM body is one of a few template instantiations.  Tiles are
 // zero-padded to 4*ks_for(Cin) channels.
-__host__ __device__ __forceinline__ int ks_for(int cin) {
+__host__ __device__ constexpr inline int ks_for(int cin) {
   const int ks = cdiv(cin, 4);
   int p = 1;
   while (p < ks) p <<= 1;

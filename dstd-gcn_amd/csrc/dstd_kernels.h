@@ -14,10 +14,13 @@ namespace dstd {
 // ---- parameter folding (one launch per forward) --------------------------
 enum FoldKind { FOLD_BN = 0, FOLD_AWR = 1, FOLD_AR = 2 };
 struct FoldJob {
-  int kind;   // FOLD_BN: o0 = w/sqrt(v+eps), o1 = b - m*o0
+  int kind;   // FOLD_BN: o0 = w/sqrt(v+eps), o1 = b - m*o0, written transposed:
+              //          input index c*V + v (BatchNorm1d channel) -> output v*C + c
+              //          so an epilogue reads 4 consecutive channels as one float4
               // FOLD_AWR: o0 = p0*p1 + p2   (A_s*W_s + R_s, model/dstdgcn.py:146-149)
               // FOLD_AR:  o0 = p0 + p1      (A_t + R_t, :158-160)
   int n;
+  int C, V;   // FOLD_BN only
   const float* p0;
   const float* p1;
   const float* p2;
@@ -87,6 +90,8 @@ struct SpatialArgs {
   float* pq;            // [B][2*npqw][T][V] or null
   int Tt;
 };
+// Folded BatchNorm vectors (bn_s, bn_h, rbn_s, rbn_h; temporal bn_s/bn_h) are
+// in the transposed [V][C] layout produced by k_fold.
 
 // ---- temporal GC + inter-block epilogue ----------------------------------
 enum TemporalEpi { TEPI_RAW = 0, TEPI_ENC = 1, TEPI_IN = 2, TEPI_OUT = 3 };
@@ -122,6 +127,12 @@ hipError_t launch_adj(AdjArgs a, hipStream_t s);
 hipError_t launch_spatial(SpatialArgs a, hipStream_t s);
 hipError_t launch_temporal(TemporalArgs a, hipStream_t s);
 hipError_t launch_transpose(const TransposeArgs& a, hipStream_t s);
+
+// shape-specialised variants (dstd_fast.hip); hipErrorNotSupported when the
+// shape has no instantiation and the generic kernel must run
+hipError_t launch_adj_fast(const AdjArgs& a, hipStream_t s, int nblocks);
+hipError_t launch_spatial_fast(const SpatialArgs& a, hipStream_t s);
+hipError_t launch_temporal_fast(const TemporalArgs& a, hipStream_t s);
 
 // tiling choices (host side, also used for workspace-free validation)
 int spatial_frames_per_wg(int T, int V, int Cin, int Cout, int G);

@@ -22,8 +22,9 @@ __global__ void k_fold(FoldArgs a) {
     if (j.kind == FOLD_BN) {
       // BatchNorm1d eval: (x - m)/sqrt(v + eps)*w + b = x*s + (b - m*s)
       const float s = j.p0[i] / sqrtf(j.p3[i] + j.eps);
-      j.o0[i] = s;
-      j.o1[i] = j.p1[i] - j.p2[i] * s;
+      const int c = i / j.V, v = i - c * j.V;
+      j.o0[v * j.C + c] = s;
+      j.o1[v * j.C + c] = j.p1[i] - j.p2[i] * s;
     } else if (j.kind == FOLD_AWR) {
       j.o0[i] = j.p0[i] * j.p1[i] + j.p2[i];
     } else {
@@ -207,6 +208,10 @@ hipError_t launch_adj(AdjArgs a, hipStream_t s) {
   a.ctiles_per_wg = rup(cdiv(nct, chunks), DSTD_WAVES);
   a.nchunks = cdiv(nct, a.ctiles_per_wg);
   const int nblocks = a.B * a.ngroups * a.nchunks;
+  {
+    const hipError_t fe = launch_adj_fast(a, s, nblocks);
+    if (fe != hipErrorNotSupported) return fe;
+  }
   const size_t lds = adj_lds_bytes(RT, a.K, a.NA);
   switch (RT) {
     case 1: return launch_adj_rt<1>(a, s, nblocks, lds);
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(256) void k_spatial(SpatialArgs a) {
       if (c >= Cout) continue;
       float val = res[it][j];
       if (a.epi) {
-        const int cv = c * V + w;
+        const int cv = w * Cout + c;
         const float r = has_res ? Fs[(NI * Cp + c) * SP + p] * a.rbn_s[cv] + a.rbn_h[cv] : xs[p * SX + c];
         val = prelu_f(val * a.bn_s[cv] + a.bn_h[cv] + r, pw);
       }
@@ -516,9 +521,9 @@ __global__ __launch_bounds__(256) void k_temporal(TemporalArgs a) {
       float val = res[it][j];
       if (a.epi == TEPI_ENC) {
         val += a.xres[o + c];
-        val = prelu_f(val * a.bn_s[c * V + v] + a.bn_h[c * V + v], pw);
+        val = prelu_f(val * a.bn_s[v * Cout + c] + a.bn_h[v * Cout + c], pw);
       } else if (a.epi == TEPI_IN) {
-        val = prelu_f(val * a.bn_s[c * V + v] + a.bn_h[c * V + v], pw);
+        val = prelu_f(val * a.bn_s[v * Cout + c] + a.bn_h[v * Cout + c], pw);
       } else if (a.epi == TEPI_OUT) {
         val += a.xres[((size_t)(n * T + T - 1) * V + v) * Cout + c];
       }
@@ -589,6 +594,10 @@ static void run_temporal(const TemporalArgs& a, hipStream_t s, int nblocks, size
 }
 
 hipError_t launch_spatial(SpatialArgs a, hipStream_t s) {
+  if (a.Tt <= 0) {
+    const hipError_t fe = launch_spatial_fast(a, s);
+    if (fe != hipErrorNotSupported) return fe;
+  }
   if (a.Tt <= 0) a.Tt = spatial_frames_per_wg(a.T, a.V, a.Cin, a.Cout, a.G);
   int NP16, SX, Cp, SP, lf;
   spatial_geom(a.Tt, a.V, a.Cin, a.Cout, a.G, a.NI, &NP16, &SX, &Cp, &SP, &lf);
@@ -604,6 +613,10 @@ hipError_t launch_spatial(SpatialArgs a, hipStream_t s) {
 }
 
 hipError_t launch_temporal(TemporalArgs a, hipStream_t s) {
+  if (a.Vt <= 0) {
+    const hipError_t fe = launch_temporal_fast(a, s);
+    if (fe != hipErrorNotSupported) return fe;
+  }
   if (a.Vt <= 0) a.Vt = temporal_joints_per_wg(a.T, a.V, a.Cin, a.Cout);
   int NP16, SX, Cp, SP, lf;
   temporal_geom(a.Vt, a.T, a.Cin, a.Cout, &NP16, &SX, &Cp, &SP, &lf);

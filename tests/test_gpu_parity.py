@@ -143,3 +143,81 @@ def test_backward_refuses_loudly():
     y = m(t(d["x"]))
     with pytest.raises(NotImplementedError):
         y.sum().backward()
+
+
+# ---- shapes outside the specialised set run the generic kernels -------------
+GENERIC_OPS = [("spatial", 32, 48, 20, 17), ("temporal", 48, 32, 20, 17), ("spatial", 5, 7, 9, 30),
+               ("temporal", 64, 64, 30, 22), ("spatial", 64, 64, 96, 22)]
+
+
+@pytest.mark.parametrize("mode,cin,cout,T,V", GENERIC_OPS)
+def test_dstdgc_generic_shapes_vs_oracle(mode, cin, cout, T, V):
+    torch.manual_seed(cin * 1000 + T)
+    ref, kpt = (T, V) if mode == "spatial" else (V, T)
+    op = DSTDGC(cin, cout, ref, kpt, mode=mode)
+    with torch.no_grad():
+        for p in op.parameters():
+            if p.dim() == 1:
+                p.copy_(0.1 * torch.randn(p.shape))
+    Ad = V if mode == "spatial" else T
+    A = 0.3 * torch.randn(1, Ad, Ad)
+    alpha = torch.tensor([0.7])
+    x = torch.randn(3, cin, T, V)
+    sd = {k: v.clone() for k, v in op.state_dict().items()}
+    y64 = O.dstdgc_forward(x, sd, A, alpha, mode).numpy()
+    opg = op.to(DEV).eval()
+    with torch.no_grad():
+        y = opg(x.to(DEV), A.to(DEV), alpha.to(DEV)).cpu().numpy()
+    assert rel_err(y, y64) <= 1e-4
+
+
+def test_dstdgcn_generic_T30():
+    """H36M with 10 in / 20 out frames (T=30): no specialisation, generic path."""
+    torch.manual_seed(3)
+    opts = dict(input_channels=6, input_time_frame=10, output_time_frame=20, st_gcnn_dropout=0.1,
+                joints_to_consider=22, num_feature=64, num_layers=2, layout="h36m")
+    m = get_model("dstdgcn", dstdgcn=opts)
+    with torch.no_grad():  # dynamic terms on, BN at non-trivial but tame stats
+        for name, p in m.named_parameters():
+            if name.endswith(("alpha_sm", "alpha_tm")):
+                p.fill_(0.5)
+            if name.endswith(("W_s", "R_t")):
+                p.copy_(0.1 * torch.randn(p.shape))
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_var.fill_(4.0)
+    x = synth(4, 30, 22, 10, 11)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    y64 = O.dstdgcn(x, sd, 2).numpy()
+    # uncalibrated BN makes the stack ill-conditioned: scale the bar by the
+    # fp32 oracle's own error, exactly as for the reference fixtures
+    ref32 = rel_err(O.dstdgcn(x, sd, 2, dtype=torch.float32).numpy(), y64)
+    m = m.to(DEV).eval()
+    with torch.no_grad():
+        y = m(x.to(DEV)).cpu().numpy()
+    assert rel_err(y, y64) <= max(1e-4, 4 * ref32), ref32
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 64), (6, 64), (64, 3)])
+def test_dstdgcb_generic_T30(cin, cout):
+    torch.manual_seed(cin + cout)
+    blk = DSTDGCB(cin, cout, 30, 22, "h36m")
+    with torch.no_grad():
+        blk.alpha_sm.fill_(0.6)
+        blk.alpha_tm.fill_(0.4)
+        blk.W_s.copy_(0.2 * torch.randn(blk.W_s.shape))
+        blk.R_t.copy_(0.1 * torch.randn(blk.R_t.shape))
+        for mod in blk.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.copy_(0.1 * torch.randn(mod.running_mean.shape))
+                mod.running_var.uniform_(0.5, 2.0)
+                mod.weight.uniform_(0.8, 1.2)
+            if isinstance(mod, torch.nn.Conv2d):
+                mod.bias.copy_(0.1 * torch.randn(mod.bias.shape))
+    x = torch.randn(2, cin, 30, 22)
+    sd = {k: v.clone() for k, v in blk.state_dict().items()}
+    y64 = O.dstdgcb_forward(x, sd).numpy()
+    blk = blk.to(DEV).eval()
+    with torch.no_grad():
+        y = blk(x.to(DEV)).cpu().numpy()
+    assert rel_err(y, y64) <= 1e-4
