@@ -186,11 +186,7 @@ static size_t adj_lds_bytes(int RT, int K, int NA) {
 
 template <int RT>
 static hipError_t launch_adj_rt(const AdjArgs& a, hipStream_t s, int nblocks, size_t lds) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)k_adj<RT>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_adj<RT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(k_adj<RT>, dim3(nblocks), dim3(256), lds, s, a);
   return hipGetLastError();
 }
@@ -565,8 +561,8 @@ int temporal_joints_per_wg(int T, int V, int Cin, int Cout) {
 }
 
 template <typename Kern>
-static void set_max_lds(Kern k) {
-  (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+static void set_max_lds(Kern k, size_t lds) {
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
 }
 
 #define DSTD_KS_DISPATCH(KSV, KERNEL, ...)                 \
@@ -581,15 +577,13 @@ static void set_max_lds(Kern k) {
 
 template <int KS>
 static void run_spatial(const SpatialArgs& a, hipStream_t s, int nblocks, size_t lds) {
-  static bool done = false;
-  if (!done) { set_max_lds(k_spatial<KS>); done = true; }
+  set_max_lds(k_spatial<KS>, lds);
   hipLaunchKernelGGL(k_spatial<KS>, dim3(nblocks), dim3(DSTD_THREADS), lds, s, a);
 }
 
 template <int KS>
 static void run_temporal(const TemporalArgs& a, hipStream_t s, int nblocks, size_t lds) {
-  static bool done = false;
-  if (!done) { set_max_lds(k_temporal<KS>); done = true; }
+  set_max_lds(k_temporal<KS>, lds);
   hipLaunchKernelGGL(k_temporal<KS>, dim3(nblocks), dim3(DSTD_THREADS), lds, s, a);
 }
 

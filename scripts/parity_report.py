@@ -1,0 +1,62 @@
+#!/usr/bin/env python
+"""Print the HIP path's error against every golden fixture (GPU box).
+
+Usage: python scripts/parity_report.py [out.json]
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dstd-gcn_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
+
+from conftest import group, load_npz, rel_err  # noqa: E402
+from model import DSTDGC, DSTDGCB, get_model  # noqa: E402
+import test_gpu_parity as G  # noqa: E402
+
+DEV = "cuda:0"
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def main():
+    rep = {}
+    d = load_npz("dstdgc_ops.npz")
+    for name, (mode, cin, cout, T, V) in G.OPS.items():
+        ref, kpt = (T, V) if mode == "spatial" else (V, T)
+        op = DSTDGC(cin, cout, ref, kpt, mode=mode)
+        op.load_state_dict({k: torch.from_numpy(v) for k, v in group(d, f"{name}/sd/").items()})
+        op = op.to(DEV).eval()
+        with torch.no_grad():
+            y = op(t(d[f"{name}/x"]), t(d[f"{name}/A"]), t(d[f"{name}/alpha"]))
+        rep["op/" + name] = (rel_err(y.cpu().numpy(), d[f"{name}/y64"]), float(d[f"{name}/ref32_err"]))
+    d = load_npz("dstdgcb.npz")
+    for name, (cin, cout, layout, T, V) in G.BLOCKS.items():
+        blk = DSTDGCB(cin, cout, T, V, layout)
+        blk.load_state_dict({k: torch.from_numpy(v) for k, v in group(d, f"{name}/sd/").items()})
+        blk = blk.to(DEV).eval()
+        with torch.no_grad():
+            y = blk(t(d[f"{name}/x"]))
+        rep["block/" + name] = (rel_err(y.cpu().numpy(), d[f"{name}/y64"]), float(d[f"{name}/ref32_err"]))
+    for tag in G.MODELS:
+        m, dd, _, _ = G.load_model(tag)
+        with torch.no_grad():
+            y = m(t(dd["x"]))
+        rep["model/" + tag] = (rel_err(y.cpu().numpy(), dd["y64"]), float(dd["ref32_err"]))
+    print(f"{'case':28s} {'hip_err':>10s} {'ref32_err':>10s}  ratio")
+    for k, (e, r) in rep.items():
+        print(f"{k:28s} {e:10.3e} {r:10.3e}  {e / max(r, 1e-30):6.2f}")
+    if len(sys.argv) > 1:
+        with open(sys.argv[1], "w") as f:
+            json.dump({k: {"hip_err": e, "ref32_err": r} for k, (e, r) in rep.items()}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
