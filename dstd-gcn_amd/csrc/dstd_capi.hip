@@ -97,8 +97,8 @@ void carve_fold(Carver& cv, BlockFold& f, int T, int V, int cout, bool res) {
 }
 
 void carve_scratch(Carver& cv, BlockScratch& s, int B, int T, int V) {
-  s.adj_s = cv.take((size_t)B * 2 * T * V * V);
-  s.adj_t = cv.take((size_t)B * V * T * T);
+  s.adj_s = cv.take((size_t)B * 2 * T * adj_ld_spatial(V));
+  s.adj_t = cv.take((size_t)B * V * adj_ld_temporal(T));
   s.pq_s = cv.take((size_t)B * 8 * T * V);
   s.pq_t = cv.take((size_t)B * 4 * T * V);
 }
@@ -189,8 +189,9 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   aa.ngroups = 2;
   aa.alpha = p->alpha_sm;
   aa.out = sc.adj_s;
-  aa.out_sN = 2L * T * V * V;
-  aa.out_sG = (long)T * V * V;
+  aa.ldo = adj_ld_spatial(V);
+  aa.out_sN = 2L * T * aa.ldo;
+  aa.out_sG = (long)T * aa.ldo;
   pf.begin(DSTD_KIND_ADJ_S, s);
   hipError_t e = launch_adj(aa, s);
   pf.end(s);
@@ -207,6 +208,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   sa.NI = 2;
   sa.G = res ? 3 : 2;
   sa.adj = sc.adj_s;
+  sa.adj_ld = adj_ld_spatial(V);
   for (int g = 0; g < 2; ++g) {
     sa.wf[g] = p->conv_s[g].wf;
     sa.bf[g] = p->conv_s[g].bf;
@@ -252,7 +254,8 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   ta.ngroups = 1;
   ta.alpha = p->alpha_tm;
   ta.out = sc.adj_t;
-  ta.out_sN = (long)V * T * T;
+  ta.ldo = adj_ld_temporal(T);
+  ta.out_sN = (long)V * ta.ldo;
   ta.out_sG = 0;
   pf.begin(DSTD_KIND_ADJ_T, s);
   e = launch_adj(ta, s);
@@ -268,6 +271,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   tt.Cin = p->cout;
   tt.Cout = p->cout;
   tt.adj = sc.adj_t;
+  tt.adj_ld = adj_ld_temporal(T);
   tt.wf = p->conv_t.wf;
   tt.bf = p->conv_t.bf;
   tt.epi = tail.epi;
@@ -328,7 +332,7 @@ void carve_op(Carver& cv, OpLayout& L, int mode, int B, int cin, int cout, int T
   L.xin = cv.take((size_t)B * T * V * cin);
   L.yout = cv.take((size_t)B * T * V * cout);
   L.pq = cv.take((size_t)B * 4 * T * V);
-  L.adj = cv.take(mode == DSTD_MODE_SPATIAL ? (size_t)B * T * V * V : (size_t)B * V * T * T);
+  L.adj = cv.take(mode == DSTD_MODE_SPATIAL ? (size_t)B * T * adj_ld_spatial(V) : (size_t)B * V * adj_ld_temporal(T));
 }
 
 struct BlockLayout {
@@ -459,13 +463,15 @@ int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, i
     aa.K = 2 * T;
     aa.NA = V;
     aa.ncol = V * V;
-    aa.out_sN = (long)T * V * V;
+    aa.ldo = adj_ld_spatial(V);
+    aa.out_sN = (long)T * aa.ldo;
   } else {
     aa.nrow = V;
     aa.K = 2 * V;
     aa.NA = T;
     aa.ncol = T * T;
-    aa.out_sN = (long)V * T * T;
+    aa.ldo = adj_ld_temporal(T);
+    aa.out_sN = (long)V * aa.ldo;
   }
   DSTD_TRY(launch_adj(aa, s));
   if (mode == DSTD_MODE_SPATIAL) {
@@ -479,6 +485,7 @@ int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, i
     sa.NI = 1;
     sa.G = 1;
     sa.adj = L.adj;
+    sa.adj_ld = adj_ld_spatial(V);
     sa.wf[0] = w->wf;
     sa.bf[0] = w->bf;
     sa.epi = 0;
@@ -493,6 +500,7 @@ int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, i
     ta.Cin = cin;
     ta.Cout = cout;
     ta.adj = L.adj;
+    ta.adj_ld = adj_ld_temporal(T);
     ta.wf = w->wf;
     ta.bf = w->bf;
     ta.epi = TEPI_RAW;

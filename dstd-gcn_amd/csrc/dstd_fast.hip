@@ -112,20 +112,35 @@ struct ConvGemm {
     if constexpr (MODE == 0 || MODE == 1) {
       constexpr int NSTEP = MODE == 0 ? 1 : NWV / MT;
       const int nt0 = MODE == 0 ? 0 : wave / MT;
-      for (int nt = nt0; nt < NT; nt += NSTEP) {
-        float bq[KS];
-        const float* xr = xs + (nt * 16 + cl) * SX + kl;
+      // two column tiles per pass: 2*MTW independent accumulator chains
+      for (int nt = nt0; nt < NT; nt += 2 * NSTEP) {
+        const bool two = nt + NSTEP < NT;
+        const int ntb = two ? nt + NSTEP : nt;
+        const float* xa = xs + (nt * 16 + cl) * SX + kl;
+        const float* xb = xs + (ntb * 16 + cl) * SX + kl;
+        f32x4 acc[MTW][2];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) bq[ks] = xr[ks * 4];
+        for (int m = 0; m < MTW; ++m) acc[m][0] = acc[m][1] = zero4();
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const float ba = xa[ks * 4], bb = xb[ks * 4];
+#pragma unroll
+          for (int m = 0; m < MTW; ++m) {
+            acc[m][0] = mfma16x16x4(af[m][ks], ba, acc[m][0]);
+            acc[m][1] = mfma16x16x4(af[m][ks], bb, acc[m][1]);
+          }
+        }
 #pragma unroll
         for (int m = 0; m < MTW; ++m) {
           const int mt = MODE == 0 ? wave + NWV * m : wave % MT;
-          f32x4 acc = zero4();
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) acc = mfma16x16x4(af[m][ks], bq[ks], acc);
           float* fo = Fs + (mt * 16 + kl * 4) * SP + nt * 16 + cl;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) fo[j * SP] = acc[j] + bias[m][j];
+          for (int j = 0; j < 4; ++j) fo[j * SP] = acc[m][0][j] + bias[m][j];
+          if (two) {
+            float* fo2 = Fs + (mt * 16 + kl * 4) * SP + ntb * 16 + cl;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) fo2[j * SP] = acc[m][1][j] + bias[m][j];
+          }
         }
       }
     } else {
@@ -146,7 +161,8 @@ struct ConvGemm {
 };
 
 // P/Q of the next DSTDGC on MFMA: out[ch][p] = sum_c w[ch][c] * hs[c][p] + b[ch]
-// over hs = Fs rows [0, CT*16).  nch = 2*npqw <= 8 output channels.
+// over hs = Fs rows [0, CT*16) (the temporal kernel's 8 channels fill half an
+// MFMA row tile; cheaper there than the cross-lane PQFuse reduction).
 template <int CT, int NT, int SP>
 struct PQGemm {
   static constexpr int KSO = CT * 4;
@@ -187,6 +203,46 @@ struct PQGemm {
   }
 };
 
+// P/Q of the next DSTDGC fused into the epilogue (conv_m1 / conv_m2,
+// model/dstdgcn.py:66-67):  out[ch][p] = sum_c w[ch][c] * h[c][p] + b[ch].
+// Each epilogue lane holds 4 consecutive channels of h at one position; it
+// forms the NCH partial dot products over those 4 channels, the 4 lane groups
+// (kl) that share the position are summed with two cross-lane xors, and the
+// CT per-16-channel partials meet in LDS, where one pass adds them.
+template <int NCH>
+struct PQFuse {
+  // LDS: weights [NCH][CP], bias [NCH], partials [CT][NCH][NP16]
+  static __device__ __forceinline__ void setup(const float* const* pqw, const float* const* pqb, int Cout, int CP,
+                                               float* wl, float* bl, int tid) {
+    for (int i = tid; i < NCH * CP; i += NTHR) {
+      const int ch = i / CP, c = i % CP;
+      wl[i] = c < Cout ? pqw[ch >> 1][(ch & 1) * Cout + c] : 0.f;
+    }
+    if (tid < NCH) bl[tid] = pqb[tid >> 1][tid & 1];
+  }
+  // all lanes of the wave must call (cross-lane reduction); 'ok' gates the write
+  static __device__ __forceinline__ void item(const float* wl, int CP, int c0, const float val[4], bool ok, int kl,
+                                              float* part_row /* partials + (mc*NCH)*NP16 + p */, int NP16) {
+    float part[NCH];
+    const float4* w4 = reinterpret_cast<const float4*>(wl + c0);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const float4 w = w4[ch * (CP / 4)];
+      part[ch] = w.x * val[0] + w.y * val[1] + w.z * val[2] + w.w * val[3];
+    }
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      part[ch] += __shfl_xor(part[ch], 16);
+      part[ch] += __shfl_xor(part[ch], 32);
+    }
+    if (ok) {
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch)
+        if ((ch & 3) == kl) part_row[ch * NP16] = part[ch];
+    }
+  }
+};
+
 }  // namespace
 
 // ===========================================================================
@@ -211,15 +267,20 @@ struct AdjGeom {
   static constexpr int SA = NA + 1;  // + one padding column
   static constexpr bool WREG = RT * KSTEPS <= 64;
   static constexpr int SR = stride_mod32(RT * 16, 16);
-  static constexpr int LDS_FLOATS = 4 * KP * SA + (WREG ? 0 : KP * SR) + 4;
+  static constexpr int OS = 20;                         // output staging row stride
+  static constexpr int STG = NWV * RT * 16 * OS;        // per-wave output staging (also W staging)
+  static constexpr int NCOLP = rup(NCOL + 1, 4);        // astat (+ padding column)
+  static_assert(STG >= K * NROW, "W staging must fit the output staging area");
+  static constexpr int LDS_FLOATS = 4 * KP * SA + (WREG ? 0 : KP * SR) + STG + NCOLP + 4;
 };
 
 template <int MODE, int NROW, int K, int NA>
-__global__ __launch_bounds__(NTHR) void k_adj_fast(AdjArgs a) {
+// 4 waves per SIMD (two 8-wave workgroups per CU): caps VGPRs at 128
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void k_adj_fast(AdjArgs a) {
   using Gm = AdjGeom<MODE, NROW, K, NA>;
   constexpr int RT = Gm::RT, KSTEPS = Gm::KSTEPS, KP = Gm::KP, NCOL = Gm::NCOL, NCT = Gm::NCT, SA = Gm::SA;
   constexpr bool WREG = Gm::WREG;
-  constexpr int SR = Gm::SR;
+  constexpr int SR = Gm::SR, OS = Gm::OS;
   constexpr int T = MODE == 0 ? NROW : NA;
   constexpr int V = MODE == 0 ? NA : NROW;
   constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
@@ -229,7 +290,9 @@ __global__ __launch_bounds__(NTHR) void k_adj_fast(AdjArgs a) {
   float* El = Ql + KP * SA;      // [KP][SA] 2^(c*P)
   float* Fl = El + KP * SA;      // [KP][SA] 2^(-c*Q)
   float* Wl = Fl + KP * SA;      // [KP][SR] (only when !WREG)
-  int* wide = reinterpret_cast<int*>(Wl + (WREG ? 0 : KP * SR));
+  float* stg = Wl + (WREG ? 0 : KP * SR);   // W staging, then per-wave output staging
+  float* asl = stg + Gm::STG;               // astat [NCOL]
+  int* wide = reinterpret_cast<int*>(asl + Gm::NCOLP);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kl = lane >> 4, cl = lane & 15;
   const int g = blockIdx.x % a.ngroups;
@@ -237,7 +300,11 @@ __global__ __launch_bounds__(NTHR) void k_adj_fast(AdjArgs a) {
   int n = blockIdx.x / a.ngroups;
   if (n >= a.B) return;
 
+  // ---- once per workgroup: W_rm (coalesced via LDS), bias rows, A-stat ----
   const float* W = a.W[g];
+  for (int i = tid; i < NROW * K; i += NTHR) stg[i] = W[i];
+  for (int i = tid; i < NCOL; i += NTHR) asl[i] = a.astat[g][i];
+  __syncthreads();
   float wr[WREG ? RT : 1][WREG ? KSTEPS : 1];
   if constexpr (WREG) {
 #pragma unroll
@@ -245,17 +312,16 @@ __global__ __launch_bounds__(NTHR) void k_adj_fast(AdjArgs a) {
 #pragma unroll
       for (int ks = 0; ks < KSTEPS; ++ks) {
         const int r = rt * 16 + cl, k = ks * 4 + kl;
-        wr[rt][ks] = (r < NROW && k < K) ? W[r * K + k] : 0.f;
+        wr[rt][ks] = (r < NROW && k < K) ? stg[r * K + k] : 0.f;
       }
   } else {
     for (int i = tid; i < KP * SR; i += NTHR) {
       const int k = i / SR, r = i % SR;
-      Wl[i] = (k < K && r < NROW) ? W[r * K + k] : 0.f;
+      Wl[i] = (k < K && r < NROW) ? stg[r * K + k] : 0.f;
     }
   }
   const float alpha = *a.alpha;
   const float* bias = a.bias[g];
-  const float* astat = a.astat[g];
   float brow[RT][4];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
@@ -279,10 +345,11 @@ __global__ __launch_bounds__(NTHR) void k_adj_fast(AdjArgs a) {
     });
   };
   fetch(n);
+  float* so = stg + wave * (RT * 16 * OS);  // this wave's output staging
 
   for (; n < a.B; n += stride) {
     if (tid == 0) *wide = 0;
-    __syncthreads();  // previous sample's readers are done; flag reset visible
+    __syncthreads();  // previous sample's readers (and the W staging) are done
     int bad = 0;
     st.store(tid, [&](int i, float2 v) {
       const int k = i / SA, c = i - (i / SA) * SA;
@@ -311,16 +378,20 @@ __global__ __launch_bounds__(NTHR) void k_adj_fast(AdjArgs a) {
       if (sep) {
         const float* pw = El + kl * SA + ca;
         const float* qw = Fl + kl * SA + cb;
+        float bv[KSTEPS];
 #pragma unroll
         for (int ks = 0; ks < KSTEPS; ++ks) {
           const float e = pw[ks * 4 * SA] * qw[ks * 4 * SA] + 1.f;
-          const float bv = 1.f - 2.f * __builtin_amdgcn_rcpf(e);
+          bv[ks] = 1.f - 2.f * __builtin_amdgcn_rcpf(e);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ++ks) {
 #pragma unroll
           for (int rt = 0; rt < RT; ++rt) {
             float av;
             if constexpr (WREG) av = wr[rt][ks];
             else av = Wl[(ks * 4 + kl) * SR + rt * 16 + cl];
-            acc[rt] = mfma16x16x4(av, bv, acc[rt]);
+            acc[rt] = mfma16x16x4(av, bv[ks], acc[rt]);
           }
         }
       } else {
@@ -337,15 +408,20 @@ __global__ __launch_bounds__(NTHR) void k_adj_fast(AdjArgs a) {
           }
         }
       }
-      if (cv) {
-        const float as = astat[col];
+      // epilogue: transpose the 16-column tile through this wave's LDS slot so
+      // each lane stores 16 contiguous bytes of one row (1 KiB per store)
+      const float as = asl[cv ? col : NCOL];
 #pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int row = rt * 16 + kl * 4 + j;
-            if (row < NROW) out[row * NCOL + col] = alpha * (acc[rt][j] + brow[rt][j]) + as;
-          }
+        for (int j = 0; j < 4; ++j) so[(rt * 16 + kl * 4 + j) * OS + cl] = alpha * (acc[rt][j] + brow[rt][j]) + as;
+      const int q = lane & 3;
+      const int c4 = ct * 16 + 4 * q;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int row = rt * 16 + (lane >> 2);
+        const float4 v = ld4(so + row * OS + 4 * q);
+        if (row < NROW && c4 < NCOL) st4(out + (size_t)row * a.ldo + c4, v);
       }
     }
   }
@@ -369,22 +445,27 @@ struct SpatialGeom {
   static constexpr int IPW = cdiv(ITEMS, NWV);
   static constexpr int ADJ = NI * TT * VP * V;
   static constexpr int NBN = (G > NI ? 4 : 2) * V * CP;  // folded BN vectors [V][Cout]
+  static constexpr int NCH = 4;                          // P_t, Q_t channels
+  static constexpr int PQL = NCH * CP + NCH;  // weights + bias; partials live in Fs group-0 rows
+  static_assert(CT * NCH * NP16 <= CP * SP, "P/Q partials must fit the dead Fs rows");
   using Conv = ConvGemm<KS, CT, G, NT, SX, SP>;
-  static constexpr int LDS_FLOATS = NP16 * SX + G * CP * SP + ADJ + 32 + NBN + Conv::WLDS;
+  static constexpr int LDS_FLOATS = NP16 * SX + G * CP * SP + ADJ + 32 + NBN + PQL + Conv::WLDS;
 };
 
 template <int V, int KS, int CT, int G, int NI, int TT>
 __global__ __launch_bounds__(NTHR) void k_spatial_fast(SpatialArgs a) {
   using Gm = SpatialGeom<V, KS, CT, G, NI, TT>;
   constexpr int SX = Gm::SX, SP = Gm::SP, CP = Gm::CP, VP = Gm::VP, NP16 = Gm::NP16;
-  constexpr int VV = V * V;
   constexpr bool HAS_RES = G > NI;
   extern __shared__ float lds[];
   float* xs = lds;                        // [NP16][SX]
   float* Fs = xs + NP16 * SX;             // [G*CP][SP]
   float* adjs = Fs + G * CP * SP;         // [NI][TT][VP][V] + zero pad
   float* bnl = adjs + Gm::ADJ + 32;       // bn_s, bn_h (, rbn_s, rbn_h) as [V][Cout]
-  float* wl = bnl + Gm::NBN;              // conv weights (mode 2 only)
+  float* pqwl = bnl + Gm::NBN;            // P/Q weights [NCH][CP]
+  float* pqbl = pqwl + Gm::NCH * CP;      // P/Q bias [NCH]
+  float* pqpart = Fs;                     // P/Q partials [CT][NCH][NP16] (group-0 rows, dead after aggregation)
+  float* wl = pqbl + Gm::NCH;             // conv weights (mode 2 only)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kl = lane >> 4, cl = lane & 15;
   const int T = a.T, Cin = a.Cin, Cout = a.Cout;
@@ -396,8 +477,8 @@ __global__ __launch_bounds__(NTHR) void k_spatial_fast(SpatialArgs a) {
   // ---- once per workgroup -------------------------------------------------
   typename Gm::Conv conv;
   conv.setup(a.wf, a.bf, Cin, Cout, wl, tid);
-  PQGemm<CT, Gm::NT, SP> pqg;
-  if (a.pq) pqg.setup(a.pqw, a.pqb, a.npqw, Cout, lane);
+  const bool want_pq = a.pq != nullptr && a.npqw == Gm::NCH / 2;
+  if (want_pq) PQFuse<Gm::NCH>::setup(a.pqw, a.pqb, Cout, CP, pqwl, pqbl, tid);
   const float pw = a.epi ? *a.prelu : 0.f;
   if (a.epi) {
     const int nv = V * Cout;
@@ -432,14 +513,15 @@ __global__ __launch_bounds__(NTHR) void k_spatial_fast(SpatialArgs a) {
       });
     }
     constexpr int PER = TT * VP * V;
-    const float* ag0 = a.adj + ((size_t)n * NI * T + t0) * VV;
+    const int ld = a.adj_ld;
+    const float* ag0 = a.adj + ((size_t)n * NI * T + t0) * ld;
     sa.load(tid, [&](int i) {
       const int gi = i / PER;
       const int ri = i - gi * PER;
       const int tt = ri / (VP * V);
       const int r = ri - tt * (VP * V);
       const int v = r / V;
-      return (tt < nf && v < V) ? ag0[(size_t)gi * T * VV + tt * VV + r] : 0.f;
+      return (tt < nf && v < V) ? ag0[((size_t)gi * T + tt) * ld + r] : 0.f;
     });
   };
   fetch(tile);
@@ -461,98 +543,126 @@ __global__ __launch_bounds__(NTHR) void k_spatial_fast(SpatialArgs a) {
     }
     sa.store(tid, [&](int i, float v) { adjs[i] = v; });
     __syncthreads();
+#ifndef DSTD_EXP_GC_NOFETCH
     if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
+#endif
 
+#ifndef DSTD_EXP_GC_NOCONV
     conv.run(xs, Fs, wl, tid);
+#endif
     __syncthreads();
 
     // ---- aggregation: y[c][tt][w] = sum_(g,v) F[(g,c)][(tt,v)] Adj_g[tt][v][w]
+    // items (independent accumulators) innermost: back-to-back MFMAs do not
+    // wait on each other's results
     f32x4 res[Gm::IPW];
+    const float* fa[Gm::IPW];
+    const float* fb[Gm::IPW];
 #pragma unroll
     for (int it = 0; it < Gm::IPW; ++it) {
       res[it] = zero4();
-      const int item = wave + it * NWV;
-      if (item >= Gm::ITEMS) continue;
+      int item = wave + it * NWV;
+      item = item < Gm::ITEMS ? item : wave;  // spare slots recompute a live item
       const int tt = item / (CT * Gm::NWT);
       const int rem = item - tt * (CT * Gm::NWT);
       const int mc = rem / Gm::NWT, nw = rem - (rem / Gm::NWT) * Gm::NWT;
-      f32x4 acc = zero4();
-#pragma unroll
-      for (int gi = 0; gi < NI; ++gi) {
-        const float* fa = Fs + (gi * CP + mc * 16 + cl) * SP + tt * V + kl;
-        const float* fb = adjs + ((gi * TT + tt) * VP + kl) * V + nw * 16 + cl;
-#pragma unroll
-        for (int ks = 0; ks < Gm::KV; ++ks) acc = mfma16x16x4(fa[ks * 4], fb[ks * 4 * V], acc);
-      }
-      res[it] = acc;
+      fa[it] = Fs + (mc * 16 + cl) * SP + tt * V + kl;
+      fb[it] = adjs + (tt * VP + kl) * V + nw * 16 + cl;
     }
+#ifndef DSTD_EXP_GC_NOAGG
+#pragma unroll
+    for (int gi = 0; gi < NI; ++gi)
+#pragma unroll
+      for (int ks = 0; ks < Gm::KV; ++ks)
+#pragma unroll
+        for (int it = 0; it < Gm::IPW; ++it)
+          res[it] = mfma16x16x4(fa[it][gi * CP * SP + ks * 4], fb[it][gi * TT * VP * V + ks * 4 * V], res[it]);
+#endif
     __syncthreads();  // Fs group-0 rows become the h tile below
 
-    // ---- epilogue: h = prelu(bn(y) + r) -> NTVC, keep h for P_t/Q_t --------
+    // ---- epilogue: h = prelu(bn(y) + r) -> NTVC; P_t/Q_t partials -> LDS --
 #pragma unroll
     for (int it = 0; it < Gm::IPW; ++it) {
       const int item = wave + it * NWV;
-      if (item >= Gm::ITEMS) continue;
+      if (item >= Gm::ITEMS) continue;  // wave-uniform
       const int tt = item / (CT * Gm::NWT);
       const int rem = item - tt * (CT * Gm::NWT);
       const int mc = rem / Gm::NWT, nw = rem - (rem / Gm::NWT) * Gm::NWT;
       const int w = nw * 16 + cl;
       const int c0 = mc * 16 + kl * 4;
-      if (w >= V || tt >= nf || c0 >= Cout) continue;
+      const bool pos_ok = w < V && tt < nf;
+      const bool ok = pos_ok && c0 < Cout;
       const int p = tt * V + w;
       float val[4] = {res[it][0], res[it][1], res[it][2], res[it][3]};
-      float* yo = a.y + ((size_t)(n * T + t0 + tt) * V + w) * Cout + c0;
-      if (Cout % 4 == 0) {
-        if (a.epi) {
-          const float4 s = ld4(bnl + w * Cout + c0), h = ld4(bnl + V * CP + w * Cout + c0);
-          float r[4];
-          if constexpr (HAS_RES) {
-            const float4 rs = ld4(bnl + 2 * V * CP + w * Cout + c0), rh = ld4(bnl + 3 * V * CP + w * Cout + c0);
-            const float* fr = Fs + (NI * CP + c0) * SP + p;
-            r[0] = fr[0] * rs.x + rh.x;
-            r[1] = fr[SP] * rs.y + rh.y;
-            r[2] = fr[2 * SP] * rs.z + rh.z;
-            r[3] = fr[3 * SP] * rs.w + rh.w;
-          } else {
-            const float* xr = xs + p * SX + c0;
-            r[0] = xr[0];
-            r[1] = xr[1];
-            r[2] = xr[2];
-            r[3] = xr[3];
-          }
-          val[0] = prelu_f(val[0] * s.x + h.x + r[0], pw);
-          val[1] = prelu_f(val[1] * s.y + h.y + r[1], pw);
-          val[2] = prelu_f(val[2] * s.z + h.z + r[2], pw);
-          val[3] = prelu_f(val[3] * s.w + h.w + r[3], pw);
-        }
-        st4(yo, make_float4(val[0], val[1], val[2], val[3]));
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Fs[(c0 + j) * SP + p] = val[j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = c0 + j;
-          if (c >= Cout) continue;
-          float v = val[j];
+      if (ok) {
+        float* yo = a.y + ((size_t)(n * T + t0 + tt) * V + w) * Cout + c0;
+        if (Cout % 4 == 0) {
           if (a.epi) {
-            const int cv = w * Cout + c;
-            float r;
-            if constexpr (HAS_RES) r = Fs[(NI * CP + c) * SP + p] * bnl[2 * V * CP + cv] + bnl[3 * V * CP + cv];
-            else r = xs[p * SX + c];
-            v = prelu_f(v * bnl[cv] + bnl[V * CP + cv] + r, pw);
+            const float4 s = ld4(bnl + w * Cout + c0), h = ld4(bnl + V * CP + w * Cout + c0);
+            float r[4];
+            if constexpr (HAS_RES) {
+              const float4 rs = ld4(bnl + 2 * V * CP + w * Cout + c0), rh = ld4(bnl + 3 * V * CP + w * Cout + c0);
+              const float* fr = Fs + (NI * CP + c0) * SP + p;
+              r[0] = fr[0] * rs.x + rh.x;
+              r[1] = fr[SP] * rs.y + rh.y;
+              r[2] = fr[2 * SP] * rs.z + rh.z;
+              r[3] = fr[3 * SP] * rs.w + rh.w;
+            } else {
+              const float* xr = xs + p * SX + c0;
+              r[0] = xr[0];
+              r[1] = xr[1];
+              r[2] = xr[2];
+              r[3] = xr[3];
+            }
+            val[0] = prelu_f(val[0] * s.x + h.x + r[0], pw);
+            val[1] = prelu_f(val[1] * s.y + h.y + r[1], pw);
+            val[2] = prelu_f(val[2] * s.z + h.z + r[2], pw);
+            val[3] = prelu_f(val[3] * s.w + h.w + r[3], pw);
           }
-          yo[j] = v;
-          Fs[c * SP + p] = v;
+#ifndef DSTD_EXP_GC_NOSTORE
+          st4(yo, make_float4(val[0], val[1], val[2], val[3]));
+#endif
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int c = c0 + j;
+            if (c >= Cout) {
+              val[j] = 0.f;
+              continue;
+            }
+            if (a.epi) {
+              const int cv = w * Cout + c;
+              float r;
+              if constexpr (HAS_RES) r = Fs[(NI * CP + c) * SP + p] * bnl[2 * V * CP + cv] + bnl[3 * V * CP + cv];
+              else r = xs[p * SX + c];
+              val[j] = prelu_f(val[j] * bnl[cv] + bnl[V * CP + cv] + r, pw);
+            }
+            yo[j] = val[j];
+          }
         }
       }
+#ifndef DSTD_EXP_GC_NOPQ
+      if (want_pq) {
+        if (!ok) val[0] = val[1] = val[2] = val[3] = 0.f;
+        PQFuse<Gm::NCH>::item(pqwl, CP, c0 < CP ? c0 : 0, val, pos_ok, kl,
+                              pqpart + (mc * Gm::NCH) * NP16 + p, NP16);
+      }
+#endif
     }
     __syncthreads();
-    if (a.pq) {
+#ifndef DSTD_EXP_GC_NOPQ
+    if (want_pq) {
       const int TV = T * V;
-      float* pqn = a.pq + (size_t)n * 2 * a.npqw * TV + t0 * V;
-      pqg.run(Fs, P, wave, lane, [=](int ch, int p, float v) { pqn[(size_t)ch * TV + p] = v; });
-      __syncthreads();
+      float* pqn = a.pq + (size_t)n * Gm::NCH * TV + t0 * V;
+      for (int i = tid; i < Gm::NCH * P; i += NTHR) {
+        const int ch = i / P, p = i - (i / P) * P;
+        float acc = pqbl[ch];
+#pragma unroll
+        for (int mc = 0; mc < CT; ++mc) acc += pqpart[(mc * Gm::NCH + ch) * NP16 + p];
+        pqn[(size_t)ch * TV + p] = acc;
+      }
     }
+#endif
   }
 }
 
@@ -583,7 +693,6 @@ template <int T, int KS, int CT, int VT>
 __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
   using Gm = TemporalGeom<T, KS, CT, VT>;
   constexpr int SX = Gm::SX, SP = Gm::SP, TP = Gm::TP, NP16 = Gm::NP16, CP = Gm::CP;
-  constexpr int TT2 = T * T;
   extern __shared__ float lds[];
   float* hs = lds;                    // [NP16][SX]
   float* Fs = hs + NP16 * SX;         // [CP][SP]
@@ -639,12 +748,13 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
         return a.h[((size_t)(n * T + t) * V + v0 + vv) * Cin + c];
       });
     }
-    const float* ag = a.adj + ((size_t)n * V + v0) * TT2;
+    const int ld = a.adj_ld;
+    const float* ag = a.adj + ((size_t)n * V + v0) * ld;
     sa.load(tid, [&](int i) {
       const int vv = i / (TP * T);
       const int r = i - vv * (TP * T);
       const int t = r / T;
-      return (vv < nv && t < T) ? ag[vv * TT2 + r] : 0.f;
+      return (vv < nv && t < T) ? ag[vv * ld + r] : 0.f;
     });
 #pragma unroll
     for (int it = 0; it < Gm::IPW; ++it) {
@@ -695,27 +805,29 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
     __syncthreads();
 
     f32x4 res[Gm::IPW];
+    const float* fa[Gm::IPW];
+    const float* fb[Gm::IPW];
 #pragma unroll
     for (int it = 0; it < Gm::IPW; ++it) {
       res[it] = zero4();
-      const int item = wave + it * NWV;
-      if (item >= Gm::ITEMS) continue;
+      int item = wave + it * NWV;
+      item = item < Gm::ITEMS ? item : wave;  // spare slots recompute a live item
       const int vv = item / (CT * Gm::NU);
       const int rem = item - vv * (CT * Gm::NU);
       const int mc = rem / Gm::NU, nu = rem - (rem / Gm::NU) * Gm::NU;
-      const float* fa = Fs + (mc * 16 + cl) * SP + vv * T + kl;
-      const float* fb = adjs + (vv * TP + kl) * T + nu * 16 + cl;
-      f32x4 acc = zero4();
-#pragma unroll
-      for (int ks = 0; ks < Gm::KT; ++ks) acc = mfma16x16x4(fa[ks * 4], fb[ks * 4 * T], acc);
-      res[it] = acc;
+      fa[it] = Fs + (mc * 16 + cl) * SP + vv * T + kl;
+      fb[it] = adjs + (vv * TP + kl) * T + nu * 16 + cl;
     }
+#pragma unroll
+    for (int ks = 0; ks < Gm::KT; ++ks)
+#pragma unroll
+      for (int it = 0; it < Gm::IPW; ++it) res[it] = mfma16x16x4(fa[it][ks * 4], fb[it][ks * 4 * T], res[it]);
     __syncthreads();
 
 #pragma unroll
     for (int it = 0; it < Gm::IPW; ++it) {
       const int item = wave + it * NWV;
-      if (item >= Gm::ITEMS) continue;
+      if (item >= Gm::ITEMS) continue;  // wave-uniform
       const int vv = item / (CT * Gm::NU);
       const int rem = item - vv * (CT * Gm::NU);
       const int mc = rem / Gm::NU, nu = rem - (rem / Gm::NU) * Gm::NU;

@@ -66,6 +66,7 @@ struct AdjArgs {
   const float* astat[2];  // [ncol], row independent
   float* out;
   long out_sN, out_sG;
+  int ldo;             // row stride of out (>= ncol, a multiple of 4 floats)
   int ctiles_per_wg, nchunks;
 };
 
@@ -74,7 +75,8 @@ struct SpatialArgs {
   const float* x;       // NTVC [B][T][V][Cin]
   int B, T, V, Cin, Cout;
   int NI, G;            // NI graphs (1 or 2); G = NI + has residual conv
-  const float* adj;     // [B][NI][T][V][V]
+  const float* adj;     // [B][NI][T][adj_ld], row = V*V values (v, w)
+  int adj_ld;
   const float* wf[3];
   const float* bf[3];
   int epi;              // 0 raw sum; 1 prelu(bn(y) + r)
@@ -98,7 +100,8 @@ enum TemporalEpi { TEPI_RAW = 0, TEPI_ENC = 1, TEPI_IN = 2, TEPI_OUT = 3 };
 struct TemporalArgs {
   const float* h;       // NTVC [B][T][V][Cin]
   int B, T, V, Cin, Cout;
-  const float* adj;     // [B][V][T][T]
+  const float* adj;     // [B][V][adj_ld], row = T*T values (t, u)
+  int adj_ld;
   const float* wf;
   const float* bf;
   int epi;
@@ -133,6 +136,11 @@ hipError_t launch_transpose(const TransposeArgs& a, hipStream_t s);
 hipError_t launch_adj_fast(const AdjArgs& a, hipStream_t s, int nblocks);
 hipError_t launch_spatial_fast(const SpatialArgs& a, hipStream_t s);
 hipError_t launch_temporal_fast(const TemporalArgs& a, hipStream_t s);
+
+// Leading dimensions of the materialised adjacencies: rows padded to a
+// multiple of 4 floats so the adjacency kernels store 16-byte vectors.
+inline int adj_ld_spatial(int V) { return ((V * V + 3) / 4) * 4; }
+inline int adj_ld_temporal(int T) { return ((T * T + 3) / 4) * 4; }
 
 // tiling choices (host side, also used for workspace-free validation)
 int spatial_frames_per_wg(int T, int V, int Cin, int Cout, int G);

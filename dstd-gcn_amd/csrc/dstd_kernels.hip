@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void k_adj(AdjArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int row = rt * 16 + kl * 4 + j;
-          if (row < nrow) out[(size_t)row * ncol + col] = alpha * (acc[rt][j] + bias[row]) + as;
+          if (row < nrow) out[(size_t)row * a.ldo + col] = alpha * (acc[rt][j] + bias[row]) + as;
         }
       }
     }
@@ -342,9 +342,9 @@ __global__ __launch_bounds__(256) void k_spatial(SpatialArgs a) {
   }
   const int VV = V * V;
   for (int gi = 0; gi < NI; ++gi) {
-    const float* ag = a.adj + (((size_t)n * NI + gi) * T + t0) * VV;
+    const float* ag = a.adj + (((size_t)n * NI + gi) * T + t0) * a.adj_ld;
     float* ad = adjs + gi * Tt * VV;
-    for (int i = tid; i < nf * VV; i += DSTD_THREADS) ad[i] = ag[i];
+    for (int i = tid; i < nf * VV; i += DSTD_THREADS) ad[i] = ag[(i / VV) * a.adj_ld + i % VV];
   }
   __syncthreads();
 
@@ -464,8 +464,8 @@ __global__ __launch_bounds__(256) void k_temporal(TemporalArgs a) {
   }
   (void)rowlen;
   const int TT = T * T;
-  const float* ag = a.adj + ((size_t)n * V + v0) * TT;
-  for (int i = tid; i < nv * TT; i += DSTD_THREADS) adjs[i] = ag[i];
+  const float* ag = a.adj + ((size_t)n * V + v0) * a.adj_ld;
+  for (int i = tid; i < nv * TT; i += DSTD_THREADS) adjs[i] = ag[(i / TT) * a.adj_ld + i % TT];
   __syncthreads();
 
   const float* wf[1] = {a.wf};

@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libdstd_gcn.so")
+# DSTD_LIB overrides the library (A/B experiments with variant builds)
+LIB_PATH = os.environ.get("DSTD_LIB") or os.path.join(os.path.dirname(_HERE), "libdstd_gcn.so")
 
 MODE_SPATIAL = 0
 MODE_TEMPORAL = 1
