@@ -1,0 +1,89 @@
+"""Data-parallel sharding of the eval forward.
+
+One process per GPU (``torch.distributed`` over RCCL; ``gloo`` in the CPU
+tests).  The DSTDGCN eval forward has no cross-sample coupling -- BatchNorm uses
+running statistics (``model/dstdgcn.py:35-50``), dropout is off, no op reduces
+over the batch -- so a global batch is partitioned into contiguous per-rank
+shards and each rank runs its shard alone: there is no exchange inside the
+forward.  The only collectives are outside it:
+
+* ``broadcast_module``  -- weights once, rank ``src`` -> all (~0.9 MB);
+* ``gather_batch``      -- per-rank outputs back to one tensor when a caller
+                           needs the whole batch (parity checks, export);
+* ``reduce_partials``   -- metric partial sums / counts (``all_reduce(SUM)``),
+                           e.g. the per-frame MPJPE sums of the test metric
+                           (``engine/prediction.py:366-404``).
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_bounds(n, world, rank):
+    """Contiguous shard ``[lo, hi)`` of ``n`` samples for ``rank``: the first
+    ``n % world`` ranks hold one extra sample, so shards differ by at most one
+    and concatenating them in rank order restores the batch."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} for world size {world}")
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def shard(x, world, rank, dim=0):
+    lo, hi = shard_bounds(x.shape[dim], world, rank)
+    return x.narrow(dim, lo, hi - lo)
+
+
+def broadcast_module(module, src=0, group=None):
+    """Broadcast every parameter and buffer of ``module`` from ``src`` in place.
+    Tensors sharing storage (the reference's ``A_s``/``R_s`` alias,
+    ``model/dstdgcn.py:107-109``) are sent once, so the alias survives."""
+    seen = set()
+    for t in list(module.parameters()) + list(module.buffers()):
+        key = (t.untyped_storage().data_ptr(), t.storage_offset(), tuple(t.shape))
+        if key in seen:
+            continue
+        seen.add(key)
+        with torch.no_grad():
+            dist.broadcast(t.data, src=src, group=group)
+
+
+def gather_batch(y_local, n_total, group=None):
+    """All-gather per-rank shards (``shard_bounds`` layout, dim 0) into the full
+    ``[n_total, ...]`` batch on every rank.  Ragged shards are padded to the
+    largest shard for the collective and trimmed afterwards."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    lo, hi = shard_bounds(n_total, world, rank)
+    if y_local.shape[0] != hi - lo:
+        raise ValueError(f"rank {rank}: shard has {y_local.shape[0]} samples, expected {hi - lo}")
+    cap = shard_bounds(n_total, world, 0)[1]
+    pad = y_local.new_zeros((cap,) + tuple(y_local.shape[1:]))
+    pad[:hi - lo] = y_local
+    bufs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad.contiguous(), group=group)
+    parts = []
+    for r in range(world):
+        a, b = shard_bounds(n_total, world, r)
+        parts.append(bufs[r][:b - a])
+    return torch.cat(parts, 0)
+
+
+def reduce_partials(*tensors, group=None):
+    """``all_reduce(SUM)`` of metric partials in one collective (the tensors
+    are packed into one fp64 buffer); returns the reduced tensors."""
+    flat = torch.cat([t.reshape(-1).to(torch.float64) for t in tensors])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    out, off = [], 0
+    for t in tensors:
+        out.append(flat[off:off + t.numel()].reshape(t.shape).to(t.dtype))
+        off += t.numel()
+    return out
+
+
+def sharded_forward(fn, x_full, group=None, gather=True):
+    """Run ``fn`` on this rank's shard of ``x_full``; optionally gather."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    y = fn(shard(x_full, world, rank))
+    return gather_batch(y, x_full.shape[0], group=group) if gather else y

@@ -1,0 +1,147 @@
+"""Multi-process (world size 2, gloo, CPU) coverage of the data-parallel path
+(SURVEY §8(e)): contiguous sharding, weight broadcast that keeps the
+A_s/R_s alias, ragged all-gather, metric all_reduce, and that a sharded eval
+forward equals the full-batch forward (the property the GPU bench's weak
+scaling rests on; the per-rank compute here is the fp64 oracle because there
+is no GPU in this leg -- on the box each rank runs the HIP path)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT, group, load_npz
+
+import dstd_dist as D
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _to_numpy(v):
+    # plain arrays through the queue: torch's shared-memory tensor hand-off
+    # dies with the worker process
+    if isinstance(v, torch.Tensor):
+        return v.numpy()
+    if isinstance(v, dict):
+        return {k: _to_numpy(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return type(v)(_to_numpy(x) for x in v)
+    return v
+
+
+def _worker(rank, world, port, fn_name, q):
+    import sys
+    for p in (ROOT, PKG, os.path.join(ROOT, "tests")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        q.put((rank, _to_numpy(globals()[fn_name](rank, world))))
+    except Exception as e:  # surface worker failures in the parent
+        q.put((rank, e))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_world(fn_name, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, v in res.items():
+        if isinstance(v, Exception):
+            raise v
+    return {r: _to_torch(v) for r, v in res.items()}
+
+
+def _to_torch(v):
+    import numpy as np
+    if isinstance(v, np.ndarray):
+        return torch.from_numpy(v)
+    if isinstance(v, dict):
+        return {k: _to_torch(x) for k, x in v.items()}
+    if isinstance(v, (list, tuple)):
+        return type(v)(_to_torch(x) for x in v)
+    return v
+
+
+@pytest.mark.parametrize("n,world", [(0, 2), (1, 2), (5, 2), (2048, 8), (257, 8), (3, 4)])
+def test_shard_bounds_partition(n, world):
+    spans = [D.shard_bounds(n, world, r) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (a, b), (c, _) in zip(spans, spans[1:]):
+        assert b == c
+    sizes = [b - a for a, b in spans]
+    assert max(sizes) - min(sizes) <= (1 if n else 0)
+    with pytest.raises(ValueError):
+        D.shard_bounds(n, world, world)
+
+
+# ---- per-rank bodies (run under gloo, world 2) -------------------------------
+def _broadcast_body(rank, world):
+    from model import DSTDGCB
+    torch.manual_seed(100 + rank)  # ranks start with different weights
+    blk = DSTDGCB(64, 64, 35, 22, "h36m")
+    with torch.no_grad():
+        for p in blk.parameters():
+            p.copy_(torch.randn(p.shape))
+    D.broadcast_module(blk, src=0)
+    alias = blk.A_s.data_ptr() == blk.R_s.data_ptr()
+    return {k: v.clone() for k, v in blk.state_dict().items()}, alias
+
+
+def _gather_body(rank, world):
+    n = 5
+    lo, hi = D.shard_bounds(n, world, rank)
+    y_local = torch.arange(lo, hi, dtype=torch.float32)[:, None].repeat(1, 3)
+    full = D.gather_batch(y_local, n)
+    sums, cnt = D.reduce_partials(torch.tensor([float(hi - lo), 2.0 * rank]), torch.tensor([hi - lo]))
+    return full, sums, cnt
+
+
+def _sharded_model_body(rank, world):
+    from oracle import dstdgcn_oracle as O
+    d = load_npz("model_h36m.npz")
+    sd = {k: torch.from_numpy(v) for k, v in group(d, "sd/").items()}
+    opts = {k[4:]: d[k].item() for k in d.files if k.startswith("opt/")}
+    x = torch.from_numpy(d["x"])  # B=4 fixture batch
+    y = D.sharded_forward(lambda xs: O.dstdgcn(xs, sd, opts["num_layers"]), x)
+    return y, torch.from_numpy(d["y64"])
+
+
+def test_broadcast_module_syncs_weights_and_keeps_alias():
+    res = run_world("_broadcast_body")
+    (sd0, a0), (sd1, a1) = res[0], res[1]
+    assert a0 and a1
+    assert sd0.keys() == sd1.keys()
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k
+
+
+def test_gather_batch_ragged_and_reduce_partials():
+    res = run_world("_gather_body")
+    for r in (0, 1):
+        full, sums, cnt = res[r]
+        assert torch.equal(full[:, 0], torch.arange(5, dtype=torch.float32))
+        assert torch.equal(sums, torch.tensor([5.0, 2.0]))
+        assert cnt.item() == 5 and cnt.dtype == torch.int64
+
+
+def test_sharded_forward_equals_full_batch():
+    res = run_world("_sharded_model_body")
+    for r in (0, 1):
+        y, y64 = res[r]
+        # fp64 oracle on a shard vs the reference's fp64 output on the batch
+        assert torch.allclose(y, y64.to(y.dtype), rtol=0, atol=1e-5 * float(y64.abs().max()))
