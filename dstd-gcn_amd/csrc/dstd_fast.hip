@@ -71,7 +71,8 @@ struct ConvGemm {
   static constexpr int CINP = 4 * KS;
   static constexpr int MODE = (MT % NWV == 0) ? 0 : ((NWV % MT == 0) ? 1 : 2);
   static constexpr int MTW = MODE == 0 ? MT / NWV : 1;
-  static constexpr int WLDS = MODE == 2 ? G * CP * CINP + G * CP : 0;  // floats of LDS (mode 2)
+  static constexpr int SW = stride_2mod4(CINP);  // LDS weight row stride (mode 2): conflict-free A reads
+  static constexpr int WLDS = MODE == 2 ? G * CP * SW + G * CP : 0;  // floats of LDS (mode 2)
   float af[MODE == 2 ? 1 : MTW][MODE == 2 ? 1 : KS];
   float bias[MODE == 2 ? 1 : MTW][4];
 
@@ -81,11 +82,11 @@ struct ConvGemm {
     if constexpr (MODE == 2) {
       for (int i = tid; i < G * CP * CINP; i += NTHR) {
         const int row = i / CINP, k = i % CINP, g = row / CP, c = row % CP;
-        wl[i] = (c < Cout && k < Cin) ? wf[g][c * Cin + k] : 0.f;
+        wl[row * SW + k] = (c < Cout && k < Cin) ? wf[g][c * Cin + k] : 0.f;
       }
       for (int i = tid; i < G * CP; i += NTHR) {
         const int g = i / CP, c = i % CP;
-        wl[G * CP * CINP + i] = c < Cout ? bf[g][c] : 0.f;
+        wl[G * CP * SW + i] = c < Cout ? bf[g][c] : 0.f;
       }
     } else {
 #pragma unroll
@@ -146,12 +147,12 @@ struct ConvGemm {
     } else {
       for (int u = wave; u < MT * NT; u += NWV) {
         const int mt = u % MT, nt = u / MT;
-        const float* ar = wl + (mt * 16 + cl) * CINP + kl;
+        const float* ar = wl + (mt * 16 + cl) * SW + kl;
         const float* xr = xs + (nt * 16 + cl) * SX + kl;
         f32x4 acc = zero4();
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) acc = mfma16x16x4(ar[ks * 4], xr[ks * 4], acc);
-        const float* bl = wl + G * CP * CINP + mt * 16 + kl * 4;
+        const float* bl = wl + G * CP * SW + mt * 16 + kl * 4;
         float* fo = Fs + (mt * 16 + kl * 4) * SP + nt * 16 + cl;
 #pragma unroll
         for (int j = 0; j < 4; ++j) fo[j * SP] = acc[j] + bl[j];
@@ -166,38 +167,31 @@ struct ConvGemm {
 template <int CT, int NT, int SP>
 struct PQGemm {
   static constexpr int KSO = CT * 4;
-  float aw[KSO];
-  float bq[4];
+  static constexpr int LDS = KSO * 64 + 16;  // A fragments [ks][lane] + bias [16]
   int nch;
+  // A operand lane map: lane (kl, cl) of k-step ks holds w[ch = cl][c = 4*ks + kl]
   __device__ __forceinline__ void setup(const float* const* pqw, const float* const* pqb, int npqw, int Cout,
-                                        int lane) {
-    const int kl = lane >> 4, cl = lane & 15;
+                                        float* wl, int tid) {
     nch = 2 * npqw;
-    const int ch = cl;
-#pragma unroll
-    for (int ks = 0; ks < KSO; ++ks) {
-      const int c = ks * 4 + kl;
-      aw[ks] = (ch < nch && c < Cout) ? pqw[ch >> 1][(ch & 1) * Cout + c] : 0.f;
+    for (int i = tid; i < KSO * 64; i += NTHR) {
+      const int ks = i >> 6, l = i & 63, ch = l & 15, c = ks * 4 + (l >> 4);
+      wl[i] = (ch < nch && c < Cout) ? pqw[ch >> 1][(ch & 1) * Cout + c] : 0.f;
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int cj = kl * 4 + j;
-      bq[j] = cj < nch ? pqb[cj >> 1][cj & 1] : 0.f;
-    }
+    if (tid < 16) wl[KSO * 64 + tid] = tid < nch ? pqb[tid >> 1][tid & 1] : 0.f;
   }
   template <typename Store>
-  __device__ __forceinline__ void run(const float* hs, int P, int wave, int lane, Store store) const {
+  __device__ __forceinline__ void run(const float* hs, const float* wl, int P, int wave, int lane, Store store) const {
     const int kl = lane >> 4, cl = lane & 15;
     for (int nt = wave; nt < NT; nt += NWV) {
       const float* hr = hs + kl * SP + nt * 16 + cl;
       f32x4 acc = zero4();
 #pragma unroll
-      for (int ks = 0; ks < KSO; ++ks) acc = mfma16x16x4(aw[ks], hr[ks * 4 * SP], acc);
+      for (int ks = 0; ks < KSO; ++ks) acc = mfma16x16x4(wl[ks * 64 + lane], hr[ks * 4 * SP], acc);
       const int p = nt * 16 + cl;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int ch = kl * 4 + j;
-        if (ch < nch && p < P) store(ch, p, acc[j] + bq[j]);
+        if (ch < nch && p < P) store(ch, p, acc[j] + wl[KSO * 64 + ch]);
       }
     }
   }
@@ -443,7 +437,10 @@ struct SpatialGeom {
   static constexpr int NWT = cdiv(V, 16);
   static constexpr int ITEMS = TT * CT * NWT;
   static constexpr int IPW = cdiv(ITEMS, NWV);
-  static constexpr int ADJ = NI * TT * VP * V;
+  // adjacency rows [gi][tt][v] at stride AS == 16 (mod 32): the two k rows a
+  // half-wave reads as MFMA B operand land on disjoint bank halves
+  static constexpr int AS = stride_mod32(V, 16);
+  static constexpr int ADJ = NI * TT * VP * AS;
   static constexpr int NBN = (G > NI ? 4 : 2) * V * CP;  // folded BN vectors [V][Cout]
   static constexpr int NCH = 4;                          // P_t, Q_t channels
   static constexpr int PQL = NCH * CP + NCH;  // weights + bias; partials live in Fs group-0 rows
@@ -460,7 +457,7 @@ __global__ __launch_bounds__(NTHR) void k_spatial_fast(SpatialArgs a) {
   extern __shared__ float lds[];
   float* xs = lds;                        // [NP16][SX]
   float* Fs = xs + NP16 * SX;             // [G*CP][SP]
-  float* adjs = Fs + G * CP * SP;         // [NI][TT][VP][V] + zero pad
+  float* adjs = Fs + G * CP * SP;         // [NI][TT][VP][AS] + zero pad
   float* bnl = adjs + Gm::ADJ + 32;       // bn_s, bn_h (, rbn_s, rbn_h) as [V][Cout]
   float* pqwl = bnl + Gm::NBN;            // P/Q weights [NCH][CP]
   float* pqbl = pqwl + Gm::NCH * CP;      // P/Q bias [NCH]
@@ -541,7 +538,7 @@ __global__ __launch_bounds__(NTHR) void k_spatial_fast(SpatialArgs a) {
     } else if constexpr (KS <= 2) {
       sx1.store(tid, [&](int i, float v) { xs[(i / Gm::CINP) * SX + i % Gm::CINP] = v; });
     }
-    sa.store(tid, [&](int i, float v) { adjs[i] = v; });
+    sa.store(tid, [&](int i, float v) { adjs[(i / V) * Gm::AS + i % V] = v; });
     __syncthreads();
 #ifndef DSTD_EXP_GC_NOFETCH
     if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
@@ -567,7 +564,7 @@ __global__ __launch_bounds__(NTHR) void k_spatial_fast(SpatialArgs a) {
       const int rem = item - tt * (CT * Gm::NWT);
       const int mc = rem / Gm::NWT, nw = rem - (rem / Gm::NWT) * Gm::NWT;
       fa[it] = Fs + (mc * 16 + cl) * SP + tt * V + kl;
-      fb[it] = adjs + (tt * VP + kl) * V + nw * 16 + cl;
+      fb[it] = adjs + (tt * VP + kl) * Gm::AS + nw * 16 + cl;
     }
 #ifndef DSTD_EXP_GC_NOAGG
 #pragma unroll
@@ -576,7 +573,7 @@ __global__ __launch_bounds__(NTHR) void k_spatial_fast(SpatialArgs a) {
       for (int ks = 0; ks < Gm::KV; ++ks)
 #pragma unroll
         for (int it = 0; it < Gm::IPW; ++it)
-          res[it] = mfma16x16x4(fa[it][gi * CP * SP + ks * 4], fb[it][gi * TT * VP * V + ks * 4 * V], res[it]);
+          res[it] = mfma16x16x4(fa[it][gi * CP * SP + ks * 4], fb[it][(gi * TT * VP + ks * 4) * Gm::AS], res[it]);
 #endif
     __syncthreads();  // Fs group-0 rows become the h tile below
 
@@ -683,10 +680,12 @@ struct TemporalGeom {
   static constexpr int NU = cdiv(T, 16);
   static constexpr int ITEMS = VT * CT * NU;
   static constexpr int IPW = cdiv(ITEMS, NWV);
-  static constexpr int ADJ = VT * TP * T;
+  static constexpr int AS = stride_mod32(T, 16);  // adjacency row stride, see SpatialGeom
+  static constexpr int ADJ = VT * TP * AS;
   static constexpr int NBN = 2 * 32 * CP;  // [V][Cout], V <= 32
   using Conv = ConvGemm<KS, CT, 1, NT, SX, SP>;
-  static constexpr int LDS_FLOATS = NP16 * SX + CP * SP + ADJ + 32 + NBN + Conv::WLDS;
+  using PQ = PQGemm<CT, NT, SP>;
+  static constexpr int LDS_FLOATS = NP16 * SX + CP * SP + ADJ + 32 + NBN + PQ::LDS + Conv::WLDS;
 };
 
 template <int T, int KS, int CT, int VT>
@@ -696,9 +695,10 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
   extern __shared__ float lds[];
   float* hs = lds;                    // [NP16][SX]
   float* Fs = hs + NP16 * SX;         // [CP][SP]
-  float* adjs = Fs + CP * SP;         // [VT][TP][T] + zero pad
+  float* adjs = Fs + CP * SP;         // [VT][TP][AS] + zero pad
   float* bnl = adjs + Gm::ADJ + 32;   // bn_s, bn_h as [V][Cout]
-  float* wl = bnl + Gm::NBN;
+  float* pql = bnl + Gm::NBN;         // P/Q weights (MFMA A fragments) + bias
+  float* wl = pql + Gm::PQ::LDS;      // conv weights (mode 2 only)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kl = lane >> 4, cl = lane & 15;
   const int V = a.V, Cin = a.Cin, Cout = a.Cout;
@@ -714,8 +714,8 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
   const float* wf1[1] = {a.wf};
   const float* bf1[1] = {a.bf};
   conv.setup(wf1, bf1, Cin, Cout, wl, tid);
-  PQGemm<CT, Gm::NT, SP> pqg;
-  if (a.pq) pqg.setup(a.pqw, a.pqb, a.npqw, Cout, lane);
+  typename Gm::PQ pqg;
+  if (a.pq) pqg.setup(a.pqw, a.pqb, a.npqw, Cout, pql, tid);
   const float pw = use_bn ? *a.prelu : 0.f;
   if (use_bn) {
     for (int i = tid; i < V * Cout; i += NTHR) {
@@ -729,7 +729,6 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
   Stager<float4, NP16 * C4> sh4;
   Stager<float, (KS > 2 ? 1 : NP16 * Gm::CINP)> sh1;
   Stager<float, VT * TP * T> sa;
-  float4 rres[Gm::IPW];  // residual for this lane's epilogue items (ENC / OUT)
   auto fetch = [&](int tl) {
     const int n = tl / nvb, v0 = (tl - n * nvb) * VT;
     const int nv = min(VT, V - v0), P = nv * T;
@@ -756,27 +755,6 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
       const int t = r / T;
       return (vv < nv && t < T) ? ag[vv * ld + r] : 0.f;
     });
-#pragma unroll
-    for (int it = 0; it < Gm::IPW; ++it) {
-      rres[it] = zf4();
-      const int item = wave + it * NWV;
-      if (!use_res || item >= Gm::ITEMS) continue;
-      const int vv = item / (CT * Gm::NU);
-      const int rem = item - vv * (CT * Gm::NU);
-      const int mc = rem / Gm::NU, nu = rem - (rem / Gm::NU) * Gm::NU;
-      const int u = nu * 16 + cl, c0 = mc * 16 + kl * 4;
-      if (u >= T || vv >= nv || c0 >= Cout) continue;
-      const int tsrc = epi == TEPI_ENC ? u : T - 1;
-      const float* r = a.xres + ((size_t)(n * T + tsrc) * V + v0 + vv) * Cout + c0;
-      if (Cout % 4 == 0) {
-        rres[it] = ld4(r);
-      } else {
-        rres[it].x = r[0];
-        if (c0 + 1 < Cout) rres[it].y = r[1];
-        if (c0 + 2 < Cout) rres[it].z = r[2];
-        if (c0 + 3 < Cout) rres[it].w = r[3];
-      }
-    }
   };
   fetch(tile);
 
@@ -794,12 +772,32 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
     } else if constexpr (KS <= 2) {
       sh1.store(tid, [&](int i, float v) { hs[(i / Gm::CINP) * SX + i % Gm::CINP] = v; });
     }
-    sa.store(tid, [&](int i, float v) { adjs[i] = v; });
-    float4 rcur[Gm::IPW];
-#pragma unroll
-    for (int it = 0; it < Gm::IPW; ++it) rcur[it] = rres[it];
+    sa.store(tid, [&](int i, float v) { adjs[(i / T) * Gm::AS + i % T] = v; });
     __syncthreads();
     if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x);
+    // residual of this lane's epilogue items (ENC: block input; OUT: last
+    // observed frame of the model input), issued now, consumed after conv + agg
+    float4 rres[Gm::IPW];
+#pragma unroll
+    for (int it = 0; it < Gm::IPW; ++it) {
+      rres[it] = zf4();
+      const int item = wave + it * NWV;
+      if (!use_res || item >= Gm::ITEMS) continue;
+      const int vv = item / (CT * Gm::NU);
+      const int rem = item - vv * (CT * Gm::NU);
+      const int mc = rem / Gm::NU, nu = rem - (rem / Gm::NU) * Gm::NU;
+      const int u = nu * 16 + cl, c0 = mc * 16 + kl * 4;
+      if (u >= T || vv >= nv || c0 >= Cout) continue;
+      const float* rp = a.xres + ((size_t)(n * T + (epi == TEPI_ENC ? u : T - 1)) * V + v0 + vv) * Cout + c0;
+      if (Cout % 4 == 0) {
+        rres[it] = ld4(rp);
+      } else {
+        rres[it].x = rp[0];
+        if (c0 + 1 < Cout) rres[it].y = rp[1];
+        if (c0 + 2 < Cout) rres[it].z = rp[2];
+        if (c0 + 3 < Cout) rres[it].w = rp[3];
+      }
+    }
 
     conv.run(hs, Fs, wl, tid);
     __syncthreads();
@@ -816,12 +814,12 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
       const int rem = item - vv * (CT * Gm::NU);
       const int mc = rem / Gm::NU, nu = rem - (rem / Gm::NU) * Gm::NU;
       fa[it] = Fs + (mc * 16 + cl) * SP + vv * T + kl;
-      fb[it] = adjs + (vv * TP + kl) * T + nu * 16 + cl;
+      fb[it] = adjs + (vv * TP + kl) * Gm::AS + nu * 16 + cl;
     }
 #pragma unroll
     for (int ks = 0; ks < Gm::KT; ++ks)
 #pragma unroll
-      for (int it = 0; it < Gm::IPW; ++it) res[it] = mfma16x16x4(fa[it][ks * 4], fb[it][ks * 4 * T], res[it]);
+      for (int it = 0; it < Gm::IPW; ++it) res[it] = mfma16x16x4(fa[it][ks * 4], fb[it][ks * 4 * Gm::AS], res[it]);
     __syncthreads();
 
 #pragma unroll
@@ -836,8 +834,8 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
       if (u >= T || vv >= nv || c0 >= Cout) continue;
       const int v = v0 + vv;
       const size_t o = ((size_t)(n * T + u) * V + v) * Cout + c0;
-      float val[4] = {res[it][0] + rcur[it].x, res[it][1] + rcur[it].y, res[it][2] + rcur[it].z,
-                      res[it][3] + rcur[it].w};
+      const float4 r = rres[it];
+      float val[4] = {res[it][0] + r.x, res[it][1] + r.y, res[it][2] + r.z, res[it][3] + r.w};
       if (Cout % 4 == 0) {
         if (use_bn) {
           const float4 s = ld4(bnl + v * Cout + c0), h = ld4(bnl + 32 * CP + v * Cout + c0);
@@ -865,7 +863,7 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
     if (a.pq) {
       const int TV = T * V;
       float* pqn = a.pq + (size_t)n * 2 * a.npqw * TV + v0;
-      pqg.run(Fs, P, wave, lane, [=](int ch, int p, float val) {
+      pqg.run(Fs, pql, P, wave, lane, [=](int ch, int p, float val) {
         const int vv = p / T, t = p - (p / T) * T;
         pqn[(size_t)ch * TV + t * V + vv] = val;
       });

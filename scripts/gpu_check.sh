@@ -18,4 +18,10 @@ if [ -n "${BENCH_ARGS+x}" ] || [ -z "${NO_BENCH:-}" ]; then
   timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 10 --warmup 3 --cpu-seconds 5} > gpurun_out/bench.log 2>&1
   st=$?; echo "bench exit $st"; tail -5 gpurun_out/bench.log
 fi
+if [ -n "${DIST_BENCH:-}" ] && [ $st -eq 0 ]; then
+  # the RCCL code path (broadcast, sharding, metric all_reduce) at one rank
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 1 --steps 5 --warmup 2 > gpurun_out/bench_dist1.log 2>&1
+  st=$?; echo "dist bench exit $st"; tail -3 gpurun_out/bench_dist1.log
+fi
 exit $st
