@@ -136,6 +136,9 @@ hipError_t launch_transpose(const TransposeArgs& a, hipStream_t s);
 hipError_t launch_adj_fast(const AdjArgs& a, hipStream_t s, int nblocks);
 hipError_t launch_spatial_fast(const SpatialArgs& a, hipStream_t s);
 hipError_t launch_temporal_fast(const TemporalArgs& a, hipStream_t s);
+// wave-independent 64 -> 64 kernels (dstd_wave.hip), tried first
+hipError_t launch_spatial_wave(const SpatialArgs& a, hipStream_t s);
+hipError_t launch_temporal_wave(const TemporalArgs& a, hipStream_t s);
 
 // Leading dimensions of the materialised adjacencies: rows padded to a
 // multiple of 4 floats so the adjacency kernels store 16-byte vectors.

@@ -589,6 +589,8 @@ static void run_temporal(const TemporalArgs& a, hipStream_t s, int nblocks, size
 
 hipError_t launch_spatial(SpatialArgs a, hipStream_t s) {
   if (a.Tt <= 0) {
+    const hipError_t we = launch_spatial_wave(a, s);
+    if (we != hipErrorNotSupported) return we;
     const hipError_t fe = launch_spatial_fast(a, s);
     if (fe != hipErrorNotSupported) return fe;
   }
@@ -608,6 +610,8 @@ hipError_t launch_spatial(SpatialArgs a, hipStream_t s) {
 
 hipError_t launch_temporal(TemporalArgs a, hipStream_t s) {
   if (a.Vt <= 0) {
+    const hipError_t we = launch_temporal_wave(a, s);
+    if (we != hipErrorNotSupported) return we;
     const hipError_t fe = launch_temporal_fast(a, s);
     if (fe != hipErrorNotSupported) return fe;
   }
