@@ -165,15 +165,14 @@ struct BlockTail {
 // block's two spatial DSTDGCs.
 hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const BlockScratch& sc, int B, int T, int V,
                      const float* x, float* h, float* y, const BlockTail& tail, hipStream_t s, Prof& pf) {
-  const int TV = T * V;
   const bool res = p->cin != p->cout;
   // (1) spatial adjacency for both graphs
   AdjArgs aa{};
   aa.pq = sc.pq_s;
-  aa.pq_sN = 8L * TV;
+  aa.pql = pq_layout_vt(8, T, V);
   for (int g = 0; g < 2; ++g) {
-    aa.p_off[g] = 4 * g * TV;
-    aa.q_off[g] = (4 * g + 2) * TV;
+    aa.p_ch[g] = 4 * g;
+    aa.q_ch[g] = 4 * g + 2;
     aa.W[g] = p->conv_s[g].wrm;
     aa.bias[g] = p->conv_s[g].brm;
     aa.astat[g] = f.astat_s + g * V * V;
@@ -228,6 +227,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   sa.pqb[1] = p->conv_t.bm2;
   sa.npqw = 2;
   sa.pq = sc.pq_t;
+  sa.pql = pq_layout_tv(4, T, V);
   sa.Tt = 0;
   pf.begin(DSTD_KIND_SPATIAL, s);
   e = launch_spatial(sa, s);
@@ -237,9 +237,9 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   // (3) temporal adjacency
   AdjArgs ta{};
   ta.pq = sc.pq_t;
-  ta.pq_sN = 4L * TV;
-  ta.p_off[0] = 0;
-  ta.q_off[0] = 2 * TV;
+  ta.pql = pq_layout_tv(4, T, V);
+  ta.p_ch[0] = 0;
+  ta.q_ch[0] = 2;
   ta.W[0] = p->conv_t.wrm;
   ta.bias[0] = p->conv_t.brm;
   ta.astat[0] = f.astat_t;
@@ -292,6 +292,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     tt.pqb[3] = q->conv_s[1].bm2;
     tt.npqw = 4;
     tt.pq = sc.pq_s;
+    tt.pql = pq_layout_vt(8, T, V);
   }
   tt.Vt = 0;
   pf.begin(DSTD_KIND_TEMPORAL, s);
@@ -318,6 +319,7 @@ hipError_t spatial_pq(const dstd_block_params* p, const float* x_ntvc, int B, in
   pa.b[3] = p->conv_s[1].bm2;
   pa.nw = 4;
   pa.pq = pq_s;
+  pa.pql = pq_layout_vt(8, T, V);
   return launch_pq(pa, s);
 }
 
@@ -441,12 +443,13 @@ int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, i
   pa.b[1] = w->bm2;
   pa.nw = 2;
   pa.pq = L.pq;
+  pa.pql = pq_layout_tv(4, T, V);
   DSTD_TRY(launch_pq(pa, s));
   AdjArgs aa{};
   aa.pq = L.pq;
-  aa.pq_sN = 4L * TV;
-  aa.p_off[0] = 0;
-  aa.q_off[0] = 2 * TV;
+  aa.pql = pa.pql;
+  aa.p_ch[0] = 0;
+  aa.q_ch[0] = 2;
   aa.W[0] = w->wrm;
   aa.bias[0] = w->brm;
   aa.astat[0] = A;  // the caller's combined adjacency is row independent
@@ -590,6 +593,7 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
   pa.b[3] = b0->conv_s[1].bm2;
   pa.nw = 4;
   pa.pq = L.sc.pq_s;
+  pa.pql = pq_layout_vt(8, T, V);
   pf.begin(DSTD_KIND_PREP, s);
   DSTD_TRY(launch_pq(pa, s));
   pf.end(s);

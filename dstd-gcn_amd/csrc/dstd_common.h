@@ -29,7 +29,9 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(e + 1.0f);
 }
 
-__device__ __forceinline__ float prelu_f(float x, float w) { return x >= 0.f ? x : w * x; }
+// PReLU: x for x >= 0, w*x otherwise -- as max(x,0) + w*min(x,0) (one of the
+// two terms is an exact zero), which needs no compare / VCC select.
+__device__ __forceinline__ float prelu_f(float x, float w) { return fmaf(w, fminf(x, 0.f), fmaxf(x, 0.f)); }
 
 __host__ __device__ constexpr inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 __host__ __device__ constexpr inline int rup(int a, int b) { return cdiv(a, b) * b; }

@@ -327,12 +327,15 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
 
   Stager<float2, KP * SA> st;
   auto fetch = [&](int nn) {
-    const float* P = a.pq + (size_t)nn * a.pq_sN + a.p_off[g];
-    const float* Q = a.pq + (size_t)nn * a.pq_sN + a.q_off[g];
+    const float* P = a.pq + (size_t)nn * a.pql.sn + a.p_ch[g] * a.pql.sch;
+    const float* Q = a.pq + (size_t)nn * a.pql.sn + a.q_ch[g] * a.pql.sch;
     st.load(tid, [&](int i) {
       const int k = i / SA, c = i - (i / SA) * SA;
       if (k < K && c < NA) {
-        const int s = MODE == 0 ? k * NA + c : (k / V) * T * V + c * V + (k % V);
+        // MODE 0: k = r*T + t', c = v;  MODE 1: k = r*V + v', c = t
+        const int r = MODE == 0 ? k / T : k / V, kk = MODE == 0 ? k % T : k % V;
+        const int s = MODE == 0 ? r * a.pql.sch + kk * a.pql.st + c * a.pql.sv
+                                : r * a.pql.sch + c * a.pql.st + kk * a.pql.sv;
         return make_float2(P[s], Q[s]);
       }
       return make_float2(0.f, 0.f);
@@ -649,14 +652,14 @@ __global__ __launch_bounds__(NTHR) void k_spatial_fast(SpatialArgs a) {
     __syncthreads();
 #ifndef DSTD_EXP_GC_NOPQ
     if (want_pq) {
-      const int TV = T * V;
-      float* pqn = a.pq + (size_t)n * Gm::NCH * TV + t0 * V;
+      const PQLayout L = a.pql;
+      float* pqn = a.pq + (size_t)n * L.sn;
       for (int i = tid; i < Gm::NCH * P; i += NTHR) {
         const int ch = i / P, p = i - (i / P) * P;
         float acc = pqbl[ch];
 #pragma unroll
         for (int mc = 0; mc < CT; ++mc) acc += pqpart[(mc * Gm::NCH + ch) * NP16 + p];
-        pqn[(size_t)ch * TV + p] = acc;
+        pqn[(size_t)ch * L.sch + (t0 + p / V) * L.st + (p % V) * L.sv] = acc;
       }
     }
 #endif
@@ -861,11 +864,11 @@ __global__ __launch_bounds__(NTHR) void k_temporal_fast(TemporalArgs a) {
     }
     __syncthreads();
     if (a.pq) {
-      const int TV = T * V;
-      float* pqn = a.pq + (size_t)n * 2 * a.npqw * TV + v0;
+      const PQLayout L = a.pql;
+      float* pqn = a.pq + (size_t)n * L.sn;
       pqg.run(Fs, pql, P, wave, lane, [=](int ch, int p, float val) {
         const int vv = p / T, t = p - (p / T) * T;
-        pqn[(size_t)ch * TV + t * V + vv] = val;
+        pqn[(size_t)ch * L.sch + t * L.st + (v0 + vv) * L.sv] = val;
       });
       __syncthreads();
     }

@@ -35,8 +35,26 @@ struct FoldArgs {
   int njobs;
 };
 
+// ---- P/Q planes ------------------------------------------------------------
+// The reduced embeddings of conv_m1 / conv_m2 (model/dstdgcn.py:66-67): element
+// (sample n, channel ch, frame t, joint v) lives at n*sn + ch*sch + t*st + v*sv.
+// The forward uses channel-innermost layouts so that a GC epilogue writes its
+// P/Q as whole 16-byte vectors: the spatial P/Q of a block ([B][V][T][8], 8
+// channels = P,Q of both spatial DSTDGCs) are written by the temporal kernel
+// one joint at a time, the temporal P/Q ([B][T][V][4]) by the spatial kernel
+// one frame at a time.
+struct PQLayout {
+  long sn;
+  int sch, st, sv;
+};
+inline PQLayout pq_layout_vt(int nch, int T, int V) { return PQLayout{(long)nch * T * V, 1, nch, nch * T}; }
+inline PQLayout pq_layout_tv(int nch, int T, int V) { return PQLayout{(long)nch * T * V, 1, nch * V, nch}; }
+inline bool pq_layout_eq(const PQLayout& a, const PQLayout& b) {
+  return a.sn == b.sn && a.sch == b.sch && a.st == b.st && a.sv == b.sv;
+}
+
 // ---- reduced embeddings P,Q (conv_m1 / conv_m2) ---------------------------
-// pq[n][2j+r][t][v] = sum_c w[j][r*Cin + c] * x[n][t][v][c] + b[j][r]
+// pq(n, 2j+r, t, v) = sum_c w[j][r*Cin + c] * x[n][t][v][c] + b[j][r]
 // (j indexes up to 4 two-row weight blocks).  With make_x6 the input is the
 // model input [B][T][V][3] and the kernel also writes x6 = cat(x, x - x[:, -1])
 // (model/dstdgcn.py:298-303) in NTVC.
@@ -49,13 +67,14 @@ struct PQArgs {
   const float* b[4];
   int nw;
   float* pq;
+  PQLayout pql;
 };
 
 // ---- dynamic adjacency: Adj = alpha * (W_rm . tanh(P - Q) + b_rm) + Astat -
 struct AdjArgs {
   const float* pq;
-  long pq_sN;          // floats per sample in pq
-  int p_off[2], q_off[2];
+  PQLayout pql;
+  int p_ch[2], q_ch[2];  // first P / Q channel of each graph (2 channels each)
   int mode;            // 0 spatial, 1 temporal (P/Q gather differs)
   int B, T, V;
   int nrow, K, NA, ncol;
@@ -89,7 +108,8 @@ struct SpatialArgs {
   const float* pqw[4];
   const float* pqb[4];
   int npqw;
-  float* pq;            // [B][2*npqw][T][V] or null
+  float* pq;            // P/Q planes (2*npqw channels) or null
+  PQLayout pql;
   int Tt;
 };
 // Folded BatchNorm vectors (bn_s, bn_h, rbn_s, rbn_h; temporal bn_s/bn_h) are
@@ -114,6 +134,7 @@ struct TemporalArgs {
   const float* pqb[4];
   int npqw;
   float* pq;
+  PQLayout pql;
   int Vt;
 };
 

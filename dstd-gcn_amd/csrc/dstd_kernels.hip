@@ -70,14 +70,13 @@ __global__ __launch_bounds__(256) void k_pq(PQArgs a) {
     for (int c = 0; c < cin; ++c) xr[c] = xi[c];
   }
   if (a.pq == nullptr) return;
-  const int nch = 2 * a.nw;
   for (int j = 0; j < a.nw; ++j) {
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const float* w = a.w[j] + r * cin;
       float s = a.b[j][r];
       for (int c = 0; c < cin; ++c) s += w[c] * xr[c];
-      a.pq[((size_t)n * nch + 2 * j + r) * TV + tv] = s;
+      a.pq[(size_t)n * a.pql.sn + (2 * j + r) * a.pql.sch + (tv / a.V) * a.pql.st + v * a.pql.sv] = s;
     }
   }
 }
@@ -117,18 +116,17 @@ __global__ __launch_bounds__(256) void k_adj(AdjArgs a) {
     const int k = i / SR, r = i % SR;
     Wl[i] = (k < K && r < nrow) ? W[r * K + k] : 0.f;
   }
-  const float* P = a.pq + (size_t)n * a.pq_sN + a.p_off[g];
-  const float* Q = a.pq + (size_t)n * a.pq_sN + a.q_off[g];
-  const int TV = a.T * a.V;
+  const float* P = a.pq + (size_t)n * a.pql.sn + a.p_ch[g] * a.pql.sch;
+  const float* Q = a.pq + (size_t)n * a.pql.sn + a.q_ch[g] * a.pql.sch;
   for (int i = tid; i < Kp * NA; i += 256) {
     const int k = i / NA, c = i % NA;
     float pv = 0.f, qv = 0.f;
     if (k < K) {
       int src;
-      if (a.mode == 0) {
-        src = k * NA + c;                         // P[r][t'][v], k = r*T+t', c = v
-      } else {
-        src = (k / a.V) * TV + c * a.V + (k % a.V);  // P[r][t][v'], k = r*V+v', c = t
+      if (a.mode == 0) {  // k = r*T + t', c = v
+        src = (k / a.T) * a.pql.sch + (k % a.T) * a.pql.st + c * a.pql.sv;
+      } else {            // k = r*V + v', c = t
+        src = (k / a.V) * a.pql.sch + c * a.pql.st + (k % a.V) * a.pql.sv;
       }
       pv = P[src];
       qv = Q[src];
@@ -287,7 +285,7 @@ __device__ __forceinline__ void conv_gemm(const float* const* wf, const float* c
 // pos(p) maps the tile column to (t*V + v) within the sample.
 template <typename PosFn>
 __device__ __forceinline__ void pq_from_tile(const float* const* pqw, const float* const* pqb, int npqw,
-                                             int C, const float* zs, int SP, int P, float* pq_n, int TV,
+                                             int C, const float* zs, int SP, int P, float* pq_n, int sch,
                                              int tid, PosFn pos) {
   const int nch = 2 * npqw;
   for (int i = tid; i < nch * P; i += DSTD_THREADS) {
@@ -296,7 +294,7 @@ __device__ __forceinline__ void pq_from_tile(const float* const* pqw, const floa
     const float* w = pqw[j] + r * C;
     float s = pqb[j][r];
     for (int c = 0; c < C; ++c) s += w[c] * zs[c * SP + p];
-    pq_n[(size_t)ch * TV + pos(p)] = s;
+    pq_n[(size_t)ch * sch + pos(p)] = s;
   }
 }
 
@@ -408,9 +406,9 @@ __global__ __launch_bounds__(256) void k_spatial(SpatialArgs a) {
   }
   if (a.pq) {
     __syncthreads();
-    const int TV = T * V;
-    pq_from_tile(a.pqw, a.pqb, a.npqw, Cout, Fs, SP, P, a.pq + (size_t)n * 2 * a.npqw * TV, TV, tid,
-                 [=](int p) { return t0 * V + p; });
+    const PQLayout L = a.pql;
+    pq_from_tile(a.pqw, a.pqb, a.npqw, Cout, Fs, SP, P, a.pq + (size_t)n * L.sn, L.sch, tid,
+                 [=](int p) { return (t0 + p / V) * L.st + (p % V) * L.sv; });
   }
 }
 
@@ -529,9 +527,9 @@ __global__ __launch_bounds__(256) void k_temporal(TemporalArgs a) {
   }
   if (a.pq) {
     __syncthreads();
-    const int TV = T * V;
-    pq_from_tile(a.pqw, a.pqb, a.npqw, Cout, Fs, SP, P, a.pq + (size_t)n * 2 * a.npqw * TV, TV, tid,
-                 [=](int p) { return (p % T) * V + v0 + p / T; });
+    const PQLayout L = a.pql;
+    pq_from_tile(a.pqw, a.pqb, a.npqw, Cout, Fs, SP, P, a.pq + (size_t)n * L.sn, L.sch, tid,
+                 [=](int p) { return (p % T) * L.st + (v0 + p / T) * L.sv; });
   }
 }
 

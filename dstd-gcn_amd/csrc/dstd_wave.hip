@@ -42,11 +42,13 @@ __device__ unsigned long long g_stamps[2][4096 * 8];
 #define STAMP_DECL                  \
   unsigned long long st_acc[8] = {}; \
   unsigned long long st_t = __builtin_amdgcn_s_memtime();
-#define STAMP(i)                                            \
-  {                                                         \
+#define STAMP(i)                                                \
+  {                                                             \
+    __builtin_amdgcn_sched_barrier(0);                          \
     const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    st_acc[i] += t_ - st_t;                                 \
-    st_t = t_;                                              \
+    st_acc[i] += t_ - st_t;                                     \
+    st_t = t_;                                                  \
+    __builtin_amdgcn_sched_barrier(0);                          \
   }
 #define STAMP_FLUSH(k)                                                         \
   if ((threadIdx.x & 63) == 0 && gw < 4096)                                    \
@@ -146,8 +148,8 @@ struct SWGeom {
   static constexpr int IMG = rup(V * V + 48, 4);  // image floats (+ slack for the padded column reads)
 };
 
-template <int V>
 // one wave per SIMD: 300+ registers hold the unit (conv tile, output, residual, prefetch)
+template <int V, bool EPI>
 __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_spatial_wave(SpatialArgs a) {
   using Gm = SWGeom<V>;
   constexpr int KQ = Gm::KQ, NQ = Gm::NQ, MT = Gm::MT, NWT = Gm::NWT, NV4 = Gm::NV4;
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int nch = a.pq ? 2 * a.npqw : 0;
   stage_pq(wql, bql, a.pqw, a.pqb, nch, tid);
   if (tid < 2 * CH) bfl[tid / CH][tid % CH] = a.bf[tid / CH][tid % CH];
-  const bool epi = a.epi != 0;
+  constexpr bool epi = EPI;
   if (epi)
     for (int i = tid; i < V * 16; i += WT) {
       const int w = i >> 4, c4 = i & 15;
@@ -275,6 +277,21 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   while (u < uend) {
     const int n = u / NP, t0 = (u - n * NP) * 2, nf = min(2, T - t0);
     const int un = u + 1;
+    // epilogue residual, issued first: it has the whole unit to land
+    float4 R[2][NWT][NCT];
+    if (epi) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        if (f >= nf) continue;
+#pragma unroll
+        for (int wt = 0; wt < NWT; ++wt) {
+          const int w = min(16 * wt + cl, V - 1);
+          const float* px = a.x + ((size_t)(n * T + t0 + f) * V + w) * CH + 4 * kl;
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct) R[f][wt][ct] = ld4(px + 16 * ct);
+        }
+      }
+    }
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
@@ -290,25 +307,6 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     conv(1);
     STAMP(3)
     __builtin_amdgcn_sched_barrier(0);
-    // epilogue residual (issued before the prefetches: vmcnt retires in order)
-    float4 R[2][NWT][NCT];
-    if (epi) {
-#pragma unroll
-      for (int f = 0; f < 2; ++f) {
-        if (f >= nf) continue;
-#pragma unroll
-        for (int wt = 0; wt < NWT; ++wt) {
-          const int w = min(16 * wt + cl, V - 1);
-          const float* px = a.x + ((size_t)(n * T + t0 + f) * V + w) * CH + 4 * kl;
-#pragma unroll
-#ifndef DSTD_ABL_NOR
-          for (int ct = 0; ct < NCT; ++ct) R[f][wt][ct] = ld4(px + 16 * ct);
-#else
-          for (int ct = 0; ct < NCT; ++ct) R[f][wt][ct] = make_float4(px[0], 0.f, 0.f, 0.f);
-#endif
-        }
-      }
-    }
 #ifndef DSTD_ABL_NOX
     if (un < uend) load_x(un);  // xa is dead after conv(1)
 #endif
@@ -367,7 +365,8 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
             for (int wt = 0; wt < NWT; ++wt) acc[f][wt] = mfma16x16x4(comp(wq, r), O[f][ct][wt][r], acc[f][wt]);
       }
-      if (kl * 4 < nch) {
+      // [B][T][V][4]: lane (0, cl) holds the 4 channels of joint w -> one 16-byte store
+      if (kl == 0) {
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
           if (f >= nf) continue;
@@ -375,16 +374,9 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
           for (int wt = 0; wt < NWT; ++wt) {
             const int w = 16 * wt + cl;
             if (w >= V) continue;
-            float* pqn = a.pq + ((size_t)n * nch * T + t0 + f) * V + w;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int ch = 4 * kl + r;
-#ifndef DSTD_ABL_NOPQST
-              if (ch < nch) pqn[(size_t)ch * T * V] = acc[f][wt][r] + bql[ch];
-#else
-              if (ch == 99) pqn[(size_t)ch * T * V] = acc[f][wt][r] + bql[ch];
-#endif
-            }
+            const f32x4 pv = acc[f][wt];
+            st4(a.pq + ((size_t)(n * T + t0 + f) * V + w) * 4,
+                make_float4(pv[0] + bql[0], pv[1] + bql[1], pv[2] + bql[2], pv[3] + bql[3]));
           }
         }
       }
@@ -411,7 +403,7 @@ struct TWGeom {
   static constexpr int IMG = rup(T * T + 48, 4);
 };
 
-template <int T, int WPE>
+template <int T, int WPE, int EPI>
 __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_temporal_wave(
     TemporalArgs a) {
   using Gm = TWGeom<T>;
@@ -428,9 +420,8 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
   const int kl = lane >> 4, cl = lane & 15;
   const int V = a.V;
   const int nunits = a.B * V;
-  const int epi = a.epi;
-  const bool use_bn = epi == TEPI_ENC || epi == TEPI_IN;
-  const bool use_res = epi == TEPI_ENC;
+  constexpr bool use_bn = EPI == TEPI_ENC || EPI == TEPI_IN;
+  constexpr bool use_res = EPI == TEPI_ENC;
 
   stage_conv_weights(wl, a.wf, tid);
   const int nch = a.pq ? 2 * a.npqw : 0;
@@ -484,6 +475,17 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
   while (u < uend) {
     const int n = u / V, v = u - n * V;
     const int un = u + 1;
+    // epilogue residual, issued first: it has the whole unit to land
+    float4 R[NUT][NCT];
+    if (use_res) {
+#pragma unroll
+      for (int ut = 0; ut < NUT; ++ut) {
+        const int uc = min(16 * ut + cl, T - 1);
+        const float* px = a.xres + ((size_t)(n * T + uc) * V + v) * CH + 4 * kl;
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) R[ut][ct] = ld4(px + 16 * ct);
+      }
+    }
     // ---- conv: D[t][c] = sum_k x[t][k] W[c][k] + b[c] ----
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct) {
@@ -542,21 +544,6 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
       }
     }
     STAMP(2)
-    // epilogue residual: issued before the next LDS-DMA, so the epilogue waits only for it
-    float4 R[NUT][NCT];
-    if (use_res) {
-#pragma unroll
-      for (int ut = 0; ut < NUT; ++ut) {
-        const int uc = min(16 * ut + cl, T - 1);
-        const float* px = a.xres + ((size_t)(n * T + uc) * V + v) * CH + 4 * kl;
-#pragma unroll
-#ifndef DSTD_ABL_NOR
-        for (int ct = 0; ct < NCT; ++ct) R[ut][ct] = ld4(px + 16 * ct);
-#else
-        for (int ct = 0; ct < NCT; ++ct) R[ut][ct] = make_float4(px[0], 0.f, 0.f, 0.f);
-#endif
-      }
-    }
     lds_reads_done();
 #ifndef DSTD_ABL_NOADJ
     if (un < uend) stage_adj(un);
@@ -592,6 +579,7 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
 #endif
       }
     }
+    STAMP(4)
     // next block's P_s/Q_s (8 channels) of the output, NUT interleaved chains
     if (nch) {
       f32x4 acc[NUT];
@@ -605,25 +593,20 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
 #pragma unroll
           for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma16x16x4(comp(wq, r), O[ct][ut][r], acc[ut]);
       }
-      if (kl * 4 < nch) {
+      STAMP(5)
+      // [B][V][T][8]: lane (kl, cl), kl < 2, holds channels 4kl..4kl+3 of frame u
+      if (kl < 2) {
 #pragma unroll
         for (int ut = 0; ut < NUT; ++ut) {
           const int uo = 16 * ut + cl;
           if (uo >= T) continue;
-          float* pqn = a.pq + ((size_t)n * nch * T + uo) * V + v;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int ch = 4 * kl + r;
-#ifndef DSTD_ABL_NOPQST
-            if (ch < nch) pqn[(size_t)ch * T * V] = acc[ut][r] + bql[ch];
-#else
-            if (ch == 99) pqn[(size_t)ch * T * V] = acc[ut][r] + bql[ch];
-#endif
-          }
+          const f32x4 pv = acc[ut];
+          st4(a.pq + ((size_t)u * T + uo) * 8 + 4 * kl,
+              make_float4(pv[0] + bql[4 * kl], pv[1] + bql[4 * kl + 1], pv[2] + bql[4 * kl + 2], pv[3] + bql[4 * kl + 3]));
         }
       }
     }
-    STAMP(4)
+    STAMP(6)
     u = un;
   }
   STAMP_FLUSH(1)
@@ -664,24 +647,36 @@ bool wave_disabled() {
   return off;
 }
 
-template <int V>
-hipError_t spatial_wave_run(const SpatialArgs& a, hipStream_t s) {
-  static const int occ = wave_occupancy(k_spatial_wave<V>);
+template <int V, bool EPI>
+hipError_t spatial_wave_launch(const SpatialArgs& a, hipStream_t s) {
+  static const int occ = wave_occupancy(k_spatial_wave<V, EPI>);
   const int units = a.B * cdiv(a.T, 2);
   int grid = wave_num_cus() * occ;
   grid = min(grid, cdiv(units, WW));
-  hipLaunchKernelGGL(k_spatial_wave<V>, dim3(grid), dim3(WT), 0, s, a);
+  hipLaunchKernelGGL((k_spatial_wave<V, EPI>), dim3(grid), dim3(WT), 0, s, a);
   return hipGetLastError();
 }
+template <int V>
+hipError_t spatial_wave_run(const SpatialArgs& a, hipStream_t s) {
+  return a.epi ? spatial_wave_launch<V, true>(a, s) : spatial_wave_launch<V, false>(a, s);
+}
 
-template <int T, int WPE>
-hipError_t temporal_wave_run(const TemporalArgs& a, hipStream_t s) {
-  static const int occ = wave_occupancy(k_temporal_wave<T, WPE>);
+template <int T, int WPE, int EPI>
+hipError_t temporal_wave_launch(const TemporalArgs& a, hipStream_t s) {
+  static const int occ = wave_occupancy(k_temporal_wave<T, WPE, EPI>);
   const int units = a.B * a.V;
   int grid = wave_num_cus() * occ;
   grid = min(grid, cdiv(units, WW));
-  hipLaunchKernelGGL((k_temporal_wave<T, WPE>), dim3(grid), dim3(WT), 0, s, a);
+  hipLaunchKernelGGL((k_temporal_wave<T, WPE, EPI>), dim3(grid), dim3(WT), 0, s, a);
   return hipGetLastError();
+}
+template <int T, int WPE>
+hipError_t temporal_wave_run(const TemporalArgs& a, hipStream_t s) {
+  switch (a.epi) {
+    case TEPI_ENC: return temporal_wave_launch<T, WPE, TEPI_ENC>(a, s);
+    case TEPI_IN: return temporal_wave_launch<T, WPE, TEPI_IN>(a, s);
+    default: return temporal_wave_launch<T, WPE, TEPI_RAW>(a, s);
+  }
 }
 
 }  // namespace
@@ -689,7 +684,7 @@ hipError_t temporal_wave_run(const TemporalArgs& a, hipStream_t s) {
 hipError_t launch_spatial_wave(const SpatialArgs& a, hipStream_t s) {
   if (wave_disabled()) return hipErrorNotSupported;
   if (a.Cin != CH || a.Cout != CH || a.NI != 2 || a.G != 2 || a.epi > 1) return hipErrorNotSupported;
-  if (a.pq && a.npqw != 2) return hipErrorNotSupported;
+  if (a.pq && (a.npqw != 2 || !pq_layout_eq(a.pql, pq_layout_tv(4, a.T, a.V)))) return hipErrorNotSupported;
   if (a.adj_ld % 4 != 0) return hipErrorNotSupported;
   switch (a.V) {
     case 22: return spatial_wave_run<22>(a, s);
@@ -702,7 +697,7 @@ hipError_t launch_spatial_wave(const SpatialArgs& a, hipStream_t s) {
 hipError_t launch_temporal_wave(const TemporalArgs& a, hipStream_t s) {
   if (wave_disabled()) return hipErrorNotSupported;
   if (a.Cin != CH || a.Cout != CH || a.V > 32 || a.epi == TEPI_OUT) return hipErrorNotSupported;
-  if (a.pq && a.npqw != 4) return hipErrorNotSupported;
+  if (a.pq && (a.npqw != 4 || !pq_layout_eq(a.pql, pq_layout_vt(8, a.T, a.V)))) return hipErrorNotSupported;
   if (a.adj_ld % 4 != 0) return hipErrorNotSupported;
   switch (a.T) {
     case 35: return temporal_wave_run<35, 2>(a, s);

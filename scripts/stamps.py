@@ -20,7 +20,7 @@ import dstd_native as native  # noqa: E402
 
 PHASES = {
     0: ["conv0(+x wait)", "adj wait", "agg0", "conv1", "R+x issue", "agg1", "glds+epilogue"],
-    1: ["conv(+x wait)", "adj wait", "x issue+agg", "R+glds issue", "epilogue"],
+    1: ["conv(+x wait)", "adj wait", "x issue+agg", "glds issue", "epilogue VALU+st", "PQ mfma", "PQ stores"],
 }
 
 
