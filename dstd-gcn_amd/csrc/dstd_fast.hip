@@ -18,6 +18,16 @@
 #include "dstd_common.h"
 #include "dstd_kernels.h"
 
+// Workgroup timeline of the adjacency kernel (debug builds, -DDSTD_STAMPS):
+// s_memrealtime (100 MHz, chip-wide) at entry, staging done, compute done, exit.
+#ifdef DSTD_STAMPS
+__device__ unsigned long long g_tl[2][2048][4];
+#define TL(m, i) \
+  if (threadIdx.x == 0 && blockIdx.x < 2048) g_tl[m][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();
+#else
+#define TL(m, i)
+#endif
+
 namespace dstd {
 
 namespace {
@@ -246,13 +256,20 @@ struct PQFuse {
 // tanh of a difference, separably: with EP = 2^(c*P), EQ = 2^(-c*Q),
 // c = 2*log2(e),   tanh(P - Q) = 1 - 2 / (EP*EQ + 1)
 // -- per MFMA operand one LDS pair, one FMA, one v_rcp_f32 and one FMA.  The
-// factors are formed once per sample.  While |c*P|, |c*Q| <= 120 they are
+// factors are formed once per workgroup.  While |c*P|, |c*Q| <= 120 they are
 // normal floats (no 0*inf) and the product under/overflows only where tanh
 // is -1/+1 to fp32 precision; a sample with a larger |P| or |Q| (never seen
 // with trained or random weights) takes the direct tanh(P - Q) path.
 // Padding rows/columns hold EP = EQ = 1 (tanh = 0) / P = Q = 0.
-// Persistent: workgroup w serves graph g = w % ngroups for samples
-// w / ngroups + k * (grid / ngroups); the next sample's P/Q are prefetched.
+//
+// Workgroup = (sample, graph, column chunk); grid = B * groups * NCHUNK.
+// The prologue issues every global load it needs (P/Q, W_rm, A-stat, bias)
+// before its first LDS write and meets ONE barrier: a workgroup timeline
+// (scripts/timeline.py) showed the earlier load -> barrier -> load chain
+// costing 3.4-5.4 us of a 16-24 us launch.  The temporal adjacency splits
+// its columns in two so that B = 256 fills every CU with two workgroups
+// (one round: all prologues start together, and a second round of
+// workgroups would pay its prologue again rather than overlap it).
 // ===========================================================================
 template <int MODE, int NROW, int K, int NA>
 struct AdjGeom {
@@ -264,8 +281,12 @@ struct AdjGeom {
   static constexpr int OS = 20;                         // output staging row stride
   static constexpr int STG = NWV * RT * 16 * OS;        // per-wave output staging (also W staging)
   static constexpr int NCOLP = rup(NCOL + 1, 4);        // astat (+ padding column)
+  static constexpr int T = MODE == 0 ? NROW : NA;
+  static constexpr int V = MODE == 0 ? NA : NROW;
+  static constexpr int NCHUNK = MODE == 0 ? 1 : 2;      // column chunks per (sample, graph): one round of workgroups at B = 256
+  static constexpr int CPC = cdiv(NCT, NCHUNK);         // column tiles per chunk
   static_assert(STG >= K * NROW, "W staging must fit the output staging area");
-  static constexpr int LDS_FLOATS = 4 * KP * SA + (WREG ? 0 : KP * SR) + STG + NCOLP + 4;
+  static constexpr int LDS_FLOATS = 4 * KP * SA + (WREG ? 0 : KP * SR) + STG + NCOLP + 16 + 4;
 };
 
 template <int MODE, int NROW, int K, int NA>
@@ -275,8 +296,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
   constexpr int RT = Gm::RT, KSTEPS = Gm::KSTEPS, KP = Gm::KP, NCOL = Gm::NCOL, NCT = Gm::NCT, SA = Gm::SA;
   constexpr bool WREG = Gm::WREG;
   constexpr int SR = Gm::SR, OS = Gm::OS;
-  constexpr int T = MODE == 0 ? NROW : NA;
-  constexpr int V = MODE == 0 ? NA : NROW;
+  constexpr int T = Gm::T, V = Gm::V;
   constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
   extern __shared__ float lds[];
   float* Pl = lds;               // [KP][SA] raw P
@@ -285,20 +305,67 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
   float* Fl = El + KP * SA;      // [KP][SA] 2^(-c*Q)
   float* Wl = Fl + KP * SA;      // [KP][SR] (only when !WREG)
   float* stg = Wl + (WREG ? 0 : KP * SR);   // W staging, then per-wave output staging
-  float* asl = stg + Gm::STG;               // astat [NCOL]
-  int* wide = reinterpret_cast<int*>(asl + Gm::NCOLP);
+  float* asl = stg + Gm::STG;               // astat [NCOL] + zero padding column
+  float* bsl = asl + Gm::NCOLP;             // bias rows [16 * RT]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kl = lane >> 4, cl = lane & 15;
-  const int g = blockIdx.x % a.ngroups;
-  const int stride = gridDim.x / a.ngroups;
-  int n = blockIdx.x / a.ngroups;
+  const int chunk = blockIdx.x % Gm::NCHUNK;
+  const int g = (blockIdx.x / Gm::NCHUNK) % a.ngroups;
+  const int n = blockIdx.x / (Gm::NCHUNK * a.ngroups);
   if (n >= a.B) return;
+  TL(MODE, 0)
 
-  // ---- once per workgroup: W_rm (coalesced via LDS), bias rows, A-stat ----
+  // ---- prologue: every global load first ----
+  // P/Q planes are channel-innermost (PQLayout sch == 1, Q right after P):
+  // P_0, P_1, Q_0, Q_1 of one (frame, joint) are one float4, read in memory order
+  const PQLayout L = a.pql;
+  const float* pqb = a.pq + (size_t)n * L.sn + a.p_ch[g];
+  Stager<float4, T * V> spq;
+  spq.load(tid, [&](int i) {
+    const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;  // memory order
+    return ld4(pqb + t * L.st + v * L.sv);
+  });
   const float* W = a.W[g];
-  for (int i = tid; i < NROW * K; i += NTHR) stg[i] = W[i];
-  for (int i = tid; i < NCOL; i += NTHR) asl[i] = a.astat[g][i];
-  __syncthreads();
+  Stager<float, NROW * K> sw;
+  sw.load(tid, [&](int i) { return W[i]; });
+  Stager<float, NCOL> sas;
+  sas.load(tid, [&](int i) { return a.astat[g][i]; });
+  const float bias_v = tid < 16 * RT && tid < NROW ? a.bias[g][tid] : 0.f;
+  const float alpha = *a.alpha;
+
+  // LDS padding (no load dependence)
+  for (int i = tid; i < KP * SA; i += NTHR) {
+    const int k = i / SA, c = i - (i / SA) * SA;
+    if (k >= K || c >= NA) {
+      Pl[i] = 0.f;
+      Ql[i] = 0.f;
+      El[i] = 1.f;
+      Fl[i] = 1.f;
+    }
+  }
+  if (tid < Gm::NCOLP - NCOL) asl[NCOL + tid] = 0.f;
+  if (tid < 16 * RT) bsl[tid] = bias_v;
+  sw.store(tid, [&](int i, float v) { stg[i] = v; });
+  sas.store(tid, [&](int i, float v) { asl[i] = v; });
+  int bad = 0;
+  spq.store(tid, [&](int i, float4 q) {
+    const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;
+    const int k0 = MODE == 0 ? t : v, c = MODE == 0 ? v : t, kstep = MODE == 0 ? T : V;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int idx = (k0 + r * kstep) * SA + c;
+      const float pv = r ? q.y : q.x, qv = r ? q.w : q.z;
+      Pl[idx] = pv;
+      Ql[idx] = qv;
+      const float ep = C2 * pv, eq = -C2 * qv;
+      bad |= !(fabsf(ep) <= 120.f && fabsf(eq) <= 120.f);
+      El[idx] = __builtin_amdgcn_exp2f(ep);
+      Fl[idx] = __builtin_amdgcn_exp2f(eq);
+    }
+  });
+  const bool sep = __syncthreads_or(bad) == 0;
+  TL(MODE, 1)
+
   float wr[WREG ? RT : 1][WREG ? KSTEPS : 1];
   if constexpr (WREG) {
 #pragma unroll
@@ -314,114 +381,75 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
       Wl[i] = (k < K && r < NROW) ? stg[r * K + k] : 0.f;
     }
   }
-  const float alpha = *a.alpha;
-  const float* bias = a.bias[g];
   float brow[RT][4];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = rt * 16 + kl * 4 + j;
-      brow[rt][j] = row < NROW ? bias[row] : 0.f;
-    }
+    for (int j = 0; j < 4; ++j) brow[rt][j] = bsl[rt * 16 + kl * 4 + j];
+  __syncthreads();  // stg (W staging) becomes the per-wave output staging
 
-  Stager<float2, KP * SA> st;
-  auto fetch = [&](int nn) {
-    const float* P = a.pq + (size_t)nn * a.pql.sn + a.p_ch[g] * a.pql.sch;
-    const float* Q = a.pq + (size_t)nn * a.pql.sn + a.q_ch[g] * a.pql.sch;
-    st.load(tid, [&](int i) {
-      const int k = i / SA, c = i - (i / SA) * SA;
-      if (k < K && c < NA) {
-        // MODE 0: k = r*T + t', c = v;  MODE 1: k = r*V + v', c = t
-        const int r = MODE == 0 ? k / T : k / V, kk = MODE == 0 ? k % T : k % V;
-        const int s = MODE == 0 ? r * a.pql.sch + kk * a.pql.st + c * a.pql.sv
-                                : r * a.pql.sch + c * a.pql.st + kk * a.pql.sv;
-        return make_float2(P[s], Q[s]);
-      }
-      return make_float2(0.f, 0.f);
-    });
-  };
-  fetch(n);
   float* so = stg + wave * (RT * 16 * OS);  // this wave's output staging
-
-  for (; n < a.B; n += stride) {
-    if (tid == 0) *wide = 0;
-    __syncthreads();  // previous sample's readers (and the W staging) are done
-    int bad = 0;
-    st.store(tid, [&](int i, float2 v) {
-      const int k = i / SA, c = i - (i / SA) * SA;
-      const bool live = k < K && c < NA;
-      Pl[i] = v.x;
-      Ql[i] = v.y;
-      const float ep = C2 * v.x, eq = -C2 * v.y;
-      bad |= live && !(fabsf(ep) <= 120.f && fabsf(eq) <= 120.f);
-      El[i] = live ? __builtin_amdgcn_exp2f(ep) : 1.f;
-      Fl[i] = live ? __builtin_amdgcn_exp2f(eq) : 1.f;
-    });
-    if (bad) *wide = 1;
-    if (n + stride < a.B) fetch(n + stride);
-    __syncthreads();
-    const bool sep = *wide == 0;
-
-    float* out = a.out + (size_t)n * a.out_sN + (size_t)g * a.out_sG;
-    for (int ct = wave; ct < NCT; ct += NWV) {
-      const int col = ct * 16 + cl;
-      const bool cv = col < NCOL;
-      const int ca = cv ? col / NA : NA;
-      const int cb = cv ? col - ca * NA : NA;
-      f32x4 acc[RT];
+  float* out = a.out + (size_t)n * a.out_sN + (size_t)g * a.out_sG;
+  const int ct_end = min(NCT, (chunk + 1) * Gm::CPC);
+  for (int ct = chunk * Gm::CPC + wave; ct < ct_end; ct += NWV) {
+    const int col = ct * 16 + cl;
+    const bool cv = col < NCOL;
+    const int ca = cv ? col / NA : NA;
+    const int cb = cv ? col - ca * NA : NA;
+    f32x4 acc[RT];
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = zero4();
-      if (sep) {
-        const float* pw = El + kl * SA + ca;
-        const float* qw = Fl + kl * SA + cb;
-        float bv[KSTEPS];
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = zero4();
+    if (sep) {
+      const float* pw = El + kl * SA + ca;
+      const float* qw = Fl + kl * SA + cb;
+      float bv[KSTEPS];
 #pragma unroll
-        for (int ks = 0; ks < KSTEPS; ++ks) {
-          const float e = pw[ks * 4 * SA] * qw[ks * 4 * SA] + 1.f;
-          bv[ks] = 1.f - 2.f * __builtin_amdgcn_rcpf(e);
-        }
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        const float e = pw[ks * 4 * SA] * qw[ks * 4 * SA] + 1.f;
+        bv[ks] = 1.f - 2.f * __builtin_amdgcn_rcpf(e);
+      }
 #pragma unroll
-        for (int ks = 0; ks < KSTEPS; ++ks) {
+      for (int ks = 0; ks < KSTEPS; ++ks) {
 #pragma unroll
-          for (int rt = 0; rt < RT; ++rt) {
-            float av;
-            if constexpr (WREG) av = wr[rt][ks];
-            else av = Wl[(ks * 4 + kl) * SR + rt * 16 + cl];
-            acc[rt] = mfma16x16x4(av, bv[ks], acc[rt]);
-          }
-        }
-      } else {
-        const float* pw = Pl + kl * SA + ca;
-        const float* qw = Ql + kl * SA + cb;
-        for (int ks = 0; ks < KSTEPS; ++ks) {
-          const float bv = fast_tanh(pw[ks * 4 * SA] - qw[ks * 4 * SA]);
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt) {
-            float av;
-            if constexpr (WREG) av = wr[rt][ks];
-            else av = Wl[(ks * 4 + kl) * SR + rt * 16 + cl];
-            acc[rt] = mfma16x16x4(av, bv, acc[rt]);
-          }
+        for (int rt = 0; rt < RT; ++rt) {
+          float av;
+          if constexpr (WREG) av = wr[rt][ks];
+          else av = Wl[(ks * 4 + kl) * SR + rt * 16 + cl];
+          acc[rt] = mfma16x16x4(av, bv[ks], acc[rt]);
         }
       }
-      // epilogue: transpose the 16-column tile through this wave's LDS slot so
-      // each lane stores 16 contiguous bytes of one row (1 KiB per store)
-      const float as = asl[cv ? col : NCOL];
+    } else {
+      const float* pw = Pl + kl * SA + ca;
+      const float* qw = Ql + kl * SA + cb;
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        const float bv = fast_tanh(pw[ks * 4 * SA] - qw[ks * 4 * SA]);
 #pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) so[(rt * 16 + kl * 4 + j) * OS + cl] = alpha * (acc[rt][j] + brow[rt][j]) + as;
-      const int q = lane & 3;
-      const int c4 = ct * 16 + 4 * q;
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        const int row = rt * 16 + (lane >> 2);
-        const float4 v = ld4(so + row * OS + 4 * q);
-        if (row < NROW && c4 < NCOL) st4(out + (size_t)row * a.ldo + c4, v);
+        for (int rt = 0; rt < RT; ++rt) {
+          float av;
+          if constexpr (WREG) av = wr[rt][ks];
+          else av = Wl[(ks * 4 + kl) * SR + rt * 16 + cl];
+          acc[rt] = mfma16x16x4(av, bv, acc[rt]);
+        }
       }
+    }
+    // epilogue: transpose the 16-column tile through this wave's LDS slot so
+    // each lane stores 16 contiguous bytes of one row (1 KiB per store)
+    const float as = asl[cv ? col : NCOL];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) so[(rt * 16 + kl * 4 + j) * OS + cl] = alpha * (acc[rt][j] + brow[rt][j]) + as;
+    const int q = lane & 3;
+    const int c4 = ct * 16 + 4 * q;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int row = rt * 16 + (lane >> 2);
+      const float4 v = ld4(so + row * OS + 4 * q);
+      if (row < NROW && c4 < NCOL) st4(out + (size_t)row * a.ldo + c4, v);
     }
   }
+  TL(MODE, 2)
+  TL(MODE, 3)
 }
 
 // ===========================================================================
@@ -907,11 +935,9 @@ hipError_t adj_fast_run(const AdjArgs& a, hipStream_t s) {
   using Gm = AdjGeom<MODE, NROW, K, NA>;
   constexpr size_t lds = (size_t)Gm::LDS_FLOATS * sizeof(float);
   static int occ = resident_per_cu(k_adj_fast<MODE, NROW, K, NA>, lds);
-  const int units = a.B * a.ngroups;
-  int grid = num_cus() * occ;
-  grid = grid > units ? units : grid;
-  grid = (grid / a.ngroups) * a.ngroups;
-  if (grid < a.ngroups) grid = a.ngroups;
+  (void)occ;  // raises the LDS cap where needed
+  if (a.ldo % 4 != 0) return hipErrorNotSupported;
+  const int grid = a.B * a.ngroups * Gm::NCHUNK;
   hipLaunchKernelGGL((k_adj_fast<MODE, NROW, K, NA>), dim3(grid), dim3(NTHR), lds, s, a);
   return hipGetLastError();
 }
@@ -977,6 +1003,11 @@ hipError_t temporal_fast_t(const TemporalArgs& a, hipStream_t s) {
 }  // namespace
 
 hipError_t launch_adj_fast(const AdjArgs& a, hipStream_t s, int) {
+  // channel-innermost P/Q planes, Q right after P, 16-byte aligned (see the prologue)
+  if (a.pql.sch != 1 || ((uintptr_t)a.pq & 15) || (a.pql.st & 3) || (a.pql.sv & 3) || (a.pql.sn & 3))
+    return hipErrorNotSupported;
+  for (int g = 0; g < a.ngroups; ++g)
+    if (a.q_ch[g] != a.p_ch[g] + 2 || (a.p_ch[g] & 3)) return hipErrorNotSupported;
   if (a.mode == 0) {
     if (a.T == 35 && a.V == 22) return adj_fast_run<0, 35, 70, 22>(a, s);
     if (a.T == 35 && a.V == 25) return adj_fast_run<0, 35, 70, 25>(a, s);
@@ -1011,3 +1042,11 @@ hipError_t launch_temporal_fast(const TemporalArgs& a, hipStream_t s) {
 }
 
 }  // namespace dstd
+
+#ifdef DSTD_STAMPS
+extern "C" int dstd_debug_timeline(int mode, unsigned long long* host, int n) {
+  if (mode < 0 || mode > 1 || n > 2048 * 4) return 1;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tl), n * sizeof(unsigned long long),
+                                  mode * 2048 * 4 * sizeof(unsigned long long));
+}
+#endif

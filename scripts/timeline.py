@@ -1,0 +1,54 @@
+#!/usr/bin/env python
+"""Workgroup timeline of the adjacency kernels (library built with -DDSTD_STAMPS).
+
+  python scripts/timeline.py dstd-gcn_amd/libdstd_gcn_stamps.so
+Runs one forward, then reads the last launch's per-workgroup s_memrealtime
+stamps (entry, staging done, compute done, exit; 100 MHz) for each mode.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dstd-gcn_amd"))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import dstd_native as native  # noqa: E402
+
+
+def main():
+    lib = os.path.abspath(sys.argv[1])
+    native._lib = None
+    os.environ["DSTD_LIB"] = lib
+    native.LIB_PATH = lib
+    L = native.lib()
+    fn = L.dstd_debug_timeline
+    fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+    dev = torch.device("cuda", 0)
+    model, opts, _ = bench.load_model("h36m", dev)
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    x = bench.synth_input(256, T, opts["joints_to_consider"], opts["input_time_frame"], 1).to(dev)
+    with torch.no_grad():
+        for _ in range(3):
+            model(x)
+        torch.cuda.synchronize()
+    buf = np.zeros(2048 * 4, dtype=np.uint64)
+    for mode in (0, 1):
+        fn(mode, buf.ctypes.data, buf.size)
+        tl = buf.reshape(2048, 4).astype(np.float64)
+        tl = tl[tl[:, 0] > 0]
+        t0 = tl[:, 0].min()
+        us = (tl - t0) / 100.0  # 100 MHz -> us
+        print(f"mode {mode}: {len(tl)} workgroups, span {us[:, 3].max():.2f} us")
+        for name, col in (("entry", 0), ("staged", 1), ("computed", 2), ("exit", 3)):
+            c = us[:, col]
+            print(f"   {name:9s} min {c.min():6.2f}  p50 {np.median(c):6.2f}  p90 {np.percentile(c, 90):6.2f}  max {c.max():6.2f}")
+        d = us[:, 2] - us[:, 1]
+        print(f"   compute   p50 {np.median(d):6.2f} us; staging p50 {np.median(us[:, 1] - us[:, 0]):6.2f} us")
+
+
+if __name__ == "__main__":
+    main()
