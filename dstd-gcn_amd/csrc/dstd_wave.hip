@@ -1,6 +1,6 @@
-// Wave-independent DSTDGC kernels for the 64 -> 64 channel blocks (the five
-// encoders and the temporal half of conv_st_in: 11 of the 14 GC launches of a
-// forward).
+// Wave-independent DSTDGC kernels: every GC launch of the forward (spatial
+// 64->64 of the encoders, 6->64 of conv_st_in and 64->3 of conv_st_out, both
+// with their residual conv; temporal 64->64 and the 3->3 output tail).
 //
 // Why a second design (profiles/r01_*, scripts/ab_kernels.py): the persistent
 // 8-wave kernels of dstd_fast.hip spend ~60% of their time outside the MFMA
@@ -65,12 +65,46 @@ namespace {
 
 constexpr int WW = 4;        // waves per workgroup
 constexpr int WT = WW * 64;  // threads per workgroup
-constexpr int CH = 64;       // Cin == Cout
-constexpr int NCT = 4;       // 16-channel tiles of CH
+
+// Channel blocking of a C-channel row.  MFMA k-step (j, s) of a conv with C
+// input channels contracts channel 16j + 4kl + s (kl = lane >> 4): lane kl of
+// a row holds the float4 chunks at 16j + 4kl, j < NJ -- for C = 64 each
+// load instruction then reads 64 contiguous bytes per row.  Output channels
+// come in NT tiles of 16.
+template <int C>
+struct Chan {
+  static constexpr int NJ = cdiv(C, 16);
+  static constexpr int NT = cdiv(C, 16);
+};
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 __device__ __forceinline__ float comp(const float4& v, int s) { return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w; }
+__device__ __forceinline__ float4 zf4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+// channels c0 .. c0+3 of a row of C floats, zero past C (C % 4 != 0: scalar loads)
+template <int C>
+__device__ __forceinline__ float4 ld_chunk(const float* row, int c0) {
+  if constexpr (C % 4 == 0) {
+    return c0 < C ? ld4(row + c0) : zf4();
+  } else {
+    float e[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) e[i] = c0 + i < C ? row[c0 + i] : 0.f;
+    return make_float4(e[0], e[1], e[2], e[3]);
+  }
+}
+// store the channels c0 .. c0+3 that exist
+template <int C>
+__device__ __forceinline__ void st_chunk(float* row, int c0, const f32x4& v) {
+  if constexpr (C % 4 == 0) {
+    if (c0 < C) st4(row + c0, make_float4(v[0], v[1], v[2], v[3]));
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (c0 + i < C) row[c0 + i] = v[i];
+  }
+}
 
 // 16-byte LDS-DMA (global_load_lds_dwordx4): lane l writes LDS byte address
 // dst + 16*l (dst wave-uniform).  Issued from inline asm on purpose: with a
@@ -97,10 +131,10 @@ __device__ __forceinline__ void adj_landed() { asm volatile("s_waitcnt vmcnt(0)"
 // LDS-DMA into the same image is issued; retire them first (WAR).
 __device__ __forceinline__ void lds_reads_done() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+
 // Each wave takes a contiguous range of units: neighbouring units write
-// neighbouring bytes (the P/Q planes are [ch][t][v]), and a range keeps those
-// writes in one wave -- one XCD's L2 -- instead of interleaving them across
-// the eight XCDs.
+// neighbouring bytes, and a range keeps those writes in one wave -- one
+// XCD's L2 -- instead of interleaving them across the eight XCDs.
 __device__ __forceinline__ int unit_range(int nunits, int& uend, int& gw) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   gw = blockIdx.x * WW + wave;
@@ -109,34 +143,58 @@ __device__ __forceinline__ int unit_range(int nunits, int& uend, int& gw) {
   return (int)(((long)gw * nunits) / nw);
 }
 
-// Conv B fragments in LDS: wl[(ct*4 + j)*64 + lane] = W[16ct + cl][16j + 4kl .. +3]
-// (k-step (j, s) contracts input channel 16j + 4kl + s).
-__device__ __forceinline__ void stage_conv_weights(float4* wl, const float* w, int tid) {
-  for (int i = tid; i < NCT * 4 * 64; i += WT) {
-    const int l = i & 63, j = (i >> 6) & 3, ct = i >> 8;
-    wl[i] = ld4(w + (16 * ct + (l & 15)) * CH + 16 * j + 4 * (l >> 4));
+// Weight fragments in LDS, wl[(ct*NJ + j)*64 + lane] = W[16ct + cl][16j + 4kl .. +3]
+// (zero outside [COUT][CIN]).  The same image serves as MFMA B operand of the
+// transposed conv (lane (kl, cl)) and as A operand of a conv in output layout
+// (lane (cl, kl)): both hold W[16ct + (lane & 15)][16j + 4(lane >> 4) + s].
+template <int CIN, int COUT>
+__device__ __forceinline__ void stage_frags(float4* wl, const float* w, int tid) {
+  constexpr int NJ = Chan<CIN>::NJ, NT = Chan<COUT>::NT;
+  for (int i = tid; i < NT * NJ * 64; i += WT) {
+    const int l = i & 63, j = (i >> 6) % NJ, ct = (i >> 6) / NJ;
+    const int c = 16 * ct + (l & 15), k0 = 16 * j + 4 * (l >> 4);
+    float e[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) e[q] = (c < COUT && k0 + q < CIN) ? w[c * CIN + k0 + q] : 0.f;
+    wl[i] = make_float4(e[0], e[1], e[2], e[3]);
   }
 }
 
-// P/Q weights as MFMA A fragments in LDS: wq[ct*64 + lane], lane (cl = channel,
-// kl) of k-step (ct, r) holds w[ch][16ct + 4kl + r]; channel ch = 2j + rr is
-// row rr of conv_m* block j.  bq[ch] = its bias.
+// P/Q weights of the next DSTDGC as MFMA A fragments: wq[ct*64 + lane], lane
+// (cl = channel, kl) of k-step (ct, r) holds w[ch][16ct + 4kl + r]; channel
+// ch = 2j + rr is row rr of conv_m* block j (C inputs).  bq[ch] = its bias.
+template <int C>
 __device__ __forceinline__ void stage_pq(float4* wq, float* bq, const float* const* pqw, const float* const* pqb,
                                          int nch, int tid) {
-  for (int i = tid; i < NCT * 64; i += WT) {
-    const int l = i & 63, ct = i >> 6, ch = l & 15, kl = l >> 4;
-    wq[i] = ch < nch ? ld4(pqw[ch >> 1] + (ch & 1) * CH + 16 * ct + 4 * kl) : make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int NT = Chan<C>::NT;
+  for (int i = tid; i < NT * 64; i += WT) {
+    const int l = i & 63, ct = i >> 6, ch = l & 15, c0 = 16 * ct + 4 * (l >> 4);
+    float e[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) e[q] = (ch < nch && c0 + q < C) ? pqw[ch >> 1][(ch & 1) * C + c0 + q] : 0.f;
+    wq[i] = make_float4(e[0], e[1], e[2], e[3]);
   }
   if (tid < 16) bq[tid] = tid < nch ? pqb[tid >> 1][tid & 1] : 0.f;
+}
+
+// folded BN vectors [V][C] -> LDS [c/4][v]: lanes (v) read consecutive float4
+template <int C>
+__device__ __forceinline__ void stage_bn(float4* dst, const float* src, int V, int tid) {
+  constexpr int C4 = 4 * Chan<C>::NT;
+  for (int i = tid; i < V * C4; i += WT) {
+    const int v = i / C4, c4 = i % C4;
+    dst[c4 * V + v] = ld_chunk<C>(src + v * C, 4 * c4);
+  }
 }
 
 }  // namespace
 
 // ===========================================================================
-// Spatial GC, 64 -> 64, two graphs, identity residual (DSTDGCB.forward,
-// model/dstdgcn.py:141-152, with DSTDGC.forward spatial :80-87):
+// Spatial GC (DSTDGCB.forward, model/dstdgcn.py:141-152, with DSTDGC.forward
+// spatial :80-87), two graphs:
 //   y[c][w] = sum_g sum_v (W_g x + b_g)[v][c] Adj_g[t][v][w]
-//   epi 1:  h = prelu(bn(y) + x);  P_t/Q_t of h for the temporal DSTDGC
+//   EPI:  h = prelu(bn(y) + r),  r = x (CIN == COUT) or bn_r(W_r x + b_r) (RES)
+//   + P_t/Q_t of h for the block's temporal DSTDGC ([B][T][V][4])
 // ===========================================================================
 template <int V>
 struct SWGeom {
@@ -149,16 +207,19 @@ struct SWGeom {
 };
 
 // one wave per SIMD: 300+ registers hold the unit (conv tile, output, residual, prefetch)
-template <int V, bool EPI>
+template <int V, int CIN, int COUT, bool RES, bool EPI>
 __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_spatial_wave(SpatialArgs a) {
   using Gm = SWGeom<V>;
   constexpr int KQ = Gm::KQ, NQ = Gm::NQ, MT = Gm::MT, NWT = Gm::NWT, NV4 = Gm::NV4;
-  __shared__ float4 wl[2][NCT * 4 * 64];  // conv B fragments per graph (32 KB)
-  __shared__ float4 bnl[2][16 * V];       // folded BN scale / shift, [c/4][w]: lanes (w) read consecutive float4
-  __shared__ float adjl[WW][2][2][Gm::IMG];  // per-wave adjacency images [g][frame]
-  __shared__ float4 wql[NCT * 64];          // P/Q A fragments
+  constexpr int NJ = Chan<CIN>::NJ, NCO = Chan<COUT>::NT;
+  static_assert(RES || CIN == COUT, "identity residual needs CIN == COUT");
+  __shared__ float4 wl[2][NCO * NJ * 64];          // conv B fragments per graph
+  __shared__ float4 wrl[RES ? NCO * NJ * 64 : 1];  // residual conv A fragments
+  __shared__ float4 bnl[RES ? 4 : 2][4 * NCO * V]; // BN scale / shift (+ residual BN), [c/4][w]
+  __shared__ float adjl[WW][2][2][Gm::IMG];        // per-wave adjacency images [g][frame]
+  __shared__ float4 wql[NCO * 64];                 // P/Q A fragments
   __shared__ float bql[16];
-  __shared__ float bfl[2][CH];              // conv biases
+  __shared__ float bfl[3][16 * NCO];               // conv biases (graphs, residual conv)
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int kl = lane >> 4, cl = lane & 15;
@@ -166,24 +227,29 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   const int NP = cdiv(T, 2);
   const int nunits = a.B * NP;
 
-  stage_conv_weights(wl[0], a.wf[0], tid);
-  stage_conv_weights(wl[1], a.wf[1], tid);
+  stage_frags<CIN, COUT>(wl[0], a.wf[0], tid);
+  stage_frags<CIN, COUT>(wl[1], a.wf[1], tid);
+  if constexpr (RES) stage_frags<CIN, COUT>(wrl, a.wf[2], tid);
   const int nch = a.pq ? 2 * a.npqw : 0;
-  stage_pq(wql, bql, a.pqw, a.pqb, nch, tid);
-  if (tid < 2 * CH) bfl[tid / CH][tid % CH] = a.bf[tid / CH][tid % CH];
-  constexpr bool epi = EPI;
-  if (epi)
-    for (int i = tid; i < V * 16; i += WT) {
-      const int w = i >> 4, c4 = i & 15;
-      bnl[0][c4 * V + w] = ld4(a.bn_s + 4 * i);
-      bnl[1][c4 * V + w] = ld4(a.bn_h + 4 * i);
+  stage_pq<COUT>(wql, bql, a.pqw, a.pqb, nch, tid);
+  for (int i = tid; i < (RES ? 3 : 2) * 16 * NCO; i += WT) {
+    const int g = i / (16 * NCO), c = i % (16 * NCO);
+    bfl[g][c] = c < COUT ? a.bf[g][c] : 0.f;
+  }
+  if constexpr (EPI) {
+    stage_bn<COUT>(bnl[0], a.bn_s, V, tid);
+    stage_bn<COUT>(bnl[1], a.bn_h, V, tid);
+    if constexpr (RES) {
+      stage_bn<COUT>(bnl[2], a.rbn_s, V, tid);
+      stage_bn<COUT>(bnl[3], a.rbn_h, V, tid);
     }
+  }
   __syncthreads();
 
   int gw, uend;
   int u = unit_range(nunits, uend, gw);
   const int wave = gw - blockIdx.x * WW;
-  const float pw = epi ? *a.prelu : 0.f;
+  const float pw = EPI ? *a.prelu : 0.f;
 
   // row (m, i = cl) of the conv tiles -> (frame, joint): k-slice Q = 4m + (i & 3)
   // holds joints 4q .. 4q+3 (q = Q % KQ) of frame Q / KQ; row i is joint 4q + (i >> 2)
@@ -197,15 +263,15 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     rowv[m] = v < V ? v : V - 1;  // padding rows read a real row; their adjacency rows are zero
   }
 
-  float4 xa[MT][4];
+  float4 xa[MT][NJ];
   auto load_x = [&](int uu) {
     const int n = uu / NP, t0 = (uu - n * NP) * 2, nf = min(2, T - t0);
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int f = min(rowf[m], nf - 1);
-      const float* px = a.x + ((size_t)(n * T + t0 + f) * V + rowv[m]) * CH + 4 * kl;
+      const float* px = a.x + ((size_t)(n * T + t0 + f) * V + rowv[m]) * CIN;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xa[m][j] = ld4(px + 16 * j);
+      for (int j = 0; j < NJ; ++j) xa[m][j] = ld_chunk<CIN>(px, 16 * j + 4 * kl);
     }
   };
   auto stage_adj = [&](int uu) {
@@ -223,26 +289,26 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       }
   };
 
-  f32x4 D[MT][NCT];
-  f32x4 O[2][NCT][NWT];
+  f32x4 D[MT][NCO];
+  f32x4 O[2][NCO][NWT];
   auto conv = [&](int g) {
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
+    for (int ct = 0; ct < NCO; ++ct) {
       const float b = bfl[g][16 * ct + cl];
 #pragma unroll
       for (int m = 0; m < MT; ++m) D[m][ct] = f32x4{b, b, b, b};
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float4 wb[NCT];
+    for (int j = 0; j < NJ; ++j) {
+      float4 wb[NCO];
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) wb[ct] = wl[g][(ct * 4 + j) * 64 + lane];
+      for (int ct = 0; ct < NCO; ++ct) wb[ct] = wl[g][(ct * NJ + j) * 64 + lane];
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int ct = 0; ct < NCT; ++ct) D[m][ct] = mfma16x16x4(comp(xa[m][j], s), comp(wb[ct], s), D[m][ct]);
+          for (int ct = 0; ct < NCO; ++ct) D[m][ct] = mfma16x16x4(comp(xa[m][j], s), comp(wb[ct], s), D[m][ct]);
     }
   };
   auto agg = [&](int g, int nf) {
@@ -262,7 +328,7 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
       for (int q = 0; q < KQ; ++q) {
         const int Q = f * KQ + q, m = Q >> 2, r = Q & 3;
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct)
+        for (int ct = 0; ct < NCO; ++ct)
 #pragma unroll
           for (int wt = 0; wt < NWT; ++wt) O[f][ct][wt] = mfma16x16x4(D[m][ct][r], b[q][wt], O[f][ct][wt]);
       }
@@ -277,25 +343,26 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
   while (u < uend) {
     const int n = u / NP, t0 = (u - n * NP) * 2, nf = min(2, T - t0);
     const int un = u + 1;
-    // epilogue residual, issued first: it has the whole unit to land
-    float4 R[2][NWT][NCT];
-    if (epi) {
+    // x at the output positions, issued first (it has the whole unit to land):
+    // the identity residual, or the B operand of the residual conv
+    float4 R[2][NWT][NJ];
+    if constexpr (EPI) {
 #pragma unroll
       for (int f = 0; f < 2; ++f) {
         if (f >= nf) continue;
 #pragma unroll
         for (int wt = 0; wt < NWT; ++wt) {
           const int w = min(16 * wt + cl, V - 1);
-          const float* px = a.x + ((size_t)(n * T + t0 + f) * V + w) * CH + 4 * kl;
+          const float* px = a.x + ((size_t)(n * T + t0 + f) * V + w) * CIN;
 #pragma unroll
-          for (int ct = 0; ct < NCT; ++ct) R[f][wt][ct] = ld4(px + 16 * ct);
+          for (int j = 0; j < NJ; ++j) R[f][wt][j] = ld_chunk<CIN>(px, 16 * j + 4 * kl);
         }
       }
     }
 #pragma unroll
     for (int f = 0; f < 2; ++f)
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct)
+      for (int ct = 0; ct < NCO; ++ct)
 #pragma unroll
         for (int wt = 0; wt < NWT; ++wt) O[f][ct][wt] = zero4();
     conv(0);
@@ -307,44 +374,73 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     conv(1);
     STAMP(3)
     __builtin_amdgcn_sched_barrier(0);
-#ifndef DSTD_ABL_NOX
     if (un < uend) load_x(un);  // xa is dead after conv(1)
-#endif
     STAMP(4)
     agg(1, nf);
     STAMP(5)
     lds_reads_done();
-#ifndef DSTD_ABL_NOADJ
     if (un < uend) stage_adj(un);
-#endif
 
-    // ---- epilogue: h = prelu(bn(y) + x) -> NTVC, then P_t/Q_t of h ----
+    // ---- epilogue: h = prelu(bn(y) + r) -> NTVC, then P_t/Q_t of h ----
+    if constexpr (EPI) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        if (f >= nf) continue;
+#pragma unroll
+        for (int wt = 0; wt < NWT; ++wt) {
+          const int wc = min(16 * wt + cl, V - 1);
+          f32x4 rc[NCO];  // residual conv, output layout: A = W_r fragments, B = x rows
+          if constexpr (RES) {
+#pragma unroll
+            for (int ct = 0; ct < NCO; ++ct) {
+              const float b = bfl[2][16 * ct + 4 * kl], b1 = bfl[2][16 * ct + 4 * kl + 1];
+              const float b2 = bfl[2][16 * ct + 4 * kl + 2], b3 = bfl[2][16 * ct + 4 * kl + 3];
+              rc[ct] = f32x4{b, b1, b2, b3};
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) {
+                const float4 wr = wrl[(ct * NJ + j) * 64 + lane];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) rc[ct] = mfma16x16x4(comp(wr, s), comp(R[f][wt][j], s), rc[ct]);
+              }
+            }
+          }
+#pragma unroll
+          for (int ct = 0; ct < NCO; ++ct) {
+            f32x4& o = O[f][ct][wt];
+            const int c4 = (4 * ct + kl) * V + wc;
+            const float4 sc = bnl[0][c4], sh = bnl[1][c4];
+            float r[4];
+            if constexpr (RES) {
+              const float4 rs = bnl[2][c4], rh = bnl[3][c4];
+              r[0] = rc[ct][0] * rs.x + rh.x;
+              r[1] = rc[ct][1] * rs.y + rh.y;
+              r[2] = rc[ct][2] * rs.z + rh.z;
+              r[3] = rc[ct][3] * rs.w + rh.w;
+            } else {
+              const float4 x4 = R[f][wt][ct];
+              r[0] = x4.x;
+              r[1] = x4.y;
+              r[2] = x4.z;
+              r[3] = x4.w;
+            }
+            o[0] = prelu_f(o[0] * sc.x + sh.x + r[0], pw);
+            o[1] = prelu_f(o[1] * sc.y + sh.y + r[1], pw);
+            o[2] = prelu_f(o[2] * sc.z + sh.z + r[2], pw);
+            o[3] = prelu_f(o[3] * sc.w + sh.w + r[3], pw);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       if (f >= nf) continue;
-      const int t = t0 + f;
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt) {
         const int w = 16 * wt + cl;
-        const int wc = w < V ? w : V - 1;
-        float* py = a.y + ((size_t)(n * T + t) * V + wc) * CH + 4 * kl;
+        if (w >= V) continue;
+        float* py = a.y + ((size_t)(n * T + t0 + f) * V + w) * COUT;
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) {
-          f32x4& o = O[f][ct][wt];
-          if (epi) {
-            const float4 sc = bnl[0][(4 * ct + kl) * V + wc], sh = bnl[1][(4 * ct + kl) * V + wc];
-            const float4 rr = R[f][wt][ct];
-            o[0] = prelu_f(o[0] * sc.x + sh.x + rr.x, pw);
-            o[1] = prelu_f(o[1] * sc.y + sh.y + rr.y, pw);
-            o[2] = prelu_f(o[2] * sc.z + sh.z + rr.z, pw);
-            o[3] = prelu_f(o[3] * sc.w + sh.w + rr.w, pw);
-          }
-#ifndef DSTD_ABL_NOST
-          if (w < V) st4(py + 16 * ct, make_float4(o[0], o[1], o[2], o[3]));
-#else
-          if (w == 99) st4(py + 16 * ct, make_float4(o[0], o[1], o[2], o[3]));
-#endif
-        }
+        for (int ct = 0; ct < NCO; ++ct) st_chunk<COUT>(py, 16 * ct + 4 * kl, O[f][ct][wt]);
       }
     }
     // P_t/Q_t of h: out[ch][w] = sum_c wq[ch][c] h[c][w] + b, with h (the output
@@ -356,7 +452,7 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
         for (int wt = 0; wt < NWT; ++wt) acc[f][wt] = zero4();
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) {
+      for (int ct = 0; ct < NCO; ++ct) {
         const float4 wq = wql[ct * 64 + lane];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -388,11 +484,12 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 }
 
 // ===========================================================================
-// Temporal GC, 64 -> 64 (DSTDGC.forward temporal, model/dstdgcn.py:88-93) with
-// the DSTDGCB tail epilogues (:161-163 and DSTDGCN.forward :306-312):
+// Temporal GC, C -> C (DSTDGC.forward temporal, model/dstdgcn.py:88-93) with
+// the DSTDGCB tail epilogues (:161-163 and DSTDGCN.forward :306-315):
 //   y[c][u] = sum_t (W x + b)[t][c] Adj[v][t][u]
 //   ENC: prelu(bn(y + xres));  IN: prelu(bn(y));  RAW: y
-//   + P_s/Q_s (8 channels) of the output for the next block's spatial DSTDGCs
+//   OUT: y + x_model[n][T-1][v][c]  (the model output, C = 3)
+//   + P_s/Q_s (8 channels, [B][V][T][8]) of the output for the next block
 // ===========================================================================
 template <int T>
 struct TWGeom {
@@ -403,35 +500,35 @@ struct TWGeom {
   static constexpr int IMG = rup(T * T + 48, 4);
 };
 
-template <int T, int WPE, int EPI>
+template <int T, int WPE, int EPI, int C>
 __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_temporal_wave(
     TemporalArgs a) {
   using Gm = TWGeom<T>;
   constexpr int KT = Gm::KT, MT = Gm::MT, NUT = Gm::NUT, NV4 = Gm::NV4;
+  constexpr int NJ = Chan<C>::NJ, NCO = Chan<C>::NT;
   constexpr int VMAX = 32;
-  __shared__ float4 wl[NCT * 4 * 64];   // conv B fragments (16 KB)
-  __shared__ float4 bnl[2][VMAX * 16];  // folded BN scale / shift, [v][c/4]
-  __shared__ float adjl[WW][Gm::IMG];   // per-wave adjacency image
-  __shared__ float4 wql[NCT * 64];      // P/Q A fragments
+  __shared__ float4 wl[NCO * NJ * 64];       // conv B fragments
+  __shared__ float4 bnl[2][4 * NCO * VMAX];  // folded BN scale / shift, [c/4][v]
+  __shared__ float adjl[WW][Gm::IMG];        // per-wave adjacency image
+  __shared__ float4 wql[NCO * 64];           // P/Q A fragments
   __shared__ float bql[16];
-  __shared__ float bfl[CH];             // conv bias
+  __shared__ float bfl[16 * NCO];            // conv bias
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int kl = lane >> 4, cl = lane & 15;
   const int V = a.V;
   const int nunits = a.B * V;
   constexpr bool use_bn = EPI == TEPI_ENC || EPI == TEPI_IN;
-  constexpr bool use_res = EPI == TEPI_ENC;
+  constexpr bool use_res = EPI == TEPI_ENC || EPI == TEPI_OUT;
 
-  stage_conv_weights(wl, a.wf, tid);
+  stage_frags<C, C>(wl, a.wf, tid);
   const int nch = a.pq ? 2 * a.npqw : 0;
-  stage_pq(wql, bql, a.pqw, a.pqb, nch, tid);
-  if (tid < CH) bfl[tid] = a.bf[tid];
-  if (use_bn)
-    for (int i = tid; i < V * 16; i += WT) {
-      bnl[0][i] = ld4(a.bn_s + 4 * i);
-      bnl[1][i] = ld4(a.bn_h + 4 * i);
-    }
+  stage_pq<C>(wql, bql, a.pqw, a.pqb, nch, tid);
+  if (tid < 16 * NCO) bfl[tid] = tid < C ? a.bf[tid] : 0.f;
+  if constexpr (use_bn) {
+    stage_bn<C>(bnl[0], a.bn_s, V, tid);
+    stage_bn<C>(bnl[1], a.bn_h, V, tid);
+  }
   __syncthreads();
 
   int gw, uend;
@@ -447,14 +544,14 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
     rowt[m] = t < T ? t : T - 1;
   }
 
-  float4 xa[MT][4];
+  float4 xa[MT][NJ];
   auto load_x = [&](int uu) {
     const int n = uu / V, v = uu - n * V;
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-      const float* px = a.h + ((size_t)(n * T + rowt[m]) * V + v) * CH + 4 * kl;
+      const float* px = a.h + ((size_t)(n * T + rowt[m]) * V + v) * C;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) xa[m][j] = ld4(px + 16 * j);
+      for (int j = 0; j < NJ; ++j) xa[m][j] = ld_chunk<C>(px, 16 * j + 4 * kl);
     }
   };
   auto stage_adj = [&](int uu) {
@@ -465,8 +562,8 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
       if (i + lane < NV4) glds16(src + 4 * i, dst + 16 * i);
   };
 
-  f32x4 D[MT][NCT];
-  f32x4 O[NCT][NUT];
+  f32x4 D[MT][NCO];
+  f32x4 O[NCO][NUT];
   if (u < uend) {
     load_x(u);
     stage_adj(u);
@@ -476,45 +573,43 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
     const int n = u / V, v = u - n * V;
     const int un = u + 1;
     // epilogue residual, issued first: it has the whole unit to land
-    float4 R[NUT][NCT];
-    if (use_res) {
+    float4 R[NUT][NCO];
+    if constexpr (use_res) {
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut) {
-        const int uc = min(16 * ut + cl, T - 1);
-        const float* px = a.xres + ((size_t)(n * T + uc) * V + v) * CH + 4 * kl;
+        const int tr = EPI == TEPI_OUT ? T - 1 : min(16 * ut + cl, T - 1);
+        const float* px = a.xres + ((size_t)(n * T + tr) * V + v) * C;
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) R[ut][ct] = ld4(px + 16 * ct);
+        for (int ct = 0; ct < NCO; ++ct) R[ut][ct] = ld_chunk<C>(px, 16 * ct + 4 * kl);
       }
     }
     // ---- conv: D[t][c] = sum_k x[t][k] W[c][k] + b[c] ----
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct) {
+    for (int ct = 0; ct < NCO; ++ct) {
       const float b = bfl[16 * ct + cl];
 #pragma unroll
       for (int m = 0; m < MT; ++m) D[m][ct] = f32x4{b, b, b, b};
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float4 wb[NCT];
+    for (int j = 0; j < NJ; ++j) {
+      float4 wb[NCO];
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) wb[ct] = wl[(ct * 4 + j) * 64 + lane];
+      for (int ct = 0; ct < NCO; ++ct) wb[ct] = wl[(ct * NJ + j) * 64 + lane];
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int ct = 0; ct < NCT; ++ct) D[m][ct] = mfma16x16x4(comp(xa[m][j], s), comp(wb[ct], s), D[m][ct]);
+          for (int ct = 0; ct < NCO; ++ct) D[m][ct] = mfma16x16x4(comp(xa[m][j], s), comp(wb[ct], s), D[m][ct]);
     }
     STAMP(0)
     adj_landed();  // before the prefetch: the wait retires every older VMEM operation
     STAMP(1)
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch below the conv: xa is reloaded in place
-#ifndef DSTD_ABL_NOX
     if (un < uend) load_x(un);
-#endif
     // ---- aggregation: y[c][u] = sum_t D[t][c] Adj[t][u] ----
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct)
+    for (int ct = 0; ct < NCO; ++ct)
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = zero4();
     {
@@ -537,7 +632,7 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
           if (Q >= KT) continue;
           const int m = Q >> 2, r = Q & 3;
 #pragma unroll
-          for (int ct = 0; ct < NCT; ++ct)
+          for (int ct = 0; ct < NCO; ++ct)
 #pragma unroll
             for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma16x16x4(D[m][ct][r], b[dq][ut], O[ct][ut]);
         }
@@ -545,38 +640,32 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
     }
     STAMP(2)
     lds_reads_done();
-#ifndef DSTD_ABL_NOADJ
     if (un < uend) stage_adj(un);
-#endif
-
     STAMP(3)
+
     // ---- epilogue ----
 #pragma unroll
     for (int ut = 0; ut < NUT; ++ut) {
       const int uo = 16 * ut + cl;
       const int uc = uo < T ? uo : T - 1;
-      float* py = a.y + ((size_t)(n * T + uc) * V + v) * CH + 4 * kl;
+      float* py = a.y + ((size_t)(n * T + uc) * V + v) * C;
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) {
+      for (int ct = 0; ct < NCO; ++ct) {
         f32x4& o = O[ct][ut];
-        if (use_res) {
+        if constexpr (use_res) {
           o[0] += R[ut][ct].x;
           o[1] += R[ut][ct].y;
           o[2] += R[ut][ct].z;
           o[3] += R[ut][ct].w;
         }
-        if (use_bn) {
-          const float4 sc = bnl[0][v * 16 + 4 * ct + kl], sh = bnl[1][v * 16 + 4 * ct + kl];
+        if constexpr (use_bn) {
+          const float4 sc = bnl[0][(4 * ct + kl) * V + v], sh = bnl[1][(4 * ct + kl) * V + v];
           o[0] = prelu_f(o[0] * sc.x + sh.x, pw);
           o[1] = prelu_f(o[1] * sc.y + sh.y, pw);
           o[2] = prelu_f(o[2] * sc.z + sh.z, pw);
           o[3] = prelu_f(o[3] * sc.w + sh.w, pw);
         }
-#ifndef DSTD_ABL_NOST
-        if (uo < T) st4(py + 16 * ct, make_float4(o[0], o[1], o[2], o[3]));
-#else
-        if (uo == 999) st4(py + 16 * ct, make_float4(o[0], o[1], o[2], o[3]));
-#endif
+        if (uo < T) st_chunk<C>(py, 16 * ct + 4 * kl, o);
       }
     }
     STAMP(4)
@@ -586,7 +675,7 @@ __global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) 
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut) acc[ut] = zero4();
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) {
+      for (int ct = 0; ct < NCO; ++ct) {
         const float4 wq = wql[ct * 64 + lane];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -647,43 +736,51 @@ bool wave_disabled() {
   return off;
 }
 
-template <int V, bool EPI>
+template <int V, int CIN, int COUT, bool RES>
 hipError_t spatial_wave_launch(const SpatialArgs& a, hipStream_t s) {
-  static const int occ = wave_occupancy(k_spatial_wave<V, EPI>);
+  static const int occ = wave_occupancy(k_spatial_wave<V, CIN, COUT, RES, true>);
   const int units = a.B * cdiv(a.T, 2);
   int grid = wave_num_cus() * occ;
   grid = min(grid, cdiv(units, WW));
-  hipLaunchKernelGGL((k_spatial_wave<V, EPI>), dim3(grid), dim3(WT), 0, s, a);
+  hipLaunchKernelGGL((k_spatial_wave<V, CIN, COUT, RES, true>), dim3(grid), dim3(WT), 0, s, a);
   return hipGetLastError();
 }
 template <int V>
 hipError_t spatial_wave_run(const SpatialArgs& a, hipStream_t s) {
-  return a.epi ? spatial_wave_launch<V, true>(a, s) : spatial_wave_launch<V, false>(a, s);
+  if (a.Cin == 64 && a.Cout == 64 && a.G == 2) return spatial_wave_launch<V, 64, 64, false>(a, s);
+  if (a.Cin == 6 && a.Cout == 64 && a.G == 3) return spatial_wave_launch<V, 6, 64, true>(a, s);
+  if (a.Cin == 64 && a.Cout == 3 && a.G == 3) return spatial_wave_launch<V, 64, 3, true>(a, s);
+  return hipErrorNotSupported;
 }
 
-template <int T, int WPE, int EPI>
+template <int T, int WPE, int EPI, int C>
 hipError_t temporal_wave_launch(const TemporalArgs& a, hipStream_t s) {
-  static const int occ = wave_occupancy(k_temporal_wave<T, WPE, EPI>);
+  static const int occ = wave_occupancy(k_temporal_wave<T, WPE, EPI, C>);
   const int units = a.B * a.V;
   int grid = wave_num_cus() * occ;
   grid = min(grid, cdiv(units, WW));
-  hipLaunchKernelGGL((k_temporal_wave<T, WPE, EPI>), dim3(grid), dim3(WT), 0, s, a);
+  hipLaunchKernelGGL((k_temporal_wave<T, WPE, EPI, C>), dim3(grid), dim3(WT), 0, s, a);
   return hipGetLastError();
 }
 template <int T, int WPE>
 hipError_t temporal_wave_run(const TemporalArgs& a, hipStream_t s) {
-  switch (a.epi) {
-    case TEPI_ENC: return temporal_wave_launch<T, WPE, TEPI_ENC>(a, s);
-    case TEPI_IN: return temporal_wave_launch<T, WPE, TEPI_IN>(a, s);
-    default: return temporal_wave_launch<T, WPE, TEPI_RAW>(a, s);
+  if (a.Cin == 64 && a.Cout == 64) {
+    switch (a.epi) {
+      case TEPI_ENC: return temporal_wave_launch<T, WPE, TEPI_ENC, 64>(a, s);
+      case TEPI_IN: return temporal_wave_launch<T, WPE, TEPI_IN, 64>(a, s);
+      case TEPI_RAW: return temporal_wave_launch<T, WPE, TEPI_RAW, 64>(a, s);
+      default: return hipErrorNotSupported;
+    }
   }
+  if (a.Cin == 3 && a.Cout == 3 && a.epi == TEPI_OUT && !a.pq) return temporal_wave_launch<T, WPE, TEPI_OUT, 3>(a, s);
+  return hipErrorNotSupported;
 }
 
 }  // namespace
 
 hipError_t launch_spatial_wave(const SpatialArgs& a, hipStream_t s) {
   if (wave_disabled()) return hipErrorNotSupported;
-  if (a.Cin != CH || a.Cout != CH || a.NI != 2 || a.G != 2 || a.epi > 1) return hipErrorNotSupported;
+  if (a.NI != 2 || a.epi != 1) return hipErrorNotSupported;
   if (a.pq && (a.npqw != 2 || !pq_layout_eq(a.pql, pq_layout_tv(4, a.T, a.V)))) return hipErrorNotSupported;
   if (a.adj_ld % 4 != 0) return hipErrorNotSupported;
   switch (a.V) {
@@ -696,7 +793,7 @@ hipError_t launch_spatial_wave(const SpatialArgs& a, hipStream_t s) {
 
 hipError_t launch_temporal_wave(const TemporalArgs& a, hipStream_t s) {
   if (wave_disabled()) return hipErrorNotSupported;
-  if (a.Cin != CH || a.Cout != CH || a.V > 32 || a.epi == TEPI_OUT) return hipErrorNotSupported;
+  if (a.V > 32) return hipErrorNotSupported;
   if (a.pq && (a.npqw != 4 || !pq_layout_eq(a.pql, pq_layout_vt(8, a.T, a.V)))) return hipErrorNotSupported;
   if (a.adj_ld % 4 != 0) return hipErrorNotSupported;
   switch (a.T) {
