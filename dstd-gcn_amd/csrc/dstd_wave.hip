@@ -206,9 +206,20 @@ struct SWGeom {
   static constexpr int IMG = rup(V * V + 48, 4);  // image floats (+ slack for the padded column reads)
 };
 
-// one wave per SIMD: 300+ registers hold the unit (conv tile, output, residual, prefetch)
+// 64 -> 64: one wave per SIMD, 300+ registers hold the unit (conv tile, output,
+// residual, prefetch).  The thinner 6 -> 64 / 64 -> 3 blocks have too little
+// MFMA work per unit to hide a unit's load latency on their own: two waves.
+// (A software-pipelined variant -- the epilogue of unit k interleaved with
+// the first conv of unit k+1 through buffer stores and sched_group_barrier --
+// measured 5-8% SLOWER at 430 registers.)
+template <int CIN, int COUT>
+constexpr int spatial_wpe() {
+  return CIN == 64 && COUT == 64 ? 1 : 2;
+}
 template <int V, int CIN, int COUT, bool RES, bool EPI>
-__global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_spatial_wave(SpatialArgs a) {
+__global__ __launch_bounds__(WT) __attribute__((amdgpu_waves_per_eu(spatial_wpe<CIN, COUT>(),
+                                                                    spatial_wpe<CIN, COUT>()))) void k_spatial_wave(
+    SpatialArgs a) {
   using Gm = SWGeom<V>;
   constexpr int KQ = Gm::KQ, NQ = Gm::NQ, MT = Gm::MT, NWT = Gm::NWT, NV4 = Gm::NV4;
   constexpr int NJ = Chan<CIN>::NJ, NCO = Chan<COUT>::NT;
