@@ -1,0 +1,147 @@
+// Training-path primitives: a strided batched fp32-MFMA
+// GEMM plus the element-wise / reduction kernels that the DSTDGC, BatchNorm
+// and PReLU backward passes are composed of.  The fused inference kernels
+// (dstd_wave.hip, dstd_fast.hip) keep nothing for a backward pass; training
+// instead materialises F, P, Q, M, E and D per op (a few MB per op at the
+// config-5 batch of 32) and runs the backward as GEMMs over those saved
+// tensors.  All launchers enqueue on the given stream and return the launch
+// status.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace dstd {
+namespace train {
+
+// C[b] = alpha * A[b] . B[b] + beta * C[b] + bias_m[m]  for b over nb1 x nb2
+// batches, or, with reduce != 0, C = alpha * sum_b A[b] . B[b] + beta*C + bias
+// (batch strides of C ignored).  Every operand is addressed through explicit
+// strides, so transposes and the spatial / temporal batch layouts need no
+// copies.  beta == 0 never reads C.
+struct Gemm {
+  int M, N, K;
+  int nb1 = 1, nb2 = 1;
+  const float* A;
+  long long a_b1 = 0, a_b2 = 0, a_m, a_k;
+  const float* B;
+  long long b_b1 = 0, b_b2 = 0, b_k, b_n;
+  float* C;
+  long long c_b1 = 0, c_b2 = 0, c_m, c_n;
+  float alpha = 1.f, beta = 0.f;
+  const float* bias_m = nullptr;
+  int reduce = 0;
+};
+
+// Scratch (floats) a reduce-GEMM may need for its split-over-batches partials.
+size_t gemm_scratch_floats(int M, int N);
+hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s);
+
+// P / Q element (n, r, a, i) lives at n*sn + r*sr + a*sa + i*si.
+struct PQView {
+  long long sn, sr, sa, si;
+};
+
+// M[n][r*A + a][i][j] = tanh(P(n,r,a,i) - Q(n,r,a,j)), r < 2.
+hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int A, int NN, float* M,
+                          hipStream_t s);
+// dZ = dM * (1 - M^2);  dP(n,r,a,i) += sum_j dZ;  dQ(n,r,a,j) -= sum_i dZ.
+hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int A, int NN, float* dP, float* dQ,
+                          hipStream_t s);
+
+// D[n][a][ij] = alpha * E[n][a][ij] + Acomb[ij]   (alpha: device scalar)
+hipError_t adj_combine(const float* E, const float* Acomb, const float* alpha, int B, int A, int NN2, float* D,
+                       hipStream_t s);
+// x[i] *= alpha (device scalar)
+hipError_t scale_by(float* x, const float* alpha, size_t n, hipStream_t s);
+
+// out[m] += scale * sum_{b < nb} sum_{j < nj} X[b*sb + m*sm + j*sj], m < M.
+hipError_t reduce_rows(const float* X, int M, int nb, int nj, long long sb, long long sm, long long sj, float* out,
+                       float scale, hipStream_t s);
+
+// out[0] += sum_i x[i] * y[i]   (two-stage, deterministic; partials >= dot_partials())
+int dot_partials();
+hipError_t dot(const float* x, const float* y, size_t n, float* out, float* partials, hipStream_t s);
+
+// out = a * b + c (b may be null: out = a + c), element-wise over n.
+hipError_t fma3(const float* a, const float* b, const float* c, float* out, size_t n, hipStream_t s);
+// out += a (* b when b != null)
+hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStream_t s);
+
+// Train-mode BatchNorm over an NCTV tensor, channel (c, v), statistics over
+// (n, t) (reference model/dstdgcn.py:35-50, nn.BatchNorm1d semantics):
+//   u = x (+ x2)                     x2: optional pre-add (encoder identity residual)
+//   z = (u - mean) * rstd * gamma + beta (+ res)
+//   out = prelu ? PReLU(z) : z       (z kept in zsave when prelu is set)
+// mean / rstd ([C*V], index c*V + v) are saved for the backward; running
+// stats are updated with `momentum` and the unbiased variance when
+// running_mean != null.
+struct BnFwd {
+  const float* x;
+  const float* x2 = nullptr;
+  const float* res = nullptr;
+  const float* gamma;
+  const float* beta;
+  float* running_mean = nullptr;
+  float* running_var = nullptr;
+  float momentum = 0.1f, eps = 1e-5f;
+  const float* prelu = nullptr;
+  float* out;
+  float* zsave = nullptr;
+  float* mean;
+  float* rstd;
+};
+hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, hipStream_t s);
+
+// Backward of BnFwd.  dout is d(out); with prelu set it is first mapped
+// through PReLU' using zsave.  Writes du = d(u) (=), dz_out = dz (= , when
+// non-null: the residual branch's gradient), accumulates dgamma, dbeta and
+// the PReLU slope partial of channel c into prelu_partial[c] (=).
+struct BnBwd {
+  const float* x;
+  const float* x2 = nullptr;
+  const float* zsave = nullptr;
+  const float* prelu = nullptr;
+  const float* dout;
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  float* du;
+  float* dz_out = nullptr;
+  float* dgamma;
+  float* dbeta;
+  float* prelu_partial = nullptr;  // [C]
+};
+hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, hipStream_t s);
+
+// out[0] += sum_{i < n} partial[i]
+hipError_t sum_into(const float* partial, int n, float* out, hipStream_t s);
+
+// Model boundary in NCTV: X0[n][c][t][v] = c < C ? x[n][t][v][c] : x[n][t][v][c-C] - x[n][T-1][v][c-C]
+hipError_t prep_nctv(const float* x, int B, int T, int V, int C, float* X0, hipStream_t s);
+// y[n][t][v][c] = O[n][c][t][v] + x[n][T-1][v][c]
+hipError_t out_ntvc(const float* O, const float* x, int B, int T, int V, int C, float* y, hipStream_t s);
+// dO[n][c][t][v] = dy[n][t][v][c]
+hipError_t out_ntvc_bwd(const float* dy, int B, int T, int V, int C, float* dO, hipStream_t s);
+
+// Inverted dropout with a counter-based hash mask: out[i] = keep(seed, i) ? in[i] / (1 - p) : 0.
+// Applying it to the upstream gradient with the same seed is the backward.
+hipError_t dropout(const float* in, float* out, size_t n, float p, unsigned long long seed, hipStream_t s);
+
+// mpjpe_error_3d (engine/utils/loss.py:52-65): loss = mean_k ||p_k - q_k||_2
+// over K = n / 3 points.  fwd: out[0] (=); bwd: dp = g * (p - q) / ||p - q|| / K
+// with g = *gscale (device scalar).
+int mpjpe_partials();
+hipError_t mpjpe_fwd(const float* p, const float* q, size_t npts, float* out, float* partials, hipStream_t s);
+hipError_t mpjpe_bwd(const float* p, const float* q, size_t npts, const float* gscale, float scale, float* dp,
+                     hipStream_t s);
+// Per-frame test metric (engine/prediction.py:366-404) without host syncs.
+// all_seqs [B][T][D] (D = 3J), outputs [B][T - t_out0][n_used] fill frames
+// t_out0.. of the dims with used_pos[d] >= 0; joint j reads the filled value
+// of joint joint_src[j] (the ignore <- equal copy).  For each k:
+// sums[k] += (1/J) * sum_{n, j} ||all_seqs - pred|| at frame frames[k].
+hipError_t frame_mpjpe(const float* all_seqs, const float* outputs, int B, int T, int D, int t_out0,
+                       const int* used_pos, int n_used, const int* joint_src, const int* frames, int n_frames,
+                       float* sums, hipStream_t s);
+
+}  // namespace train
+}  // namespace dstd

@@ -1,0 +1,648 @@
+// Training-path kernels (see dstd_train.h).  Everything here is generic over
+// strides and small: the config-5 training batch is 32 sequences per GPU, so
+// these kernels favour simple, deterministic reductions (fixed-order partials,
+// no float atomics) over the hand-scheduled pipelines of the inference path.
+#include "dstd_common.h"
+#include "dstd_train.h"
+
+#include <algorithm>
+
+namespace dstd {
+namespace train {
+namespace {
+
+constexpr int kRedThreads = 256;
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  // wave64 butterfly, then one float per wave through LDS
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  return t;
+}
+
+// ---------------------------------------------------------------------------
+// Strided batched GEMM on v_mfma_f32_16x16x4_f32.
+// Workgroup = 4 waves in a 2x2 grid over a TM x TN tile of C; each wave owns a
+// (TM/2) x (TN/2) sub-tile = FM x FN MFMA fragments.  K advances 16 at a time
+// through LDS tiles As[k][m], Bs[k][n] (k-major: a fragment read is 16
+// consecutive floats per k row).  Global loads pick the thread->element map
+// whose fastest index is the operand's unit stride, so row- and column-major
+// operands both load in contiguous runs.
+// ---------------------------------------------------------------------------
+template <int TM, int TN>
+__global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, float* partial) {
+  constexpr int KT = 16;
+  constexpr int LA = TM + 4, LB = TN + 4;
+  constexpr int FM = TM / 32, FN = TN / 32;
+  constexpr int EA = TM * KT / 256, EB = TN * KT / 256;
+  __shared__ float As[KT * LA];
+  __shared__ float Bs[KT * LB];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+  const int wm = (wave >> 1) * (TM / 2), wn = (wave & 1) * (TN / 2);
+  const bool a_kfast = g.a_k == 1 && g.a_m != 1;
+  const bool b_kfast = g.b_k == 1 && g.b_n != 1;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = zero4();
+
+  const int nbat = g.nb1 * g.nb2;
+  int b_lo, b_hi;
+  if (g.reduce) {
+    const int per = (nbat + nsplit - 1) / nsplit;
+    b_lo = blockIdx.z * per;
+    b_hi = min(nbat, b_lo + per);
+  } else {
+    b_lo = blockIdx.z;
+    b_hi = b_lo + 1;
+  }
+
+  for (int b = b_lo; b < b_hi; ++b) {
+    const int b1 = b / g.nb2, b2 = b - b1 * g.nb2;
+    const float* Ab = g.A + b1 * g.a_b1 + b2 * g.a_b2;
+    const float* Bb = g.B + b1 * g.b_b1 + b2 * g.b_b2;
+    for (int k0 = 0; k0 < g.K; k0 += KT) {
+      float ra[EA], rb[EB];
+#pragma unroll
+      for (int e = 0; e < EA; ++e) {
+        const int idx = tid + 256 * e;
+        const int m = a_kfast ? idx / KT : idx % TM;
+        const int k = a_kfast ? idx % KT : idx / TM;
+        const int gm = m0 + m, gk = k0 + k;
+        ra[e] = (gm < g.M && gk < g.K) ? Ab[gm * g.a_m + gk * g.a_k] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < EB; ++e) {
+        const int idx = tid + 256 * e;
+        const int n = b_kfast ? idx / KT : idx % TN;
+        const int k = b_kfast ? idx % KT : idx / TN;
+        const int gn = n0 + n, gk = k0 + k;
+        rb[e] = (gn < g.N && gk < g.K) ? Bb[gk * g.b_k + gn * g.b_n] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < EA; ++e) {
+        const int idx = tid + 256 * e;
+        const int m = a_kfast ? idx / KT : idx % TM;
+        const int k = a_kfast ? idx % KT : idx / TM;
+        As[k * LA + m] = ra[e];
+      }
+#pragma unroll
+      for (int e = 0; e < EB; ++e) {
+        const int idx = tid + 256 * e;
+        const int n = b_kfast ? idx / KT : idx % TN;
+        const int k = b_kfast ? idx % KT : idx / TN;
+        Bs[k * LB + n] = rb[e];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < KT / 4; ++kk) {
+        const int kr = kk * 4 + (lane >> 4);
+        float av[FM], bv[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) av[i] = As[kr * LA + wm + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bv[j] = Bs[kr * LB + wn + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j] = mfma16x16x4(av[i], bv[j], acc[i][j]);
+      }
+    }
+  }
+
+  // epilogue: C/D[row = (lane>>4)*4 + r][col = lane&15]
+  if (partial) {
+    float* P = partial + (size_t)blockIdx.z * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int gm = m0 + wm + i * 16 + (lane >> 4) * 4 + r, gn = n0 + wn + j * 16 + (lane & 15);
+          if (gm < g.M && gn < g.N) P[(size_t)gm * g.N + gn] = acc[i][j][r];
+        }
+    return;
+  }
+  const int b1 = g.reduce ? 0 : blockIdx.z / g.nb2, b2 = g.reduce ? 0 : blockIdx.z - b1 * g.nb2;
+  float* Cb = g.C + b1 * g.c_b1 + b2 * g.c_b2;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm + i * 16 + (lane >> 4) * 4 + r, gn = n0 + wn + j * 16 + (lane & 15);
+        if (gm < g.M && gn < g.N) {
+          float v = g.alpha * acc[i][j][r];
+          if (g.bias_m) v += g.bias_m[gm];
+          float* c = Cb + gm * g.c_m + gn * g.c_n;
+          if (g.beta != 0.f) v += g.beta * *c;
+          *c = v;
+        }
+      }
+}
+
+// C = alpha * sum_z partial[z] + bias + beta * C   (fixed order over z)
+__global__ void k_gemm_finish(Gemm g, int nsplit, const float* partial) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= g.M * g.N) return;
+  const int m = idx / g.N, n = idx - m * g.N;
+  float s = 0.f;
+  for (int z = 0; z < nsplit; ++z) s += partial[(size_t)z * g.M * g.N + idx];
+  float v = g.alpha * s;
+  if (g.bias_m) v += g.bias_m[m];
+  float* c = g.C + m * g.c_m + n * g.c_n;
+  if (g.beta != 0.f) v += g.beta * *c;
+  *c = v;
+}
+
+constexpr int kMaxSplit = 64;
+
+// ---------------------------------------------------------------------------
+// tanh outer difference
+// ---------------------------------------------------------------------------
+__global__ void k_tanh_outer_fwd(const float* P, const float* Q, PQView v, int A, int NN, float* M) {
+  // one workgroup per (n, r, a); M block [NN][NN]
+  const int blk = blockIdx.x;
+  const int n = blk / (2 * A), ra = blk - n * 2 * A, r = ra / A, a = ra - r * A;
+  const float* p = P + n * v.sn + r * v.sr + a * v.sa;
+  const float* q = Q + n * v.sn + r * v.sr + a * v.sa;
+  float* m = M + (size_t)blk * NN * NN;
+  for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
+    const int i = e / NN, j = e - i * NN;
+    m[e] = tanhf(p[i * v.si] - q[j * v.si]);
+  }
+}
+
+__global__ void k_tanh_outer_bwd(const float* M, const float* dM, PQView v, int A, int NN, float* dP, float* dQ) {
+  extern __shared__ float dz[];  // [NN][NN+1]
+  const int blk = blockIdx.x;
+  const int n = blk / (2 * A), ra = blk - n * 2 * A, r = ra / A, a = ra - r * A;
+  const float* m = M + (size_t)blk * NN * NN;
+  const float* dm = dM + (size_t)blk * NN * NN;
+  for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
+    const int i = e / NN, j = e - i * NN;
+    const float t = m[e];
+    dz[i * (NN + 1) + j] = dm[e] * (1.f - t * t);
+  }
+  __syncthreads();
+  const size_t base = n * v.sn + r * v.sr + a * v.sa;
+  for (int i = threadIdx.x; i < 2 * NN; i += blockDim.x) {
+    float s = 0.f;
+    if (i < NN) {
+      for (int j = 0; j < NN; ++j) s += dz[i * (NN + 1) + j];
+      dP[base + i * v.si] += s;
+    } else {
+      const int j = i - NN;
+      for (int k = 0; k < NN; ++k) s += dz[k * (NN + 1) + j];
+      dQ[base + j * v.si] -= s;
+    }
+  }
+}
+
+__global__ void k_adj_combine(const float* E, const float* Acomb, const float* alpha, size_t n, int NN2, float* D) {
+  const float al = *alpha;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    D[e] = fmaf(al, E[e], Acomb[e % NN2]);
+}
+
+__global__ void k_scale_by(float* x, const float* alpha, size_t n) {
+  const float al = *alpha;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    x[e] *= al;
+}
+
+__global__ void k_reduce_rows(const float* X, int nb, int nj, long long sb, long long sm, long long sj, float* out,
+                              float scale) {
+  __shared__ float red[kRedThreads / 64];
+  const int m = blockIdx.x;
+  const long long tot = (long long)nb * nj;
+  float s = 0.f;
+  for (long long e = threadIdx.x; e < tot; e += blockDim.x) {
+    const long long b = e / nj, j = e - b * nj;
+    s += X[b * sb + m * sm + j * sj];
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[m] += scale * s;
+}
+
+constexpr int kDotBlocks = 256;
+
+__global__ void k_dot_partial(const float* x, const float* y, size_t n, float* partials) {
+  __shared__ float red[kRedThreads / 64];
+  float s = 0.f;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    s = fmaf(x[e], y[e], s);
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__global__ void k_sum_into(const float* partials, int n, float* out) {
+  __shared__ float red[kRedThreads / 64];
+  float s = 0.f;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) s += partials[e];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[0] += s;
+}
+
+__global__ void k_fma3(const float* a, const float* b, const float* c, float* out, size_t n) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    out[e] = b ? fmaf(a[e], b[e], c[e]) : a[e] + c[e];
+}
+
+__global__ void k_acc_mul(const float* a, const float* b, float* out, size_t n) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
+    out[e] += b ? a[e] * b[e] : a[e];
+}
+
+// ---------------------------------------------------------------------------
+// Train-mode BatchNorm.  One workgroup per feature channel c; thread
+// (slice s, joint v) walks rows (n, t) = s, s + S, ... so a wave reads runs of
+// V consecutive floats.  Per-v sums are combined over slices in LDS in a fixed
+// order (deterministic).
+// ---------------------------------------------------------------------------
+struct BnGeom {
+  int V, S, rows;
+  __device__ BnGeom(int V_, int B, int T) : V(V_), S(kRedThreads / V_), rows(B * T) {}
+};
+
+__device__ __forceinline__ float slice_sum(float v, float* lds, int V, int S) {
+  // lds: [S][V]; returns the total over slices for this thread's v (all threads)
+  const int tid = threadIdx.x;
+  __syncthreads();
+  if (tid < S * V) lds[tid] = v;
+  __syncthreads();
+  const int jv = tid % V;
+  float t = 0.f;
+  for (int s = 0; s < S; ++s) t += lds[s * V + jv];
+  return t;
+}
+
+__global__ __launch_bounds__(kRedThreads) void k_bn_train_fwd(BnFwd a, int B, int C, int T, int V) {
+  __shared__ float lds[kRedThreads];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const BnGeom G(V, B, T);
+  const bool act = tid < G.S * V;
+  const int v = tid % V, s0 = tid / V;
+  const size_t TV = (size_t)T * V, CTV = (size_t)C * TV;
+  auto at = [&](int row) -> size_t {
+    const int n = row / T, t = row - n * T;
+    return n * CTV + c * TV + (size_t)t * V + v;
+  };
+  auto u_of = [&](size_t i) { return a.x2 ? a.x[i] + a.x2[i] : a.x[i]; };
+  float s = 0.f;
+  if (act)
+    for (int row = s0; row < G.rows; row += G.S) s += u_of(at(row));
+  const float mean = slice_sum(s, lds, V, G.S) / G.rows;
+  float q = 0.f;
+  if (act)
+    for (int row = s0; row < G.rows; row += G.S) {
+      const float d = u_of(at(row)) - mean;
+      q = fmaf(d, d, q);
+    }
+  const float var = slice_sum(q, lds, V, G.S) / G.rows;
+  const float rstd = 1.f / sqrtf(var + a.eps);
+  const int ch = c * V + v;
+  if (tid < V) {
+    a.mean[ch] = mean;
+    a.rstd[ch] = rstd;
+    if (a.running_mean) {
+      const float unb = G.rows > 1 ? var * G.rows / (G.rows - 1) : var;
+      a.running_mean[ch] = (1.f - a.momentum) * a.running_mean[ch] + a.momentum * mean;
+      a.running_var[ch] = (1.f - a.momentum) * a.running_var[ch] + a.momentum * unb;
+    }
+  }
+  if (!act) return;
+  const float sc = rstd * a.gamma[ch], sh = a.beta[ch] - mean * sc;
+  const float w = a.prelu ? *a.prelu : 0.f;
+  for (int row = s0; row < G.rows; row += G.S) {
+    const size_t i = at(row);
+    float z = fmaf(u_of(i), sc, sh);
+    if (a.res) z += a.res[i];
+    if (a.prelu) {
+      a.zsave[i] = z;
+      a.out[i] = prelu_f(z, w);
+    } else {
+      a.out[i] = z;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kRedThreads) void k_bn_train_bwd(BnBwd a, int B, int C, int T, int V) {
+  __shared__ float lds[kRedThreads];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const BnGeom G(V, B, T);
+  const bool act = tid < G.S * V;
+  const int v = tid % V, s0 = tid / V;
+  const size_t TV = (size_t)T * V, CTV = (size_t)C * TV;
+  const int ch = c * V + v;
+  auto at = [&](int row) -> size_t {
+    const int n = row / T, t = row - n * T;
+    return n * CTV + c * TV + (size_t)t * V + v;
+  };
+  const float w = a.prelu ? *a.prelu : 0.f;
+  // PReLU' (torch convention: slope for z <= 0)
+  auto dz_of = [&](size_t i) {
+    const float d = a.dout[i];
+    return (a.prelu && !(a.zsave[i] > 0.f)) ? w * d : d;
+  };
+  const float mean = act ? a.mean[ch] : 0.f, rstd = act ? a.rstd[ch] : 0.f;
+  float sd = 0.f, sdx = 0.f, sw = 0.f;
+  if (act)
+    for (int row = s0; row < G.rows; row += G.S) {
+      const size_t i = at(row);
+      const float dz = dz_of(i);
+      const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
+      sd += dz;
+      sdx = fmaf(dz, (u - mean) * rstd, sdx);
+      if (a.prelu) sw = fmaf(a.dout[i], fminf(a.zsave[i], 0.f), sw);
+    }
+  const float dbeta = slice_sum(sd, lds, V, G.S);
+  const float dgamma = slice_sum(sdx, lds, V, G.S);
+  if (a.prelu_partial) {
+    __shared__ float red[kRedThreads / 64];
+    const float tw = block_sum(act ? sw : 0.f, red);
+    if (tid == 0) a.prelu_partial[c] = tw;
+  }
+  if (tid < V) {
+    a.dgamma[ch] += dgamma;
+    a.dbeta[ch] += dbeta;
+  }
+  if (!act) return;
+  const float g = a.gamma[ch] * rstd, inv = 1.f / G.rows;
+  for (int row = s0; row < G.rows; row += G.S) {
+    const size_t i = at(row);
+    const float dz = dz_of(i);
+    const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
+    const float xh = (u - mean) * rstd;
+    a.du[i] = g * (dz - dbeta * inv - xh * dgamma * inv);
+    if (a.dz_out) a.dz_out[i] = dz;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// model boundary, loss and metric
+// ---------------------------------------------------------------------------
+__global__ void k_prep_nctv(const float* x, int B, int T, int V, int C, float* X0) {
+  const size_t tot = (size_t)B * 2 * C * T * V;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    size_t r = e;
+    const int v = r % V; r /= V;
+    const int t = r % T; r /= T;
+    const int c = r % (2 * C);
+    const int n = r / (2 * C);
+    const float* xs = x + (size_t)n * T * V * C;
+    const int cc = c < C ? c : c - C;
+    const float val = xs[((size_t)t * V + v) * C + cc];
+    X0[e] = c < C ? val : val - xs[((size_t)(T - 1) * V + v) * C + cc];
+  }
+}
+
+__global__ void k_out_ntvc(const float* O, const float* x, int B, int T, int V, int C, float* y) {
+  const size_t tot = (size_t)B * T * V * C;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    size_t r = e;
+    const int c = r % C; r /= C;
+    const int v = r % V; r /= V;
+    const int t = r % T;
+    const int n = r / T;
+    y[e] = O[(((size_t)n * C + c) * T + t) * V + v] + x[(((size_t)n * T + T - 1) * V + v) * C + c];
+  }
+}
+
+__global__ void k_out_ntvc_bwd(const float* dy, int B, int T, int V, int C, float* dO) {
+  const size_t tot = (size_t)B * T * V * C;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    size_t r = e;
+    const int v = r % V; r /= V;
+    const int t = r % T; r /= T;
+    const int c = r % C;
+    const int n = r / C;
+    dO[e] = dy[(((size_t)n * T + t) * V + v) * C + c];
+  }
+}
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+
+__global__ void k_dropout(const float* in, float* out, size_t n, float p, unsigned long long seed) {
+  const float keep_scale = 1.f / (1.f - p);
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const unsigned long long h = mix64(seed * 0x9e3779b97f4a7c15ULL + e);
+    const float u = (float)(h >> 40) * (1.f / 16777216.f);  // [0, 1), 24 bits
+    out[e] = u >= p ? in[e] * keep_scale : 0.f;
+  }
+}
+
+constexpr int kLossBlocks = 128;
+
+__global__ void k_mpjpe_partial(const float* p, const float* q, size_t npts, float* partials) {
+  __shared__ float red[kRedThreads / 64];
+  float s = 0.f;
+  for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < npts; k += (size_t)gridDim.x * blockDim.x) {
+    const float dx = p[3 * k] - q[3 * k], dy = p[3 * k + 1] - q[3 * k + 1], dz = p[3 * k + 2] - q[3 * k + 2];
+    s += sqrtf(dx * dx + dy * dy + dz * dz);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+__global__ void k_mpjpe_final(const float* partials, int n, size_t npts, float* out) {
+  __shared__ float red[kRedThreads / 64];
+  float s = 0.f;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) s += partials[e];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) out[0] = s / (float)npts;
+}
+
+__global__ void k_mpjpe_bwd(const float* p, const float* q, size_t npts, const float* gscale, float scale,
+                            float* dp) {
+  const float g = (gscale ? *gscale : 1.f) * scale / (float)npts;
+  for (size_t k = blockIdx.x * (size_t)blockDim.x + threadIdx.x; k < npts; k += (size_t)gridDim.x * blockDim.x) {
+    const float dx = p[3 * k] - q[3 * k], dy = p[3 * k + 1] - q[3 * k + 1], dz = p[3 * k + 2] - q[3 * k + 2];
+    const float nrm = sqrtf(dx * dx + dy * dy + dz * dz);
+    // torch.norm backward: 0 at the kink
+    const float f = nrm > 0.f ? g / nrm : 0.f;
+    dp[3 * k] = f * dx;
+    dp[3 * k + 1] = f * dy;
+    dp[3 * k + 2] = f * dz;
+  }
+}
+
+// one workgroup per eval frame
+__global__ void k_frame_mpjpe(const float* seqs, const float* outs, int B, int T, int D, int t_out0,
+                              const int* used_pos, int n_used, const int* joint_src, const int* frames,
+                              float* sums) {
+  __shared__ float red[kRedThreads / 64];
+  const int k = blockIdx.x, f = frames[k], J = D / 3;
+  float s = 0.f;
+  for (int e = threadIdx.x; e < B * J; e += blockDim.x) {
+    const int n = e / J, j = e - n * J;
+    const float* tg = seqs + ((size_t)n * T + f) * D;
+    const int src = joint_src[j];
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int d = 3 * src + c;
+      const int u = used_pos[d];
+      const float pv = (u >= 0 && f >= t_out0) ? outs[((size_t)n * (T - t_out0) + (f - t_out0)) * n_used + u] : tg[d];
+      const float df = tg[3 * j + c] - pv;
+      acc = fmaf(df, df, acc);
+    }
+    s += sqrtf(acc);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) sums[k] += s / J;
+}
+
+int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 4096); }
+
+}  // namespace
+
+size_t gemm_scratch_floats(int M, int N) { return (size_t)kMaxSplit * M * N; }
+
+hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
+  if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  const int TM = g.M <= 32 ? 32 : 64, TN = g.N <= 32 ? 32 : 64;
+  const int tiles = cdiv(g.M, TM) * cdiv(g.N, TN);
+  const int nbat = g.nb1 * g.nb2;
+  int nsplit = 1;
+  if (g.reduce && scratch) {
+    // enough workgroups to cover the chip, each with a few batches
+    nsplit = std::min(std::min(kMaxSplit, nbat), std::max(1, 512 / tiles));
+  }
+  dim3 grid(cdiv(g.N, TN), cdiv(g.M, TM), g.reduce ? nsplit : nbat);
+  float* part = nsplit > 1 ? scratch : nullptr;
+  if (TM == 32 && TN == 32) k_gemm<32, 32><<<grid, 256, 0, s>>>(g, nsplit, part);
+  else if (TM == 32) k_gemm<32, 64><<<grid, 256, 0, s>>>(g, nsplit, part);
+  else if (TN == 32) k_gemm<64, 32><<<grid, 256, 0, s>>>(g, nsplit, part);
+  else k_gemm<64, 64><<<grid, 256, 0, s>>>(g, nsplit, part);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || nsplit == 1) return e;
+  k_gemm_finish<<<cdiv(g.M * g.N, 256), 256, 0, s>>>(g, nsplit, part);
+  return hipGetLastError();
+}
+
+hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int A, int NN, float* M, hipStream_t s) {
+  k_tanh_outer_fwd<<<B * 2 * A, 256, 0, s>>>(P, Q, v, A, NN, M);
+  return hipGetLastError();
+}
+
+hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int A, int NN, float* dP, float* dQ,
+                          hipStream_t s) {
+  const size_t lds = (size_t)NN * (NN + 1) * sizeof(float);
+  k_tanh_outer_bwd<<<B * 2 * A, 256, lds, s>>>(M, dM, v, A, NN, dP, dQ);
+  return hipGetLastError();
+}
+
+hipError_t adj_combine(const float* E, const float* Acomb, const float* alpha, int B, int A, int NN2, float* D,
+                       hipStream_t s) {
+  const size_t n = (size_t)B * A * NN2;
+  k_adj_combine<<<grid_for(n), 256, 0, s>>>(E, Acomb, alpha, n, NN2, D);
+  return hipGetLastError();
+}
+
+hipError_t scale_by(float* x, const float* alpha, size_t n, hipStream_t s) {
+  k_scale_by<<<grid_for(n), 256, 0, s>>>(x, alpha, n);
+  return hipGetLastError();
+}
+
+hipError_t reduce_rows(const float* X, int M, int nb, int nj, long long sb, long long sm, long long sj, float* out,
+                       float scale, hipStream_t s) {
+  k_reduce_rows<<<M, kRedThreads, 0, s>>>(X, nb, nj, sb, sm, sj, out, scale);
+  return hipGetLastError();
+}
+
+int dot_partials() { return kDotBlocks; }
+
+hipError_t dot(const float* x, const float* y, size_t n, float* out, float* partials, hipStream_t s) {
+  k_dot_partial<<<kDotBlocks, kRedThreads, 0, s>>>(x, y, n, partials);
+  k_sum_into<<<1, kRedThreads, 0, s>>>(partials, kDotBlocks, out);
+  return hipGetLastError();
+}
+
+hipError_t sum_into(const float* partial, int n, float* out, hipStream_t s) {
+  k_sum_into<<<1, kRedThreads, 0, s>>>(partial, n, out);
+  return hipGetLastError();
+}
+
+hipError_t fma3(const float* a, const float* b, const float* c, float* out, size_t n, hipStream_t s) {
+  k_fma3<<<grid_for(n), 256, 0, s>>>(a, b, c, out, n);
+  return hipGetLastError();
+}
+
+hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStream_t s) {
+  k_acc_mul<<<grid_for(n), 256, 0, s>>>(a, b, out, n);
+  return hipGetLastError();
+}
+
+hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, hipStream_t s) {
+  k_bn_train_fwd<<<C, kRedThreads, 0, s>>>(a, B, C, T, V);
+  return hipGetLastError();
+}
+
+hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, hipStream_t s) {
+  k_bn_train_bwd<<<C, kRedThreads, 0, s>>>(a, B, C, T, V);
+  return hipGetLastError();
+}
+
+hipError_t prep_nctv(const float* x, int B, int T, int V, int C, float* X0, hipStream_t s) {
+  k_prep_nctv<<<grid_for((size_t)B * 2 * C * T * V), 256, 0, s>>>(x, B, T, V, C, X0);
+  return hipGetLastError();
+}
+
+hipError_t out_ntvc(const float* O, const float* x, int B, int T, int V, int C, float* y, hipStream_t s) {
+  k_out_ntvc<<<grid_for((size_t)B * C * T * V), 256, 0, s>>>(O, x, B, T, V, C, y);
+  return hipGetLastError();
+}
+
+hipError_t out_ntvc_bwd(const float* dy, int B, int T, int V, int C, float* dO, hipStream_t s) {
+  k_out_ntvc_bwd<<<grid_for((size_t)B * C * T * V), 256, 0, s>>>(dy, B, T, V, C, dO);
+  return hipGetLastError();
+}
+
+hipError_t dropout(const float* in, float* out, size_t n, float p, unsigned long long seed, hipStream_t s) {
+  k_dropout<<<grid_for(n), 256, 0, s>>>(in, out, n, p, seed);
+  return hipGetLastError();
+}
+
+int mpjpe_partials() { return kLossBlocks; }
+
+hipError_t mpjpe_fwd(const float* p, const float* q, size_t npts, float* out, float* partials, hipStream_t s) {
+  k_mpjpe_partial<<<kLossBlocks, kRedThreads, 0, s>>>(p, q, npts, partials);
+  k_mpjpe_final<<<1, kRedThreads, 0, s>>>(partials, kLossBlocks, npts, out);
+  return hipGetLastError();
+}
+
+hipError_t mpjpe_bwd(const float* p, const float* q, size_t npts, const float* gscale, float scale, float* dp,
+                     hipStream_t s) {
+  k_mpjpe_bwd<<<grid_for(npts), 256, 0, s>>>(p, q, npts, gscale, scale, dp);
+  return hipGetLastError();
+}
+
+hipError_t frame_mpjpe(const float* all_seqs, const float* outputs, int B, int T, int D, int t_out0,
+                       const int* used_pos, int n_used, const int* joint_src, const int* frames, int n_frames,
+                       float* sums, hipStream_t s) {
+  k_frame_mpjpe<<<n_frames, kRedThreads, 0, s>>>(all_seqs, outputs, B, T, D, t_out0, used_pos, n_used, joint_src,
+                                                 frames, sums);
+  return hipGetLastError();
+}
+
+}  // namespace train
+}  // namespace dstd

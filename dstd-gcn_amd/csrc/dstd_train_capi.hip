@@ -1,0 +1,714 @@
+// C ABI of the training path (include/dstd_gcn_train.h): saved-buffer and
+// workspace carving plus the launch sequences of the train-mode forward and
+// the backward of DSTDGC / DSTDGCB / DSTDGCN, and the engine's loss / metric.
+//
+// Index conventions shared by both DSTDGC modes ("rows" a = the adjacency
+// index, "nodes" i, j = what the adjacency mixes):
+//   spatial  (model/dstdgcn.py:83-87): a = t (A = T rows), i = v (NN = V)
+//   temporal (model/dstdgcn.py:88-93): a = v (A = V rows), i = t (NN = T)
+// An NCTV activation X[n][c][t][v] is addressed as n*C*TV + c*TV + a*ps_a +
+// i*ps_i with (ps_a, ps_i) = (V, 1) spatial and (1, V) temporal, so every
+// step below is one strided GEMM or element-wise kernel for either mode.
+#include <string.h>
+
+#include <algorithm>
+#include <initializer_list>
+#include <vector>
+
+#include "../../include/dstd_gcn_train.h"
+#include "dstd_common.h"
+#include "dstd_train.h"
+
+using namespace dstd::train;
+
+namespace {
+
+constexpr int kMaxT = 96;
+constexpr int kMaxV = 32;
+constexpr int kMaxC = 64;
+
+struct Carver {
+  char* base;
+  size_t off = 0;
+  float* take(size_t nfloats) {
+    off = (off + 255) & ~size_t(255);
+    float* p = base ? reinterpret_cast<float*>(base + off) : nullptr;
+    off += nfloats * sizeof(float);
+    return p;
+  }
+};
+
+#define DSTD_TRY(expr)                    \
+  do {                                    \
+    hipError_t _e = (expr);               \
+    if (_e != hipSuccess) return (int)_e; \
+  } while (0)
+
+#define DSTD_TRYH(expr)                  \
+  do {                                   \
+    hipError_t _e = (expr);              \
+    if (_e != hipSuccess) return _e;     \
+  } while (0)
+
+bool shape_ok(int B, int T, int V) { return B > 0 && T > 1 && V > 0 && T <= kMaxT && V <= kMaxV; }
+bool ch_ok(int c) { return c >= 1 && c <= kMaxC; }
+bool gc_ok(const dstd_gc_weights* w) {
+  return w && w->wf && w->bf && w->wm1 && w->bm1 && w->wm2 && w->bm2 && w->wrm && w->brm;
+}
+bool gg_ok(const dstd_gc_grads* g) {
+  return g && g->wf && g->bf && g->wm1 && g->bm1 && g->wm2 && g->bm2 && g->wrm && g->brm;
+}
+bool bn_ok(const dstd_bn& b) { return b.weight && b.bias && b.running_mean && b.running_var; }
+bool bng_ok(const dstd_bn_grads& b) { return b.weight && b.bias; }
+bool block_ok(const dstd_block_params* p) {
+  if (!p || !p->A_s || !p->W_s || !p->R_s || !p->A_t || !p->R_t || !p->alpha_sm || !p->alpha_tm || !p->prelu)
+    return false;
+  if (!ch_ok(p->cin) || !ch_ok(p->cout)) return false;
+  if (!gc_ok(&p->conv_s[0]) || !gc_ok(&p->conv_s[1]) || !gc_ok(&p->conv_t) || !bn_ok(p->bn)) return false;
+  if (p->cin != p->cout && (!p->res_w || !p->res_b || !bn_ok(p->res_bn))) return false;
+  return true;
+}
+bool block_grads_ok(const dstd_block_params* p, const dstd_block_grads* g) {
+  if (!g || !g->W_s || !g->R_s || !g->R_t || !g->alpha_sm || !g->alpha_tm || !g->prelu) return false;
+  if (!gg_ok(&g->conv_s[0]) || !gg_ok(&g->conv_s[1]) || !gg_ok(&g->conv_t) || !bng_ok(g->bn)) return false;
+  if (p->cin != p->cout && (!g->res_w || !g->res_b || !bng_ok(g->res_bn))) return false;
+  return true;
+}
+bool model_ok(const dstd_model_params* p) {
+  if (!p || p->num_layers < 0 || p->num_layers > DSTD_MAX_LAYERS || p->in_channels != 6) return false;
+  if (!block_ok(&p->st_in) || !bn_ok(p->bn_in) || !p->prelu || !block_ok(&p->st_out)) return false;
+  for (int i = 0; i < p->num_layers; ++i)
+    if (!block_ok(&p->enc[i]) || !bn_ok(p->enc_bn[i]) || !p->enc_prelu[i]) return false;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// one DSTDGC
+// ---------------------------------------------------------------------------
+struct OpGeom {
+  int B, cin, cout, T, V, TV;
+  int A, NN, NN2;
+  long long ps_a, ps_i;
+  OpGeom(int mode, int B_, int cin_, int cout_, int T_, int V_)
+      : B(B_), cin(cin_), cout(cout_), T(T_), V(V_), TV(T_ * V_) {
+    const bool sp = mode == DSTD_MODE_SPATIAL;
+    A = sp ? T : V;
+    NN = sp ? V : T;
+    NN2 = NN * NN;
+    ps_a = sp ? V : 1;
+    ps_i = sp ? 1 : V;
+  }
+  PQView pq() const { return PQView{2LL * TV, (long long)TV, ps_a, ps_i}; }
+};
+
+struct OpSaved {
+  float *F, *P, *Q, *M, *E, *D;
+};
+void carve_op_saved(Carver& cv, OpSaved& s, const OpGeom& g) {
+  s.F = cv.take((size_t)g.B * g.cout * g.TV);
+  s.P = cv.take((size_t)g.B * 2 * g.TV);
+  s.Q = cv.take((size_t)g.B * 2 * g.TV);
+  s.M = cv.take((size_t)g.B * 2 * g.A * g.NN2);
+  s.E = cv.take((size_t)g.B * g.A * g.NN2);
+  s.D = cv.take((size_t)g.B * g.A * g.NN2);
+}
+
+struct OpWs {
+  float *dF, *dD, *dM, *dP, *dQ, *gs, *part;
+};
+// Sized for the largest of the given op geometries (one workspace serves every
+// op of a block / model in turn).
+void carve_op_ws(Carver& cv, OpWs& w, std::initializer_list<OpGeom> gl) {
+  size_t nF = 0, nD = 0, nPQ = 0, nmn = 0;
+  for (const OpGeom& g : gl) {
+    nF = std::max(nF, (size_t)g.B * g.cout * g.TV);
+    nD = std::max(nD, (size_t)g.B * g.A * g.NN2);
+    nPQ = std::max(nPQ, (size_t)g.B * 2 * g.TV);
+    nmn = std::max(nmn, (size_t)std::max(std::max(g.cout * g.cin, 2 * g.A * g.A), 2 * g.cin));
+  }
+  w.dF = cv.take(nF);
+  w.dD = cv.take(nD);
+  w.dM = cv.take(2 * nD);
+  w.dP = cv.take(nPQ);
+  w.dQ = cv.take(nPQ);
+  w.gs = cv.take(gemm_scratch_floats((int)nmn, 1));
+  w.part = cv.take(std::max(dot_partials(), mpjpe_partials()));
+}
+
+// 1x1 conv as GEMMs over NCTV (W [cout][cin]).
+Gemm conv_fwd(const float* W, const float* bias, const float* X, float* Y, int B, int cin, int cout, int TV) {
+  Gemm g;
+  g.M = cout, g.N = TV, g.K = cin, g.nb1 = B;
+  g.A = W, g.a_m = cin, g.a_k = 1;
+  g.B = X, g.b_b1 = (long long)cin * TV, g.b_k = TV, g.b_n = 1;
+  g.C = Y, g.c_b1 = (long long)cout * TV, g.c_m = TV, g.c_n = 1;
+  g.bias_m = bias;
+  return g;
+}
+Gemm conv_dx(const float* W, const float* dY, float* dX, int B, int cin, int cout, int TV) {
+  Gemm g;
+  g.M = cin, g.N = TV, g.K = cout, g.nb1 = B;
+  g.A = W, g.a_m = 1, g.a_k = cin;
+  g.B = dY, g.b_b1 = (long long)cout * TV, g.b_k = TV, g.b_n = 1;
+  g.C = dX, g.c_b1 = (long long)cin * TV, g.c_m = TV, g.c_n = 1;
+  g.beta = 1.f;
+  return g;
+}
+Gemm conv_dw(const float* dY, const float* X, float* dW, int B, int cin, int cout, int TV) {
+  Gemm g;
+  g.M = cout, g.N = cin, g.K = TV, g.nb1 = B, g.reduce = 1;
+  g.A = dY, g.a_b1 = (long long)cout * TV, g.a_m = TV, g.a_k = 1;
+  g.B = X, g.b_b1 = (long long)cin * TV, g.b_k = 1, g.b_n = TV;
+  g.C = dW, g.c_m = cin, g.c_n = 1;
+  g.beta = 1.f;
+  return g;
+}
+hipError_t conv_bwd(const float* W, const float* X, const float* dY, float* dX, float* dW, float* db, int B, int cin,
+                    int cout, int TV, float* gs, hipStream_t s) {
+  if (dX) DSTD_TRYH(gemm(conv_dx(W, dY, dX, B, cin, cout, TV), gs, s));
+  DSTD_TRYH(gemm(conv_dw(dY, X, dW, B, cin, cout, TV), gs, s));
+  return reduce_rows(dY, cout, B, TV, (long long)cout * TV, TV, 1, db, 1.f, s);
+}
+
+// y (beta_y: 0 '=' / 1 '+=') = DSTDGC(x, Acomb, alpha); fills sv.
+hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* Acomb, const float* alpha,
+                  float* y, float beta_y, const OpSaved& sv, hipStream_t s) {
+  DSTD_TRYH(gemm(conv_fwd(w->wf, w->bf, x, sv.F, g.B, g.cin, g.cout, g.TV), nullptr, s));   // :81
+  DSTD_TRYH(gemm(conv_fwd(w->wm1, w->bm1, x, sv.P, g.B, g.cin, 2, g.TV), nullptr, s));     // :82
+  DSTD_TRYH(gemm(conv_fwd(w->wm2, w->bm2, x, sv.Q, g.B, g.cin, 2, g.TV), nullptr, s));
+  DSTD_TRYH(tanh_outer_fwd(sv.P, sv.Q, g.pq(), g.B, g.A, g.NN, sv.M, s));                  // :84 / :90
+  Gemm e;  // E = conv_rm(M): [A x 2A] . [2A x NN^2] + b_rm           :85 / :91
+  e.M = g.A, e.N = g.NN2, e.K = 2 * g.A, e.nb1 = g.B;
+  e.A = w->wrm, e.a_m = 2 * g.A, e.a_k = 1;
+  e.B = sv.M, e.b_b1 = 2LL * g.A * g.NN2, e.b_k = g.NN2, e.b_n = 1;
+  e.C = sv.E, e.c_b1 = (long long)g.A * g.NN2, e.c_m = g.NN2, e.c_n = 1;
+  e.bias_m = w->brm;
+  DSTD_TRYH(gemm(e, nullptr, s));
+  DSTD_TRYH(adj_combine(sv.E, Acomb, alpha, g.B, g.A, g.NN2, sv.D, s));                    // :86 / :92
+  Gemm a;  // y[c][j] = sum_i F[c][i] D[i][j] per (n, a)               :87 / :93
+  a.M = g.cout, a.N = g.NN, a.K = g.NN, a.nb1 = g.B, a.nb2 = g.A;
+  a.A = sv.F, a.a_b1 = (long long)g.cout * g.TV, a.a_b2 = g.ps_a, a.a_m = g.TV, a.a_k = g.ps_i;
+  a.B = sv.D, a.b_b1 = (long long)g.A * g.NN2, a.b_b2 = g.NN2, a.b_k = g.NN, a.b_n = 1;
+  a.C = y, a.c_b1 = (long long)g.cout * g.TV, a.c_b2 = g.ps_a, a.c_m = g.TV, a.c_n = g.ps_i;
+  a.beta = beta_y;
+  return gemm(a, nullptr, s);
+}
+
+hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* alpha, const OpSaved& sv,
+                  const float* dy, float* dx, const dstd_gc_grads* gr, float* dA, float* dalpha, const OpWs& ws,
+                  hipStream_t s) {
+  const size_t nadj = (size_t)g.B * g.A * g.NN2;
+  Gemm f;  // dF[c][i] = sum_j dy[c][j] D[i][j]
+  f.M = g.cout, f.N = g.NN, f.K = g.NN, f.nb1 = g.B, f.nb2 = g.A;
+  f.A = dy, f.a_b1 = (long long)g.cout * g.TV, f.a_b2 = g.ps_a, f.a_m = g.TV, f.a_k = g.ps_i;
+  f.B = sv.D, f.b_b1 = (long long)g.A * g.NN2, f.b_b2 = g.NN2, f.b_k = 1, f.b_n = g.NN;
+  f.C = ws.dF, f.c_b1 = (long long)g.cout * g.TV, f.c_b2 = g.ps_a, f.c_m = g.TV, f.c_n = g.ps_i;
+  DSTD_TRYH(gemm(f, nullptr, s));
+  Gemm d;  // dD[i][j] = sum_c F[c][i] dy[c][j]
+  d.M = g.NN, d.N = g.NN, d.K = g.cout, d.nb1 = g.B, d.nb2 = g.A;
+  d.A = sv.F, d.a_b1 = (long long)g.cout * g.TV, d.a_b2 = g.ps_a, d.a_m = g.ps_i, d.a_k = g.TV;
+  d.B = dy, d.b_b1 = (long long)g.cout * g.TV, d.b_b2 = g.ps_a, d.b_k = g.TV, d.b_n = g.ps_i;
+  d.C = ws.dD, d.c_b1 = (long long)g.A * g.NN2, d.c_b2 = g.NN2, d.c_m = g.NN, d.c_n = 1;
+  DSTD_TRYH(gemm(d, nullptr, s));
+  // Adj = alpha * E + A:  dalpha = <dD, E>, dA = sum_{n,a} dD, dE = alpha dD
+  DSTD_TRYH(dot(ws.dD, sv.E, nadj, dalpha, ws.part, s));
+  DSTD_TRYH(reduce_rows(ws.dD, g.NN2, g.B, g.A, (long long)g.A * g.NN2, 1, g.NN2, dA, 1.f, s));
+  DSTD_TRYH(scale_by(ws.dD, alpha, nadj, s));
+  float* dE = ws.dD;
+  DSTD_TRYH(reduce_rows(dE, g.A, g.B, g.NN2, (long long)g.A * g.NN2, g.NN2, 1, gr->brm, 1.f, s));
+  Gemm wr;  // dWrm[a][k] = sum_{n,ij} dE[n][a][ij] M[n][k][ij]
+  wr.M = g.A, wr.N = 2 * g.A, wr.K = g.NN2, wr.nb1 = g.B, wr.reduce = 1;
+  wr.A = dE, wr.a_b1 = (long long)g.A * g.NN2, wr.a_m = g.NN2, wr.a_k = 1;
+  wr.B = sv.M, wr.b_b1 = 2LL * g.A * g.NN2, wr.b_k = 1, wr.b_n = g.NN2;
+  wr.C = gr->wrm, wr.c_m = 2 * g.A, wr.c_n = 1;
+  wr.beta = 1.f;
+  DSTD_TRYH(gemm(wr, ws.gs, s));
+  Gemm dm;  // dM[n][k][ij] = sum_a Wrm[a][k] dE[n][a][ij]
+  dm.M = 2 * g.A, dm.N = g.NN2, dm.K = g.A, dm.nb1 = g.B;
+  dm.A = w->wrm, dm.a_m = 1, dm.a_k = 2 * g.A;
+  dm.B = dE, dm.b_b1 = (long long)g.A * g.NN2, dm.b_k = g.NN2, dm.b_n = 1;
+  dm.C = ws.dM, dm.c_b1 = 2LL * g.A * g.NN2, dm.c_m = g.NN2, dm.c_n = 1;
+  DSTD_TRYH(gemm(dm, nullptr, s));
+  const size_t npq = (size_t)g.B * 2 * g.TV;
+  DSTD_TRYH(hipMemsetAsync(ws.dP, 0, npq * sizeof(float), s));
+  DSTD_TRYH(hipMemsetAsync(ws.dQ, 0, npq * sizeof(float), s));
+  DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.A, g.NN, ws.dP, ws.dQ, s));
+  DSTD_TRYH(conv_bwd(w->wf, x, ws.dF, dx, gr->wf, gr->bf, g.B, g.cin, g.cout, g.TV, ws.gs, s));
+  DSTD_TRYH(conv_bwd(w->wm1, x, ws.dP, dx, gr->wm1, gr->bm1, g.B, g.cin, 2, g.TV, ws.gs, s));
+  return conv_bwd(w->wm2, x, ws.dQ, dx, gr->wm2, gr->bm2, g.B, g.cin, 2, g.TV, ws.gs, s);
+}
+
+// ---------------------------------------------------------------------------
+// one DSTDGCB
+// ---------------------------------------------------------------------------
+struct BlockSaved {
+  float *as, *at;
+  OpSaved op[3];
+  float *ysp, *z, *h, *mean, *rstd;
+  float *rc, *r, *rmean, *rrstd;
+};
+void carve_block_saved(Carver& cv, BlockSaved& s, int B, int cin, int cout, int T, int V) {
+  const size_t act = (size_t)B * cout * T * V;
+  s.as = cv.take(2 * V * V);
+  s.at = cv.take(T * T);
+  for (int i = 0; i < 2; ++i) carve_op_saved(cv, s.op[i], OpGeom(DSTD_MODE_SPATIAL, B, cin, cout, T, V));
+  carve_op_saved(cv, s.op[2], OpGeom(DSTD_MODE_TEMPORAL, B, cout, cout, T, V));
+  s.ysp = cv.take(act);
+  s.z = cv.take(act);
+  s.h = cv.take(act);
+  s.mean = cv.take(cout * V);
+  s.rstd = cv.take(cout * V);
+  const bool res = cin != cout;
+  s.rc = res ? cv.take(act) : nullptr;
+  s.r = res ? cv.take(act) : nullptr;
+  s.rmean = res ? cv.take(cout * V) : nullptr;
+  s.rrstd = res ? cv.take(cout * V) : nullptr;
+}
+
+struct BlockWs {
+  OpWs op;
+  float *dh, *dysp, *dr, *drc, *dAs, *pp;
+};
+struct Chans {
+  int cin, cout;
+};
+// Sized for the largest of the given blocks.
+void carve_block_ws(Carver& cv, BlockWs& w, int B, int T, int V, std::initializer_list<Chans> bl) {
+  std::vector<OpGeom> gl;
+  int cmax = 0;
+  bool res = false;
+  for (const Chans& c : bl) {
+    gl.emplace_back(DSTD_MODE_SPATIAL, B, c.cin, c.cout, T, V);
+    gl.emplace_back(DSTD_MODE_TEMPORAL, B, c.cout, c.cout, T, V);
+    cmax = std::max(cmax, c.cout);
+    res = res || c.cin != c.cout;
+  }
+  size_t nF = 0, nD = 0, nPQ = 0, nmn = 0;
+  for (const OpGeom& g : gl) {
+    nF = std::max(nF, (size_t)g.B * g.cout * g.TV);
+    nD = std::max(nD, (size_t)g.B * g.A * g.NN2);
+    nPQ = std::max(nPQ, (size_t)g.B * 2 * g.TV);
+    nmn = std::max(nmn, (size_t)std::max(std::max(g.cout * g.cin, 2 * g.A * g.A), 2 * g.cin));
+  }
+  w.op.dF = cv.take(nF);
+  w.op.dD = cv.take(nD);
+  w.op.dM = cv.take(2 * nD);
+  w.op.dP = cv.take(nPQ);
+  w.op.dQ = cv.take(nPQ);
+  w.op.gs = cv.take(gemm_scratch_floats((int)nmn, 1));
+  w.op.part = cv.take(std::max(dot_partials(), mpjpe_partials()));
+  const size_t act = (size_t)B * cmax * T * V;
+  w.dh = cv.take(act);
+  w.dysp = cv.take(act);
+  w.dr = cv.take(act);
+  w.drc = res ? cv.take(act) : nullptr;
+  w.dAs = cv.take(V * V);
+  w.pp = cv.take(cmax);
+}
+
+hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum, float* y,
+                     const BlockSaved& S, hipStream_t s) {
+  const int cin = p->cin, cout = p->cout, TV = T * V;
+  const bool res = cin != cout;
+  // A_s*W_s + R_s, A_t + R_t (model/dstdgcn.py:146-149, 157-160)
+  DSTD_TRYH(fma3(p->A_s, p->W_s, p->R_s, S.as, (size_t)2 * V * V, s));
+  DSTD_TRYH(fma3(p->A_t, nullptr, p->R_t, S.at, (size_t)T * T, s));
+  const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
+  for (int i = 0; i < 2; ++i)  // :145-150
+    DSTD_TRYH(op_fwd(gs, x, &p->conv_s[i], S.as + i * V * V, p->alpha_sm, S.ysp, i ? 1.f : 0.f, S.op[i], s));
+  const float* r = x;
+  if (res) {  // residual Conv1x1 + BatchNorm (:117-121)
+    DSTD_TRYH(gemm(conv_fwd(p->res_w, p->res_b, x, S.rc, B, cin, cout, TV), nullptr, s));
+    BnFwd rb;
+    rb.x = S.rc;
+    rb.gamma = p->res_bn.weight;
+    rb.beta = p->res_bn.bias;
+    rb.running_mean = const_cast<float*>(p->res_bn.running_mean);
+    rb.running_var = const_cast<float*>(p->res_bn.running_var);
+    rb.momentum = momentum;
+    rb.eps = p->res_bn.eps;
+    rb.out = S.r;
+    rb.mean = S.rmean;
+    rb.rstd = S.rrstd;
+    DSTD_TRYH(bn_train_fwd(rb, B, cout, T, V, s));
+    r = S.r;
+  }
+  BnFwd bb;  // h = PReLU(BN(y) + r)  (:151-154)
+  bb.x = S.ysp;
+  bb.res = r;
+  bb.gamma = p->bn.weight;
+  bb.beta = p->bn.bias;
+  bb.running_mean = const_cast<float*>(p->bn.running_mean);
+  bb.running_var = const_cast<float*>(p->bn.running_var);
+  bb.momentum = momentum;
+  bb.eps = p->bn.eps;
+  bb.prelu = p->prelu;
+  bb.out = S.h;
+  bb.zsave = S.z;
+  bb.mean = S.mean;
+  bb.rstd = S.rstd;
+  DSTD_TRYH(bn_train_fwd(bb, B, cout, T, V, s));
+  const OpGeom gt(DSTD_MODE_TEMPORAL, B, cout, cout, T, V);  // :156-162
+  return op_fwd(gt, S.h, &p->conv_t, S.at, p->alpha_tm, y, 0.f, S.op[2], s);
+}
+
+hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, int V, const BlockSaved& S,
+                     const float* dy, float* dx, const dstd_block_grads* g, const BlockWs& W, hipStream_t s) {
+  const int cin = p->cin, cout = p->cout, TV = T * V;
+  const bool res = cin != cout;
+  const size_t act = (size_t)B * cout * TV;
+  DSTD_TRYH(hipMemsetAsync(W.dh, 0, act * sizeof(float), s));
+  const OpGeom gt(DSTD_MODE_TEMPORAL, B, cout, cout, T, V);
+  // A_t + R_t: dR_t = dA
+  DSTD_TRYH(op_bwd(gt, S.h, &p->conv_t, p->alpha_tm, S.op[2], dy, W.dh, &g->conv_t, g->R_t, g->alpha_tm, W.op, s));
+  BnBwd bb;
+  bb.x = S.ysp;
+  bb.zsave = S.z;
+  bb.prelu = p->prelu;
+  bb.dout = W.dh;
+  bb.mean = S.mean;
+  bb.rstd = S.rstd;
+  bb.gamma = p->bn.weight;
+  bb.du = W.dysp;
+  bb.dz_out = W.dr;
+  bb.dgamma = g->bn.weight;
+  bb.dbeta = g->bn.bias;
+  bb.prelu_partial = W.pp;
+  DSTD_TRYH(bn_train_bwd(bb, B, cout, T, V, s));
+  DSTD_TRYH(sum_into(W.pp, cout, g->prelu, s));
+  if (res) {
+    BnBwd rb;
+    rb.x = S.rc;
+    rb.dout = W.dr;
+    rb.mean = S.rmean;
+    rb.rstd = S.rrstd;
+    rb.gamma = p->res_bn.weight;
+    rb.du = W.drc;
+    rb.dgamma = g->res_bn.weight;
+    rb.dbeta = g->res_bn.bias;
+    DSTD_TRYH(bn_train_bwd(rb, B, cout, T, V, s));
+    DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, s));
+  } else if (dx) {
+    DSTD_TRYH(acc_mul(W.dr, nullptr, dx, act, s));
+  }
+  const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
+  for (int i = 0; i < 2; ++i) {
+    // A_s*W_s + R_s with A_s constant: dR_s = dA, dW_s = dA * A_s
+    DSTD_TRYH(hipMemsetAsync(W.dAs, 0, (size_t)V * V * sizeof(float), s));
+    DSTD_TRYH(op_bwd(gs, x, &p->conv_s[i], p->alpha_sm, S.op[i], W.dysp, dx, &g->conv_s[i], W.dAs, g->alpha_sm,
+                     W.op, s));
+    DSTD_TRYH(acc_mul(W.dAs, nullptr, g->R_s + i * V * V, (size_t)V * V, s));
+    DSTD_TRYH(acc_mul(W.dAs, p->A_s + i * V * V, g->W_s + i * V * V, (size_t)V * V, s));
+  }
+  return hipSuccess;
+}
+
+// ---------------------------------------------------------------------------
+// whole DSTDGCN
+// ---------------------------------------------------------------------------
+struct ModelSaved {
+  float *X0, *y0, *z0, *hp0, *m0, *r0, *o;
+  float* h[DSTD_MAX_LAYERS + 1];
+  float *yb[DSTD_MAX_LAYERS], *ze[DSTD_MAX_LAYERS], *me[DSTD_MAX_LAYERS], *re[DSTD_MAX_LAYERS];
+  BlockSaved st_in, st_out, enc[DSTD_MAX_LAYERS];
+};
+void carve_model_saved(Carver& cv, ModelSaved& s, int B, int T, int V, int C, int L) {
+  const size_t act = (size_t)B * C * T * V;
+  s.X0 = cv.take((size_t)B * 6 * T * V);
+  carve_block_saved(cv, s.st_in, B, 6, C, T, V);
+  s.y0 = cv.take(act);
+  s.z0 = cv.take(act);
+  s.hp0 = cv.take(act);
+  s.m0 = cv.take(C * V);
+  s.r0 = cv.take(C * V);
+  for (int i = 0; i <= L; ++i) s.h[i] = cv.take(act);
+  for (int i = 0; i < L; ++i) {
+    carve_block_saved(cv, s.enc[i], B, C, C, T, V);
+    s.yb[i] = cv.take(act);
+    s.ze[i] = cv.take(act);
+    s.me[i] = cv.take(C * V);
+    s.re[i] = cv.take(C * V);
+  }
+  carve_block_saved(cv, s.st_out, B, C, 3, T, V);
+  s.o = cv.take((size_t)B * 3 * T * V);
+}
+
+struct ModelWs {
+  BlockWs blk;
+  float *dO, *dha, *dhb, *du, *pp;
+};
+void carve_model_ws(Carver& cv, ModelWs& w, int B, int T, int V, int C) {
+  carve_block_ws(cv, w.blk, B, T, V, {{6, C}, {C, C}, {C, 3}});
+  const size_t act = (size_t)B * C * T * V;
+  w.dO = cv.take((size_t)B * 3 * T * V);
+  w.dha = cv.take(act);
+  w.dhb = cv.take(act);
+  w.du = cv.take(act);
+  w.pp = cv.take(C);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t dstd_dstdgc_train_saved_bytes(int mode, int B, int cin, int cout, int T, int V) {
+  Carver cv{nullptr};
+  OpSaved s;
+  carve_op_saved(cv, s, OpGeom(mode, B, cin, cout, T, V));
+  return cv.off + 256;
+}
+
+size_t dstd_dstdgc_train_workspace_bytes(int mode, int B, int cin, int cout, int T, int V) {
+  Carver cv{nullptr};
+  OpWs w;
+  carve_op_ws(cv, w, {OpGeom(mode, B, cin, cout, T, V)});
+  return cv.off + 256;
+}
+
+int dstd_dstdgc_train_fwd(int mode, const float* x, int B, int cin, int cout, int T, int V,
+                          const dstd_gc_weights* w, const float* A, const float* alpha, float* y, void* saved,
+                          size_t saved_bytes, void* stream) {
+  if (!x || !y || !A || !alpha || !gc_ok(w) || !saved) return DSTD_EINVAL;
+  if (mode != DSTD_MODE_SPATIAL && mode != DSTD_MODE_TEMPORAL) return DSTD_EINVAL;
+  if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
+  if (!shape_ok(B, T, V) || !ch_ok(cin) || !ch_ok(cout)) return DSTD_ELIMIT;
+  if (saved_bytes < dstd_dstdgc_train_saved_bytes(mode, B, cin, cout, T, V)) return DSTD_EWORKSPACE;
+  const OpGeom g(mode, B, cin, cout, T, V);
+  Carver cv{(char*)saved};
+  OpSaved sv;
+  carve_op_saved(cv, sv, g);
+  DSTD_TRY(op_fwd(g, x, w, A, alpha, y, 0.f, sv, (hipStream_t)stream));
+  return DSTD_OK;
+}
+
+int dstd_dstdgc_train_bwd(int mode, const float* x, int B, int cin, int cout, int T, int V,
+                          const dstd_gc_weights* w, const float* alpha, const void* saved, size_t saved_bytes,
+                          const float* dy, float* dx, const dstd_gc_grads* g, float* dA, float* dalpha,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  if (!x || !dy || !alpha || !gc_ok(w) || !gg_ok(g) || !dA || !dalpha || !saved || !workspace) return DSTD_EINVAL;
+  if (mode != DSTD_MODE_SPATIAL && mode != DSTD_MODE_TEMPORAL) return DSTD_EINVAL;
+  if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
+  if (!shape_ok(B, T, V) || !ch_ok(cin) || !ch_ok(cout)) return DSTD_ELIMIT;
+  if (saved_bytes < dstd_dstdgc_train_saved_bytes(mode, B, cin, cout, T, V)) return DSTD_EWORKSPACE;
+  if (workspace_bytes < dstd_dstdgc_train_workspace_bytes(mode, B, cin, cout, T, V)) return DSTD_EWORKSPACE;
+  const OpGeom geo(mode, B, cin, cout, T, V);
+  Carver cs{(char*)const_cast<void*>(saved)};
+  OpSaved sv;
+  carve_op_saved(cs, sv, geo);
+  Carver cw{(char*)workspace};
+  OpWs ws;
+  carve_op_ws(cw, ws, {geo});
+  DSTD_TRY(op_bwd(geo, x, w, alpha, sv, dy, dx, g, dA, dalpha, ws, (hipStream_t)stream));
+  return DSTD_OK;
+}
+
+size_t dstd_block_train_saved_bytes(int B, int cin, int cout, int T, int V) {
+  Carver cv{nullptr};
+  BlockSaved s;
+  carve_block_saved(cv, s, B, cin, cout, T, V);
+  return cv.off + 256;
+}
+
+size_t dstd_block_train_workspace_bytes(int B, int cin, int cout, int T, int V) {
+  Carver cv{nullptr};
+  BlockWs w;
+  carve_block_ws(cv, w, B, T, V, {{cin, cout}});
+  return cv.off + 256;
+}
+
+int dstd_block_train_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum, float* y,
+                         void* saved, size_t saved_bytes, void* stream) {
+  if (!block_ok(p) || !x || !y || !saved) return DSTD_EINVAL;
+  if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
+  if (!shape_ok(B, T, V)) return DSTD_ELIMIT;
+  if (saved_bytes < dstd_block_train_saved_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
+  Carver cv{(char*)saved};
+  BlockSaved S;
+  carve_block_saved(cv, S, B, p->cin, p->cout, T, V);
+  DSTD_TRY(block_fwd(p, x, B, T, V, momentum, y, S, (hipStream_t)stream));
+  return DSTD_OK;
+}
+
+int dstd_block_train_bwd(const dstd_block_params* p, const float* x, int B, int T, int V, const void* saved,
+                         size_t saved_bytes, const float* dy, float* dx, const dstd_block_grads* g,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+  if (!block_ok(p) || !block_grads_ok(p, g) || !x || !dy || !saved || !workspace) return DSTD_EINVAL;
+  if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
+  if (!shape_ok(B, T, V)) return DSTD_ELIMIT;
+  if (saved_bytes < dstd_block_train_saved_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
+  if (workspace_bytes < dstd_block_train_workspace_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
+  Carver cs{(char*)const_cast<void*>(saved)};
+  BlockSaved S;
+  carve_block_saved(cs, S, B, p->cin, p->cout, T, V);
+  Carver cw{(char*)workspace};
+  BlockWs W;
+  carve_block_ws(cw, W, B, T, V, {{p->cin, p->cout}});
+  DSTD_TRY(block_bwd(p, x, B, T, V, S, dy, dx, g, W, (hipStream_t)stream));
+  return DSTD_OK;
+}
+
+size_t dstd_model_train_saved_bytes(int B, int T, int V, int num_feature, int num_layers) {
+  Carver cv{nullptr};
+  ModelSaved s;
+  carve_model_saved(cv, s, B, T, V, num_feature, std::min(std::max(num_layers, 0), DSTD_MAX_LAYERS));
+  return cv.off + 256;
+}
+
+size_t dstd_model_train_workspace_bytes(int B, int T, int V, int num_feature, int num_layers) {
+  (void)num_layers;
+  Carver cv{nullptr};
+  ModelWs w;
+  carve_model_ws(cv, w, B, T, V, num_feature);
+  return cv.off + 256;
+}
+
+int dstd_model_train_fwd(const dstd_model_params* p, const float* x, int B, float momentum, float dropout_p,
+                         unsigned long long seed, float* y, void* saved, size_t saved_bytes, void* stream) {
+  if (!model_ok(p) || !x || !y || !saved || !(dropout_p >= 0.f && dropout_p < 1.f)) return DSTD_EINVAL;
+  const int T = p->T, V = p->V, C = p->num_feature, L = p->num_layers;
+  if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
+  if (!shape_ok(B, T, V) || !ch_ok(C)) return DSTD_ELIMIT;
+  if (p->st_in.cin != 6 || p->st_in.cout != C || p->st_out.cin != C || p->st_out.cout != 3) return DSTD_EINVAL;
+  if (saved_bytes < dstd_model_train_saved_bytes(B, T, V, C, L)) return DSTD_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  Carver cv{(char*)saved};
+  ModelSaved S;
+  carve_model_saved(cv, S, B, T, V, C, L);
+  const size_t act = (size_t)B * C * T * V;
+  DSTD_TRY(prep_nctv(x, B, T, V, 3, S.X0, s));                                   // :298-303
+  DSTD_TRY(block_fwd(&p->st_in, S.X0, B, T, V, momentum, S.y0, S.st_in, s));      // :305
+  BnFwd b0;                                                                      // :306-308
+  b0.x = S.y0;
+  b0.gamma = p->bn_in.weight;
+  b0.beta = p->bn_in.bias;
+  b0.running_mean = const_cast<float*>(p->bn_in.running_mean);
+  b0.running_var = const_cast<float*>(p->bn_in.running_var);
+  b0.momentum = momentum;
+  b0.eps = p->bn_in.eps;
+  b0.prelu = p->prelu;
+  b0.out = dropout_p > 0.f ? S.hp0 : S.h[0];
+  b0.zsave = S.z0;
+  b0.mean = S.m0;
+  b0.rstd = S.r0;
+  DSTD_TRY(bn_train_fwd(b0, B, C, T, V, s));
+  if (dropout_p > 0.f) DSTD_TRY(dropout(S.hp0, S.h[0], act, dropout_p, seed, s));  // do_in
+  for (int i = 0; i < L; ++i) {                                                  // :310-311
+    DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s));
+    BnFwd be;  // BN(block(h) + h) -> PReLU  (:278-285, Identity residual :247-248)
+    be.x = S.yb[i];
+    be.x2 = S.h[i];
+    be.gamma = p->enc_bn[i].weight;
+    be.beta = p->enc_bn[i].bias;
+    be.running_mean = const_cast<float*>(p->enc_bn[i].running_mean);
+    be.running_var = const_cast<float*>(p->enc_bn[i].running_var);
+    be.momentum = momentum;
+    be.eps = p->enc_bn[i].eps;
+    be.prelu = p->enc_prelu[i];
+    be.out = S.h[i + 1];
+    be.zsave = S.ze[i];
+    be.mean = S.me[i];
+    be.rstd = S.re[i];
+    DSTD_TRY(bn_train_fwd(be, B, C, T, V, s));
+  }
+  DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s));  // :313
+  DSTD_TRY(out_ntvc(S.o, x, B, T, V, 3, y, s));                                  // :314-315
+  return DSTD_OK;
+}
+
+int dstd_model_train_bwd(const dstd_model_params* p, const float* x, int B, float dropout_p,
+                         unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
+                         const dstd_model_grads* g, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!model_ok(p) || !g || !x || !dy || !saved || !workspace || !(dropout_p >= 0.f && dropout_p < 1.f))
+    return DSTD_EINVAL;
+  const int T = p->T, V = p->V, C = p->num_feature, L = p->num_layers;
+  if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
+  if (!shape_ok(B, T, V) || !ch_ok(C)) return DSTD_ELIMIT;
+  if (!block_grads_ok(&p->st_in, &g->st_in) || !block_grads_ok(&p->st_out, &g->st_out) || !bng_ok(g->bn_in) ||
+      !g->prelu)
+    return DSTD_EINVAL;
+  for (int i = 0; i < L; ++i)
+    if (!block_grads_ok(&p->enc[i], &g->enc[i]) || !bng_ok(g->enc_bn[i]) || !g->enc_prelu[i]) return DSTD_EINVAL;
+  if (saved_bytes < dstd_model_train_saved_bytes(B, T, V, C, L)) return DSTD_EWORKSPACE;
+  if (workspace_bytes < dstd_model_train_workspace_bytes(B, T, V, C, L)) return DSTD_EWORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  Carver cs{(char*)const_cast<void*>(saved)};
+  ModelSaved S;
+  carve_model_saved(cs, S, B, T, V, C, L);
+  Carver cw{(char*)workspace};
+  ModelWs W;
+  carve_model_ws(cw, W, B, T, V, C);
+  const size_t act = (size_t)B * C * T * V;
+  DSTD_TRY(out_ntvc_bwd(dy, B, T, V, 3, W.dO, s));
+  float* dha = W.dha;
+  float* dhb = W.dhb;
+  DSTD_TRY(hipMemsetAsync(dha, 0, act * sizeof(float), s));
+  DSTD_TRY(block_bwd(&p->st_out, S.h[L], B, T, V, S.st_out, W.dO, dha, &g->st_out, W.blk, s));
+  for (int i = L - 1; i >= 0; --i) {
+    BnBwd be;
+    be.x = S.yb[i];
+    be.x2 = S.h[i];
+    be.zsave = S.ze[i];
+    be.prelu = p->enc_prelu[i];
+    be.dout = dha;
+    be.mean = S.me[i];
+    be.rstd = S.re[i];
+    be.gamma = p->enc_bn[i].weight;
+    be.du = W.du;
+    be.dgamma = g->enc_bn[i].weight;
+    be.dbeta = g->enc_bn[i].bias;
+    be.prelu_partial = W.pp;
+    DSTD_TRY(bn_train_bwd(be, B, C, T, V, s));
+    DSTD_TRY(sum_into(W.pp, C, g->enc_prelu[i], s));
+    // u = block(h) + h: dh = du (identity path) + block backward
+    DSTD_TRY(hipMemcpyAsync(dhb, W.du, act * sizeof(float), hipMemcpyDeviceToDevice, s));
+    DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s));
+    std::swap(dha, dhb);
+  }
+  if (dropout_p > 0.f) DSTD_TRY(dropout(dha, dha, act, dropout_p, seed, s));
+  BnBwd b0;
+  b0.x = S.y0;
+  b0.zsave = S.z0;
+  b0.prelu = p->prelu;
+  b0.dout = dha;
+  b0.mean = S.m0;
+  b0.rstd = S.r0;
+  b0.gamma = p->bn_in.weight;
+  b0.du = W.du;
+  b0.dgamma = g->bn_in.weight;
+  b0.dbeta = g->bn_in.bias;
+  b0.prelu_partial = W.pp;
+  DSTD_TRY(bn_train_bwd(b0, B, C, T, V, s));
+  DSTD_TRY(sum_into(W.pp, C, g->prelu, s));
+  DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, nullptr, &g->st_in, W.blk, s));
+  return DSTD_OK;
+}
+
+size_t dstd_loss_workspace_bytes(void) { return (size_t)mpjpe_partials() * sizeof(float) + 256; }
+
+int dstd_mpjpe_fwd(const float* pred, const float* targ, size_t n_points, float* loss, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  if (!pred || !targ || !loss || !workspace || n_points == 0) return DSTD_EINVAL;
+  if (workspace_bytes < dstd_loss_workspace_bytes()) return DSTD_EWORKSPACE;
+  DSTD_TRY(mpjpe_fwd(pred, targ, n_points, loss, (float*)workspace, (hipStream_t)stream));
+  return DSTD_OK;
+}
+
+int dstd_mpjpe_bwd(const float* pred, const float* targ, size_t n_points, const float* grad_loss, float scale,
+                   float* dpred, void* stream) {
+  if (!pred || !targ || !dpred || n_points == 0) return DSTD_EINVAL;
+  DSTD_TRY(mpjpe_bwd(pred, targ, n_points, grad_loss, scale, dpred, (hipStream_t)stream));
+  return DSTD_OK;
+}
+
+int dstd_frame_mpjpe(const float* all_seqs, const float* outputs, int B, int T, int D, int t_out0,
+                     const int* used_pos, int n_used, const int* joint_src, const int* frames, int n_frames,
+                     float* sums, void* stream) {
+  if (!all_seqs || !outputs || !used_pos || !joint_src || !frames || !sums) return DSTD_EINVAL;
+  if (B <= 0 || T <= 0 || D <= 0 || D % 3 || n_used <= 0 || n_frames <= 0 || t_out0 < 0 || t_out0 >= T)
+    return DSTD_EINVAL;
+  DSTD_TRY(frame_mpjpe(all_seqs, outputs, B, T, D, t_out0, used_pos, n_used, joint_src, frames, n_frames, sums,
+                       (hipStream_t)stream));
+  return DSTD_OK;
+}
+
+}  // extern "C"

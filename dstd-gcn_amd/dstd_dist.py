@@ -13,6 +13,11 @@ forward.  The only collectives are outside it:
 * ``reduce_partials``   -- metric partial sums / counts (``all_reduce(SUM)``),
                            e.g. the per-frame MPJPE sums of the test metric
                            (``engine/prediction.py:366-404``).
+
+Training (config 5) has one real exchange per step: the data-parallel
+gradient average, ``allreduce_grads`` -- one flat bucket (~0.75 MB for the
+3DPW model), a single ring all-reduce over xGMI.  Train-mode BatchNorm keeps
+per-rank batch statistics (the DDP default).
 """
 import torch
 import torch.distributed as dist
@@ -87,3 +92,21 @@ def sharded_forward(fn, x_full, group=None, gather=True):
     rank = dist.get_rank(group)
     y = fn(shard(x_full, world, rank))
     return gather_batch(y, x_full.shape[0], group=group) if gather else y
+
+
+def allreduce_grads(params, group=None):
+    """Average ``.grad`` of ``params`` over the ranks with ONE all-reduce of a
+    flat fp32 bucket (the whole model's gradient is under 1 MB, far below any
+    useful bucket split on xGMI).  Parameters without a gradient are skipped
+    (identically on every rank: the set only depends on requires_grad)."""
+    world = dist.get_world_size(group)
+    grads = [p.grad for p in params if p.grad is not None]
+    if world == 1 or not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    flat.div_(world)
+    off = 0
+    for g in grads:
+        g.copy_(flat[off:off + g.numel()].view_as(g))
+        off += g.numel()

@@ -52,6 +52,27 @@ class Profile(ctypes.Structure):
                 ("block", ctypes.POINTER(ctypes.c_int))]
 
 
+class GCGrads(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("wf", "bf", "wm1", "bm1", "wm2", "bm2", "wrm", "brm")]
+
+
+class BNGrads(ctypes.Structure):
+    _fields_ = [("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p)]
+
+
+class BlockGrads(ctypes.Structure):
+    _fields_ = [("W_s", ctypes.c_void_p), ("R_s", ctypes.c_void_p), ("R_t", ctypes.c_void_p),
+                ("alpha_sm", ctypes.c_void_p), ("alpha_tm", ctypes.c_void_p),
+                ("conv_s", GCGrads * 2), ("conv_t", GCGrads), ("bn", BNGrads), ("prelu", ctypes.c_void_p),
+                ("res_w", ctypes.c_void_p), ("res_b", ctypes.c_void_p), ("res_bn", BNGrads)]
+
+
+class ModelGrads(ctypes.Structure):
+    _fields_ = [("st_in", BlockGrads), ("bn_in", BNGrads), ("prelu", ctypes.c_void_p),
+                ("enc", BlockGrads * MAX_LAYERS), ("enc_bn", BNGrads * MAX_LAYERS),
+                ("enc_prelu", ctypes.c_void_p * MAX_LAYERS), ("st_out", BlockGrads)]
+
+
 KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL = range(6)
 KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temporal_gc")
 
@@ -90,6 +111,37 @@ def lib():
         L.dstd_events_destroy.argtypes = [ci, ctypes.POINTER(ctypes.c_void_p)]
         L.dstd_event_elapsed_ms.restype = ci
         L.dstd_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_float)]
+        # training path (include/dstd_gcn_train.h)
+        u64, f32 = ctypes.c_ulonglong, ctypes.c_float
+        for n, k in (("dstd_dstdgc_train_saved_bytes", 6), ("dstd_dstdgc_train_workspace_bytes", 6),
+                     ("dstd_block_train_saved_bytes", 5), ("dstd_block_train_workspace_bytes", 5),
+                     ("dstd_model_train_saved_bytes", 5), ("dstd_model_train_workspace_bytes", 5)):
+            getattr(L, n).restype = sz
+            getattr(L, n).argtypes = [ci] * k
+        L.dstd_dstdgc_train_fwd.restype = ci
+        L.dstd_dstdgc_train_fwd.argtypes = [ci, vp, ci, ci, ci, ci, ci, ctypes.POINTER(GCWeights), vp, vp, vp, vp, sz,
+                                            vp]
+        L.dstd_dstdgc_train_bwd.restype = ci
+        L.dstd_dstdgc_train_bwd.argtypes = [ci, vp, ci, ci, ci, ci, ci, ctypes.POINTER(GCWeights), vp, vp, sz, vp, vp,
+                                            ctypes.POINTER(GCGrads), vp, vp, vp, sz, vp]
+        L.dstd_block_train_fwd.restype = ci
+        L.dstd_block_train_fwd.argtypes = [ctypes.POINTER(BlockParams), vp, ci, ci, ci, f32, vp, vp, sz, vp]
+        L.dstd_block_train_bwd.restype = ci
+        L.dstd_block_train_bwd.argtypes = [ctypes.POINTER(BlockParams), vp, ci, ci, ci, vp, sz, vp, vp,
+                                           ctypes.POINTER(BlockGrads), vp, sz, vp]
+        L.dstd_model_train_fwd.restype = ci
+        L.dstd_model_train_fwd.argtypes = [ctypes.POINTER(ModelParams), vp, ci, f32, f32, u64, vp, vp, sz, vp]
+        L.dstd_model_train_bwd.restype = ci
+        L.dstd_model_train_bwd.argtypes = [ctypes.POINTER(ModelParams), vp, ci, f32, u64, vp, sz, vp,
+                                           ctypes.POINTER(ModelGrads), vp, sz, vp]
+        L.dstd_loss_workspace_bytes.restype = sz
+        L.dstd_loss_workspace_bytes.argtypes = []
+        L.dstd_mpjpe_fwd.restype = ci
+        L.dstd_mpjpe_fwd.argtypes = [vp, vp, sz, vp, vp, sz, vp]
+        L.dstd_mpjpe_bwd.restype = ci
+        L.dstd_mpjpe_bwd.argtypes = [vp, vp, sz, vp, f32, vp, vp]
+        L.dstd_frame_mpjpe.restype = ci
+        L.dstd_frame_mpjpe.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, vp, vp, ci, vp, vp]
         _lib = L
     return _lib
 
@@ -97,6 +149,11 @@ def lib():
 EXPORTS = ("dstd_version", "dstd_error_string", "dstd_dstdgc_workspace_bytes", "dstd_block_workspace_bytes",
            "dstd_model_workspace_bytes", "dstd_dstdgc_fwd", "dstd_block_fwd", "dstd_model_fwd",
            "dstd_model_fwd_profiled", "dstd_events_create", "dstd_events_destroy", "dstd_event_elapsed_ms")
+TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_bytes", "dstd_dstdgc_train_fwd",
+                 "dstd_dstdgc_train_bwd", "dstd_block_train_saved_bytes", "dstd_block_train_workspace_bytes",
+                 "dstd_block_train_fwd", "dstd_block_train_bwd", "dstd_model_train_saved_bytes",
+                 "dstd_model_train_workspace_bytes", "dstd_model_train_fwd", "dstd_model_train_bwd",
+                 "dstd_loss_workspace_bytes", "dstd_mpjpe_fwd", "dstd_mpjpe_bwd", "dstd_frame_mpjpe")
 
 
 def check(code, what):
@@ -173,3 +230,60 @@ def block_struct(blk):
         p.res_w, p.res_b = ptr(conv.weight, "residual.0.weight"), ptr(conv.bias, "residual.0.bias")
         p.res_bn = bn_struct(bnw)
     return p
+
+
+# ---------------------------------------------------------------------------
+# gradient structs (training path)
+# ---------------------------------------------------------------------------
+class GradArena:
+    """One zeroed fp32 buffer with a slice per parameter (the backward kernels
+    accumulate into it); ``ptr(p)`` is p's slice, ``views()`` the gradients in
+    the order given, None for parameters that do not require grad (A_s, A_t
+    and anything frozen)."""
+
+    def __init__(self, params, device):
+        self.params = list(params)
+        self.offsets = {}
+        n = 0
+        for p in self.params:
+            if id(p) not in self.offsets:
+                self.offsets[id(p)] = n
+                n += (p.numel() + 63) // 64 * 64
+        self.buf = torch.zeros(max(n, 1), dtype=torch.float32, device=device)
+
+    def ptr(self, p):
+        return self.buf.data_ptr() + 4 * self.offsets[id(p)]
+
+    def views(self):
+        out = []
+        for p in self.params:
+            off = self.offsets[id(p)]
+            out.append(self.buf[off:off + p.numel()].view(p.shape) if p.requires_grad else None)
+        return out
+
+
+def gc_grads(dstdgc, arena):
+    g = GCGrads()
+    for f, conv in (("f", dstdgc.conv_f), ("m1", dstdgc.conv_m1), ("m2", dstdgc.conv_m2), ("rm", dstdgc.conv_rm)):
+        setattr(g, "w" + f, arena.ptr(conv.weight))
+        setattr(g, "b" + f, arena.ptr(conv.bias))
+    return g
+
+
+def bn_grads(bnw, arena):
+    return BNGrads(arena.ptr(bnw.bn.weight), arena.ptr(bnw.bn.bias))
+
+
+def block_grads(blk, arena):
+    g = BlockGrads()
+    g.W_s, g.R_s, g.R_t = arena.ptr(blk.W_s), arena.ptr(blk.R_s), arena.ptr(blk.R_t)
+    g.alpha_sm, g.alpha_tm = arena.ptr(blk.alpha_sm), arena.ptr(blk.alpha_tm)
+    g.conv_s[0] = gc_grads(blk.conv_s[0], arena)
+    g.conv_s[1] = gc_grads(blk.conv_s[1], arena)
+    g.conv_t = gc_grads(blk.conv_t[0], arena)
+    g.bn = bn_grads(blk.bn, arena)
+    g.prelu = arena.ptr(blk.prelu.weight)
+    if blk.in_channels != blk.out_channels:
+        g.res_w, g.res_b = arena.ptr(blk.residual[0].weight), arena.ptr(blk.residual[0].bias)
+        g.res_bn = bn_grads(blk.residual[1], arena)
+    return g

@@ -1,0 +1,283 @@
+"""PredictionEngine / ModelWrapper (reference engine/prediction.py).
+
+Same constructor, method names, arguments, return values and checkpoint
+format as the reference, driving the MI355X model:
+
+* ``train`` (:198-317): train-mode forward (native, batch-statistics BN),
+  mpjpe loss, the inverse-time augmentation pass, ``all_loss / 2``, native
+  backward, Adam step, StepLR at epoch end.  Losses accumulate on the GPU; the
+  epoch synchronises once when it reports its average.  Under
+  ``torch.distributed`` (one process per GPU) gradients are averaged with one
+  flat all-reduce per step (dstd_dist.allreduce_grads).
+* ``test`` (:319-430): eval forward, then the per-frame MPJPE of every batch
+  in one kernel (dstd_frame_mpjpe) accumulating on the device; one
+  synchronisation per call instead of one ``.item()`` per frame and batch.
+* ``save`` / ``recover`` (:159-182): the same ``{"lr", "err", "model",
+  "optimizer", "scheduler", "epoch"}`` dict with ``model.``-prefixed keys;
+  recover loads with ``weights_only=True``.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.optim as optim
+
+import dstd_native as native
+
+from .loss import LOSSES, AccumLoss, DeviceAccum
+from .transform import TRANSFORMS
+
+
+class ModelWrapper(nn.Module):
+    """Model + weighted losses (prediction.py:21-104); single output."""
+
+    def __init__(self, model, loss, n_out=1):
+        super(ModelWrapper, self).__init__()
+        self.model = model
+        self.n_out = n_out
+        if n_out != 1:
+            raise NotImplementedError("ModelWrapper: multi-output models (n_out > 1) are not built")
+        self.all_loss = set()
+        self.loss_funcs = {}
+        for ls in loss.keys():
+            name = loss[ls][0]
+            if name not in LOSSES:
+                raise NotImplementedError(f"loss '{name}' is not built (shipped configs use jl2 only)")
+            self.loss_funcs[ls] = (LOSSES[name], loss[ls][1])
+            if ls in self.all_loss:
+                raise ValueError("Redundant Error", ls)
+            self.all_loss.add(ls)
+
+    def forward(self, inputs, training=True):
+        outputs = self.model(inputs)
+        if training:
+            return outputs
+        return outputs[-1] if isinstance(outputs, list) else outputs
+
+    def calc_loss(self, pred, gt, loss_type="all", wgts=None):
+        if loss_type != "all" and loss_type != "sum" and loss_type not in self.all_loss:
+            raise ValueError(f"Invalid loss type {loss_type}")
+        if loss_type == "all":
+            return {ls: w * fn(pred, gt, wgts) for ls, (fn, w) in self.loss_funcs.items()}
+        if loss_type == "sum":
+            loss = 0
+            for fn, w in self.loss_funcs.values():
+                loss = loss + w * fn(pred, gt, wgts)
+            return loss
+        return self.loss_funcs[loss_type]
+
+
+def _to_dev(x, dev):
+    if isinstance(x, list):
+        return [t.float().to(dev, non_blocking=True) for t in x]
+    return x.float().to(dev, non_blocking=True)
+
+
+class PredictionEngine:
+
+    def __init__(self, config, model, logger, device=None):
+        self.model = ModelWrapper(model, config["loss"], config["n_out"])
+        self.config = config
+        self.logger = logger
+        self.device = torch.device(device) if device is not None else next(model.parameters()).device
+        self.reset()
+        if config["transform"] not in TRANSFORMS:
+            raise NotImplementedError(f"transform '{config['transform']}' is not built (shipped configs use tsc)")
+        self.transform_func, self.inverse_func = TRANSFORMS[config["transform"]]
+        logger.info("Trainable number of parameters of the network is: " +
+                    str(sum(p.numel() for p in model.parameters() if p.requires_grad)))
+        logger.info("Total number of parameters of the network is: " + str(sum(p.numel() for p in model.parameters())))
+
+    def transform(self, x):
+        if self.transform_func is None:
+            return x
+        return [self.transform_func(s) for s in x] if isinstance(x, list) else self.transform_func(x)
+
+    def inverse(self, x):
+        if self.inverse_func is None:
+            return x
+        return [self.inverse_func(s) for s in x] if isinstance(x, list) else self.inverse_func(x)
+
+    def reset(self):
+        self.lr = self.config["learn"]["lr"]
+        self.best_err = float("inf")
+        self.optimizer, self.scheduler = self._setup_learn(self.model.parameters(), self.config["learn"]["opt"])
+
+    def recover(self, checkpoint_path, model_only=False):
+        state = torch.load(checkpoint_path, map_location=self.device, weights_only=True)
+        err = state["err"]
+        epoch = state["epoch"]
+        if not model_only:
+            self.model.load_state_dict(state["model"])
+            self.optimizer.load_state_dict(state["optimizer"])
+            self.lr = state["lr"]
+        self.logger.info("load from lr {}, curr_avg {} from {}.".format(state["lr"], err, checkpoint_path))
+        return epoch, err
+
+    def save(self, checkpoint_path, err, epoch, is_best=False):
+        state = {
+            "lr": self.lr,
+            "err": err,
+            "model": self.model.state_dict(),
+            "optimizer": self.optimizer.state_dict(),
+            "scheduler": self.scheduler.state_dict(),
+            "epoch": epoch,
+        }
+        torch.save(state, checkpoint_path + "/last.pth")
+        if is_best:
+            torch.save(state, checkpoint_path + "/best.pth")
+
+    def _setup_learn(self, params, opt_type="adam"):
+        if opt_type != "adam":
+            raise NotImplementedError(f"optimizer '{opt_type}' (shipped configs use adam)")
+        optimizer = optim.Adam(params, lr=self.config["learn"]["lr"], weight_decay=self.config["learn"]["weight_decay"])
+        scheduler = optim.lr_scheduler.StepLR(optimizer, step_size=self.config["learn"]["step_size"],
+                                              gamma=self.config["learn"]["gamma"])
+        return optimizer, scheduler
+
+    # ------------------------------------------------------------------
+    def train(self, train_loader, epoch, time_tsfm=None, scale_tsfm=None, weights=None, max_iter=-1):
+        dev = self.device
+        t_l = {key_loss: DeviceAccum(dev) for key_loss in self.config["loss"]}
+        self.model.train()
+        distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        num_iter = len(train_loader) if max_iter == -1 else min(len(train_loader), max_iter)
+        for i, (inputs, inputs_inv, targets, all_seqs) in enumerate(train_loader):
+            inputs, inputs_inv, targets = _to_dev(inputs, dev), _to_dev(inputs_inv, dev), _to_dev(targets, dev)
+            N = inputs[0].shape[0] if isinstance(inputs, list) else inputs.shape[0]
+            if time_tsfm is not None:
+                inputs = time_tsfm.transform(inputs)
+            inputs = self.transform(inputs)
+            outputs = self.inverse(self.model(inputs, False))
+            if scale_tsfm is not None:
+                outputs = scale_tsfm.inverse(outputs)
+            if time_tsfm is not None:
+                outputs = time_tsfm.inverse(outputs)
+            t = outputs.shape[1]
+            targets_l = targets[:, -t:] if t != targets.shape[1] else targets
+            loss = self.model.calc_loss(outputs, targets_l, "all", weights)
+            all_loss = 0
+            for ls in loss:
+                all_loss = all_loss + loss[ls]
+                t_l[ls].update(loss[ls] * N, N)
+            if self.config["inverse"]:  # time-reversed augmentation pass (:267-287)
+                if time_tsfm is not None:
+                    inputs_inv = time_tsfm.transform(inputs_inv)
+                inputs_inv = self.transform(inputs_inv)
+                outputs_inv = self.inverse(self.model(inputs_inv, True))
+                targets_inv = targets.flip(1)
+                t = outputs_inv.shape[1]
+                targets_il = targets_inv[:, -t:] if t != targets_inv.shape[1] else targets_inv
+                if time_tsfm is not None:
+                    outputs_inv = time_tsfm.inverse(outputs_inv)
+                if scale_tsfm is not None:
+                    outputs_inv = scale_tsfm.inverse(outputs_inv)
+                loss_inv = self.model.calc_loss(outputs_inv, targets_il, "all", weights)
+                for ls in loss_inv:
+                    all_loss = all_loss + loss_inv[ls]
+                all_loss = all_loss / 2
+            self.optimizer.zero_grad()
+            all_loss.backward()
+            if distributed:
+                from dstd_dist import allreduce_grads
+                allreduce_grads(self.model.parameters())
+            if self.config.get("clip", -1) > 0:
+                nn.utils.clip_grad_norm_(self.model.model.parameters(), max_norm=self.config["clip"])
+            self.optimizer.step()
+            if i >= num_iter - 1:
+                break
+        desc = f"epoch: {epoch + 1}|train|" + "".join("{}:{:.2f}|".format(ls, t_l[ls].avg) for ls in t_l)
+        self.logger.info(desc)
+        self.scheduler.step()
+        self.lr = self.scheduler.get_last_lr()[0]
+        return sum(t_l[ls].avg for ls in t_l)
+
+    # ------------------------------------------------------------------
+    def test(self, test_loader, input_n=10, eval_frame=None, dim_used=None, joint_to_ignore=None, joint_equal=None,
+             time_tsfm=None, scale_tsfm=None, action=None, save_path=None):
+        assert eval_frame is not None
+        dev = self.device
+        L = native.lib()
+        sums = torch.zeros(len(eval_frame), dtype=torch.float32, device=dev)
+        N = 0
+        save_results = dict() if save_path is not None else None
+        index_cache = {}
+        self.model.eval()
+        with torch.no_grad():
+            for i, (inputs, _, _, all_seqs) in enumerate(test_loader):
+                inputs = _to_dev(inputs, dev)
+                all_seqs = all_seqs.float().to(dev, non_blocking=True).contiguous()
+                outputs = self.inverse(self.model(self.transform(inputs), False))
+                if isinstance(outputs, list):
+                    outputs = outputs[0]
+                    n, t = outputs.shape[:2]
+                    outputs = outputs.view(n, t, -1)
+                if scale_tsfm is not None:
+                    outputs = scale_tsfm.inverse(outputs)
+                if time_tsfm is not None:
+                    outputs = time_tsfm.inverse(outputs)
+                outputs = outputs.contiguous()
+                n, seq_len, D = all_seqs.shape
+                t_out0 = input_n if outputs.shape[1] != seq_len else 0
+                key = (D, seq_len, t_out0)
+                if key not in index_cache:
+                    index_cache[key] = self._metric_indices(D, outputs.shape[2], seq_len, input_n, eval_frame,
+                                                            dim_used, joint_to_ignore, joint_equal)
+                used_pos, joint_src, frames = index_cache[key]
+                code = L.dstd_frame_mpjpe(native.ptr(all_seqs, "all_seqs"), native.ptr(outputs, "outputs"), n,
+                                          seq_len, D, t_out0, used_pos.data_ptr(), outputs.shape[2],
+                                          joint_src.data_ptr(), frames.data_ptr(), len(eval_frame), sums.data_ptr(),
+                                          native.stream_handle(dev))
+                native.check(code, "dstd_frame_mpjpe")
+                N += n
+                if save_results is not None:
+                    pred = self._fill_pred(all_seqs, outputs, used_pos, joint_src, t_out0)[:, input_n:]
+                    targ = all_seqs.view(n, seq_len, -1, 3)[:, input_n:]
+                    for k, v in (("result", pred), ("target", targ)):
+                        a = v.cpu().numpy()
+                        save_results[k] = a if k not in save_results else np.concatenate((save_results[k], a), 0)
+            if action is None:
+                action = "NA"
+            t_metric = sums.double().cpu().numpy() / N  # the one synchronisation
+            self.logger.info(f"action: {action}|test|loss:{t_metric.mean():.2f}")
+            if save_results is not None:
+                np.savez(save_path + ".npz", target=save_results["target"], result=save_results["result"])
+        # t_l.avg of the reference = sum over (batch, frame) of metric_k / (N * frames)
+        return float(t_metric.mean()), t_metric
+
+    def _metric_indices(self, D, n_out_dims, seq_len, input_n, eval_frame, dim_used, joint_to_ignore, joint_equal):
+        """Device index tables of the metric: used_pos[d] (position of dim d in
+        the outputs or -1, :371-381), joint_src[j] (the ignore <- equal copy,
+        :382-389) and the absolute eval frames (input_n + eval_frame[k])."""
+        used_pos = np.full(D, -1, dtype=np.int32)
+        if dim_used is None or np.any(np.asarray(dim_used, dtype=object) == None):  # noqa: E711
+            used_pos[:] = np.arange(D)
+        else:
+            used_pos[np.asarray(dim_used, dtype=np.int64)] = np.arange(len(dim_used))
+        if used_pos.max() + 1 != n_out_dims:
+            raise ValueError(f"test: outputs have {n_out_dims} dims, dim_used selects {used_pos.max() + 1}")
+        joint_src = np.arange(D // 3, dtype=np.int32)
+        if joint_to_ignore is not None and not np.any(np.asarray(joint_to_ignore, dtype=object) == None):  # noqa
+            assert joint_to_ignore.shape == joint_equal.shape
+            joint_src[np.asarray(joint_to_ignore)] = np.asarray(joint_equal)
+        frames = np.asarray([input_n + f for f in eval_frame], dtype=np.int32)
+        if frames.max() >= seq_len:
+            raise ValueError(f"eval frame {frames.max()} outside the {seq_len}-frame sequence")
+        dev = self.device
+        return (torch.from_numpy(used_pos).to(dev), torch.from_numpy(joint_src).to(dev),
+                torch.from_numpy(frames).to(dev))
+
+    @staticmethod
+    def _fill_pred(all_seqs, outputs, used_pos, joint_src, t_out0):
+        """pred_3d of :369-389 as a tensor (only for save_path)."""
+        n, T, D = all_seqs.shape
+        pred = all_seqs.clone()
+        up = used_pos.long()
+        sel = torch.nonzero(up >= 0).squeeze(1)
+        pred[:, t_out0:, sel] = outputs[:, :, up[sel]]
+        J = D // 3
+        src = (joint_src.long()[:, None] * 3 + torch.arange(3, device=pred.device)[None]).reshape(-1)
+        return pred[:, :, src].view(n, T, J, 3)
+
+
+__all__ = ["ModelWrapper", "PredictionEngine", "AccumLoss"]

@@ -11,11 +11,21 @@ include/dstd_gcn.h:
   DSTDGCB.forward  -> dstd_block_fwd    (reference :141-163)
   DSTDGCN.forward  -> dstd_model_fwd    (reference :293-317)
 
-There is no CPU / eager fallback: a tensor off the GPU, a missing library or a
-train-mode call raises.  Train mode (batch-statistics BatchNorm and the
-backward pass) is not built yet and raises
-NotImplementedError; outputs carry a grad_fn whose backward raises, so a
-silent zero gradient is impossible.
+Training runs through include/dstd_gcn_train.h:
+
+  DSTDGC  with autograd       -> dstd_dstdgc_train_fwd / _bwd
+  DSTDGCB in train mode       -> dstd_block_train_fwd / _bwd (batch-stat BN)
+  DSTDGCN in train mode       -> dstd_model_train_fwd / _bwd
+
+each wrapped in a torch.autograd.Function whose backward is the native
+backward, with the reference's gradient semantics (A_s / A_t constant, R_s
+aliasing A_s's storage, alpha_sm shared by both spatial convs).
+
+There is no CPU / eager fallback: a tensor off the GPU or a missing library
+raises.  An eval-mode DSTDGCB / DSTDGCN output that needs a gradient carries a
+grad_fn whose backward raises (the reference would back-propagate through
+running-statistics BN there; no shipped recipe does), so a silent wrong
+gradient is impossible.
 """
 import math
 
@@ -51,7 +61,8 @@ def weights_init(m):
 
 
 class _ForwardOnly(torch.autograd.Function):
-    """Marks native outputs: forward is identity, backward refuses loudly."""
+    """Marks eval-mode block / model outputs: forward is identity, backward
+    refuses loudly (train-mode modules carry the native backward instead)."""
 
     @staticmethod
     def forward(ctx, y, *deps):
@@ -59,8 +70,8 @@ class _ForwardOnly(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
-        raise NotImplementedError("DSTD native backward kernels are not built yet (SURVEY §8(f) row 1); "
-                                  "gradients through the MI355X forward are unavailable")
+        raise NotImplementedError("backward through an eval-mode DSTDGCB / DSTDGCN (running-statistics BN) is not "
+                                  "built; call .train() for the native training path")
 
 
 def _mark(y, *deps):
@@ -71,10 +82,157 @@ def _mark(y, *deps):
     return y
 
 
-def _no_train(module):
-    if module.training:
-        raise NotImplementedError(f"{type(module).__name__}: train-mode forward (batch-statistics BatchNorm + "
-                                  "backward) is not built yet (SURVEY §8(f) row 1); call .eval()")
+def _needs_grad(*ts):
+    return torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in ts)
+
+
+def _bn_modules(module):
+    return [m for m in module.modules() if isinstance(m, nn.BatchNorm1d)]
+
+
+def _bn_momentum(module):
+    moms = {m.momentum for m in _bn_modules(module)}
+    if len(moms) != 1 or None in moms:
+        raise NotImplementedError(f"native train-mode BN needs one fixed momentum for every BatchNorm, got {moms}")
+    return float(moms.pop())
+
+
+def _count_batch(module):
+    """nn.BatchNorm1d bumps num_batches_tracked once per train forward."""
+    t = [m.num_batches_tracked for m in _bn_modules(module) if m.num_batches_tracked is not None]
+    if t:
+        torch._foreach_add_(t, 1)
+
+
+class _OpTrain(torch.autograd.Function):
+    """DSTDGC forward + native backward (reference :80-94 under autograd)."""
+
+    @staticmethod
+    def forward(ctx, mod, mode, x, A, alpha, *params):
+        L = native.lib()
+        B, cin, T, V = x.shape
+        dev = x.device
+        cout = mod.out_channels
+        y = torch.empty(B, cout, T, V, dtype=torch.float32, device=dev)
+        nbytes = L.dstd_dstdgc_train_saved_bytes(mode, B, cin, cout, T, V)
+        saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        w = native.gc_weights(mod)
+        code = L.dstd_dstdgc_train_fwd(mode, native.ptr(x, "x"), B, cin, cout, T, V, w, native.ptr(A, "A"),
+                                       native.ptr(alpha, "alpha_m"), native.ptr(y, "y"), saved.data_ptr(), nbytes,
+                                       native.stream_handle(dev))
+        native.check(code, "dstd_dstdgc_train_fwd")
+        ctx.mod, ctx.mode, ctx.saved_buf = mod, mode, saved
+        ctx.save_for_backward(x, A, alpha)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = native.lib()
+        x, A, alpha = ctx.saved_tensors
+        mod, mode = ctx.mod, ctx.mode
+        B, cin, T, V = x.shape
+        dev = x.device
+        cout = mod.out_channels
+        dy = dy.contiguous()
+        params = list(mod.parameters())
+        arena = native.GradArena(params, dev)
+        dx = torch.zeros_like(x) if ctx.needs_input_grad[2] else None
+        dA = torch.zeros_like(A)
+        dalpha = torch.zeros_like(alpha)
+        nbytes = L.dstd_dstdgc_train_workspace_bytes(mode, B, cin, cout, T, V)
+        ws = native.workspace(dev, nbytes)
+        code = L.dstd_dstdgc_train_bwd(mode, native.ptr(x, "x"), B, cin, cout, T, V, native.gc_weights(mod),
+                                       native.ptr(alpha, "alpha_m"), ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(),
+                                       native.ptr(dy, "dy"), dx.data_ptr() if dx is not None else None,
+                                       native.gc_grads(mod, arena), native.ptr(dA, "dA"),
+                                       native.ptr(dalpha, "dalpha"), ws.data_ptr(), ws.numel(),
+                                       native.stream_handle(dev))
+        native.check(code, "dstd_dstdgc_train_bwd")
+        ctx.saved_buf = None
+        return (None, None, dx, dA, dalpha, *arena.views())
+
+
+class _BlockTrain(torch.autograd.Function):
+    """Train-mode DSTDGCB forward + native backward (reference :141-163)."""
+
+    @staticmethod
+    def forward(ctx, blk, x, *params):
+        L = native.lib()
+        B, cin, T, V = x.shape
+        dev = x.device
+        y = torch.empty(B, blk.out_channels, T, V, dtype=torch.float32, device=dev)
+        nbytes = L.dstd_block_train_saved_bytes(B, cin, blk.out_channels, T, V)
+        saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        p = native.block_struct(blk)
+        code = L.dstd_block_train_fwd(p, native.ptr(x, "x"), B, T, V, _bn_momentum(blk), native.ptr(y, "y"),
+                                      saved.data_ptr(), nbytes, native.stream_handle(dev))
+        native.check(code, "dstd_block_train_fwd")
+        _count_batch(blk)
+        ctx.blk, ctx.saved_buf = blk, saved
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = native.lib()
+        (x,) = ctx.saved_tensors
+        blk = ctx.blk
+        B, cin, T, V = x.shape
+        dev = x.device
+        dy = dy.contiguous()
+        arena = native.GradArena(list(blk.parameters()), dev)
+        dx = torch.zeros_like(x) if ctx.needs_input_grad[1] else None
+        nbytes = L.dstd_block_train_workspace_bytes(B, cin, blk.out_channels, T, V)
+        ws = native.workspace(dev, nbytes)
+        code = L.dstd_block_train_bwd(native.block_struct(blk), native.ptr(x, "x"), B, T, V,
+                                      ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(), native.ptr(dy, "dy"),
+                                      dx.data_ptr() if dx is not None else None, native.block_grads(blk, arena),
+                                      ws.data_ptr(), ws.numel(), native.stream_handle(dev))
+        native.check(code, "dstd_block_train_bwd")
+        ctx.saved_buf = None
+        return (None, dx, *arena.views())
+
+
+class _ModelTrain(torch.autograd.Function):
+    """Train-mode DSTDGCN forward + native backward (reference :293-317)."""
+
+    @staticmethod
+    def forward(ctx, model, x, *params):
+        L = native.lib()
+        n, t, v, c = x.shape
+        dev = x.device
+        p = model._native_params()
+        y = torch.empty_like(x)
+        nbytes = L.dstd_model_train_saved_bytes(n, t, v, model.num_feature, model.num_layers)
+        saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        drop = float(model.do_in.p)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop > 0 else 0
+        code = L.dstd_model_train_fwd(p, native.ptr(x, "x"), n, _bn_momentum(model), drop, seed,
+                                      native.ptr(y, "y"), saved.data_ptr(), nbytes, native.stream_handle(dev))
+        native.check(code, "dstd_model_train_fwd")
+        _count_batch(model)
+        ctx.model, ctx.saved_buf, ctx.drop, ctx.seed = model, saved, drop, seed
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = native.lib()
+        (x,) = ctx.saved_tensors
+        model = ctx.model
+        n, t, v, c = x.shape
+        dev = x.device
+        dy = dy.contiguous()
+        arena = native.GradArena(list(model.parameters()), dev)
+        g = model._native_grads(arena)
+        nbytes = L.dstd_model_train_workspace_bytes(n, t, v, model.num_feature, model.num_layers)
+        ws = native.workspace(dev, nbytes)
+        code = L.dstd_model_train_bwd(model._native_params(), native.ptr(x, "x"), n, ctx.drop, ctx.seed,
+                                      ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(), native.ptr(dy, "dy"), g,
+                                      ws.data_ptr(), ws.numel(), native.stream_handle(dev))
+        native.check(code, "dstd_model_train_bwd")
+        ctx.saved_buf = None
+        return (None, None, *arena.views())
 
 
 class BatchNorm(nn.Module):
@@ -135,6 +293,9 @@ class DSTDGC(nn.Module):
             alpha_m = torch.full((1,), float(alpha_m), dtype=torch.float32, device=dev)
         alpha = alpha_m.reshape(1).contiguous()
         mode = native.MODE_SPATIAL if self.mode == "spatial" else native.MODE_TEMPORAL
+        params = list(self.parameters())
+        if _needs_grad(x, A, alpha, *params):
+            return _OpTrain.apply(self, mode, x, A, alpha, *params)
         y = torch.empty(B, self.out_channels, T, V, dtype=torch.float32, device=dev)
         nbytes = L.dstd_dstdgc_workspace_bytes(mode, B, cin, self.out_channels, T, V)
         ws = native.workspace(dev, nbytes)
@@ -143,7 +304,7 @@ class DSTDGC(nn.Module):
                                  native.ptr(A, "A"), native.ptr(alpha, "alpha_m"), native.ptr(y, "y"),
                                  ws.data_ptr(), ws.numel(), native.stream_handle(dev))
         native.check(code, "dstd_dstdgc_fwd")
-        return _mark(y, x, A, alpha, *self.parameters())
+        return y
 
 
 class DSTDGCB(nn.Module):
@@ -186,11 +347,12 @@ class DSTDGCB(nn.Module):
         self.R_s.data.uniform_(-stdt, stdt)
 
     def forward(self, x):
-        _no_train(self)
         L = native.lib()
         B, cin, T, V = x.shape
         x = x.contiguous()
         native.require_device(x, "x")
+        if self.training:
+            return _BlockTrain.apply(self, x, *self.parameters())
         dev = x.device
         y = torch.empty(B, self.out_channels, T, V, dtype=torch.float32, device=dev)
         nbytes = L.dstd_block_workspace_bytes(B, cin, self.out_channels, T, V)
@@ -290,16 +452,29 @@ class DSTDGCN(nn.Module):
         self._native = (ptrs, p)
         return p
 
+    def _native_grads(self, arena):
+        g = native.ModelGrads()
+        g.st_in = native.block_grads(self.conv_st_in.stgcn[0][0], arena)
+        g.bn_in = native.bn_grads(self.bn_in, arena)
+        g.prelu = arena.ptr(self.prelu.weight)
+        for i, enc in enumerate(self.encoders):
+            g.enc[i] = native.block_grads(enc[0].stgcn[0][0], arena)
+            g.enc_bn[i] = native.bn_grads(enc[1], arena)
+            g.enc_prelu[i] = arena.ptr(enc[2].weight)
+        g.st_out = native.block_grads(self.conv_st_out.stgcn[0][0], arena)
+        return g
+
     def forward(self, x):
         n, t, v, c = x.shape
         assert t == self.input_time_frame + self.output_time_frame
-        _no_train(self)
         if c != self.input_channels // 2 or v != self.joints_to_consider:
             raise ValueError(f"DSTDGCN: expected [N, {t}, {self.joints_to_consider}, {self.input_channels // 2}], "
                              f"got {list(x.shape)}")
         L = native.lib()
         x = x.contiguous()
         native.require_device(x, "x")
+        if self.training:
+            return _ModelTrain.apply(self, x, *self.parameters())
         dev = x.device
         p = self._native_params()
         y = torch.empty_like(x)

@@ -17,6 +17,11 @@ import torch
 
 BN_EPS = 1e-5  # nn.BatchNorm1d default, model/dstdgcn.py:42
 
+# When a list, every train-mode batchnorm() call appends (batch mean, unbiased
+# batch variance) in call order -- what nn.BatchNorm1d folds into its running
+# statistics (tests compare the native running-stat updates against it).
+BN_RECORD = None
+
 
 def _t(a, dtype):
     if torch.is_tensor(a):
@@ -68,6 +73,8 @@ def batchnorm(x, p, training=False, eps=BN_EPS):
     if training:
         mean = xc.mean(dim=(0, 2))
         var = xc.var(dim=(0, 2), unbiased=False)
+        if BN_RECORD is not None:
+            BN_RECORD.append((mean.detach().clone(), xc.var(dim=(0, 2), unbiased=True).detach().clone()))
     else:
         mean, var = p["running_mean"], p["running_var"]
     y = (xc - mean.view(1, -1, 1)) / torch.sqrt(var.view(1, -1, 1) + eps)
@@ -110,7 +117,11 @@ def dstdgcn(x, sd, num_layers, dtype=torch.float64, training=False):
 
     x: [N, T, V, 3]; sd: reference state dict (numpy or tensors)."""
     sd = {k: _t(v, dtype) for k, v in sd.items() if not k.endswith("num_batches_tracked")}
-    x = _t(x, dtype)
+    return dstdgcn_fn(_t(x, dtype), sd, num_layers, training)
+
+
+def dstdgcn_fn(x, sd, num_layers, training=False):
+    """dstdgcn() on tensors used as given (autograd flows through them)."""
     residual = x[:, -1:]                                              # :299
     h = torch.cat((x, x - residual), dim=-1).permute(0, 3, 1, 2)      # :298-303
     h = dstdgcb(h, sub(sd, "conv_st_in.stgcn.0.0."), training)        # :305 (residual=None)
@@ -139,3 +150,74 @@ def mpjpe_error_3d(outputs, targets):
     n, t, vc = outputs.shape
     d = (outputs.reshape(-1, 3) - targets.reshape(-1, 3)).norm(dim=1)
     return d.mean()
+
+
+# ---------------------------------------------------------------------------
+# engine restatements (engine/prediction.py, engine/utils/loss.py)
+# ---------------------------------------------------------------------------
+def test_metric(all_seqs, outputs, input_n, eval_frame, dim_used, joint_to_ignore, joint_equal):
+    """PredictionEngine.test per-frame MPJPE for one batch (prediction.py:366-404),
+    numpy.  Returns (metric_k * n for each k) as the reference accumulates it."""
+    import numpy as np
+    all_seqs = np.asarray(all_seqs, dtype=np.float64)
+    outputs = np.asarray(outputs, dtype=np.float64)
+    n, seq_len, D = all_seqs.shape
+    pred = all_seqs.copy()
+    if outputs.shape[1] != seq_len:                                   # :371-381
+        pred[:, input_n:, dim_used] = outputs
+    else:
+        pred[:, :, dim_used] = outputs
+    ign = np.concatenate((joint_to_ignore * 3, joint_to_ignore * 3 + 1, joint_to_ignore * 3 + 2))
+    eq = np.concatenate((joint_equal * 3, joint_equal * 3 + 1, joint_equal * 3 + 2))
+    pred[:, :, ign] = pred[:, :, eq]                                  # :382-389
+    p = pred.reshape(n, seq_len, -1, 3)[:, input_n:]
+    t = all_seqs.reshape(n, seq_len, -1, 3)[:, input_n:]
+    return np.array([np.linalg.norm(t[:, j] - p[:, j], axis=-1).mean() * n for j in eval_frame])
+
+
+def train_params(sd0, dtype=torch.float64):
+    """Leaf tensors for training: every state-dict parameter except A_s / A_t
+    requires grad; BN running statistics are dropped (train-mode BN never
+    reads them)."""
+    P = {k: _t(v, dtype).clone() for k, v in sd0.items()
+         if not k.endswith(("num_batches_tracked", "running_mean", "running_var"))}
+    for k in P:
+        if not k.endswith((".A_s", ".A_t")):
+            P[k].requires_grad_(True)
+    return P
+
+
+def step_loss(P, batch, num_layers, inverse=True):
+    """Losses of one PredictionEngine.train step (prediction.py:231-287):
+    returns (loss, all_loss) with all_loss = (loss + loss_inv) / 2 when
+    ``inverse``.  A_s re-reads R_s's values (the storage alias, :107-109)."""
+    dtype = next(iter(P.values())).dtype
+    inp, inv, seq = (_t(a, dtype) for a in batch)
+    B, T, VC = inp.shape
+    for k in list(P):
+        if k.endswith(".A_s"):
+            P[k] = P[k[:-3] + "R_s"].detach()
+    out = dstdgcn_fn(inp.view(B, T, VC // 3, 3), P, num_layers, training=True).reshape(B, T, VC)
+    loss = mpjpe_error_3d(out, seq)
+    if not inverse:
+        return loss, loss
+    out_i = dstdgcn_fn(inv.view(B, T, VC // 3, 3), P, num_layers, training=True).reshape(B, T, VC)
+    return loss, (loss + mpjpe_error_3d(out_i, seq.flip(1))) / 2
+
+
+def train_curve(sd0, batches, steps, num_layers, lr=3e-3, weight_decay=0.0, inverse=True, dtype=torch.float64):
+    """PredictionEngine.train for ``steps`` one-batch epochs (prediction.py:198-317):
+    train-mode forward, mpjpe loss, the time-reversed pass, all_loss / 2,
+    Adam(lr, weight_decay).  ``batches``: list of (inputs, inputs_inv,
+    targets) as [B, T, V*3] arrays.  Returns the per-step loss of the forward
+    pass (the t_l average the engine reports)."""
+    P = train_params(sd0, dtype)
+    opt = torch.optim.Adam([v for v in P.values() if v.requires_grad], lr=lr, weight_decay=weight_decay)
+    losses = []
+    for step in range(steps):
+        loss, all_loss = step_loss(P, batches[step % len(batches)], num_layers, inverse)
+        opt.zero_grad()
+        all_loss.backward()
+        opt.step()
+        losses.append(float(loss.detach()))
+    return losses

@@ -14,8 +14,8 @@ H36M = dict(input_channels=6, input_time_frame=10, output_time_frame=25, st_gcnn
             joints_to_consider=22, num_feature=64, num_layers=5, layout="h36m")
 
 
-def header_symbols():
-    src = open(os.path.join(ROOT, "include", "dstd_gcn.h")).read()
+def header_symbols(name="dstd_gcn.h"):
+    src = open(os.path.join(ROOT, "include", name)).read()
     return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\*?\s+\*?(dstd_\w+)\s*\(", src, re.M)))
 
 
@@ -26,6 +26,38 @@ def test_library_exports_every_header_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(native.EXPORTS)
+
+
+def test_library_exports_every_training_header_symbol():
+    L = native.lib()
+    syms = header_symbols("dstd_gcn_train.h")
+    assert len(syms) == 16, syms
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(native.TRAIN_EXPORTS)
+
+
+def test_train_sizes_and_argument_checks_without_gpu():
+    L = native.lib()
+    # saved activations grow linearly with the batch
+    a = L.dstd_model_train_saved_bytes(8, 40, 23, 64, 5)
+    b = L.dstd_model_train_saved_bytes(16, 40, 23, 64, 5)
+    assert 0 < a < b and abs((b - a) - (a - L.dstd_model_train_saved_bytes(0, 40, 23, 64, 5))) < 1 << 20
+    assert L.dstd_model_train_workspace_bytes(8, 40, 23, 64, 5) > 0
+    assert L.dstd_block_train_saved_bytes(4, 6, 64, 35, 22) > L.dstd_block_train_saved_bytes(4, 64, 64, 35, 22) // 2
+    assert L.dstd_dstdgc_train_saved_bytes(1, 4, 64, 64, 35, 22) > 0
+    assert L.dstd_loss_workspace_bytes() > 0
+    # null pointers / bad shapes are rejected before any device work
+    w = native.GCWeights()
+    g = native.GCGrads()
+    assert L.dstd_dstdgc_train_fwd(0, None, 4, 64, 64, 35, 22, w, None, None, None, None, 0, None) == -1
+    assert L.dstd_dstdgc_train_bwd(0, None, 4, 64, 64, 35, 22, w, None, None, 0, None, None, g, None, None, None, 0,
+                                   None) == -1
+    assert L.dstd_block_train_fwd(None, None, 4, 35, 22, 0.1, None, None, 0, None) == -1
+    assert L.dstd_model_train_fwd(None, None, 4, 0.1, 0.0, 0, None, None, 0, None) == -1
+    assert L.dstd_model_train_bwd(None, None, 4, 0.0, 0, None, 0, None, None, None, 0, None) == -1
+    assert L.dstd_mpjpe_fwd(None, None, 10, None, None, 0, None) == -1
+    assert L.dstd_frame_mpjpe(None, None, 1, 35, 96, 0, None, 66, None, None, 6, None, None) == -1
 
 
 def test_version_and_errors():
@@ -92,7 +124,10 @@ def test_cpu_forward_fails_loudly():
         op(torch.zeros(1, 64, 35, 22), torch.zeros(1, 22, 22), 1.0)
 
 
-def test_train_mode_not_built_yet():
-    m = get_model("dstdgcn", dstdgcn=H36M)
-    with pytest.raises(NotImplementedError):
+def test_train_mode_on_cpu_fails_loudly():
+    m = get_model("dstdgcn", dstdgcn=H36M).train()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
         m(torch.zeros(2, 35, 22, 3))
+    blk = DSTDGCB(64, 64, 35, 22, "h36m").train()
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        blk(torch.zeros(2, 64, 35, 22))

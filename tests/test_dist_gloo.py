@@ -145,3 +145,27 @@ def test_sharded_forward_equals_full_batch():
         y, y64 = res[r]
         # fp64 oracle on a shard vs the reference's fp64 output on the batch
         assert torch.allclose(y, y64.to(y.dtype), rtol=0, atol=1e-5 * float(y64.abs().max()))
+
+
+def _allreduce_grads_body(rank, world):
+    torch.manual_seed(7)  # same module on every rank
+    lin = torch.nn.Linear(4, 3)
+    frozen = torch.nn.Parameter(torch.ones(2), requires_grad=False)
+    x = torch.full((5, 4), float(rank + 1))
+    lin(x).sum().backward()
+    local = [p.grad.clone() for p in lin.parameters()]
+    D.allreduce_grads(list(lin.parameters()) + [frozen])
+    return local, [p.grad.clone() for p in lin.parameters()], frozen.grad is None
+
+
+def test_allreduce_grads_averages_one_bucket():
+    """Data-parallel training exchange: every rank ends with the
+    mean of the per-rank gradients; parameters without a gradient are skipped."""
+    res = run_world("_allreduce_grads_body")
+    mean = [(a + b) / 2 for a, b in zip(res[0][0], res[1][0])]
+    for r in (0, 1):
+        local, avg, frozen_none = res[r]
+        assert frozen_none
+        for m, a in zip(mean, avg):
+            assert torch.allclose(m, a)
+    assert not torch.allclose(res[0][0][0], res[1][0][0])
