@@ -55,8 +55,10 @@ hipError_t adj_combine(const float* E, const float* Acomb, const float* alpha, i
 hipError_t scale_by(float* x, const float* alpha, size_t n, hipStream_t s);
 
 // out[m] += scale * sum_{b < nb} sum_{j < nj} X[b*sb + m*sm + j*sj], m < M.
+// scratch >= reduce_scratch_floats(M).
+size_t reduce_scratch_floats(int M);
 hipError_t reduce_rows(const float* X, int M, int nb, int nj, long long sb, long long sm, long long sj, float* out,
-                       float scale, hipStream_t s);
+                       float scale, float* scratch, hipStream_t s);
 
 // out[0] += sum_i x[i] * y[i]   (two-stage, deterministic; partials >= dot_partials())
 int dot_partials();
@@ -90,12 +92,12 @@ struct BnFwd {
   float* mean;
   float* rstd;
 };
-hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, hipStream_t s);
+hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s);
 
 // Backward of BnFwd.  dout is d(out); with prelu set it is first mapped
 // through PReLU' using zsave.  Writes du = d(u) (=), dz_out = dz (= , when
-// non-null: the residual branch's gradient), accumulates dgamma, dbeta and
-// the PReLU slope partial of channel c into prelu_partial[c] (=).
+// non-null: the residual branch's gradient), accumulates dgamma, dbeta and,
+// with prelu set, the slope gradient into *dprelu.
 struct BnBwd {
   const float* x;
   const float* x2 = nullptr;
@@ -109,9 +111,10 @@ struct BnBwd {
   float* dz_out = nullptr;
   float* dgamma;
   float* dbeta;
-  float* prelu_partial = nullptr;  // [C]
 };
-hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, hipStream_t s);
+// scratch (both directions) >= bn_scratch_floats(B, C, T, V)
+size_t bn_scratch_floats(int B, int C, int T, int V);
+hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scratch, float* dprelu, hipStream_t s);
 
 // out[0] += sum_{i < n} partial[i]
 hipError_t sum_into(const float* partial, int n, float* out, hipStream_t s);

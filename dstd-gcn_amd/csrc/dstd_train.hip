@@ -36,7 +36,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // operands both load in contiguous runs.
 // ---------------------------------------------------------------------------
 template <int TM, int TN>
-__global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, float* partial) {
+__global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int kc_len, float* partial) {
   constexpr int KT = 16;
   constexpr int LA = TM + 4, LB = TN + 4;
   constexpr int FM = TM / 32, FN = TN / 32;
@@ -56,22 +56,27 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, float* partial
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = zero4();
 
+  // work units: (batch, K chunk); a reduce GEMM spreads units over nsplit
+  // workgroups (split-K across and within batches), a batched one runs one
+  // batch with the whole K per workgroup
   const int nbat = g.nb1 * g.nb2;
-  int b_lo, b_hi;
+  int u_lo, u_hi;
   if (g.reduce) {
-    const int per = (nbat + nsplit - 1) / nsplit;
-    b_lo = blockIdx.z * per;
-    b_hi = min(nbat, b_lo + per);
+    const int units = nbat * kch, per = (units + nsplit - 1) / nsplit;
+    u_lo = blockIdx.z * per;
+    u_hi = min(units, u_lo + per);
   } else {
-    b_lo = blockIdx.z;
-    b_hi = b_lo + 1;
+    u_lo = blockIdx.z;
+    u_hi = u_lo + 1;
   }
 
-  for (int b = b_lo; b < b_hi; ++b) {
+  for (int u = u_lo; u < u_hi; ++u) {
+    const int b = u / kch, kc = u - b * kch;
     const int b1 = b / g.nb2, b2 = b - b1 * g.nb2;
     const float* Ab = g.A + b1 * g.a_b1 + b2 * g.a_b2;
     const float* Bb = g.B + b1 * g.b_b1 + b2 * g.b_b2;
-    for (int k0 = 0; k0 < g.K; k0 += KT) {
+    const int k_end = min(g.K, (kc + 1) * kc_len);
+    for (int k0 = kc * kc_len; k0 < k_end; k0 += KT) {
       float ra[EA], rb[EB];
 #pragma unroll
       for (int e = 0; e < EA; ++e) {
@@ -79,7 +84,7 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, float* partial
         const int m = a_kfast ? idx / KT : idx % TM;
         const int k = a_kfast ? idx % KT : idx / TM;
         const int gm = m0 + m, gk = k0 + k;
-        ra[e] = (gm < g.M && gk < g.K) ? Ab[gm * g.a_m + gk * g.a_k] : 0.f;
+        ra[e] = (gm < g.M && gk < k_end) ? Ab[gm * g.a_m + gk * g.a_k] : 0.f;
       }
 #pragma unroll
       for (int e = 0; e < EB; ++e) {
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, float* partial
         const int n = b_kfast ? idx / KT : idx % TN;
         const int k = b_kfast ? idx % KT : idx / TN;
         const int gn = n0 + n, gk = k0 + k;
-        rb[e] = (gn < g.N && gk < g.K) ? Bb[gk * g.b_k + gn * g.b_n] : 0.f;
+        rb[e] = (gn < g.N && gk < k_end) ? Bb[gk * g.b_k + gn * g.b_n] : 0.f;
       }
       __syncthreads();
 #pragma unroll
@@ -154,21 +159,31 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, float* partial
       }
 }
 
-// C = alpha * sum_z partial[z] + bias + beta * C   (fixed order over z)
-__global__ void k_gemm_finish(Gemm g, int nsplit, const float* partial) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= g.M * g.N) return;
-  const int m = idx / g.N, n = idx - m * g.N;
+// C = alpha * sum_z partial[z] + bias + beta * C.  Workgroup = 16 outputs x
+// 16 partial slices (slice s sums z = s, s + 16, ...), slices combined in LDS
+// in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void k_gemm_finish(Gemm g, int nsplit, const float* partial) {
+  __shared__ float red[16][17];
+  const int el = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int idx = blockIdx.x * 16 + el;
+  const int MN = g.M * g.N;
   float s = 0.f;
-  for (int z = 0; z < nsplit; ++z) s += partial[(size_t)z * g.M * g.N + idx];
-  float v = g.alpha * s;
+  if (idx < MN)
+    for (int z = sl; z < nsplit; z += 16) s += partial[(size_t)z * MN + idx];
+  red[sl][el] = s;
+  __syncthreads();
+  if (sl != 0 || idx >= MN) return;
+  float t = 0.f;
+  for (int k = 0; k < 16; ++k) t += red[k][el];
+  const int m = idx / g.N, n = idx - m * g.N;
+  float v = g.alpha * t;
   if (g.bias_m) v += g.bias_m[m];
   float* c = g.C + m * g.c_m + n * g.c_n;
   if (g.beta != 0.f) v += g.beta * *c;
   *c = v;
 }
 
-constexpr int kMaxSplit = 64;
+constexpr int kMaxSplit = 128;
 
 // ---------------------------------------------------------------------------
 // tanh outer difference
@@ -224,18 +239,57 @@ __global__ void k_scale_by(float* x, const float* alpha, size_t n) {
     x[e] *= al;
 }
 
-__global__ void k_reduce_rows(const float* X, int nb, int nj, long long sb, long long sm, long long sj, float* out,
-                              float scale) {
+// ---------------------------------------------------------------------------
+// Strided sums out[m] += scale * sum_{b, j} X[b*sb + m*sm + j*sj], two stages:
+// (m, split) partials in a fixed order, then a per-m finish.  Stage 1 maps
+// threads to whichever index is contiguous: j (bias / conv_rm-bias grads) or m
+// (the adjacency gradient dA, summed over samples and rows).
+// ---------------------------------------------------------------------------
+constexpr int kRedSplit = 64;
+
+__global__ void k_red_part_j(const float* X, int M, int nb, int nj, long long sb, long long sm, long long sj,
+                             int splits, float* part) {
   __shared__ float red[kRedThreads / 64];
-  const int m = blockIdx.x;
-  const long long tot = (long long)nb * nj;
+  const int m = blockIdx.x, sp = blockIdx.y;
+  const long long tot = (long long)nb * nj, per = (tot + splits - 1) / splits;
+  const long long lo = sp * per, hi = min(tot, lo + per);
   float s = 0.f;
-  for (long long e = threadIdx.x; e < tot; e += blockDim.x) {
+  for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) {
     const long long b = e / nj, j = e - b * nj;
     s += X[b * sb + m * sm + j * sj];
   }
   s = block_sum(s, red);
-  if (threadIdx.x == 0) out[m] += scale * s;
+  if (threadIdx.x == 0) part[(size_t)sp * M + m] = s;
+}
+
+__global__ void k_red_part_m(const float* X, int M, int nb, int nj, long long sb, long long sj, int splits,
+                             float* part) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x, sp = blockIdx.y;
+  if (m >= M) return;
+  const long long tot = (long long)nb * nj, per = (tot + splits - 1) / splits;
+  const long long lo = sp * per, hi = min(tot, lo + per);
+  float s = 0.f;
+  for (long long e = lo; e < hi; ++e) {
+    const long long b = e / nj, j = e - b * nj;
+    s += X[b * sb + m + j * sj];
+  }
+  part[(size_t)sp * M + m] = s;
+}
+
+// out[m] += scale * sum_sp part[sp][m]; 16 outputs x 16 split slices per workgroup
+__global__ __launch_bounds__(256) void k_red_finish(const float* part, int M, int splits, float* out, float scale) {
+  __shared__ float red[16][17];
+  const int el = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int m = blockIdx.x * 16 + el;
+  float s = 0.f;
+  if (m < M)
+    for (int sp = sl; sp < splits; sp += 16) s += part[(size_t)sp * M + m];
+  red[sl][el] = s;
+  __syncthreads();
+  if (sl != 0 || m >= M) return;
+  float t = 0.f;
+  for (int k = 0; k < 16; ++k) t += red[k][el];
+  out[m] += scale * t;
 }
 
 constexpr int kDotBlocks = 256;
@@ -267,15 +321,27 @@ __global__ void k_acc_mul(const float* a, const float* b, float* out, size_t n) 
     out[e] += b ? a[e] * b[e] : a[e];
 }
 
+
 // ---------------------------------------------------------------------------
-// Train-mode BatchNorm.  One workgroup per feature channel c; thread
-// (slice s, joint v) walks rows (n, t) = s, s + S, ... so a wave reads runs of
-// V consecutive floats.  Per-v sums are combined over slices in LDS in a fixed
-// order (deterministic).
+// Train-mode BatchNorm, channel (c, v) of an NCTV tensor, statistics over the
+// B*T rows (n, t).  Three launches each way so the work spreads over
+// C x splits workgroups instead of C:
+//   fwd: per-(c, split) chunk mean / M2 (two passes over the chunk), Chan
+//        merge per channel (mean, rstd, running stats), element-wise apply;
+//   bwd: per-(c, split) sums of dz and dz*xhat (+ the PReLU-slope partial),
+//        merge (dgamma, dbeta), element-wise du.
+// Inside a workgroup thread (slice s, joint v) walks the chunk's rows s,
+// s + S, ... so a wave reads runs of V consecutive floats; slice sums are
+// combined in LDS in a fixed order (deterministic).
 // ---------------------------------------------------------------------------
-struct BnGeom {
-  int V, S, rows;
-  __device__ BnGeom(int V_, int B, int T) : V(V_), S(kRedThreads / V_), rows(B * T) {}
+struct BnChunk {
+  int V, S, rows, r0, r1;
+  __device__ BnChunk(int V_, int B, int T, int splits)
+      : V(V_), S(kRedThreads / V_), rows(B * T) {
+    const int per = (rows + splits - 1) / splits;
+    r0 = blockIdx.y * per;
+    r1 = min(rows, r0 + per);
+  }
 };
 
 __device__ __forceinline__ float slice_sum(float v, float* lds, int V, int S) {
@@ -290,46 +356,74 @@ __device__ __forceinline__ float slice_sum(float v, float* lds, int V, int S) {
   return t;
 }
 
-__global__ __launch_bounds__(kRedThreads) void k_bn_train_fwd(BnFwd a, int B, int C, int T, int V) {
+__device__ __forceinline__ size_t bn_at(int row, int c, int v, int C, int T, int V) {
+  const int n = row / T, t = row - n * T;
+  return ((size_t)n * C + c) * T * V + (size_t)t * V + v;
+}
+
+// part: [splits][C*V][2] = (chunk mean, chunk M2)
+__global__ __launch_bounds__(kRedThreads) void k_bn_stats_part(BnFwd a, int B, int C, int T, int V, int splits,
+                                                               float* part) {
   __shared__ float lds[kRedThreads];
   const int c = blockIdx.x, tid = threadIdx.x;
-  const BnGeom G(V, B, T);
+  const BnChunk G(V, B, T, splits);
   const bool act = tid < G.S * V;
   const int v = tid % V, s0 = tid / V;
-  const size_t TV = (size_t)T * V, CTV = (size_t)C * TV;
-  auto at = [&](int row) -> size_t {
-    const int n = row / T, t = row - n * T;
-    return n * CTV + c * TV + (size_t)t * V + v;
-  };
+  const int cnt = max(G.r1 - G.r0, 0);
   auto u_of = [&](size_t i) { return a.x2 ? a.x[i] + a.x2[i] : a.x[i]; };
   float s = 0.f;
   if (act)
-    for (int row = s0; row < G.rows; row += G.S) s += u_of(at(row));
-  const float mean = slice_sum(s, lds, V, G.S) / G.rows;
+    for (int row = G.r0 + s0; row < G.r1; row += G.S) s += u_of(bn_at(row, c, v, C, T, V));
+  const float mean = cnt ? slice_sum(s, lds, V, G.S) / cnt : slice_sum(0.f, lds, V, G.S);
   float q = 0.f;
   if (act)
-    for (int row = s0; row < G.rows; row += G.S) {
-      const float d = u_of(at(row)) - mean;
+    for (int row = G.r0 + s0; row < G.r1; row += G.S) {
+      const float d = u_of(bn_at(row, c, v, C, T, V)) - mean;
       q = fmaf(d, d, q);
     }
-  const float var = slice_sum(q, lds, V, G.S) / G.rows;
-  const float rstd = 1.f / sqrtf(var + a.eps);
-  const int ch = c * V + v;
+  const float m2 = slice_sum(q, lds, V, G.S);
   if (tid < V) {
-    a.mean[ch] = mean;
-    a.rstd[ch] = rstd;
-    if (a.running_mean) {
-      const float unb = G.rows > 1 ? var * G.rows / (G.rows - 1) : var;
-      a.running_mean[ch] = (1.f - a.momentum) * a.running_mean[ch] + a.momentum * mean;
-      a.running_var[ch] = (1.f - a.momentum) * a.running_var[ch] + a.momentum * unb;
-    }
+    float* p = part + ((size_t)blockIdx.y * C * V + c * V + v) * 2;
+    p[0] = mean;
+    p[1] = m2;
   }
-  if (!act) return;
-  const float sc = rstd * a.gamma[ch], sh = a.beta[ch] - mean * sc;
+}
+
+__global__ void k_bn_stats_merge(BnFwd a, int B, int C, int T, int V, int splits, const float* part) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= C * V) return;
+  const int rows = B * T, per = (rows + splits - 1) / splits;
+  float mean = 0.f;
+  for (int sp = 0; sp < splits; ++sp) {
+    const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+    mean += cnt * part[((size_t)sp * C * V + ch) * 2];
+  }
+  mean /= rows;
+  float m2 = 0.f;
+  for (int sp = 0; sp < splits; ++sp) {
+    const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+    const float* p = part + ((size_t)sp * C * V + ch) * 2;
+    const float d = p[0] - mean;
+    m2 += p[1] + cnt * d * d;
+  }
+  const float var = m2 / rows;
+  a.mean[ch] = mean;
+  a.rstd[ch] = 1.f / sqrtf(var + a.eps);
+  if (a.running_mean) {
+    const float unb = rows > 1 ? m2 / (rows - 1) : var;
+    a.running_mean[ch] = (1.f - a.momentum) * a.running_mean[ch] + a.momentum * mean;
+    a.running_var[ch] = (1.f - a.momentum) * a.running_var[ch] + a.momentum * unb;
+  }
+}
+
+__global__ void k_bn_apply(BnFwd a, size_t n, int CV, int TV, int V) {
   const float w = a.prelu ? *a.prelu : 0.f;
-  for (int row = s0; row < G.rows; row += G.S) {
-    const size_t i = at(row);
-    float z = fmaf(u_of(i), sc, sh);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)((i / TV) % (CV / V)), v = (int)(i % V);
+    const int ch = c * V + v;
+    const float sc = a.rstd[ch] * a.gamma[ch], sh = a.beta[ch] - a.mean[ch] * sc;
+    const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
+    float z = fmaf(u, sc, sh);
     if (a.res) z += a.res[i];
     if (a.prelu) {
       a.zsave[i] = z;
@@ -340,54 +434,71 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_train_fwd(BnFwd a, int B, in
   }
 }
 
-__global__ __launch_bounds__(kRedThreads) void k_bn_train_bwd(BnBwd a, int B, int C, int T, int V) {
+// part: [splits][C*V][2] = (sum dz, sum dz*xhat); wpart: [splits][C] PReLU slope partials
+__global__ __launch_bounds__(kRedThreads) void k_bn_bwd_part(BnBwd a, int B, int C, int T, int V, int splits,
+                                                             float* part, float* wpart) {
   __shared__ float lds[kRedThreads];
   const int c = blockIdx.x, tid = threadIdx.x;
-  const BnGeom G(V, B, T);
+  const BnChunk G(V, B, T, splits);
   const bool act = tid < G.S * V;
   const int v = tid % V, s0 = tid / V;
-  const size_t TV = (size_t)T * V, CTV = (size_t)C * TV;
   const int ch = c * V + v;
-  auto at = [&](int row) -> size_t {
-    const int n = row / T, t = row - n * T;
-    return n * CTV + c * TV + (size_t)t * V + v;
-  };
   const float w = a.prelu ? *a.prelu : 0.f;
-  // PReLU' (torch convention: slope for z <= 0)
-  auto dz_of = [&](size_t i) {
-    const float d = a.dout[i];
-    return (a.prelu && !(a.zsave[i] > 0.f)) ? w * d : d;
-  };
   const float mean = act ? a.mean[ch] : 0.f, rstd = act ? a.rstd[ch] : 0.f;
   float sd = 0.f, sdx = 0.f, sw = 0.f;
   if (act)
-    for (int row = s0; row < G.rows; row += G.S) {
-      const size_t i = at(row);
-      const float dz = dz_of(i);
+    for (int row = G.r0 + s0; row < G.r1; row += G.S) {
+      const size_t i = bn_at(row, c, v, C, T, V);
+      const float d = a.dout[i];
+      // PReLU' (torch convention: the slope for z <= 0)
+      const float dz = (a.prelu && !(a.zsave[i] > 0.f)) ? w * d : d;
       const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
       sd += dz;
       sdx = fmaf(dz, (u - mean) * rstd, sdx);
-      if (a.prelu) sw = fmaf(a.dout[i], fminf(a.zsave[i], 0.f), sw);
+      if (a.prelu) sw = fmaf(d, fminf(a.zsave[i], 0.f), sw);
     }
-  const float dbeta = slice_sum(sd, lds, V, G.S);
-  const float dgamma = slice_sum(sdx, lds, V, G.S);
-  if (a.prelu_partial) {
+  const float t0 = slice_sum(sd, lds, V, G.S);
+  const float t1 = slice_sum(sdx, lds, V, G.S);
+  if (tid < V) {
+    float* p = part + ((size_t)blockIdx.y * C * V + ch) * 2;
+    p[0] = t0;
+    p[1] = t1;
+  }
+  if (a.prelu) {
     __shared__ float red[kRedThreads / 64];
     const float tw = block_sum(act ? sw : 0.f, red);
-    if (tid == 0) a.prelu_partial[c] = tw;
+    if (tid == 0) wpart[(size_t)blockIdx.y * C + c] = tw;
   }
-  if (tid < V) {
-    a.dgamma[ch] += dgamma;
-    a.dbeta[ch] += dbeta;
+}
+
+// sums[ch] = (sum dz, sum dz*xhat) for the apply pass; dgamma / dbeta accumulate
+__global__ void k_bn_bwd_merge(BnBwd a, int CV, int splits, const float* part, float* sums) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= CV) return;
+  float sd = 0.f, sdx = 0.f;
+  for (int sp = 0; sp < splits; ++sp) {
+    const float* p = part + ((size_t)sp * CV + ch) * 2;
+    sd += p[0];
+    sdx += p[1];
   }
-  if (!act) return;
-  const float g = a.gamma[ch] * rstd, inv = 1.f / G.rows;
-  for (int row = s0; row < G.rows; row += G.S) {
-    const size_t i = at(row);
-    const float dz = dz_of(i);
+  sums[2 * ch] = sd;
+  sums[2 * ch + 1] = sdx;
+  a.dbeta[ch] += sd;
+  a.dgamma[ch] += sdx;
+}
+
+__global__ void k_bn_bwd_apply(BnBwd a, size_t n, int CV, int TV, int V, int rows, const float* sums) {
+  const float w = a.prelu ? *a.prelu : 0.f;
+  const float inv = 1.f / rows;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)((i / TV) % (CV / V)), v = (int)(i % V);
+    const int ch = c * V + v;
+    const float d = a.dout[i];
+    const float dz = (a.prelu && !(a.zsave[i] > 0.f)) ? w * d : d;
     const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
+    const float mean = a.mean[ch], rstd = a.rstd[ch];
     const float xh = (u - mean) * rstd;
-    a.du[i] = g * (dz - dbeta * inv - xh * dgamma * inv);
+    a.du[i] = a.gamma[ch] * rstd * (dz - sums[2 * ch] * inv - xh * sums[2 * ch + 1] * inv);
     if (a.dz_out) a.dz_out[i] = dz;
   }
 }
@@ -522,20 +633,26 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   const int TM = g.M <= 32 ? 32 : 64, TN = g.N <= 32 ? 32 : 64;
   const int tiles = cdiv(g.M, TM) * cdiv(g.N, TN);
   const int nbat = g.nb1 * g.nb2;
-  int nsplit = 1;
+  int nsplit = 1, kch = 1, kc_len = rup(std::max(g.K, 1), 16);
   if (g.reduce && scratch) {
-    // enough workgroups to cover the chip, each with a few batches
-    nsplit = std::min(std::min(kMaxSplit, nbat), std::max(1, 512 / tiles));
+    // ~1024 workgroups, each reducing >= 64 values of K: split the K range of
+    // every batch into kch chunks so small batch counts still fill the chip
+    const int ksteps = cdiv(g.K, 16);
+    nsplit = std::max(1, std::min(kMaxSplit, 512 / tiles));
+    kch = std::max(1, std::min(cdiv(nsplit, nbat), cdiv(ksteps, 4)));
+    kc_len = cdiv(ksteps, kch) * 16;
+    kch = cdiv(g.K, kc_len);
+    nsplit = std::min(nsplit, nbat * kch);
   }
   dim3 grid(cdiv(g.N, TN), cdiv(g.M, TM), g.reduce ? nsplit : nbat);
   float* part = nsplit > 1 ? scratch : nullptr;
-  if (TM == 32 && TN == 32) k_gemm<32, 32><<<grid, 256, 0, s>>>(g, nsplit, part);
-  else if (TM == 32) k_gemm<32, 64><<<grid, 256, 0, s>>>(g, nsplit, part);
-  else if (TN == 32) k_gemm<64, 32><<<grid, 256, 0, s>>>(g, nsplit, part);
-  else k_gemm<64, 64><<<grid, 256, 0, s>>>(g, nsplit, part);
+  if (TM == 32 && TN == 32) k_gemm<32, 32><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
+  else if (TM == 32) k_gemm<32, 64><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
+  else if (TN == 32) k_gemm<64, 32><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
+  else k_gemm<64, 64><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nsplit == 1) return e;
-  k_gemm_finish<<<cdiv(g.M * g.N, 256), 256, 0, s>>>(g, nsplit, part);
+  k_gemm_finish<<<cdiv(g.M * g.N, 16), 256, 0, s>>>(g, nsplit, part);
   return hipGetLastError();
 }
 
@@ -563,9 +680,22 @@ hipError_t scale_by(float* x, const float* alpha, size_t n, hipStream_t s) {
   return hipGetLastError();
 }
 
+size_t reduce_scratch_floats(int M) { return (size_t)kRedSplit * M; }
+
 hipError_t reduce_rows(const float* X, int M, int nb, int nj, long long sb, long long sm, long long sj, float* out,
-                       float scale, hipStream_t s) {
-  k_reduce_rows<<<M, kRedThreads, 0, s>>>(X, nb, nj, sb, sm, sj, out, scale);
+                       float scale, float* scratch, hipStream_t s) {
+  const long long tot = (long long)nb * nj;
+  const bool by_m = sm == 1 && M > 1;
+  // ~1024 workgroups, each with a useful amount of work
+  const long long want = by_m ? std::min(kRedSplit, 1024 / cdiv(M, kRedThreads)) : std::min(kRedSplit, std::max(1, 1024 / M));
+  const int splits = (int)std::max<long long>(1, std::min<long long>(want, by_m ? (tot + 15) / 16 : (tot + 1023) / 1024));
+  if (by_m)
+    k_red_part_m<<<dim3(cdiv(M, kRedThreads), splits), kRedThreads, 0, s>>>(X, M, nb, nj, sb, sj, splits, scratch);
+  else
+    k_red_part_j<<<dim3(M, splits), kRedThreads, 0, s>>>(X, M, nb, nj, sb, sm, sj, splits, scratch);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  k_red_finish<<<cdiv(M, 16), 256, 0, s>>>(scratch, M, splits, out, scale);
   return hipGetLastError();
 }
 
@@ -592,13 +722,31 @@ hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStre
   return hipGetLastError();
 }
 
-hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, hipStream_t s) {
-  k_bn_train_fwd<<<C, kRedThreads, 0, s>>>(a, B, C, T, V);
+int bn_splits(int B, int T) { return std::max(1, std::min(16, cdiv(B * T, 64))); }
+
+size_t bn_scratch_floats(int B, int C, int T, int V) {
+  return (size_t)bn_splits(B, T) * C * V * 2 + (size_t)bn_splits(B, T) * C + (size_t)2 * C * V;
+}
+
+hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s) {
+  const int splits = bn_splits(B, T);
+  k_bn_stats_part<<<dim3(C, splits), kRedThreads, 0, s>>>(a, B, C, T, V, splits, scratch);
+  k_bn_stats_merge<<<cdiv(C * V, 256), 256, 0, s>>>(a, B, C, T, V, splits, scratch);
+  const size_t n = (size_t)B * C * T * V;
+  k_bn_apply<<<grid_for(n), 256, 0, s>>>(a, n, C * V, T * V, V);
   return hipGetLastError();
 }
 
-hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, hipStream_t s) {
-  k_bn_train_bwd<<<C, kRedThreads, 0, s>>>(a, B, C, T, V);
+hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scratch, float* dprelu, hipStream_t s) {
+  const int splits = bn_splits(B, T);
+  float* part = scratch;
+  float* wpart = part + (size_t)splits * C * V * 2;
+  float* sums = wpart + (size_t)splits * C;
+  k_bn_bwd_part<<<dim3(C, splits), kRedThreads, 0, s>>>(a, B, C, T, V, splits, part, wpart);
+  k_bn_bwd_merge<<<cdiv(C * V, 256), 256, 0, s>>>(a, C * V, splits, part, sums);
+  if (a.prelu) k_sum_into<<<1, kRedThreads, 0, s>>>(wpart, splits * C, dprelu);
+  const size_t n = (size_t)B * C * T * V;
+  k_bn_bwd_apply<<<grid_for(n), 256, 0, s>>>(a, n, C * V, T * V, V, B * T, sums);
   return hipGetLastError();
 }
 

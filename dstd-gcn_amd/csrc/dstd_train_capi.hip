@@ -114,17 +114,23 @@ void carve_op_saved(Carver& cv, OpSaved& s, const OpGeom& g) {
 }
 
 struct OpWs {
-  float *dF, *dD, *dM, *dP, *dQ, *gs, *part;
+  float *dF, *dD, *dM, *dP, *dQ, *gs, *part, *red;
 };
+// Reduction / BatchNorm scratch for the largest of the given geometries.
+size_t red_floats(const OpGeom& g) {
+  return std::max(reduce_scratch_floats(std::max(std::max(g.NN2, g.cout), std::max(g.A, g.cin))),
+                  bn_scratch_floats(g.B, std::max(g.cin, g.cout), g.T, g.V));
+}
 // Sized for the largest of the given op geometries (one workspace serves every
 // op of a block / model in turn).
-void carve_op_ws(Carver& cv, OpWs& w, std::initializer_list<OpGeom> gl) {
-  size_t nF = 0, nD = 0, nPQ = 0, nmn = 0;
+void carve_op_ws(Carver& cv, OpWs& w, const std::vector<OpGeom>& gl) {
+  size_t nF = 0, nD = 0, nPQ = 0, nmn = 0, nred = 0;
   for (const OpGeom& g : gl) {
     nF = std::max(nF, (size_t)g.B * g.cout * g.TV);
     nD = std::max(nD, (size_t)g.B * g.A * g.NN2);
     nPQ = std::max(nPQ, (size_t)g.B * 2 * g.TV);
     nmn = std::max(nmn, (size_t)std::max(std::max(g.cout * g.cin, 2 * g.A * g.A), 2 * g.cin));
+    nred = std::max(nred, red_floats(g));
   }
   w.dF = cv.take(nF);
   w.dD = cv.take(nD);
@@ -133,6 +139,7 @@ void carve_op_ws(Carver& cv, OpWs& w, std::initializer_list<OpGeom> gl) {
   w.dQ = cv.take(nPQ);
   w.gs = cv.take(gemm_scratch_floats((int)nmn, 1));
   w.part = cv.take(std::max(dot_partials(), mpjpe_partials()));
+  w.red = cv.take(nred);
 }
 
 // 1x1 conv as GEMMs over NCTV (W [cout][cin]).
@@ -164,10 +171,10 @@ Gemm conv_dw(const float* dY, const float* X, float* dW, int B, int cin, int cou
   return g;
 }
 hipError_t conv_bwd(const float* W, const float* X, const float* dY, float* dX, float* dW, float* db, int B, int cin,
-                    int cout, int TV, float* gs, hipStream_t s) {
+                    int cout, int TV, float* gs, float* red, hipStream_t s) {
   if (dX) DSTD_TRYH(gemm(conv_dx(W, dY, dX, B, cin, cout, TV), gs, s));
   DSTD_TRYH(gemm(conv_dw(dY, X, dW, B, cin, cout, TV), gs, s));
-  return reduce_rows(dY, cout, B, TV, (long long)cout * TV, TV, 1, db, 1.f, s);
+  return reduce_rows(dY, cout, B, TV, (long long)cout * TV, TV, 1, db, 1.f, red, s);
 }
 
 // y (beta_y: 0 '=' / 1 '+=') = DSTDGC(x, Acomb, alpha); fills sv.
@@ -212,10 +219,10 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   DSTD_TRYH(gemm(d, nullptr, s));
   // Adj = alpha * E + A:  dalpha = <dD, E>, dA = sum_{n,a} dD, dE = alpha dD
   DSTD_TRYH(dot(ws.dD, sv.E, nadj, dalpha, ws.part, s));
-  DSTD_TRYH(reduce_rows(ws.dD, g.NN2, g.B, g.A, (long long)g.A * g.NN2, 1, g.NN2, dA, 1.f, s));
+  DSTD_TRYH(reduce_rows(ws.dD, g.NN2, g.B, g.A, (long long)g.A * g.NN2, 1, g.NN2, dA, 1.f, ws.red, s));
   DSTD_TRYH(scale_by(ws.dD, alpha, nadj, s));
   float* dE = ws.dD;
-  DSTD_TRYH(reduce_rows(dE, g.A, g.B, g.NN2, (long long)g.A * g.NN2, g.NN2, 1, gr->brm, 1.f, s));
+  DSTD_TRYH(reduce_rows(dE, g.A, g.B, g.NN2, (long long)g.A * g.NN2, g.NN2, 1, gr->brm, 1.f, ws.red, s));
   Gemm wr;  // dWrm[a][k] = sum_{n,ij} dE[n][a][ij] M[n][k][ij]
   wr.M = g.A, wr.N = 2 * g.A, wr.K = g.NN2, wr.nb1 = g.B, wr.reduce = 1;
   wr.A = dE, wr.a_b1 = (long long)g.A * g.NN2, wr.a_m = g.NN2, wr.a_k = 1;
@@ -233,9 +240,9 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   DSTD_TRYH(hipMemsetAsync(ws.dP, 0, npq * sizeof(float), s));
   DSTD_TRYH(hipMemsetAsync(ws.dQ, 0, npq * sizeof(float), s));
   DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.A, g.NN, ws.dP, ws.dQ, s));
-  DSTD_TRYH(conv_bwd(w->wf, x, ws.dF, dx, gr->wf, gr->bf, g.B, g.cin, g.cout, g.TV, ws.gs, s));
-  DSTD_TRYH(conv_bwd(w->wm1, x, ws.dP, dx, gr->wm1, gr->bm1, g.B, g.cin, 2, g.TV, ws.gs, s));
-  return conv_bwd(w->wm2, x, ws.dQ, dx, gr->wm2, gr->bm2, g.B, g.cin, 2, g.TV, ws.gs, s);
+  DSTD_TRYH(conv_bwd(w->wf, x, ws.dF, dx, gr->wf, gr->bf, g.B, g.cin, g.cout, g.TV, ws.gs, ws.red, s));
+  DSTD_TRYH(conv_bwd(w->wm1, x, ws.dP, dx, gr->wm1, gr->bm1, g.B, g.cin, 2, g.TV, ws.gs, ws.red, s));
+  return conv_bwd(w->wm2, x, ws.dQ, dx, gr->wm2, gr->bm2, g.B, g.cin, 2, g.TV, ws.gs, ws.red, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -246,6 +253,7 @@ struct BlockSaved {
   OpSaved op[3];
   float *ysp, *z, *h, *mean, *rstd;
   float *rc, *r, *rmean, *rrstd;
+  float* red;  // BatchNorm statistics scratch of the forward
 };
 void carve_block_saved(Carver& cv, BlockSaved& s, int B, int cin, int cout, int T, int V) {
   const size_t act = (size_t)B * cout * T * V;
@@ -263,6 +271,7 @@ void carve_block_saved(Carver& cv, BlockSaved& s, int B, int cin, int cout, int 
   s.r = res ? cv.take(act) : nullptr;
   s.rmean = res ? cv.take(cout * V) : nullptr;
   s.rrstd = res ? cv.take(cout * V) : nullptr;
+  s.red = cv.take(bn_scratch_floats(B, cout, T, V));
 }
 
 struct BlockWs {
@@ -283,20 +292,7 @@ void carve_block_ws(Carver& cv, BlockWs& w, int B, int T, int V, std::initialize
     cmax = std::max(cmax, c.cout);
     res = res || c.cin != c.cout;
   }
-  size_t nF = 0, nD = 0, nPQ = 0, nmn = 0;
-  for (const OpGeom& g : gl) {
-    nF = std::max(nF, (size_t)g.B * g.cout * g.TV);
-    nD = std::max(nD, (size_t)g.B * g.A * g.NN2);
-    nPQ = std::max(nPQ, (size_t)g.B * 2 * g.TV);
-    nmn = std::max(nmn, (size_t)std::max(std::max(g.cout * g.cin, 2 * g.A * g.A), 2 * g.cin));
-  }
-  w.op.dF = cv.take(nF);
-  w.op.dD = cv.take(nD);
-  w.op.dM = cv.take(2 * nD);
-  w.op.dP = cv.take(nPQ);
-  w.op.dQ = cv.take(nPQ);
-  w.op.gs = cv.take(gemm_scratch_floats((int)nmn, 1));
-  w.op.part = cv.take(std::max(dot_partials(), mpjpe_partials()));
+  carve_op_ws(cv, w.op, gl);
   const size_t act = (size_t)B * cmax * T * V;
   w.dh = cv.take(act);
   w.dysp = cv.take(act);
@@ -330,7 +326,7 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.out = S.r;
     rb.mean = S.rmean;
     rb.rstd = S.rrstd;
-    DSTD_TRYH(bn_train_fwd(rb, B, cout, T, V, s));
+    DSTD_TRYH(bn_train_fwd(rb, B, cout, T, V, S.red, s));
     r = S.r;
   }
   BnFwd bb;  // h = PReLU(BN(y) + r)  (:151-154)
@@ -347,7 +343,7 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.zsave = S.z;
   bb.mean = S.mean;
   bb.rstd = S.rstd;
-  DSTD_TRYH(bn_train_fwd(bb, B, cout, T, V, s));
+  DSTD_TRYH(bn_train_fwd(bb, B, cout, T, V, S.red, s));
   const OpGeom gt(DSTD_MODE_TEMPORAL, B, cout, cout, T, V);  // :156-162
   return op_fwd(gt, S.h, &p->conv_t, S.at, p->alpha_tm, y, 0.f, S.op[2], s);
 }
@@ -373,9 +369,7 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.dz_out = W.dr;
   bb.dgamma = g->bn.weight;
   bb.dbeta = g->bn.bias;
-  bb.prelu_partial = W.pp;
-  DSTD_TRYH(bn_train_bwd(bb, B, cout, T, V, s));
-  DSTD_TRYH(sum_into(W.pp, cout, g->prelu, s));
+  DSTD_TRYH(bn_train_bwd(bb, B, cout, T, V, W.op.red, g->prelu, s));
   if (res) {
     BnBwd rb;
     rb.x = S.rc;
@@ -386,8 +380,8 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.du = W.drc;
     rb.dgamma = g->res_bn.weight;
     rb.dbeta = g->res_bn.bias;
-    DSTD_TRYH(bn_train_bwd(rb, B, cout, T, V, s));
-    DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, s));
+    DSTD_TRYH(bn_train_bwd(rb, B, cout, T, V, W.op.red, nullptr, s));
+    DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, W.op.red, s));
   } else if (dx) {
     DSTD_TRYH(acc_mul(W.dr, nullptr, dx, act, s));
   }
@@ -411,6 +405,7 @@ struct ModelSaved {
   float* h[DSTD_MAX_LAYERS + 1];
   float *yb[DSTD_MAX_LAYERS], *ze[DSTD_MAX_LAYERS], *me[DSTD_MAX_LAYERS], *re[DSTD_MAX_LAYERS];
   BlockSaved st_in, st_out, enc[DSTD_MAX_LAYERS];
+  float* red;
 };
 void carve_model_saved(Carver& cv, ModelSaved& s, int B, int T, int V, int C, int L) {
   const size_t act = (size_t)B * C * T * V;
@@ -431,6 +426,7 @@ void carve_model_saved(Carver& cv, ModelSaved& s, int B, int T, int V, int C, in
   }
   carve_block_saved(cv, s.st_out, B, C, 3, T, V);
   s.o = cv.take((size_t)B * 3 * T * V);
+  s.red = cv.take(bn_scratch_floats(B, C, T, V));
 }
 
 struct ModelWs {
@@ -590,7 +586,7 @@ int dstd_model_train_fwd(const dstd_model_params* p, const float* x, int B, floa
   b0.zsave = S.z0;
   b0.mean = S.m0;
   b0.rstd = S.r0;
-  DSTD_TRY(bn_train_fwd(b0, B, C, T, V, s));
+  DSTD_TRY(bn_train_fwd(b0, B, C, T, V, S.red, s));
   if (dropout_p > 0.f) DSTD_TRY(dropout(S.hp0, S.h[0], act, dropout_p, seed, s));  // do_in
   for (int i = 0; i < L; ++i) {                                                  // :310-311
     DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s));
@@ -608,7 +604,7 @@ int dstd_model_train_fwd(const dstd_model_params* p, const float* x, int B, floa
     be.zsave = S.ze[i];
     be.mean = S.me[i];
     be.rstd = S.re[i];
-    DSTD_TRY(bn_train_fwd(be, B, C, T, V, s));
+    DSTD_TRY(bn_train_fwd(be, B, C, T, V, S.red, s));
   }
   DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s));  // :313
   DSTD_TRY(out_ntvc(S.o, x, B, T, V, 3, y, s));                                  // :314-315
@@ -656,9 +652,7 @@ int dstd_model_train_bwd(const dstd_model_params* p, const float* x, int B, floa
     be.du = W.du;
     be.dgamma = g->enc_bn[i].weight;
     be.dbeta = g->enc_bn[i].bias;
-    be.prelu_partial = W.pp;
-    DSTD_TRY(bn_train_bwd(be, B, C, T, V, s));
-    DSTD_TRY(sum_into(W.pp, C, g->enc_prelu[i], s));
+    DSTD_TRY(bn_train_bwd(be, B, C, T, V, W.blk.op.red, g->enc_prelu[i], s));
     // u = block(h) + h: dh = du (identity path) + block backward
     DSTD_TRY(hipMemcpyAsync(dhb, W.du, act * sizeof(float), hipMemcpyDeviceToDevice, s));
     DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s));
@@ -676,9 +670,7 @@ int dstd_model_train_bwd(const dstd_model_params* p, const float* x, int B, floa
   b0.du = W.du;
   b0.dgamma = g->bn_in.weight;
   b0.dbeta = g->bn_in.bias;
-  b0.prelu_partial = W.pp;
-  DSTD_TRY(bn_train_bwd(b0, B, C, T, V, s));
-  DSTD_TRY(sum_into(W.pp, C, g->prelu, s));
+  DSTD_TRY(bn_train_bwd(b0, B, C, T, V, W.blk.op.red, g->prelu, s));
   DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, nullptr, &g->st_in, W.blk, s));
   return DSTD_OK;
 }
