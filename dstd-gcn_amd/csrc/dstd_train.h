@@ -30,6 +30,7 @@ struct Gemm {
   float alpha = 1.f, beta = 0.f;
   const float* bias_m = nullptr;
   int reduce = 0;
+  int b_ones_last = 0;  // B(k, N-1) = 1: the last output column is sum_k A(m, k) (bias gradients)
 };
 
 // Scratch (floats) a reduce-GEMM may need for its split-over-batches partials.
@@ -44,13 +45,40 @@ struct PQView {
 // M[n][r*A + a][i][j] = tanh(P(n,r,a,i) - Q(n,r,a,j)), r < 2.
 hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int A, int NN, float* M,
                           hipStream_t s);
-// dZ = dM * (1 - M^2);  dP(n,r,a,i) += sum_j dZ;  dQ(n,r,a,j) -= sum_i dZ.
+// dZ = dM * (1 - M^2);  dP(n,r,a,i) = sum_j dZ;  dQ(n,r,a,j) = -sum_i dZ.
 hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int A, int NN, float* dP, float* dQ,
                           hipStream_t s);
 
 // D[n][a][ij] = alpha * E[n][a][ij] + Acomb[ij]   (alpha: device scalar)
 hipError_t adj_combine(const float* E, const float* Acomb, const float* alpha, int B, int A, int NN2, float* D,
                        hipStream_t s);
+// Backward of adj_combine + the conv_rm bias, fused: dD -> dE = alpha * dD in
+// place, and dalpha += <dD, E>, dA[ij] += sum_{n,a} dD, dbrm[a] += sum_{n,ij} dE.
+// scratch >= adj_bwd_scratch_floats(B, A, NN2).
+size_t adj_bwd_scratch_floats(int B, int A, int NN2);
+hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
+                   float* dalpha, float* scratch, hipStream_t s);
+
+// Batched strided 2-D copies in one launch: dst[r*dst_ld + c] (+)= src[r*src_ld + c].
+struct CopyJob {
+  const float* src;
+  float* dst;
+  int rows, cols, src_ld, dst_ld, accumulate;
+};
+constexpr int kMaxCopyJobs = 64;
+struct CopyJobs {
+  int n = 0;
+  CopyJob j[kMaxCopyJobs];
+  bool add(const float* src, float* dst, int rows, int cols, int src_ld, int dst_ld, int accumulate) {
+    if (n >= kMaxCopyJobs) return false;
+    j[n++] = CopyJob{src, dst, rows, cols, src_ld, dst_ld, accumulate};
+    return true;
+  }
+};
+hipError_t copy_jobs(const CopyJobs& js, hipStream_t s);
+// dR_s += dA; dW_s += dA * A_s   (both graphs, n = 2*V*V)
+hipError_t adj_param_grads(const float* dA, const float* A_s, float* dR_s, float* dW_s, size_t n, hipStream_t s);
+
 // x[i] *= alpha (device scalar)
 hipError_t scale_by(float* x, const float* alpha, size_t n, hipStream_t s);
 

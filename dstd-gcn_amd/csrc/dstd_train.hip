@@ -92,7 +92,8 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
         const int n = b_kfast ? idx / KT : idx % TN;
         const int k = b_kfast ? idx % KT : idx / TN;
         const int gn = n0 + n, gk = k0 + k;
-        rb[e] = (gn < g.N && gk < k_end) ? Bb[gk * g.b_k + gn * g.b_n] : 0.f;
+        rb[e] = (gn < g.N && gk < k_end) ? ((g.b_ones_last && gn == g.N - 1) ? 1.f : Bb[gk * g.b_k + gn * g.b_n])
+                                         : 0.f;
       }
       __syncthreads();
 #pragma unroll
@@ -218,11 +219,11 @@ __global__ void k_tanh_outer_bwd(const float* M, const float* dM, PQView v, int 
     float s = 0.f;
     if (i < NN) {
       for (int j = 0; j < NN; ++j) s += dz[i * (NN + 1) + j];
-      dP[base + i * v.si] += s;
+      dP[base + i * v.si] = s;
     } else {
       const int j = i - NN;
       for (int k = 0; k < NN; ++k) s += dz[k * (NN + 1) + j];
-      dQ[base + j * v.si] -= s;
+      dQ[base + j * v.si] = -s;
     }
   }
 }
@@ -231,6 +232,87 @@ __global__ void k_adj_combine(const float* E, const float* Acomb, const float* a
   const float al = *alpha;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
     D[e] = fmaf(al, E[e], Acomb[e % NN2]);
+}
+
+// Fused adjacency backward, stage 1: workgroup (row a, sample chunk); each
+// thread owns entries ij and walks the chunk's samples (no atomics).
+__global__ __launch_bounds__(256) void k_adj_bwd_part(float* dD, const float* E, const float* alpha, int B, int A,
+                                                      int NN2, int nch, float* pdA, float* pbr, float* pal) {
+  __shared__ float red[4];
+  const int a = blockIdx.x, ch = blockIdx.y;
+  const int per = (B + nch - 1) / nch, n0 = ch * per, n1 = min(B, n0 + per);
+  const float al = *alpha;
+  float sbr = 0.f, sal = 0.f;
+  for (int ij = threadIdx.x; ij < NN2; ij += blockDim.x) {
+    float sa = 0.f;
+    for (int n = n0; n < n1; ++n) {
+      const size_t i = ((size_t)n * A + a) * NN2 + ij;
+      const float d = dD[i];
+      sa += d;
+      sal = fmaf(d, E[i], sal);
+      dD[i] = al * d;
+    }
+    pdA[((size_t)ch * A + a) * NN2 + ij] = sa;
+    sbr += sa;
+  }
+  sbr = block_sum(sbr, red);
+  sal = block_sum(sal, red);
+  if (threadIdx.x == 0) {
+    pbr[ch * A + a] = al * sbr;
+    pal[ch * A + a] = sal;
+  }
+}
+
+// stage 2: blocks [0, cdiv(NN2,16)) finish dA (16 outputs x 16 slices over the
+// A*nch partial rows); the last block finishes dbrm and dalpha.
+__global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* pdA, const float* pbr, const float* pal, int A,
+                                                        int NN2, int nch, float* dA, float* dbrm, float* dalpha) {
+  __shared__ float lds[16][17];
+  __shared__ float red[4];
+  const int nblk = (NN2 + 15) / 16;
+  if ((int)blockIdx.x < nblk) {
+    const int el = threadIdx.x & 15, sl = threadIdx.x >> 4;
+    const int ij = blockIdx.x * 16 + el;
+    float s = 0.f;
+    if (ij < NN2)
+      for (int r = sl; r < A * nch; r += 16) s += pdA[(size_t)r * NN2 + ij];
+    lds[sl][el] = s;
+    __syncthreads();
+    if (sl == 0 && ij < NN2) {
+      float t = 0.f;
+      for (int k = 0; k < 16; ++k) t += lds[k][el];
+      dA[ij] += t;
+    }
+    return;
+  }
+  for (int a = threadIdx.x; a < A; a += blockDim.x) {
+    float t = 0.f;
+    for (int c = 0; c < nch; ++c) t += pbr[c * A + a];
+    dbrm[a] += t;
+  }
+  float t = 0.f;
+  for (int i = threadIdx.x; i < A * nch; i += blockDim.x) t += pal[i];
+  t = block_sum(t, red);
+  if (threadIdx.x == 0) dalpha[0] += t;
+}
+
+__global__ void k_copy_jobs(CopyJobs js) {
+  const CopyJob& j = js.j[blockIdx.y];
+  const int tot = j.rows * j.cols;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
+    const int r = e / j.cols, c = e - r * j.cols;
+    const float v = j.src[(size_t)r * j.src_ld + c];
+    float* d = j.dst + (size_t)r * j.dst_ld + c;
+    *d = j.accumulate ? *d + v : v;
+  }
+}
+
+__global__ void k_adj_param_grads(const float* dA, const float* A_s, float* dR_s, float* dW_s, size_t n) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    const float d = dA[e];
+    dR_s[e] += d;
+    dW_s[e] += d * A_s[e];
+  }
 }
 
 __global__ void k_scale_by(float* x, const float* alpha, size_t n) {
@@ -672,6 +754,37 @@ hipError_t adj_combine(const float* E, const float* Acomb, const float* alpha, i
                        hipStream_t s) {
   const size_t n = (size_t)B * A * NN2;
   k_adj_combine<<<grid_for(n), 256, 0, s>>>(E, Acomb, alpha, n, NN2, D);
+  return hipGetLastError();
+}
+
+int adj_bwd_chunks(int B, int A) { return std::max(1, std::min(std::min(B, 16), cdiv(512, A))); }
+
+size_t adj_bwd_scratch_floats(int B, int A, int NN2) {
+  const int nch = adj_bwd_chunks(B, A);
+  return (size_t)nch * A * NN2 + 2 * (size_t)nch * A + 64;
+}
+
+hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
+                   float* dalpha, float* scratch, hipStream_t s) {
+  const int nch = adj_bwd_chunks(B, A);
+  float* pdA = scratch;
+  float* pbr = pdA + (size_t)nch * A * NN2;
+  float* pal = pbr + (size_t)nch * A;
+  k_adj_bwd_part<<<dim3(A, nch), 256, 0, s>>>(dD, E, alpha, B, A, NN2, nch, pdA, pbr, pal);
+  k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(pdA, pbr, pal, A, NN2, nch, dA, dbrm, dalpha);
+  return hipGetLastError();
+}
+
+hipError_t copy_jobs(const CopyJobs& js, hipStream_t s) {
+  if (js.n == 0) return hipSuccess;
+  int mx = 1;
+  for (int i = 0; i < js.n; ++i) mx = std::max(mx, js.j[i].rows * js.j[i].cols);
+  k_copy_jobs<<<dim3(std::min(cdiv(mx, 256), 64), js.n), 256, 0, s>>>(js);
+  return hipGetLastError();
+}
+
+hipError_t adj_param_grads(const float* dA, const float* A_s, float* dR_s, float* dW_s, size_t n, hipStream_t s) {
+  k_adj_param_grads<<<grid_for(n), 256, 0, s>>>(dA, A_s, dR_s, dW_s, n);
   return hipGetLastError();
 }
 

@@ -98,45 +98,58 @@ struct OpGeom {
     ps_a = sp ? V : 1;
     ps_i = sp ? 1 : V;
   }
-  PQView pq() const { return PQView{2LL * TV, (long long)TV, ps_a, ps_i}; }
+  int CG() const { return cout + 4; }  // rows of the packed conv output G = [F; P; Q]
+  // P (Q) rows of G: element (n, r, a, i) at n*CG*TV + r*TV + a*ps_a + i*ps_i
+  PQView pq() const { return PQView{(long long)CG() * TV, (long long)TV, ps_a, ps_i}; }
 };
 
+// Saved state of one train-mode DSTDGC.  conv_f / conv_m1 / conv_m2 run as ONE
+// GEMM with the packed weights Wp = [W_f; W_m1; W_m2] ([cout+4][cin]) into
+// G = [F; P; Q] ([B][cout+4][T*V]); M, E, D as in the forward (§3.2).
 struct OpSaved {
-  float *F, *P, *Q, *M, *E, *D;
+  float *Wp, *bp, *G, *M, *E, *D;
 };
 void carve_op_saved(Carver& cv, OpSaved& s, const OpGeom& g) {
-  s.F = cv.take((size_t)g.B * g.cout * g.TV);
-  s.P = cv.take((size_t)g.B * 2 * g.TV);
-  s.Q = cv.take((size_t)g.B * 2 * g.TV);
+  s.Wp = cv.take((size_t)g.CG() * g.cin);
+  s.bp = cv.take(g.CG());
+  s.G = cv.take((size_t)g.B * g.CG() * g.TV);
   s.M = cv.take((size_t)g.B * 2 * g.A * g.NN2);
   s.E = cv.take((size_t)g.B * g.A * g.NN2);
   s.D = cv.take((size_t)g.B * g.A * g.NN2);
 }
+// Copy jobs packing one op's conv weights into Wp / bp.
+bool pack_jobs(CopyJobs& js, const dstd_gc_weights* w, const OpSaved& sv, const OpGeom& g) {
+  return js.add(w->wf, sv.Wp, g.cout, g.cin, g.cin, g.cin, 0) &&
+         js.add(w->wm1, sv.Wp + (size_t)g.cout * g.cin, 2, g.cin, g.cin, g.cin, 0) &&
+         js.add(w->wm2, sv.Wp + (size_t)(g.cout + 2) * g.cin, 2, g.cin, g.cin, g.cin, 0) &&
+         js.add(w->bf, sv.bp, 1, g.cout, g.cout, g.cout, 0) && js.add(w->bm1, sv.bp + g.cout, 1, 2, 2, 2, 0) &&
+         js.add(w->bm2, sv.bp + g.cout + 2, 1, 2, 2, 2, 0);
+}
 
 struct OpWs {
-  float *dF, *dD, *dM, *dP, *dQ, *gs, *part, *red;
+  float *dG, *dD, *dM, *gW, *gs, *part, *red;
 };
-// Reduction / BatchNorm scratch for the largest of the given geometries.
+// Reduction / BatchNorm / adjacency-backward scratch for a geometry.
 size_t red_floats(const OpGeom& g) {
-  return std::max(reduce_scratch_floats(std::max(std::max(g.NN2, g.cout), std::max(g.A, g.cin))),
-                  bn_scratch_floats(g.B, std::max(g.cin, g.cout), g.T, g.V));
+  return std::max(std::max(reduce_scratch_floats(std::max(std::max(g.NN2, g.CG()), std::max(g.A, g.cin))),
+                           bn_scratch_floats(g.B, std::max(g.cin, g.cout), g.T, g.V)),
+                  adj_bwd_scratch_floats(g.B, g.A, g.NN2));
 }
 // Sized for the largest of the given op geometries (one workspace serves every
 // op of a block / model in turn).
 void carve_op_ws(Carver& cv, OpWs& w, const std::vector<OpGeom>& gl) {
-  size_t nF = 0, nD = 0, nPQ = 0, nmn = 0, nred = 0;
+  size_t nG = 0, nD = 0, nW = 0, nmn = 0, nred = 0;
   for (const OpGeom& g : gl) {
-    nF = std::max(nF, (size_t)g.B * g.cout * g.TV);
+    nG = std::max(nG, (size_t)g.B * g.CG() * g.TV);
     nD = std::max(nD, (size_t)g.B * g.A * g.NN2);
-    nPQ = std::max(nPQ, (size_t)g.B * 2 * g.TV);
-    nmn = std::max(nmn, (size_t)std::max(std::max(g.cout * g.cin, 2 * g.A * g.A), 2 * g.cin));
+    nW = std::max(nW, (size_t)g.CG() * (g.cin + 1));
+    nmn = std::max(nmn, (size_t)std::max(std::max(g.CG() * (g.cin + 1), 2 * g.A * g.A), g.cout * g.cin));
     nred = std::max(nred, red_floats(g));
   }
-  w.dF = cv.take(nF);
+  w.dG = cv.take(nG);
   w.dD = cv.take(nD);
   w.dM = cv.take(2 * nD);
-  w.dP = cv.take(nPQ);
-  w.dQ = cv.take(nPQ);
+  w.gW = cv.take(nW);
   w.gs = cv.take(gemm_scratch_floats((int)nmn, 1));
   w.part = cv.take(std::max(dot_partials(), mpjpe_partials()));
   w.red = cv.take(nred);
@@ -177,13 +190,15 @@ hipError_t conv_bwd(const float* W, const float* X, const float* dY, float* dX, 
   return reduce_rows(dY, cout, B, TV, (long long)cout * TV, TV, 1, db, 1.f, red, s);
 }
 
-// y (beta_y: 0 '=' / 1 '+=') = DSTDGC(x, Acomb, alpha); fills sv.
+// y (beta_y: 0 '=' / 1 '+=') = DSTDGC(x, Acomb, alpha); fills sv.  The packed
+// weights sv.Wp / sv.bp must already hold the op's conv weights (pack_jobs).
 hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* Acomb, const float* alpha,
                   float* y, float beta_y, const OpSaved& sv, hipStream_t s) {
-  DSTD_TRYH(gemm(conv_fwd(w->wf, w->bf, x, sv.F, g.B, g.cin, g.cout, g.TV), nullptr, s));   // :81
-  DSTD_TRYH(gemm(conv_fwd(w->wm1, w->bm1, x, sv.P, g.B, g.cin, 2, g.TV), nullptr, s));     // :82
-  DSTD_TRYH(gemm(conv_fwd(w->wm2, w->bm2, x, sv.Q, g.B, g.cin, 2, g.TV), nullptr, s));
-  DSTD_TRYH(tanh_outer_fwd(sv.P, sv.Q, g.pq(), g.B, g.A, g.NN, sv.M, s));                  // :84 / :90
+  // conv_f, conv_m1, conv_m2 in one GEMM                         :81-82
+  DSTD_TRYH(gemm(conv_fwd(sv.Wp, sv.bp, x, sv.G, g.B, g.cin, g.CG(), g.TV), nullptr, s));
+  const float* P = sv.G + (size_t)g.cout * g.TV;
+  const float* Q = P + 2 * (size_t)g.TV;
+  DSTD_TRYH(tanh_outer_fwd(P, Q, g.pq(), g.B, g.A, g.NN, sv.M, s));                        // :84 / :90
   Gemm e;  // E = conv_rm(M): [A x 2A] . [2A x NN^2] + b_rm           :85 / :91
   e.M = g.A, e.N = g.NN2, e.K = 2 * g.A, e.nb1 = g.B;
   e.A = w->wrm, e.a_m = 2 * g.A, e.a_k = 1;
@@ -194,7 +209,7 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   DSTD_TRYH(adj_combine(sv.E, Acomb, alpha, g.B, g.A, g.NN2, sv.D, s));                    // :86 / :92
   Gemm a;  // y[c][j] = sum_i F[c][i] D[i][j] per (n, a)               :87 / :93
   a.M = g.cout, a.N = g.NN, a.K = g.NN, a.nb1 = g.B, a.nb2 = g.A;
-  a.A = sv.F, a.a_b1 = (long long)g.cout * g.TV, a.a_b2 = g.ps_a, a.a_m = g.TV, a.a_k = g.ps_i;
+  a.A = sv.G, a.a_b1 = (long long)g.CG() * g.TV, a.a_b2 = g.ps_a, a.a_m = g.TV, a.a_k = g.ps_i;
   a.B = sv.D, a.b_b1 = (long long)g.A * g.NN2, a.b_b2 = g.NN2, a.b_k = g.NN, a.b_n = 1;
   a.C = y, a.c_b1 = (long long)g.cout * g.TV, a.c_b2 = g.ps_a, a.c_m = g.TV, a.c_n = g.ps_i;
   a.beta = beta_y;
@@ -204,25 +219,22 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
 hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* alpha, const OpSaved& sv,
                   const float* dy, float* dx, const dstd_gc_grads* gr, float* dA, float* dalpha, const OpWs& ws,
                   hipStream_t s) {
-  const size_t nadj = (size_t)g.B * g.A * g.NN2;
-  Gemm f;  // dF[c][i] = sum_j dy[c][j] D[i][j]
+  const long long ldG = (long long)g.CG() * g.TV;
+  Gemm f;  // dF[c][i] = sum_j dy[c][j] D[i][j]  -> rows [0, cout) of dG
   f.M = g.cout, f.N = g.NN, f.K = g.NN, f.nb1 = g.B, f.nb2 = g.A;
   f.A = dy, f.a_b1 = (long long)g.cout * g.TV, f.a_b2 = g.ps_a, f.a_m = g.TV, f.a_k = g.ps_i;
   f.B = sv.D, f.b_b1 = (long long)g.A * g.NN2, f.b_b2 = g.NN2, f.b_k = 1, f.b_n = g.NN;
-  f.C = ws.dF, f.c_b1 = (long long)g.cout * g.TV, f.c_b2 = g.ps_a, f.c_m = g.TV, f.c_n = g.ps_i;
+  f.C = ws.dG, f.c_b1 = ldG, f.c_b2 = g.ps_a, f.c_m = g.TV, f.c_n = g.ps_i;
   DSTD_TRYH(gemm(f, nullptr, s));
   Gemm d;  // dD[i][j] = sum_c F[c][i] dy[c][j]
   d.M = g.NN, d.N = g.NN, d.K = g.cout, d.nb1 = g.B, d.nb2 = g.A;
-  d.A = sv.F, d.a_b1 = (long long)g.cout * g.TV, d.a_b2 = g.ps_a, d.a_m = g.ps_i, d.a_k = g.TV;
+  d.A = sv.G, d.a_b1 = ldG, d.a_b2 = g.ps_a, d.a_m = g.ps_i, d.a_k = g.TV;
   d.B = dy, d.b_b1 = (long long)g.cout * g.TV, d.b_b2 = g.ps_a, d.b_k = g.TV, d.b_n = g.ps_i;
   d.C = ws.dD, d.c_b1 = (long long)g.A * g.NN2, d.c_b2 = g.NN2, d.c_m = g.NN, d.c_n = 1;
   DSTD_TRYH(gemm(d, nullptr, s));
-  // Adj = alpha * E + A:  dalpha = <dD, E>, dA = sum_{n,a} dD, dE = alpha dD
-  DSTD_TRYH(dot(ws.dD, sv.E, nadj, dalpha, ws.part, s));
-  DSTD_TRYH(reduce_rows(ws.dD, g.NN2, g.B, g.A, (long long)g.A * g.NN2, 1, g.NN2, dA, 1.f, ws.red, s));
-  DSTD_TRYH(scale_by(ws.dD, alpha, nadj, s));
-  float* dE = ws.dD;
-  DSTD_TRYH(reduce_rows(dE, g.A, g.B, g.NN2, (long long)g.A * g.NN2, g.NN2, 1, gr->brm, 1.f, ws.red, s));
+  // Adj = alpha * (conv_rm(M)) + A:  dalpha, dA, d b_rm, and dE = alpha dD in place
+  DSTD_TRYH(adj_bwd(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, dA, gr->brm, dalpha, ws.red, s));
+  const float* dE = ws.dD;
   Gemm wr;  // dWrm[a][k] = sum_{n,ij} dE[n][a][ij] M[n][k][ij]
   wr.M = g.A, wr.N = 2 * g.A, wr.K = g.NN2, wr.nb1 = g.B, wr.reduce = 1;
   wr.A = dE, wr.a_b1 = (long long)g.A * g.NN2, wr.a_m = g.NN2, wr.a_k = 1;
@@ -236,13 +248,25 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   dm.B = dE, dm.b_b1 = (long long)g.A * g.NN2, dm.b_k = g.NN2, dm.b_n = 1;
   dm.C = ws.dM, dm.c_b1 = 2LL * g.A * g.NN2, dm.c_m = g.NN2, dm.c_n = 1;
   DSTD_TRYH(gemm(dm, nullptr, s));
-  const size_t npq = (size_t)g.B * 2 * g.TV;
-  DSTD_TRYH(hipMemsetAsync(ws.dP, 0, npq * sizeof(float), s));
-  DSTD_TRYH(hipMemsetAsync(ws.dQ, 0, npq * sizeof(float), s));
-  DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.A, g.NN, ws.dP, ws.dQ, s));
-  DSTD_TRYH(conv_bwd(w->wf, x, ws.dF, dx, gr->wf, gr->bf, g.B, g.cin, g.cout, g.TV, ws.gs, ws.red, s));
-  DSTD_TRYH(conv_bwd(w->wm1, x, ws.dP, dx, gr->wm1, gr->bm1, g.B, g.cin, 2, g.TV, ws.gs, ws.red, s));
-  return conv_bwd(w->wm2, x, ws.dQ, dx, gr->wm2, gr->bm2, g.B, g.cin, 2, g.TV, ws.gs, ws.red, s);
+  // dP, dQ -> rows [cout, cout+4) of dG
+  float* dP = ws.dG + (size_t)g.cout * g.TV;
+  DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.A, g.NN, dP, dP + 2 * (size_t)g.TV, s));
+  // the three 1x1 convs at once: dx += Wp^T dG;  [dWp | dbp] = sum dG [x; 1]^T
+  if (dx) DSTD_TRYH(gemm(conv_dx(sv.Wp, ws.dG, dx, g.B, g.cin, g.CG(), g.TV), ws.gs, s));
+  Gemm gw = conv_dw(ws.dG, x, ws.gW, g.B, g.cin + 1, g.CG(), g.TV);
+  gw.b_ones_last = 1;
+  gw.beta = 0.f;
+  gw.b_b1 = (long long)g.cin * g.TV;
+  DSTD_TRYH(gemm(gw, ws.gs, s));
+  const int ld = g.cin + 1;
+  CopyJobs js;
+  js.add(ws.gW, gr->wf, g.cout, g.cin, ld, g.cin, 1);
+  js.add(ws.gW + (size_t)g.cout * ld, gr->wm1, 2, g.cin, ld, g.cin, 1);
+  js.add(ws.gW + (size_t)(g.cout + 2) * ld, gr->wm2, 2, g.cin, ld, g.cin, 1);
+  js.add(ws.gW + g.cin, gr->bf, g.cout, 1, ld, 1, 1);
+  js.add(ws.gW + (size_t)g.cout * ld + g.cin, gr->bm1, 2, 1, ld, 1, 1);
+  js.add(ws.gW + (size_t)(g.cout + 2) * ld + g.cin, gr->bm2, 2, 1, ld, 1, 1);
+  return copy_jobs(js, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -298,7 +322,7 @@ void carve_block_ws(Carver& cv, BlockWs& w, int B, int T, int V, std::initialize
   w.dysp = cv.take(act);
   w.dr = cv.take(act);
   w.drc = res ? cv.take(act) : nullptr;
-  w.dAs = cv.take(V * V);
+  w.dAs = cv.take(2 * V * V);
   w.pp = cv.take(cmax);
 }
 
@@ -310,6 +334,12 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
   DSTD_TRYH(fma3(p->A_s, p->W_s, p->R_s, S.as, (size_t)2 * V * V, s));
   DSTD_TRYH(fma3(p->A_t, nullptr, p->R_t, S.at, (size_t)T * T, s));
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
+  const OpGeom gt(DSTD_MODE_TEMPORAL, B, cout, cout, T, V);
+  CopyJobs js;  // conv weights of the block's three ops -> packed [W_f; W_m1; W_m2]
+  pack_jobs(js, &p->conv_s[0], S.op[0], gs);
+  pack_jobs(js, &p->conv_s[1], S.op[1], gs);
+  pack_jobs(js, &p->conv_t, S.op[2], gt);
+  DSTD_TRYH(copy_jobs(js, s));
   for (int i = 0; i < 2; ++i)  // :145-150
     DSTD_TRYH(op_fwd(gs, x, &p->conv_s[i], S.as + i * V * V, p->alpha_sm, S.ysp, i ? 1.f : 0.f, S.op[i], s));
   const float* r = x;
@@ -344,8 +374,7 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.mean = S.mean;
   bb.rstd = S.rstd;
   DSTD_TRYH(bn_train_fwd(bb, B, cout, T, V, S.red, s));
-  const OpGeom gt(DSTD_MODE_TEMPORAL, B, cout, cout, T, V);  // :156-162
-  return op_fwd(gt, S.h, &p->conv_t, S.at, p->alpha_tm, y, 0.f, S.op[2], s);
+  return op_fwd(gt, S.h, &p->conv_t, S.at, p->alpha_tm, y, 0.f, S.op[2], s);  // :156-162
 }
 
 hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, int V, const BlockSaved& S,
@@ -386,15 +415,12 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
     DSTD_TRYH(acc_mul(W.dr, nullptr, dx, act, s));
   }
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
-  for (int i = 0; i < 2; ++i) {
-    // A_s*W_s + R_s with A_s constant: dR_s = dA, dW_s = dA * A_s
-    DSTD_TRYH(hipMemsetAsync(W.dAs, 0, (size_t)V * V * sizeof(float), s));
-    DSTD_TRYH(op_bwd(gs, x, &p->conv_s[i], p->alpha_sm, S.op[i], W.dysp, dx, &g->conv_s[i], W.dAs, g->alpha_sm,
-                     W.op, s));
-    DSTD_TRYH(acc_mul(W.dAs, nullptr, g->R_s + i * V * V, (size_t)V * V, s));
-    DSTD_TRYH(acc_mul(W.dAs, p->A_s + i * V * V, g->W_s + i * V * V, (size_t)V * V, s));
-  }
-  return hipSuccess;
+  DSTD_TRYH(hipMemsetAsync(W.dAs, 0, (size_t)2 * V * V * sizeof(float), s));
+  for (int i = 0; i < 2; ++i)
+    DSTD_TRYH(op_bwd(gs, x, &p->conv_s[i], p->alpha_sm, S.op[i], W.dysp, dx, &g->conv_s[i], W.dAs + i * V * V,
+                     g->alpha_sm, W.op, s));
+  // A_s*W_s + R_s with A_s constant: dR_s = dA, dW_s = dA * A_s (both graphs)
+  return adj_param_grads(W.dAs, p->A_s, g->R_s, g->W_s, (size_t)2 * V * V, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -473,6 +499,9 @@ int dstd_dstdgc_train_fwd(int mode, const float* x, int B, int cin, int cout, in
   Carver cv{(char*)saved};
   OpSaved sv;
   carve_op_saved(cv, sv, g);
+  CopyJobs js;
+  pack_jobs(js, w, sv, g);
+  DSTD_TRY(copy_jobs(js, (hipStream_t)stream));
   DSTD_TRY(op_fwd(g, x, w, A, alpha, y, 0.f, sv, (hipStream_t)stream));
   return DSTD_OK;
 }
