@@ -142,6 +142,19 @@ def lib():
         L.dstd_mpjpe_bwd.argtypes = [vp, vp, sz, vp, f32, vp, vp]
         L.dstd_frame_mpjpe.restype = ci
         L.dstd_frame_mpjpe.argtypes = [vp, vp, ci, ci, ci, ci, vp, ci, vp, vp, ci, vp, vp]
+        # non-refine ST_GCNN_layer branch (include/dstd_gcn_aux.h)
+        L.dstd_ctg_workspace_bytes.restype = sz
+        L.dstd_ctg_workspace_bytes.argtypes = [ci] * 4
+        L.dstd_ctg_fwd.restype = ci
+        L.dstd_ctg_fwd.argtypes = [vp, ci, ci, ci, ci, vp, vp, vp, vp, vp, sz, vp]
+        L.dstd_ctg_bwd.restype = ci
+        L.dstd_ctg_bwd.argtypes = [vp, ci, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
+        L.dstd_conv2d_workspace_bytes.restype = sz
+        L.dstd_conv2d_workspace_bytes.argtypes = [ci] * 11
+        L.dstd_conv2d_fwd.restype = ci
+        L.dstd_conv2d_fwd.argtypes = [vp, ci, ci, ci, ci, vp, vp] + [ci] * 7 + [vp, vp, sz, vp]
+        L.dstd_conv2d_bwd.restype = ci
+        L.dstd_conv2d_bwd.argtypes = [vp, ci, ci, ci, ci, vp] + [ci] * 7 + [vp, vp, vp, vp, vp, sz, vp]
         _lib = L
     return _lib
 
@@ -154,6 +167,8 @@ TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_b
                  "dstd_block_train_fwd", "dstd_block_train_bwd", "dstd_model_train_saved_bytes",
                  "dstd_model_train_workspace_bytes", "dstd_model_train_fwd", "dstd_model_train_bwd",
                  "dstd_loss_workspace_bytes", "dstd_mpjpe_fwd", "dstd_mpjpe_bwd", "dstd_frame_mpjpe")
+AUX_EXPORTS = ("dstd_ctg_workspace_bytes", "dstd_ctg_fwd", "dstd_ctg_bwd", "dstd_conv2d_workspace_bytes",
+               "dstd_conv2d_fwd", "dstd_conv2d_bwd")
 
 
 def check(code, what):

@@ -4,7 +4,7 @@
 class with ``model_opts[model_type]`` (the yaml ``model.dstdgcn`` section);
 unknown names raise KeyError exactly like the reference's dict lookup.
 """
-from .dstdgcn import DSTDGC, DSTDGCB, DSTDGCN, BatchNorm, ST_GCNN_layer  # noqa: F401
+from .dstdgcn import DSTDGC, DSTDGCB, DSTDGCN, BatchNorm, Conv2d, ConvTemporalGraphical, ST_GCNN_layer  # noqa: F401
 
 _REGISTRY = {"dstdgcn": DSTDGCN}
 

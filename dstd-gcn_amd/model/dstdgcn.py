@@ -364,10 +364,123 @@ class DSTDGCB(nn.Module):
         return _mark(y, x, *self.parameters())
 
 
+def _ptr_or_none(t):
+    return t.data_ptr() if t is not None else None
+
+
+class _CTGFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, Tm, A, A_fixed):
+        L = native.lib()
+        B, C, T, V = x.shape
+        dev = x.device
+        y = torch.empty_like(x)
+        ws = native.workspace(dev, L.dstd_ctg_workspace_bytes(B, C, T, V))
+        code = L.dstd_ctg_fwd(native.ptr(x, "x"), B, C, T, V, native.ptr(Tm, "T"), native.ptr(A, "A"),
+                              native.ptr(A_fixed, "A_fixed"), native.ptr(y, "y"), ws.data_ptr(), ws.numel(),
+                              native.stream_handle(dev))
+        native.check(code, "dstd_ctg_fwd")
+        ctx.save_for_backward(x, Tm, A, A_fixed)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = native.lib()
+        x, Tm, A, A_fixed = ctx.saved_tensors
+        B, C, T, V = x.shape
+        dev = x.device
+        dy = dy.contiguous()
+        dx = torch.zeros_like(x) if ctx.needs_input_grad[0] else None
+        dTm, dA = torch.zeros_like(Tm), torch.zeros_like(A)
+        ws = native.workspace(dev, L.dstd_ctg_workspace_bytes(B, C, T, V))
+        code = L.dstd_ctg_bwd(native.ptr(x, "x"), B, C, T, V, native.ptr(Tm, "T"), native.ptr(A, "A"),
+                              native.ptr(A_fixed, "A_fixed"), native.ptr(dy, "dy"), _ptr_or_none(dx), dTm.data_ptr(),
+                              dA.data_ptr(), ws.data_ptr(), ws.numel(), native.stream_handle(dev))
+        native.check(code, "dstd_ctg_bwd")
+        return dx, dTm, dA, None
+
+
+class ConvTemporalGraphical(nn.Module):
+    """Learnable temporal (T [V,T,T]) then spatial (A [T,V,V] + fixed skeleton)
+    graph mixing (reference :166-188).  Only reachable through
+    ST_GCNN_layer(refine=False), which no shipped config builds."""
+
+    def __init__(self, time_dim, joints_dim, layout="h36m"):
+        super().__init__()
+        self.A = nn.Parameter(torch.FloatTensor(time_dim, joints_dim, joints_dim))
+        stdv = 1.0 / math.sqrt(self.A.size(1))
+        self.A.data.uniform_(-stdv, stdv)
+        self.T = nn.Parameter(torch.FloatTensor(joints_dim, time_dim, time_dim))
+        stdv = 1.0 / math.sqrt(self.T.size(1))
+        self.T.data.uniform_(-stdv, stdv)
+        adj = Graph(layout).get_adjacency()[np.newaxis, :]
+        self.A_fixed = nn.Parameter(torch.FloatTensor(adj), requires_grad=False)
+
+    def forward(self, x):
+        x = x.contiguous()
+        native.require_device(x, "x")
+        return _CTGFn.apply(x, self.T.contiguous(), self.A.contiguous(), self.A_fixed.contiguous())
+
+
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, geom):
+        L = native.lib()
+        B, cin, H, W = x.shape
+        cout, kh, kw, sh, sw, ph, pw = geom
+        Ho, Wo = (H + 2 * ph - kh) // sh + 1, (W + 2 * pw - kw) // sw + 1
+        dev = x.device
+        y = torch.empty(B, cout, Ho, Wo, dtype=torch.float32, device=dev)
+        nbytes = L.dstd_conv2d_workspace_bytes(B, cin, cout, H, W, kh, kw, sh, sw, ph, pw)
+        ws = native.workspace(dev, nbytes)
+        code = L.dstd_conv2d_fwd(native.ptr(x, "x"), B, cin, H, W, native.ptr(weight, "weight"), _ptr_or_none(bias),
+                                 cout, kh, kw, sh, sw, ph, pw, native.ptr(y, "y"), ws.data_ptr(), ws.numel(),
+                                 native.stream_handle(dev))
+        native.check(code, "dstd_conv2d_fwd")
+        ctx.geom = geom
+        ctx.save_for_backward(x, weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        L = native.lib()
+        x, weight, bias = ctx.saved_tensors
+        B, cin, H, W = x.shape
+        cout, kh, kw, sh, sw, ph, pw = ctx.geom
+        dev = x.device
+        dy = dy.contiguous()
+        dx = torch.zeros_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.zeros_like(weight)
+        db = torch.zeros_like(bias) if bias is not None else None
+        nbytes = L.dstd_conv2d_workspace_bytes(B, cin, cout, H, W, kh, kw, sh, sw, ph, pw)
+        ws = native.workspace(dev, nbytes)
+        code = L.dstd_conv2d_bwd(native.ptr(x, "x"), B, cin, H, W, native.ptr(weight, "weight"), cout, kh, kw, sh, sw,
+                                 ph, pw, native.ptr(dy, "dy"), _ptr_or_none(dx), dw.data_ptr(), _ptr_or_none(db),
+                                 ws.data_ptr(), ws.numel(), native.stream_handle(dev))
+        native.check(code, "dstd_conv2d_bwd")
+        return dx, dw, db, None
+
+
+class Conv2d(nn.Conv2d):
+    """nn.Conv2d (same parameters / state_dict) computed by the native kernels
+    (include/dstd_gcn_aux.h); groups = dilation = 1, zero padding."""
+
+    def forward(self, x):
+        if self.groups != 1 or self.dilation != (1, 1) or self.padding_mode != "zeros" or isinstance(self.padding,
+                                                                                                       str):
+            raise NotImplementedError("native Conv2d: groups=1, dilation=1, numeric zero padding only")
+        x = x.contiguous()
+        native.require_device(x, "x")
+        geom = (self.out_channels, *self.kernel_size, *self.stride, *self.padding)
+        return _Conv2dFn.apply(x, self.weight.contiguous(), None if self.bias is None else self.bias.contiguous(),
+                               geom)
+
+
 class ST_GCNN_layer(nn.Module):
     """Wrapper of one DSTDGCB plus an optional residual (reference :191-249).
-    Only ``refine=True`` exists in the shipped configs; the STS-GCN style
-    ``refine=False`` branch (ConvTemporalGraphical) is not built."""
+    Every shipped config builds ``refine=True``; the STS-GCN style
+    ``refine=False`` branch (ConvTemporalGraphical + a k_t x k_v Conv2d,
+    :218-223) runs on the native kernels of include/dstd_gcn_aux.h."""
 
     def __init__(self, in_channels, out_channels, kernel_size, stride, time_dim, joints_dim, bias=True,
                  refine=False, residual=True, layout="h36m"):
@@ -376,23 +489,30 @@ class ST_GCNN_layer(nn.Module):
         self.refine = refine
         assert self.kernel_size[0] % 2 == 1
         assert self.kernel_size[1] % 2 == 1
-        if not refine:
-            raise NotImplementedError("ST_GCNN_layer(refine=False) (ConvTemporalGraphical) is unreachable in the "
-                                      "shipped configs and not built (SURVEY §8(f) row 4)")
-        self.stgcn = nn.ModuleList([nn.Sequential(DSTDGCB(in_channels, out_channels, time_dim, joints_dim, layout))])
+        padding = ((self.kernel_size[0] - 1) // 2, (self.kernel_size[1] - 1) // 2)
+        if refine:
+            self.stgcn = nn.ModuleList(
+                [nn.Sequential(DSTDGCB(in_channels, out_channels, time_dim, joints_dim, layout))])
+        else:
+            self.stgcn = nn.Sequential(ConvTemporalGraphical(time_dim, joints_dim, layout),
+                                       Conv2d(in_channels, out_channels, (self.kernel_size[0], self.kernel_size[1]),
+                                              (stride, stride), padding))
         if not residual:
             self.residual = None
         elif stride != 1 or in_channels != out_channels:
-            self.residual = nn.Conv2d(in_channels, out_channels, kernel_size=1, stride=1)
+            self.residual = Conv2d(in_channels, out_channels, kernel_size=1, stride=1)
         else:
             self.residual = nn.Identity()
         self.apply(weights_init)
 
     def forward(self, x):
-        y = None
-        for stb in self.stgcn:
-            z = stb(x)
-            y = z if y is None else y + z
+        if self.refine:
+            y = None
+            for stb in self.stgcn:
+                z = stb(x)
+                y = z if y is None else y + z
+        else:
+            y = self.stgcn(x)
         if self.residual is not None:
             y = y + self.residual(x)
         return y

@@ -134,6 +134,24 @@ def dstdgcn_fn(x, sd, num_layers, training=False):
     return y.permute(0, 2, 3, 1) + residual                           # :314-315
 
 
+def ctg(x, p):
+    """ConvTemporalGraphical.forward (model/dstdgcn.py:185-188)."""
+    x = torch.einsum("nctv,vtq->ncqv", x, p["T"])
+    return torch.einsum("nctv,tvw->nctw", x, p["A"] + p["A_fixed"])
+
+
+def st_gcnn_layer_plain(x, p, kernel_size, stride):
+    """ST_GCNN_layer(refine=False).forward (model/dstdgcn.py:218-223, 234-249):
+    ConvTemporalGraphical, then Conv2d(kernel_size, stride, 'same' padding),
+    plus the residual (Conv2d 1x1 when present in ``p``, else identity)."""
+    pad = ((kernel_size[0] - 1) // 2, (kernel_size[1] - 1) // 2)
+    y = ctg(x, sub(p, "stgcn.0."))
+    y = torch.nn.functional.conv2d(y, p["stgcn.1.weight"], p["stgcn.1.bias"], stride=stride, padding=pad)
+    if "residual.weight" in p:
+        return y + torch.nn.functional.conv2d(x, p["residual.weight"], p["residual.bias"])
+    return y + x
+
+
 def dstdgcb_forward(x, sd, dtype=torch.float64):
     sd = {k: _t(v, dtype) for k, v in sd.items() if not k.endswith("num_batches_tracked")}
     return dstdgcb(_t(x, dtype), sd)

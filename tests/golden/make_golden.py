@@ -19,8 +19,10 @@ Fixture list (all committed):
   model_<cfg>.npz     whole DSTDGCN (h36m, cmu, 3dpw, h36m75) at B=4
   engine.npz          mpjpe_error_3d + PredictionEngine.test metric + 3DPW loss curve
   train_grads.npz     fp64 gradients / loss curve of the engine.npz training run
+  plain_layers.npz    ST_GCNN_layer(refine=False): ConvTemporalGraphical + KxK conv
 
-``python tests/golden/make_golden.py train`` regenerates train_grads.npz only.
+``python tests/golden/make_golden.py train`` / ``plain`` regenerates
+train_grads.npz / plain_layers.npz only.
 """
 import copy
 import os
@@ -366,6 +368,31 @@ def gen_train_grads(gen):
     np.savez_compressed(os.path.join(HERE, "train_grads.npz"), **out)
 
 
+def gen_plain_layers(gen):
+    """ST_GCNN_layer(refine=False): ConvTemporalGraphical + k_t x k_v Conv2d
+    (model/dstdgcn.py:166-188, 218-223) -- dead in the shipped configs, kept
+    for API completeness."""
+    from model.dstdgcn import ST_GCNN_layer  # reference
+    cases = [("p_64_32_k31", 64, 32, [3, 1], 1, 35, 22), ("p_16_16_k33", 16, 16, [3, 3], 1, 20, 22),
+             ("p_8_12_k11", 8, 12, [1, 1], 1, 10, 22)]
+    out = {}
+    for name, cin, cout, ks, stride, T, V in cases:
+        layer = ST_GCNN_layer(cin, cout, ks, stride, T, V, True, False, True, "h36m")
+        with torch.no_grad():
+            for m in layer.modules():
+                if isinstance(m, torch.nn.Conv2d):
+                    m.bias.copy_(0.1 * torch.randn(m.bias.shape, generator=gen))
+        x = torch.randn(2, cin, T, V, generator=gen)
+        with torch.no_grad():
+            y32 = layer(x).numpy()
+        y64 = run64(layer, x)
+        out[f"{name}/x"] = x.numpy()
+        put_outputs(out, f"{name}/", y32, y64)
+        for k, v in sd_numpy(layer).items():
+            out[f"{name}/sd/{k}"] = v
+    np.savez_compressed(os.path.join(HERE, "plain_layers.npz"), **out)
+
+
 def main():
     torch.set_num_threads(8)
     gen = torch.Generator().manual_seed(20250725)
@@ -373,12 +400,16 @@ def main():
     if sys.argv[1:] == ["train"]:
         gen_train_grads(gen)
         return
+    if sys.argv[1:] == ["plain"]:
+        gen_plain_layers(gen)
+        return
     gen_graphs()
     gen_ops(gen)
     gen_blocks(gen)
     gen_models(gen)
     gen_engine(gen)
     gen_train_grads(gen)
+    gen_plain_layers(gen)
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

@@ -131,3 +131,31 @@ def test_train_mode_on_cpu_fails_loudly():
     blk = DSTDGCB(64, 64, 35, 22, "h36m").train()
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         blk(torch.zeros(2, 64, 35, 22))
+
+
+def test_library_exports_every_aux_header_symbol():
+    L = native.lib()
+    syms = header_symbols("dstd_gcn_aux.h")
+    assert len(syms) == 6, syms
+    for s in syms:
+        assert hasattr(L, s), s
+    assert set(syms) == set(native.AUX_EXPORTS)
+    assert L.dstd_ctg_fwd(None, 2, 8, 10, 22, None, None, None, None, None, 0, None) == -1
+    assert L.dstd_conv2d_fwd(None, 2, 8, 10, 22, None, None, 8, 3, 1, 1, 1, 1, 0, None, None, 0, None) == -1
+
+
+def test_plain_st_gcnn_layer_schema_matches_reference():
+    """ST_GCNN_layer(refine=False) builds ConvTemporalGraphical + Conv2d with
+    the reference's parameter names and shapes (plain_layers.npz state dicts)."""
+    from model import ST_GCNN_layer
+    d = load_npz("plain_layers.npz")
+    for name, (cin, cout, ks, T) in {"p_64_32_k31": (64, 32, [3, 1], 35), "p_16_16_k33": (16, 16, [3, 3], 20),
+                                     "p_8_12_k11": (8, 12, [1, 1], 10)}.items():
+        layer = ST_GCNN_layer(cin, cout, ks, 1, T, 22, True, False, True, "h36m")
+        ref = group(d, f"{name}/sd/")
+        sd = layer.state_dict()
+        assert list(sd.keys()) == list(ref.keys())
+        for k in ref:
+            assert tuple(sd[k].shape) == ref[k].shape, k
+        assert np.array_equal(sd["stgcn.0.A_fixed"].numpy(), ref["stgcn.0.A_fixed"])
+        layer.load_state_dict({k: torch.from_numpy(v) for k, v in ref.items()})

@@ -311,3 +311,56 @@ def test_engine_test_metric_matches_reference():
     ref = d["test/metric"]
     assert np.abs(metric - ref).max() / np.abs(ref).max() < 2e-4
     assert abs(avg - float(d["test/avg"])) / float(d["test/avg"]) < 2e-4
+
+
+# ---- ST_GCNN_layer(refine=False): ConvTemporalGraphical + KxK conv (§8(f) row 4) ----
+PLAIN = {"p_64_32_k31": (64, 32, [3, 1], 35), "p_16_16_k33": (16, 16, [3, 3], 20), "p_8_12_k11": (8, 12, [1, 1], 10)}
+
+
+@pytest.mark.parametrize("name", list(PLAIN))
+def test_plain_st_gcnn_layer_forward_backward(name):
+    from model import ST_GCNN_layer
+    cin, cout, ks, T = PLAIN[name]
+    d = load_npz("plain_layers.npz")
+    sd = group(d, f"{name}/sd/")
+    layer = ST_GCNN_layer(cin, cout, ks, 1, T, 22, True, False, True, "h36m")
+    layer.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    layer = layer.to(DEV)
+    x = torch.from_numpy(d[f"{name}/x"])
+    xg = x.to(DEV).requires_grad_(True)
+    y = layer(xg)
+    assert rel(y, torch.from_numpy(d[f"{name}/y64"])) < 1e-4
+    w = torch.randn(y.shape)
+    (y * w.to(DEV)).sum().backward()
+    P = {k: torch.from_numpy(v).double().requires_grad_(not k.endswith("A_fixed")) for k, v in sd.items()}
+    x64 = x.double().requires_grad_(True)
+    (O.st_gcnn_layer_plain(x64, P, ks, 1) * w.double()).sum().backward()
+    assert rel(xg.grad, x64.grad) < 1e-4
+    for k, p in layer.named_parameters():
+        if k.endswith("A_fixed"):
+            assert p.grad is None
+            continue
+        assert rel(p.grad, P[k].grad) < 1e-4, k
+
+
+def test_native_conv2d_strided_padded():
+    """The KxK Conv2d kernels on a stride-2, asymmetric-padding case."""
+    from model import Conv2d
+    torch.manual_seed(3)
+    conv = Conv2d(5, 7, (3, 5), stride=(2, 1), padding=(1, 2))
+    x = torch.randn(2, 5, 11, 9)
+    ref = torch.nn.functional.conv2d(x.double(), conv.weight.double(), conv.bias.double(), stride=(2, 1),
+                                     padding=(1, 2))
+    conv = conv.to(DEV)
+    xg = x.to(DEV).requires_grad_(True)
+    y = conv(xg)
+    assert y.shape == ref.shape and rel(y, ref) < 1e-5
+    w = torch.randn(ref.shape)
+    (y * w.to(DEV)).sum().backward()
+    x64 = x.double().requires_grad_(True)
+    W64 = conv.weight.detach().cpu().double().requires_grad_(True)
+    b64 = conv.bias.detach().cpu().double().requires_grad_(True)
+    (torch.nn.functional.conv2d(x64, W64, b64, stride=(2, 1), padding=(1, 2)) * w.double()).sum().backward()
+    assert rel(xg.grad, x64.grad) < 1e-5
+    assert rel(conv.weight.grad, W64.grad) < 1e-5
+    assert rel(conv.bias.grad, b64.grad) < 1e-5

@@ -97,3 +97,17 @@ def test_oracle_train_curve():
     ref32 = d["train/losses"]
     assert abs(ref32[0] - c64[0]) / c64[0] < 1e-5
     assert np.abs(ref32 - c64).max() / c64.max() < 0.06
+
+
+PLAIN = {"p_64_32_k31": ([3, 1], 1), "p_16_16_k33": ([3, 3], 1), "p_8_12_k11": ([1, 1], 1)}
+
+
+@pytest.mark.parametrize("name", list(PLAIN))
+def test_oracle_plain_st_gcnn_layer(name):
+    """ST_GCNN_layer(refine=False) (ConvTemporalGraphical + KxK conv) vs the
+    reference's own fp64 output (plain_layers.npz)."""
+    d = load_npz("plain_layers.npz")
+    p = {k: torch.from_numpy(v).double() for k, v in group(d, f"{name}/sd/").items()}
+    ks, stride = PLAIN[name]
+    y = O.st_gcnn_layer_plain(torch.from_numpy(d[f"{name}/x"]).double(), p, ks, stride)
+    assert rel_err(y.numpy(), d[f"{name}/y64"]) < 1e-6
