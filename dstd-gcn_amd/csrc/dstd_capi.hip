@@ -1,11 +1,15 @@
 // C ABI (include/dstd_gcn.h): argument checking, workspace carving and the
 // launch sequence of one DSTDGC / DSTDGCB / DSTDGCN forward.
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
 
 #include <vector>
 
 #include "../../include/dstd_gcn.h"
 #include "dstd_common.h"
+#include "dstd_hilo.h"
 #include "dstd_kernels.h"
 
 using namespace dstd;
@@ -78,6 +82,29 @@ struct BlockFold {
   float* rbn_h;
   float* astat_s;  // [2][V][V]
   float* astat_t;  // [T][T]
+  // split-f16 weight images (k_hl_prep, dstd_hilo.h) of the 64 -> 64 GC kernels
+  uint4* hl_ws[2];  // conv_s[g].conv_f
+  uint4* hl_pqs;    // conv_t.conv_m1/m2 (P/Q written by the spatial kernel)
+  uint4* hl_wt;     // conv_t.conv_f
+  uint4* hl_pqt;    // next block's conv_s[*].conv_m1/m2 (P/Q written by the temporal kernel)
+  float* hl_scale;  // [5]: 2^-s of ws0, ws1, pqs, wt, pqt
+};
+
+// Split-f16 GC kernels (dstd_hilo.hip) where the shape has them: 1 (default),
+// or 0 for the exact-fp32 kernels everywhere (env DSTD_HILO=0 or
+// dstd_set_gc_precision).
+int g_hl_mode = -1;
+bool hl_on() {
+  if (g_hl_mode < 0) {
+    const char* e = getenv("DSTD_HILO");
+    g_hl_mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_hl_mode == 1;
+}
+
+// Which GC launches of a block run the split-f16 kernels.
+struct BlockHL {
+  bool s, t;
 };
 
 struct BlockScratch {
@@ -94,11 +121,28 @@ void carve_fold(Carver& cv, BlockFold& f, int T, int V, int cout, bool res) {
   f.rbn_h = res ? cv.take((size_t)cout * V) : nullptr;
   f.astat_s = cv.take((size_t)2 * V * V);
   f.astat_t = cv.take((size_t)T * T);
+  auto img = [&](int n) { return reinterpret_cast<uint4*>(cv.take((size_t)4 * n)); };
+  f.hl_ws[0] = img(kHLConvImg);
+  f.hl_ws[1] = img(kHLConvImg);
+  f.hl_pqs = img(kHLPQImg);
+  f.hl_wt = img(kHLConvImg);
+  f.hl_pqt = img(kHLPQImg);
+  f.hl_scale = cv.take(8);
+}
+
+// adjacency scratch: the larger of the fp32 rows and the split-f16 planes
+size_t adj_s_floats(int B, int T, int V) {
+  const size_t row = std::max((size_t)adj_ld_spatial(V), (size_t)V * hl_sl_spatial(V));
+  return (size_t)B * 2 * T * row;
+}
+size_t adj_t_floats(int B, int T, int V) {
+  const size_t row = std::max((size_t)adj_ld_temporal(T), (size_t)T * hl_sl_temporal(T));
+  return (size_t)B * V * row;
 }
 
 void carve_scratch(Carver& cv, BlockScratch& s, int B, int T, int V) {
-  s.adj_s = cv.take((size_t)B * 2 * T * adj_ld_spatial(V));
-  s.adj_t = cv.take((size_t)B * V * adj_ld_temporal(T));
+  s.adj_s = cv.take(adj_s_floats(B, T, V));
+  s.adj_t = cv.take(adj_t_floats(B, T, V));
   s.pq_s = cv.take((size_t)B * 8 * T * V);
   s.pq_t = cv.take((size_t)B * 4 * T * V);
 }
@@ -151,6 +195,37 @@ hipError_t run_fold(const FoldList& jobs, hipStream_t s) {
   return hipSuccess;
 }
 
+using HLList = std::vector<HLJob>;
+
+hipError_t run_hl_prep(const HLList& jobs, hipStream_t s) {
+  for (size_t i = 0; i < jobs.size(); i += kMaxHLJobs) {
+    HLPrepArgs ha{};
+    for (size_t j = i; j < jobs.size() && j < i + kMaxHLJobs; ++j) ha.jobs[ha.njobs++] = jobs[j];
+    hipError_t e = launch_hl_prep(ha, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+void add_hl_conv(HLList& l, const float* w, uint4* img, float* sc) {
+  HLJob j{};
+  j.kind = HLJ_CONV;
+  j.w[0] = w;
+  j.nblk = 1;
+  j.img = img;
+  j.inv_scale = sc;
+  l.push_back(j);
+}
+void add_hl_pq(HLList& l, const float* const* w, int nblk, uint4* img, float* sc) {
+  HLJob j{};
+  j.kind = HLJ_PQ;
+  for (int i = 0; i < nblk; ++i) j.w[i] = w[i];
+  j.nblk = nblk;
+  j.img = img;
+  j.inv_scale = sc;
+  l.push_back(j);
+}
+
 // What the temporal kernel does after the block (see TemporalEpi).
 struct BlockTail {
   int epi;
@@ -161,10 +236,41 @@ struct BlockTail {
   const dstd_block_params* next;  // next block: its spatial P/Q are produced here
 };
 
+BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V) {
+  BlockHL r{false, false};
+  if (!hl_on()) return r;
+  r.s = p->cin == 64 && p->cout == 64 && spatial_hl_supported(T, V);
+  r.t = p->cout == 64 && temporal_hl_supported(T, V) &&
+        (tail.epi == TEPI_ENC || tail.epi == TEPI_IN || tail.epi == TEPI_RAW) &&
+        (!tail.next || tail.next->cin == 64);
+  return r;
+}
+
+// Weight images of the block's split-f16 launches.
+void add_block_hl_jobs(HLList& l, const dstd_block_params* p, const BlockFold& f, const BlockTail& tail,
+                       const BlockHL& hl) {
+  if (hl.s) {
+    add_hl_conv(l, p->conv_s[0].wf, f.hl_ws[0], f.hl_scale + 0);
+    add_hl_conv(l, p->conv_s[1].wf, f.hl_ws[1], f.hl_scale + 1);
+    const float* w[2] = {p->conv_t.wm1, p->conv_t.wm2};
+    add_hl_pq(l, w, 2, f.hl_pqs, f.hl_scale + 2);
+  }
+  if (hl.t) {
+    add_hl_conv(l, p->conv_t.wf, f.hl_wt, f.hl_scale + 3);
+    if (tail.next) {
+      const dstd_block_params* q = tail.next;
+      const float* w[4] = {q->conv_s[0].wm1, q->conv_s[0].wm2, q->conv_s[1].wm1, q->conv_s[1].wm2};
+      add_hl_pq(l, w, 4, f.hl_pqt, f.hl_scale + 4);
+    }
+  }
+}
+
 // One DSTDGCB on NTVC activations.  pq_s must already hold P/Q of x for the
-// block's two spatial DSTDGCs.
+// block's two spatial DSTDGCs; the block's weight images (add_block_hl_jobs)
+// must be prepared when hl says so.
 hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const BlockScratch& sc, int B, int T, int V,
-                     const float* x, float* h, float* y, const BlockTail& tail, hipStream_t s, Prof& pf) {
+                     const float* x, float* h, float* y, const BlockTail& tail, hipStream_t s, Prof& pf,
+                     const BlockHL& hl) {
   const bool res = p->cin != p->cout;
   // (1) spatial adjacency for both graphs
   AdjArgs aa{};
@@ -188,15 +294,49 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   aa.ngroups = 2;
   aa.alpha = p->alpha_sm;
   aa.out = sc.adj_s;
-  aa.ldo = adj_ld_spatial(V);
-  aa.out_sN = 2L * T * aa.ldo;
-  aa.out_sG = (long)T * aa.ldo;
+  if (hl.s) {  // split-f16 planes [B][2][T][2][V][SL]
+    aa.hl = 1;
+    aa.ncol = V * hl_sl_spatial(V);
+    aa.ldo = 2 * aa.ncol;
+    aa.out_sG = (long)T * aa.ncol;
+    aa.out_sN = 2 * aa.out_sG;
+  } else {
+    aa.ldo = adj_ld_spatial(V);
+    aa.out_sN = 2L * T * aa.ldo;
+    aa.out_sG = (long)T * aa.ldo;
+  }
   pf.begin(DSTD_KIND_ADJ_S, s);
   hipError_t e = launch_adj(aa, s);
   pf.end(s);
   if (e != hipSuccess) return e;
 
   // (2) spatial GC + bn + residual + prelu, P_t/Q_t of h
+  if (hl.s) {
+    SpatialHLArgs ha{};
+    ha.x = x;
+    ha.B = B;
+    ha.T = T;
+    ha.V = V;
+    ha.adj = reinterpret_cast<const uint16_t*>(sc.adj_s);
+    for (int g = 0; g < 2; ++g) {
+      ha.wimg[g] = f.hl_ws[g];
+      ha.wscale[g] = f.hl_scale + g;
+      ha.bf[g] = p->conv_s[g].bf;
+    }
+    ha.bn_s = f.bn_s;
+    ha.bn_h = f.bn_h;
+    ha.prelu = p->prelu;
+    ha.y = h;
+    ha.pqimg = f.hl_pqs;
+    ha.pqscale = f.hl_scale + 2;
+    ha.pqb[0] = p->conv_t.bm1;
+    ha.pqb[1] = p->conv_t.bm2;
+    ha.pq = sc.pq_t;
+    pf.begin(DSTD_KIND_SPATIAL, s);
+    e = launch_spatial_hl(ha, s);
+    pf.end(s);
+    if (e != hipSuccess) return e;
+  } else {
   SpatialArgs sa{};
   sa.x = x;
   sa.B = B;
@@ -233,6 +373,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   e = launch_spatial(sa, s);
   pf.end(s);
   if (e != hipSuccess) return e;
+  }
 
   // (3) temporal adjacency
   AdjArgs ta{};
@@ -254,15 +395,53 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   ta.ngroups = 1;
   ta.alpha = p->alpha_tm;
   ta.out = sc.adj_t;
-  ta.ldo = adj_ld_temporal(T);
-  ta.out_sN = (long)V * ta.ldo;
   ta.out_sG = 0;
+  if (hl.t) {  // split-f16 planes [B][V][2][T][SL]
+    ta.hl = 1;
+    ta.ncol = T * hl_sl_temporal(T);
+    ta.ldo = 2 * ta.ncol;
+    ta.out_sN = (long)V * ta.ncol;
+  } else {
+    ta.ldo = adj_ld_temporal(T);
+    ta.out_sN = (long)V * ta.ldo;
+  }
   pf.begin(DSTD_KIND_ADJ_T, s);
   e = launch_adj(ta, s);
   pf.end(s);
   if (e != hipSuccess) return e;
 
   // (4) temporal GC + tail epilogue (+ next block's spatial P/Q)
+  if (hl.t) {
+    TemporalHLArgs ht{};
+    ht.h = h;
+    ht.B = B;
+    ht.T = T;
+    ht.V = V;
+    ht.adj = reinterpret_cast<const uint16_t*>(sc.adj_t);
+    ht.wimg = f.hl_wt;
+    ht.wscale = f.hl_scale + 3;
+    ht.bf = p->conv_t.bf;
+    ht.epi = tail.epi;
+    ht.xres = tail.xres;
+    ht.bn_s = tail.bn_s;
+    ht.bn_h = tail.bn_h;
+    ht.prelu = tail.prelu;
+    ht.y = y;
+    if (tail.next) {
+      const dstd_block_params* q = tail.next;
+      ht.pqimg = f.hl_pqt;
+      ht.pqscale = f.hl_scale + 4;
+      ht.pqb[0] = q->conv_s[0].bm1;
+      ht.pqb[1] = q->conv_s[0].bm2;
+      ht.pqb[2] = q->conv_s[1].bm1;
+      ht.pqb[3] = q->conv_s[1].bm2;
+      ht.pq = sc.pq_s;
+    }
+    pf.begin(DSTD_KIND_TEMPORAL, s);
+    e = launch_temporal_hl(ht, s);
+    pf.end(s);
+    return e;
+  }
   TemporalArgs tt{};
   tt.h = h;
   tt.B = B;
@@ -529,8 +708,12 @@ int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int
   DSTD_TRY(to_layout(x, L.xin, B, p->cin, T * V, 1, s));
   DSTD_TRY(spatial_pq(p, L.xin, B, T, V, L.sc.pq_s, s));
   BlockTail tail{TEPI_RAW, nullptr, nullptr, nullptr, nullptr, nullptr};
+  const BlockHL hl = block_hl(p, tail, T, V);
+  HLList hj;
+  add_block_hl_jobs(hj, p, L.f, tail, hl);
+  DSTD_TRY(run_hl_prep(hj, s));
   Prof pf;
-  DSTD_TRY(run_block(p, L.f, L.sc, B, T, V, L.xin, L.h, L.yout, tail, s, pf));
+  DSTD_TRY(run_block(p, L.f, L.sc, B, T, V, L.xin, L.h, L.yout, tail, s, pf, hl));
   DSTD_TRY(to_layout(L.yout, y, B, p->cout, T * V, 0, s));
   return DSTD_OK;
 }
@@ -598,35 +781,70 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
   DSTD_TRY(launch_pq(pa, s));
   pf.end(s);
 
-  // conv_st_in -> bn_in -> prelu (dropout is identity in eval)
-  float* cur = L.act[0];
-  float* h = L.act[1];
-  float* out = L.act[2];
+  // conv_st_in -> bn_in -> prelu (dropout is identity in eval); encoders
+  // x = prelu_e(bn_e(DSTDGCB(x) + x)); conv_st_out + output residual written
+  // straight into y [B][T][V][3].  Buffers rotate over act[0..2].
+  const int NB = L_ + 2;
+  const dstd_block_params* blk[DSTD_MAX_LAYERS + 2];
+  const BlockFold* fold[DSTD_MAX_LAYERS + 2];
+  BlockTail tails[DSTD_MAX_LAYERS + 2];
+  BlockHL hls[DSTD_MAX_LAYERS + 2];
+  const float* xin[DSTD_MAX_LAYERS + 2];
+  float* hbuf[DSTD_MAX_LAYERS + 2];
+  float* ybuf[DSTD_MAX_LAYERS + 2];
   {
-    BlockTail tail{TEPI_IN, nullptr, L.bnin_s, L.bnin_h, p->prelu, L_ > 0 ? &p->enc[0] : &p->st_out};
-    pf.block = 0;
-    DSTD_TRY(run_block(&p->st_in, L.f_in, L.sc, B, T, V, cur, h, out, tail, s, pf));
+    float* cur = L.act[0];
+    float* h = L.act[1];
+    float* out = L.act[2];
+    blk[0] = &p->st_in;
+    fold[0] = &L.f_in;
+    tails[0] = BlockTail{TEPI_IN, nullptr, L.bnin_s, L.bnin_h, p->prelu, L_ > 0 ? &p->enc[0] : &p->st_out};
+    xin[0] = cur;
+    hbuf[0] = h;
+    ybuf[0] = out;
+    for (int i = 0; i < L_; ++i) {
+      float* xi = out;
+      float* hh = cur;
+      float* yy = h;
+      blk[1 + i] = &p->enc[i];
+      fold[1 + i] = &L.f_enc[i];
+      tails[1 + i] = BlockTail{TEPI_ENC, xi, L.ebn_s[i], L.ebn_h[i], p->enc_prelu[i], i + 1 < L_ ? &p->enc[i + 1] : &p->st_out};
+      xin[1 + i] = xi;
+      hbuf[1 + i] = hh;
+      ybuf[1 + i] = yy;
+      cur = xi;
+      h = hh;
+      out = yy;
+    }
+    blk[NB - 1] = &p->st_out;
+    fold[NB - 1] = &L.f_out;
+    tails[NB - 1] = BlockTail{TEPI_OUT, x, nullptr, nullptr, nullptr, nullptr};
+    xin[NB - 1] = out;
+    hbuf[NB - 1] = h;
+    ybuf[NB - 1] = y;
   }
-  // encoders: x = prelu_e(bn_e(DSTDGCB(x) + x))
-  for (int i = 0; i < L_; ++i) {
-    float* xin = out;
-    float* hh = cur;
-    float* yy = h;
-    BlockTail tail{TEPI_ENC, xin, L.ebn_s[i], L.ebn_h[i], p->enc_prelu[i], i + 1 < L_ ? &p->enc[i + 1] : &p->st_out};
-    pf.block = 1 + i;
-    DSTD_TRY(run_block(&p->enc[i], L.f_enc[i], L.sc, B, T, V, xin, hh, yy, tail, s, pf));
-    cur = xin;
-    h = hh;
-    out = yy;
+  HLList hj;
+  for (int b = 0; b < NB; ++b) {
+    hls[b] = block_hl(blk[b], tails[b], T, V);
+    add_block_hl_jobs(hj, blk[b], *fold[b], tails[b], hls[b]);
   }
-  // conv_st_out + output residual, written straight into y [B][T][V][3]
-  {
-    BlockTail tail{TEPI_OUT, x, nullptr, nullptr, nullptr, nullptr};
-    pf.block = 1 + L_;
-    DSTD_TRY(run_block(&p->st_out, L.f_out, L.sc, B, T, V, out, h, y, tail, s, pf));
+  pf.begin(DSTD_KIND_FOLD, s);
+  DSTD_TRY(run_hl_prep(hj, s));
+  pf.end(s);
+  for (int b = 0; b < NB; ++b) {
+    pf.block = b;
+    DSTD_TRY(run_block(blk[b], *fold[b], L.sc, B, T, V, xin[b], hbuf[b], ybuf[b], tails[b], s, pf, hls[b]));
   }
   return DSTD_OK;
 }
+
+int dstd_set_gc_precision(int mode) {
+  if (mode != 0 && mode != 1) return DSTD_EINVAL;
+  g_hl_mode = mode;
+  return DSTD_OK;
+}
+
+int dstd_get_gc_precision(void) { return hl_on() ? 1 : 0; }
 
 int dstd_events_create(int n, void** events) {
   if (n < 0 || (n > 0 && !events)) return DSTD_EINVAL;

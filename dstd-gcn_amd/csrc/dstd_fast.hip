@@ -17,6 +17,7 @@
 // use the generic kernels.
 #include "dstd_common.h"
 #include "dstd_kernels.h"
+#include "dstd_hilo.h"
 
 // Workgroup timeline of the adjacency kernel (debug builds, -DDSTD_STAMPS):
 // s_memrealtime (100 MHz, chip-wide) at entry, staging done, compute done, exit.
@@ -271,16 +272,21 @@ struct PQFuse {
 // (one round: all prologues start together, and a second round of
 // workgroups would pay its prologue again rather than overlap it).
 // ===========================================================================
-template <int MODE, int NROW, int K, int NA>
+template <int MODE, int NROW, int K, int NA, bool HL>
 struct AdjGeom {
   static constexpr int RT = cdiv(NROW, 16), KSTEPS = cdiv(K, 4), KP = 4 * KSTEPS;
-  static constexpr int NCOL = NA * NA, NCT = cdiv(NCOL, 16);
+  // HL: columns (q, slot) with the slot order of the split-f16 GC kernels
+  // (dstd_hilo.h): spatial joints interleaved, temporal frames sequential
+  using SM = SlotMap<NA, MODE == 0>;
+  static constexpr int SL = HL ? SM::SL : NA;
+  static constexpr int NCOL = NA * SL, NCT = cdiv(NCOL, 16);
+  static constexpr int NAA = NA * NA;  // A-stat entries
   static constexpr int SA = NA + 1;  // + one padding column
   static constexpr bool WREG = RT * KSTEPS <= 64;
   static constexpr int SR = stride_mod32(RT * 16, 16);
   static constexpr int OS = 20;                         // output staging row stride
   static constexpr int STG = NWV * RT * 16 * OS;        // per-wave output staging (also W staging)
-  static constexpr int NCOLP = rup(NCOL + 1, 4);        // astat (+ padding column)
+  static constexpr int NCOLP = rup(NAA + 1, 4);         // astat (+ padding column)
   static constexpr int T = MODE == 0 ? NROW : NA;
   static constexpr int V = MODE == 0 ? NA : NROW;
   static constexpr int NCHUNK = MODE == 0 ? 1 : 2;      // column chunks per (sample, graph): one round of workgroups at B = 256
@@ -289,10 +295,11 @@ struct AdjGeom {
   static constexpr int LDS_FLOATS = 4 * KP * SA + (WREG ? 0 : KP * SR) + STG + NCOLP + 16 + 4;
 };
 
-template <int MODE, int NROW, int K, int NA>
+template <int MODE, int NROW, int K, int NA, bool HL>
 // 4 waves per SIMD (two 8-wave workgroups per CU): caps VGPRs at 128
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void k_adj_fast(AdjArgs a) {
-  using Gm = AdjGeom<MODE, NROW, K, NA>;
+  using Gm = AdjGeom<MODE, NROW, K, NA, HL>;
+  constexpr int SL = Gm::SL, NAA = Gm::NAA;
   constexpr int RT = Gm::RT, KSTEPS = Gm::KSTEPS, KP = Gm::KP, NCOL = Gm::NCOL, NCT = Gm::NCT, SA = Gm::SA;
   constexpr bool WREG = Gm::WREG;
   constexpr int SR = Gm::SR, OS = Gm::OS;
@@ -328,7 +335,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
   const float* W = a.W[g];
   Stager<float, NROW * K> sw;
   sw.load(tid, [&](int i) { return W[i]; });
-  Stager<float, NCOL> sas;
+  Stager<float, NAA> sas;
   sas.load(tid, [&](int i) { return a.astat[g][i]; });
   const float bias_v = tid < 16 * RT && tid < NROW ? a.bias[g][tid] : 0.f;
   const float alpha = *a.alpha;
@@ -343,7 +350,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
       Fl[i] = 1.f;
     }
   }
-  if (tid < Gm::NCOLP - NCOL) asl[NCOL + tid] = 0.f;
+  if (tid < Gm::NCOLP - NAA) asl[NAA + tid] = 0.f;
   if (tid < 16 * RT) bsl[tid] = bias_v;
   sw.store(tid, [&](int i, float v) { stg[i] = v; });
   sas.store(tid, [&](int i, float v) { asl[i] = v; });
@@ -393,9 +400,17 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
   const int ct_end = min(NCT, (chunk + 1) * Gm::CPC);
   for (int ct = chunk * Gm::CPC + wave; ct < ct_end; ct += NWV) {
     const int col = ct * 16 + cl;
-    const bool cv = col < NCOL;
-    const int ca = cv ? col / NA : NA;
-    const int cb = cv ? col - ca * NA : NA;
+    // ca: P index (contracted by the GC kernel), cb: Q index (its output column)
+    int ca, cb;
+    if constexpr (HL) {
+      const int q = col / SL, pi = Gm::SM::slot_idx(col - q * SL);
+      ca = col < NCOL && pi < NA ? pi : NA;
+      cb = col < NCOL && pi < NA ? q : NA;
+    } else {
+      ca = col < NCOL ? col / NA : NA;
+      cb = col < NCOL ? col - ca * NA : NA;
+    }
+    const bool cv = ca < NA;
     f32x4 acc[RT];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) acc[rt] = zero4();
@@ -434,18 +449,36 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
     }
     // epilogue: transpose the 16-column tile through this wave's LDS slot so
     // each lane stores 16 contiguous bytes of one row (1 KiB per store)
-    const float as = asl[cv ? col : NCOL];
+    const float as = asl[cv ? ca * NA + cb : NAA];
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) so[(rt * 16 + kl * 4 + j) * OS + cl] = alpha * (acc[rt][j] + brow[rt][j]) + as;
-    const int q = lane & 3;
-    const int c4 = ct * 16 + 4 * q;
+      for (int j = 0; j < 4; ++j)
+        so[(rt * 16 + kl * 4 + j) * OS + cl] = cv ? alpha * (acc[rt][j] + brow[rt][j]) + as : 0.f;
+    if constexpr (HL) {
+      // (row, 8-column group) per lane: 8 values -> hi / lo halves, one
+      // 16-byte store per plane; row stride ldo and plane stride NCOL in halves
+      uint16_t* oh = reinterpret_cast<uint16_t*>(out);
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int row = rt * 16 + (lane >> 2);
-      const float4 v = ld4(so + row * OS + 4 * q);
-      if (row < NROW && c4 < NCOL) st4(out + (size_t)row * a.ldo + c4, v);
+      for (int it = 0; it < cdiv(RT * 32, 64); ++it) {
+        const int item = lane + 64 * it, row = item >> 1, c8 = ct * 16 + 8 * (item & 1);
+        if (row < NROW && c8 < NCOL) {
+          const float4 v0 = ld4(so + row * OS + 8 * (item & 1)), v1 = ld4(so + row * OS + 8 * (item & 1) + 4);
+          uint4 hi, lo;
+          split8(v0, v1, hi, lo);
+          *reinterpret_cast<uint4*>(oh + (size_t)row * a.ldo + c8) = hi;
+          *reinterpret_cast<uint4*>(oh + (size_t)row * a.ldo + NCOL + c8) = lo;
+        }
+      }
+    } else {
+      const int q = lane & 3;
+      const int c4 = ct * 16 + 4 * q;
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int row = rt * 16 + (lane >> 2);
+        const float4 v = ld4(so + row * OS + 4 * q);
+        if (row < NROW && c4 < NCOL) st4(out + (size_t)row * a.ldo + c4, v);
+      }
     }
   }
   TL(MODE, 2)
@@ -930,16 +963,20 @@ int resident_per_cu(K k, size_t lds) {
   return nb;
 }
 
+template <int MODE, int NROW, int K, int NA, bool HL>
+hipError_t adj_fast_run_hl(const AdjArgs& a, hipStream_t s) {
+  using Gm = AdjGeom<MODE, NROW, K, NA, HL>;
+  constexpr size_t lds = (size_t)Gm::LDS_FLOATS * sizeof(float);
+  static int occ = resident_per_cu(k_adj_fast<MODE, NROW, K, NA, HL>, lds);
+  (void)occ;  // raises the LDS cap where needed
+  if (HL ? (a.ldo != 2 * Gm::NCOL || a.ncol != Gm::NCOL) : a.ldo % 4 != 0) return hipErrorNotSupported;
+  const int grid = a.B * a.ngroups * Gm::NCHUNK;
+  hipLaunchKernelGGL((k_adj_fast<MODE, NROW, K, NA, HL>), dim3(grid), dim3(NTHR), lds, s, a);
+  return hipGetLastError();
+}
 template <int MODE, int NROW, int K, int NA>
 hipError_t adj_fast_run(const AdjArgs& a, hipStream_t s) {
-  using Gm = AdjGeom<MODE, NROW, K, NA>;
-  constexpr size_t lds = (size_t)Gm::LDS_FLOATS * sizeof(float);
-  static int occ = resident_per_cu(k_adj_fast<MODE, NROW, K, NA>, lds);
-  (void)occ;  // raises the LDS cap where needed
-  if (a.ldo % 4 != 0) return hipErrorNotSupported;
-  const int grid = a.B * a.ngroups * Gm::NCHUNK;
-  hipLaunchKernelGGL((k_adj_fast<MODE, NROW, K, NA>), dim3(grid), dim3(NTHR), lds, s, a);
-  return hipGetLastError();
+  return a.hl ? adj_fast_run_hl<MODE, NROW, K, NA, true>(a, s) : adj_fast_run_hl<MODE, NROW, K, NA, false>(a, s);
 }
 
 template <int V, int KS, int CT, int G, int NI, int TT>

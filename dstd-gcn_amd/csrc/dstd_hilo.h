@@ -1,0 +1,179 @@
+// Split-f16 ("hi/lo") operand format of the 64 -> 64 GC kernels (dstd_hilo.hip).
+//
+// gfx950 runs v_mfma_f32_16x16x32_f16 at 16 cycles for 16x16x32 MACs; the
+// exact-fp32 v_mfma_f32_16x16x4_f32 needs 8 x 32 cycles for the same work.  An
+// fp32 operand a is carried as a pair of f16 values, a_hi = f16(a) and
+// a_lo = f16(a - a_hi) (22 significant bits), and a product as
+//   a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi     (three MFMAs, fp32 accumulate)
+// -- 5.3x fewer MFMA cycles than fp32.  Weights are pre-scaled by a power of
+// two (max|w| * 2^s < 2^14) so that their low halves stay normal f16 numbers;
+// the accumulator is scaled back by 2^-s (exact).  Activations, adjacency
+// entries and tanh values are O(1) and split unscaled.  Emulated on the
+// fixtures (scripts/split_precision.py) the whole-model error against the
+// fp64 reference stays at the level of an fp32 run (0.6-1.1x the reference's
+// own fp32 error), per op 0.5-0.9x.
+//
+// MFMA 16x16x32 f16 lane maps: A[i = lane&15][k = 8*(lane>>4) + e],
+// B[k = 8*(lane>>4) + e][j = lane&15], e = 0..7; C/D as for every 16x16 MFMA,
+// D[4*(lane>>4) + r][lane&15].
+//
+// The contraction of an aggregation (joint v of the spatial GC, frame t of
+// the temporal GC) runs in K-steps of 32 slots.  Slot e = 4*mm + r of lane
+// group kg in K-step s is row 4*kg + r of conv tile 2*s + mm -- so the conv
+// accumulators of tiles 2s and 2s+1 ARE the A operand of K-step s (after the
+// hi/lo split) -- and stands for index
+//   interleaved (IL): 32*s + 8*kg + 4*mm + r     (spatial: 22 joints in 3 groups)
+//   sequential      : 32*s + 16*mm + 4*kg + r    (temporal: tile m = frames 16m..16m+15)
+// The adjacency writer stores, per output column (w / u) and per plane
+// (hi, lo), the slot groups (s, kg) that hold a valid index, 8 halves each,
+// in slot order: one 16-byte load per lane gives a B fragment.
+#pragma once
+#include "dstd_common.h"
+
+namespace dstd {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// 8 fp32 values -> hi = f16(v) (round to nearest), lo = f16(v - hi)
+__device__ __forceinline__ void split8(const float4& a, const float4& b, f16x8& hi, f16x8& lo) {
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const _Float16 h = (_Float16)v[e];
+    hi[e] = h;
+    lo[e] = (_Float16)(v[e] - (float)h);
+  }
+}
+__device__ __forceinline__ void split8(const float4& a, const float4& b, uint4& hi, uint4& lo) {
+  f16x8 h, l;
+  split8(a, b, h, l);
+  hi = __builtin_bit_cast(uint4, h);
+  lo = __builtin_bit_cast(uint4, l);
+}
+
+template <int N, bool IL>
+struct SlotMap {
+  static constexpr int NS = cdiv(N, 32);  // K-steps
+  __host__ __device__ static constexpr int idx(int s, int kg, int e) {
+    return IL ? 32 * s + 8 * kg + e : 32 * s + 16 * (e >> 2) + 4 * kg + (e & 3);
+  }
+  // conv tile m, row i -> index
+  __host__ __device__ static constexpr int row_idx(int m, int i) { return idx(m >> 1, i >> 2, 4 * (m & 1) + (i & 3)); }
+  // lane groups of K-step s that hold a valid index (always a prefix kg < ng)
+  __host__ __device__ static constexpr int ng(int s) {
+    int g = 0;
+    for (int kg = 0; kg < 4; ++kg)
+      for (int e = 0; e < 8; ++e)
+        if (idx(s, kg, e) < N) g = kg + 1;
+    return g;
+  }
+  __host__ __device__ static constexpr int goff(int s) {
+    int o = 0;
+    for (int q = 0; q < s; ++q) o += ng(q);
+    return o;
+  }
+  static constexpr int NG = goff(NS);  // stored groups per row
+  static constexpr int SL = 8 * NG;    // halves per row and plane
+  __host__ __device__ static constexpr bool tile_used(int m) {
+    for (int i = 0; i < 16; ++i)
+      if (row_idx(m, i) < N) return true;
+    return false;
+  }
+  __host__ __device__ static constexpr int ntiles() {
+    int t = 0;
+    for (int m = 0; m < 2 * NS; ++m)
+      if (tile_used(m)) t = m + 1;
+    return t;
+  }
+  static constexpr int MT = ntiles();  // conv row tiles
+  // stored slot (0 .. SL-1) -> index (>= N: padding, stored as zero)
+  __host__ __device__ static constexpr int slot_idx(int sl) {
+    const int G = sl >> 3, e = sl & 7;
+    int s = 0;
+    while (s + 1 < NS && goff(s + 1) <= G) ++s;
+    return idx(s, G - goff(s), e);
+  }
+};
+
+// Halves per adjacency row (one output column, one plane) on the host.
+inline int hl_sl_spatial(int V) { return 8 * cdiv(V, 8); }
+inline int hl_sl_temporal(int T) {
+  int g = 0;
+  for (int s = 0; s < cdiv(T, 32); ++s) {
+    int n = 0;
+    for (int kg = 0; kg < 4; ++kg)
+      for (int e = 0; e < 8; ++e)
+        if (32 * s + 16 * (e >> 2) + 4 * kg + (e & 3) < T) n = kg + 1;
+    g += n;
+  }
+  return 8 * g;
+}
+
+// ---- weight images (one k_hl_prep launch per forward) --------------------
+// HLJ_CONV: B fragments of a transposed 64 -> 64 conv, W[c][k] (c out, k in):
+//   img[((ct*2 + ks)*2 + plane)*64 + lane] = 8 halves of 2^s * W[16ct + j][32ks + 8kg + e]
+//   (j = lane&15, kg = lane>>4), 16 KiB.
+// HLJ_PQ: A fragments of the P/Q conv of the next DSTDGC(s): row ch = 2*blk + rr
+//   of w[blk][rr*64 + c], slot (kg, e = 4mm + r) of K-step ks <-> c = 16*(2ks+mm) + 4kg + r:
+//   img[(ks*2 + plane)*64 + lane], 4 KiB.
+enum HLJobKind { HLJ_CONV = 0, HLJ_PQ = 1 };
+struct HLJob {
+  int kind;
+  const float* w[4];  // HLJ_CONV: w[0] = [64][64]; HLJ_PQ: nblk two-row blocks [2][64]
+  int nblk;
+  uint4* img;
+  float* inv_scale;   // 2^-s
+};
+constexpr int kMaxHLJobs = 48;
+struct HLPrepArgs {
+  HLJob jobs[kMaxHLJobs];
+  int njobs;
+};
+constexpr int kHLConvImg = 4 * 2 * 2 * 64;  // uint4 per HLJ_CONV image
+constexpr int kHLPQImg = 2 * 2 * 64;        // uint4 per HLJ_PQ image
+
+// ---- GC kernel arguments --------------------------------------------------
+struct SpatialHLArgs {
+  const float* x;            // NTVC [B][T][V][64]
+  int B, T, V;
+  const uint16_t* adj;       // [B][2][T][2 planes][V][SL] halves
+  const uint4* wimg[2];      // HLJ_CONV images of conv_s[g].conv_f
+  const float* wscale[2];
+  const float* bf[2];        // conv_f biases
+  const float* bn_s;         // folded BN [V][64]
+  const float* bn_h;
+  const float* prelu;
+  float* y;                  // NTVC [B][T][V][64]
+  const uint4* pqimg;        // HLJ_PQ image of conv_t.conv_m1/m2 (4 channels)
+  const float* pqscale;
+  const float* pqb[2];
+  float* pq;                 // [B][T][V][4]
+};
+
+struct TemporalHLArgs {
+  const float* h;            // NTVC [B][T][V][64]
+  int B, T, V;
+  const uint16_t* adj;       // [B][V][2 planes][T][SL] halves
+  const uint4* wimg;
+  const float* wscale;
+  const float* bf;
+  int epi;                   // TemporalEpi: ENC, IN or RAW
+  const float* xres;
+  const float* bn_s;
+  const float* bn_h;
+  const float* prelu;
+  float* y;
+  const uint4* pqimg;        // HLJ_PQ image of the next block's spatial conv_m1/m2 (8 channels) or null
+  const float* pqscale;
+  const float* pqb[4];
+  float* pq;                 // [B][V][T][8]
+};
+
+hipError_t launch_hl_prep(const HLPrepArgs& a, hipStream_t s);
+// hipErrorNotSupported when the shape has no instantiation
+hipError_t launch_spatial_hl(const SpatialHLArgs& a, hipStream_t s);
+hipError_t launch_temporal_hl(const TemporalHLArgs& a, hipStream_t s);
+bool spatial_hl_supported(int T, int V);
+bool temporal_hl_supported(int T, int V);
+
+}  // namespace dstd

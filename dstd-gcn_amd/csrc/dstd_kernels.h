@@ -85,7 +85,10 @@ struct AdjArgs {
   const float* astat[2];  // [ncol], row independent
   float* out;
   long out_sN, out_sG;
-  int ldo;             // row stride of out (>= ncol, a multiple of 4 floats)
+  int ldo;             // row stride of out (>= ncol, a multiple of 4 floats; hl: 2*ncol halves)
+  int hl;              // 1: split-f16 planes in the slot order of dstd_hilo.h: out holds halves,
+                       //    ldo counts halves (2 * ncol), out_sN / out_sG still count floats,
+                       //    ncol = NA * SL
   int ctiles_per_wg, nchunks;
 };
 

@@ -204,7 +204,7 @@ hipError_t launch_adj(AdjArgs a, hipStream_t s) {
   const int nblocks = a.B * a.ngroups * a.nchunks;
   {
     const hipError_t fe = launch_adj_fast(a, s, nblocks);
-    if (fe != hipErrorNotSupported) return fe;
+    if (fe != hipErrorNotSupported || a.hl) return fe;  // the split-f16 layout has no generic writer
   }
   const size_t lds = adj_lds_bytes(RT, a.K, a.NA);
   switch (RT) {

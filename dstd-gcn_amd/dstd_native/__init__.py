@@ -111,6 +111,10 @@ def lib():
         L.dstd_events_destroy.argtypes = [ci, ctypes.POINTER(ctypes.c_void_p)]
         L.dstd_event_elapsed_ms.restype = ci
         L.dstd_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_float)]
+        L.dstd_set_gc_precision.restype = ci
+        L.dstd_set_gc_precision.argtypes = [ci]
+        L.dstd_get_gc_precision.restype = ci
+        L.dstd_get_gc_precision.argtypes = []
         # training path (include/dstd_gcn_train.h)
         u64, f32 = ctypes.c_ulonglong, ctypes.c_float
         for n, k in (("dstd_dstdgc_train_saved_bytes", 6), ("dstd_dstdgc_train_workspace_bytes", 6),
@@ -161,7 +165,8 @@ def lib():
 
 EXPORTS = ("dstd_version", "dstd_error_string", "dstd_dstdgc_workspace_bytes", "dstd_block_workspace_bytes",
            "dstd_model_workspace_bytes", "dstd_dstdgc_fwd", "dstd_block_fwd", "dstd_model_fwd",
-           "dstd_model_fwd_profiled", "dstd_events_create", "dstd_events_destroy", "dstd_event_elapsed_ms")
+           "dstd_model_fwd_profiled", "dstd_events_create", "dstd_events_destroy", "dstd_event_elapsed_ms",
+           "dstd_set_gc_precision", "dstd_get_gc_precision")
 TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_bytes", "dstd_dstdgc_train_fwd",
                  "dstd_dstdgc_train_bwd", "dstd_block_train_saved_bytes", "dstd_block_train_workspace_bytes",
                  "dstd_block_train_fwd", "dstd_block_train_bwd", "dstd_model_train_saved_bytes",
@@ -169,6 +174,17 @@ TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_b
                  "dstd_loss_workspace_bytes", "dstd_mpjpe_fwd", "dstd_mpjpe_bwd", "dstd_frame_mpjpe")
 AUX_EXPORTS = ("dstd_ctg_workspace_bytes", "dstd_ctg_fwd", "dstd_ctg_bwd", "dstd_conv2d_workspace_bytes",
                "dstd_conv2d_fwd", "dstd_conv2d_bwd")
+
+
+def set_gc_precision(mode):
+    """Arithmetic of the 64->64 graph convolutions (include/dstd_gcn.h):
+    "split" (split-f16 MFMA, default) or "fp32" (exact-fp32 MFMA).  Returns the
+    previous mode."""
+    modes = {"fp32": 0, "split": 1}
+    L = lib()
+    prev = "split" if L.dstd_get_gc_precision() == 1 else "fp32"
+    check(L.dstd_set_gc_precision(modes[mode]), "dstd_set_gc_precision")
+    return prev
 
 
 def check(code, what):

@@ -155,6 +155,19 @@ int dstd_events_create(int n, void** events);
 int dstd_events_destroy(int n, void** events);
 int dstd_event_elapsed_ms(void* start, void* stop, float* ms);
 
+/* Arithmetic of the 64 -> 64 graph convolutions of dstd_block_fwd /
+ * dstd_model_fwd (process-wide; default from env DSTD_HILO, else 1):
+ *   1  split-f16 MFMA (each fp32 operand as an f16 hi/lo pair, three
+ *      v_mfma_f32_16x16x32_f16 per product, fp32 accumulation; 22-bit
+ *      operands) where the shape has kernels: (T, V) in {(35,22), (35,25),
+ *      (40,23), (75,22)};
+ *   0  exact-fp32 MFMA (v_mfma_f32_16x16x4_f32) everywhere.
+ * Outputs of both stay within the parity bar against the reference
+ * (tests/test_gpu_parity.py).  No counterpart in the reference (pure fp32
+ * ATen, model/dstdgcn.py:80-94).  Returns DSTD_EINVAL for other modes. */
+int dstd_set_gc_precision(int mode);
+int dstd_get_gc_precision(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,10 +22,23 @@ def header_symbols(name="dstd_gcn.h"):
 def test_library_exports_every_header_symbol():
     L = native.lib()
     syms = header_symbols()
-    assert len(syms) == 12, syms
+    assert len(syms) == 14, syms
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(native.EXPORTS)
+
+
+def test_gc_precision_switch_without_gpu():
+    """The arithmetic switch of the 64->64 GC kernels is host state only."""
+    L = native.lib()
+    prev = L.dstd_get_gc_precision()
+    assert prev in (0, 1)
+    assert L.dstd_set_gc_precision(2) == -1  # DSTD_EINVAL
+    assert native.set_gc_precision("fp32") in ("fp32", "split")
+    assert L.dstd_get_gc_precision() == 0
+    assert native.set_gc_precision("split") == "fp32"
+    assert L.dstd_get_gc_precision() == 1
+    L.dstd_set_gc_precision(prev)
 
 
 def test_library_exports_every_training_header_symbol():

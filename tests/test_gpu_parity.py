@@ -6,12 +6,17 @@ fp64) and vs the CPU oracle.  Tolerance:
 The 21-op stack amplifies a 1e-7 rounding difference ~10^3x:
 any fp32 summation order lands at ~0.5-2x ref32_err (measured, see
 scripts/parity_report.py), while every op and block stays at ~1x.
+
+Blocks and whole models run under both GC arithmetics of the library
+(dstd_set_gc_precision): "split" (split-f16 MFMA, 22-bit operands, the
+default) and "fp32" (exact-fp32 MFMA); both must meet the same bars.
 """
 import numpy as np
 import pytest
 import torch
 
 from conftest import group, load_npz, rel_err
+import dstd_native
 from model import DSTDGC, DSTDGCB, DSTDGCN, get_model
 from oracle import dstdgcn_oracle as O
 
@@ -41,6 +46,13 @@ def t(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
+@pytest.fixture(params=["split", "fp32"])
+def precision(request):
+    prev = dstd_native.set_gc_precision(request.param)
+    yield request.param
+    dstd_native.set_gc_precision(prev)
+
+
 def load_model(tag):
     d = load_npz(f"model_{tag}.npz")
     opts = {k[4:]: d[k].item() for k in d.files if k.startswith("opt/")}
@@ -65,7 +77,7 @@ def test_dstdgc_op(name):
 
 
 @pytest.mark.parametrize("name", list(BLOCKS))
-def test_dstdgcb_block(name):
+def test_dstdgcb_block(name, precision):
     cin, cout, layout, T, V = BLOCKS[name]
     d = load_npz("dstdgcb.npz")
     blk = DSTDGCB(cin, cout, T, V, layout)
@@ -77,7 +89,7 @@ def test_dstdgcb_block(name):
 
 
 @pytest.mark.parametrize("tag", MODELS)
-def test_dstdgcn_model(tag):
+def test_dstdgcn_model(tag, precision):
     m, d, _, _ = load_model(tag)
     with torch.no_grad():
         y = m(t(d["x"]))
@@ -93,7 +105,7 @@ def synth(B, T, V, Tin, seed):
     return x
 
 
-def test_large_batch_vs_oracle_and_sample_independence():
+def test_large_batch_vs_oracle_and_sample_independence(precision):
     """B=256 (the bench workload): samples checked against the fp64 oracle,
     and every sample equals its own B=1 run bit for bit (no cross-sample
     coupling in eval; the property behind data-parallel sharding)."""
@@ -112,7 +124,7 @@ def test_large_batch_vs_oracle_and_sample_independence():
 
 
 @pytest.mark.parametrize("B", [1, 3, 257])
-def test_ragged_batches(B):
+def test_ragged_batches(B, precision):
     m, d, sd, opts = load_model("3dpw")
     T = opts["input_time_frame"] + opts["output_time_frame"]
     x = synth(B, T, 23, opts["input_time_frame"], B)
@@ -122,6 +134,32 @@ def test_ragged_batches(B):
     k = min(B, 3)
     y64 = O.dstdgcn(x[:k], sd, opts["num_layers"]).numpy()
     assert rel_err(y[:k].numpy(), y64) <= max(1e-4, 4 * float(d["ref32_err"]))
+
+
+def test_split_vs_fp32_bench_batch():
+    """The bench workload (H36M B=256) under both arithmetics: each against
+    the fp64 oracle on a sample subset, and against each other on the whole
+    batch (a size-independent agreement check: the split path may differ
+    from the fp32 path by at most the parity bar)."""
+    m, d, sd, opts = load_model("h36m")
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    x = synth(256, T, 22, opts["input_time_frame"], 21).to(DEV)
+    prev = dstd_native.set_gc_precision("fp32")
+    try:
+        with torch.no_grad():
+            y32 = m(x).cpu()
+        dstd_native.set_gc_precision("split")
+        with torch.no_grad():
+            ys = m(x).cpu()
+    finally:
+        dstd_native.set_gc_precision(prev)
+    tol = max(1e-4, 4 * float(d["ref32_err"]))
+    assert torch.isfinite(ys).all()
+    assert rel_err(ys.numpy(), y32.numpy()) <= tol
+    picks = [0, 100, 255]
+    y64 = O.dstdgcn(x[picks].cpu(), sd, opts["num_layers"]).numpy()
+    assert rel_err(ys[picks].numpy(), y64) <= tol
+    assert rel_err(y32[picks].numpy(), y64) <= tol
 
 
 def test_deterministic_repeat():
