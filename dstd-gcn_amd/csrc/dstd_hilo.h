@@ -34,21 +34,48 @@ namespace dstd {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-// 8 fp32 values -> hi = f16(v) (round to nearest), lo = f16(v - hi)
-__device__ __forceinline__ void split8(const float4& a, const float4& b, f16x8& hi, f16x8& lo) {
-  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const _Float16 h = (_Float16)v[e];
-    hi[e] = h;
-    lo[e] = (_Float16)(v[e] - (float)h);
-  }
-}
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+
+// 8 fp32 values -> packed hi = f16(v) (v_cvt_pk_f16_f32, round to nearest
+// even) and packed lo = f16(v - hi) (v_fma_mixlo/hi_f16: the difference is
+// formed exactly inside the fma and rounded once) -- 1.5 VALU per value
+// instead of 2.5 for convert / convert back / subtract / convert.
+// The trailing s_nop 1 covers the VALU-write -> MFMA-read hazard (2 wait
+// states): hipcc's hazard recognizer does not see inside inline asm, and an
+// MFMA reading lo right after the block read stale values (measured).
 __device__ __forceinline__ void split8(const float4& a, const float4& b, uint4& hi, uint4& lo) {
-  f16x8 h, l;
+  hi.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a.x, a.y}, f16x2_t));
+  hi.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a.z, a.w}, f16x2_t));
+  hi.z = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){b.x, b.y}, f16x2_t));
+  hi.w = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){b.z, b.w}, f16x2_t));
+#ifdef DSTD_SPLIT_CVT
+  const f16x2_t h0 = __builtin_bit_cast(f16x2_t, hi.x), h1 = __builtin_bit_cast(f16x2_t, hi.y);
+  const f16x2_t h2 = __builtin_bit_cast(f16x2_t, hi.z), h3 = __builtin_bit_cast(f16x2_t, hi.w);
+  lo.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a.x - (float)h0[0], a.y - (float)h0[1]}, f16x2_t));
+  lo.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a.z - (float)h1[0], a.w - (float)h1[1]}, f16x2_t));
+  lo.z = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){b.x - (float)h2[0], b.y - (float)h2[1]}, f16x2_t));
+  lo.w = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){b.z - (float)h3[0], b.w - (float)h3[1]}, f16x2_t));
+#else
+  asm("v_fma_mixlo_f16 %0, %4, 1.0, -%12 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %5, 1.0, -%12 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %1, %6, 1.0, -%13 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %7, 1.0, -%13 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %2, %8, 1.0, -%14 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %2, %9, 1.0, -%14 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %3, %10, 1.0, -%15 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %3, %11, 1.0, -%15 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "s_nop 1"
+      : "=&v"(lo.x), "=&v"(lo.y), "=&v"(lo.z), "=&v"(lo.w)
+      : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w), "v"(hi.x), "v"(hi.y),
+        "v"(hi.z), "v"(hi.w));
+#endif
+}
+__device__ __forceinline__ void split8(const float4& a, const float4& b, f16x8& hi, f16x8& lo) {
+  uint4 h, l;
   split8(a, b, h, l);
-  hi = __builtin_bit_cast(uint4, h);
-  lo = __builtin_bit_cast(uint4, l);
+  hi = __builtin_bit_cast(f16x8, h);
+  lo = __builtin_bit_cast(f16x8, l);
 }
 
 template <int N, bool IL>

@@ -62,6 +62,27 @@ __device__ __forceinline__ int unit_range(int nunits, int& uend) {
   return (int)(((long)gw * nunits) / nw);
 }
 
+// Raw buffer access: every global load / store of the unit loop goes through
+// a buffer resource over the unit's own rows, and a lane with nothing to
+// load / store gets an out-of-range offset (loads return 0, stores are
+// dropped).  No exec-mask branches in the loop, so hipcc's vmcnt bookkeeping
+// stays exact across the loop back-edge (with branchy loads / stores it
+// waited for the previous unit's stores at the top of every unit).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ uint4 bldu4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+
 // folded BN vectors [V][64] -> LDS [c/4][v]
 __device__ __forceinline__ void stage_bn64(float4* dst, const float* src, int V, int tid) {
   for (int i = tid; i < V * 16; i += HT) {
@@ -161,33 +182,44 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   int uend;
   int u = unit_range(a.B * T, uend);
   const float pw = *a.prelu;
-  const int jrow0 = min(SM::row_idx(0, cl), V - 1), jrow1 = min(SM::row_idx(1, cl), V - 1);
-  const size_t adj_unit = (size_t)2 * V * SL;  // halves per (n, g, t)
+  // x rows of the two conv tiles: joint of tile m, row cl; k-step ks, lane group kl
+  const uint32_t xo0 = (uint32_t)(min(SM::row_idx(0, cl), V - 1) * 64 + 8 * kl) * 4;
+  const uint32_t xo1 = (uint32_t)(min(SM::row_idx(1, cl), V - 1) * 64 + 8 * kl) * 4;
+  constexpr uint32_t unit_bytes = V * 64 * 4;     // one frame of x / y
+  constexpr uint32_t adj_bytes = 2 * V * SL * 2;  // one (n, g, t) adjacency: 2 planes of V x SL halves
+  // per output tile wt: this lane's joint w = 16wt + cl (OOB past V)
+  uint32_t wro[NWT], wadj[NWT], wpq[NWT];
+#pragma unroll
+  for (int wt = 0; wt < NWT; ++wt) {
+    const int w = 16 * wt + cl;
+    wro[wt] = w < V ? (uint32_t)(w * 64 + 4 * kl) * 4 : OOB;
+    wadj[wt] = w < V && kl < NG ? (uint32_t)(w * SL + 8 * kl) * 2 : OOB;
+    wpq[wt] = w < V && kl == 0 ? (uint32_t)w * 16 : OOB;
+  }
 
   float4 xr[2][2][2];  // [tile][k-step][half]: channels 32ks + 8kl .. +7 of the tile row
   auto load_x = [&](int uu) {
-    const float* b = a.x + (size_t)uu * V * 64 + 8 * kl;
+    const auto r = rsrc(a.x + (size_t)uu * V * 64, unit_bytes);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      xr[0][ks][0] = ld4(b + jrow0 * 64 + 32 * ks);
-      xr[0][ks][1] = ld4(b + jrow0 * 64 + 32 * ks + 4);
-      xr[1][ks][0] = ld4(b + jrow1 * 64 + 32 * ks);
-      xr[1][ks][1] = ld4(b + jrow1 * 64 + 32 * ks + 4);
+      xr[0][ks][0] = bld4(r, xo0 + 128 * ks);
+      xr[0][ks][1] = bld4(r, xo0 + 128 * ks + 16);
+      xr[1][ks][0] = bld4(r, xo1 + 128 * ks);
+      xr[1][ks][1] = bld4(r, xo1 + 128 * ks + 16);
     }
   };
   uint4 ab[2][NWT][2];  // adjacency B fragments [graph][w tile][plane]
   auto load_adj = [&](int uu) {
     const int n = uu / T, t = uu - n * T;
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < 2; ++g) {
+      const auto r = rsrc(a.adj + ((size_t)(n * 2 + g) * T + t) * (adj_bytes / 2), adj_bytes);
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt) {
-        const int w = 16 * wt + cl;
-        const uint16_t* p = a.adj + ((size_t)(n * 2 + g) * T + t) * adj_unit + w * SL + 8 * kl;
-        const bool ok = w < V && kl < NG;
-        ab[g][wt][0] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
-        ab[g][wt][1] = ok ? *reinterpret_cast<const uint4*>(p + V * SL) : make_uint4(0, 0, 0, 0);
+        ab[g][wt][0] = bldu4(r, wadj[wt]);
+        ab[g][wt][1] = bldu4(r, wadj[wt] + V * SL * 2);
       }
+    }
   };
   if (u < uend) {
     load_x(u);
@@ -196,15 +228,13 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   while (u < uend) {
     const int un = u + 1;
     const int lz = lane + opaque_zero();
-    float* yrow = a.y + (size_t)u * V * 64;
+    const auto rx = rsrc(a.x + (size_t)u * V * 64, unit_bytes);
     // identity residual at the output positions (w = 16wt + cl, channels 16ct + 4kl ..)
     float4 R[4][NWT];
 #pragma unroll
-    for (int wt = 0; wt < NWT; ++wt) {
-      const float* p = a.x + ((size_t)u * V + min(16 * wt + cl, V - 1)) * 64 + 4 * kl;
+    for (int wt = 0; wt < NWT; ++wt)
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) R[ct][wt] = ld4(p + 16 * ct);
-    }
+      for (int ct = 0; ct < 4; ++ct) R[ct][wt] = bld4(rx, wro[wt] + 64 * ct);
     f16x8 xh[2][2], xo[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -277,9 +307,10 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     if (un < uend) load_adj(un);
 
     // ---- epilogue: h = prelu(bn(y) + x) -> NTVC ----
+    const auto ry = rsrc(a.y + (size_t)u * V * 64, unit_bytes);
 #pragma unroll
     for (int wt = 0; wt < NWT; ++wt) {
-      const int w = 16 * wt + cl, wc = min(w, V - 1);
+      const int wc = min(16 * wt + cl, V - 1);
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         f32x4& o = O[ct][wt];
@@ -288,7 +319,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         o[1] = prelu_f(fmaf(o[1], sc.y, sh.y) + R[ct][wt].y, pw);
         o[2] = prelu_f(fmaf(o[2], sc.z, sh.z) + R[ct][wt].z, pw);
         o[3] = prelu_f(fmaf(o[3], sc.w, sh.w) + R[ct][wt].w, pw);
-        if (w < V) st4(yrow + w * 64 + 16 * ct + 4 * kl, make_float4(o[0], o[1], o[2], o[3]));
+        bst4(ry, wro[wt] + 64 * ct, make_float4(o[0], o[1], o[2], o[3]));
       }
     }
     // ---- P_t/Q_t of h: out[ch][w] = sum_c wq[ch][c] h[c][w] + b ----
@@ -298,25 +329,24 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const f16x8 qh = as_h8(pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(pql[(ks * 2 + 1) * 64 + lz]);
+      f16x8 hh[NWT], hl[NWT];
 #pragma unroll
-      for (int wt = 0; wt < NWT; ++wt) {
-        f16x8 hh, hl;
-        split_acc(O[2 * ks][wt], O[2 * ks + 1][wt], hh, hl);
-        acc[wt] = mfma32(qo, hh, acc[wt]);
-        acc[wt] = mfma32(qh, hl, acc[wt]);
-        acc[wt] = mfma32(qh, hh, acc[wt]);
-      }
+      for (int wt = 0; wt < NWT; ++wt) split_acc(O[2 * ks][wt], O[2 * ks + 1][wt], hh[wt], hl[wt]);
+#pragma unroll
+      for (int wt = 0; wt < NWT; ++wt) acc[wt] = mfma32(qo, hh[wt], acc[wt]);
+#pragma unroll
+      for (int wt = 0; wt < NWT; ++wt) acc[wt] = mfma32(qh, hl[wt], acc[wt]);
+#pragma unroll
+      for (int wt = 0; wt < NWT; ++wt) acc[wt] = mfma32(qh, hh[wt], acc[wt]);
     }
-    if (kl == 0) {
+    {
       const float s = scl[2];
+      const auto rp = rsrc(a.pq + (size_t)u * V * 4, V * 16);
 #pragma unroll
-      for (int wt = 0; wt < NWT; ++wt) {
-        const int w = 16 * wt + cl;
-        if (w < V)
-          st4(a.pq + ((size_t)u * V + w) * 4,
-              make_float4(fmaf(acc[wt][0], s, bql[0]), fmaf(acc[wt][1], s, bql[1]), fmaf(acc[wt][2], s, bql[2]),
-                          fmaf(acc[wt][3], s, bql[3])));
-      }
+      for (int wt = 0; wt < NWT; ++wt)
+        bst4(rp, wpq[wt],
+             make_float4(fmaf(acc[wt][0], s, bql[0]), fmaf(acc[wt][1], s, bql[1]), fmaf(acc[wt][2], s, bql[2]),
+                         fmaf(acc[wt][3], s, bql[3])));
     }
     u = un;
   }
@@ -372,27 +402,39 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
   int uend;
   int u = unit_range(a.B * V, uend);
   const float pw = use_bn ? *a.prelu : 0.f;
-  const size_t adj_unit = (size_t)2 * T * SL;  // halves per (n, v)
+  // a unit's rows: frame t of joint v at t * V * 64 floats from the unit base
+  const uint32_t col_bytes = (uint32_t)((T - 1) * V + 1) * 64 * 4;
+  const uint32_t frame_bytes = (uint32_t)V * 64 * 4;
+  constexpr uint32_t adj_bytes = 2 * T * SL * 2;  // one (n, v): 2 planes of T x SL halves
+  uint32_t xoff[MT];  // conv rows: frame 16m + cl, channels 8kl ..
+#pragma unroll
+  for (int m = 0; m < MT; ++m) xoff[m] = (uint32_t)min(16 * m + cl, T - 1) * frame_bytes + 32 * kl;
+  uint32_t uoff[NUT], upq[NUT];  // output frame uo = 16ut + cl (OOB past T), channels 4kl ..
+#pragma unroll
+  for (int ut = 0; ut < NUT; ++ut) {
+    const int uo = 16 * ut + cl;
+    uoff[ut] = uo < T ? (uint32_t)uo * frame_bytes + 16 * kl : OOB;
+    upq[ut] = uo < T && kl < 2 ? (uint32_t)(uo * 8 + 4 * kl) * 4 : OOB;
+  }
 
   float4 xr[MT][2][2];  // tile m row cl = frame 16m + cl
   auto load_x = [&](int uu) {
     const int n = uu / V, v = uu - n * V;
-    const float* b = a.h + ((size_t)n * T * V + v) * 64 + 8 * kl;
+    const auto r = rsrc(a.h + ((size_t)n * T * V + v) * 64, col_bytes);
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const float* p = b + (size_t)min(16 * m + cl, T - 1) * V * 64;
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        xr[m][ks][0] = ld4(p + 32 * ks);
-        xr[m][ks][1] = ld4(p + 32 * ks + 4);
+        xr[m][ks][0] = bld4(r, xoff[m] + 128 * ks);
+        xr[m][ks][1] = bld4(r, xoff[m] + 128 * ks + 16);
       }
-    }
   };
   if (u < uend) load_x(u);
   while (u < uend) {
     const int n = u / V, v = u - n * V;
     const int un = u + 1;
     const int lz = lane + opaque_zero();
+    const size_t cbase = ((size_t)n * T * V + v) * 64;
     f16x8 xh[MT][2], xo[MT][2];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -437,18 +479,16 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
     for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = zero4();
-    const uint16_t* adj = a.adj + (size_t)u * adj_unit + 8 * kl;
+    const auto radj = rsrc(a.adj + (size_t)u * (adj_bytes / 2), adj_bytes);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      const bool okg = kl < SM::ng(s);
       uint4 bh[NUT], bo[NUT];
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut) {
         const int uo = 16 * ut + cl;
-        const uint16_t* p = adj + uo * SL + 8 * SM::goff(s);
-        const bool ok = okg && uo < T;
-        bh[ut] = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
-        bo[ut] = ok ? *reinterpret_cast<const uint4*>(p + T * SL) : make_uint4(0, 0, 0, 0);
+        const uint32_t off = uo < T && kl < SM::ng(s) ? (uint32_t)(uo * SL + 8 * (SM::goff(s) + kl)) * 2 : OOB;
+        bh[ut] = bldu4(radj, off);
+        bo[ut] = bldu4(radj, off + T * SL * 2);
       }
       f16x8 dh[4], dl[4];
 #pragma unroll
@@ -466,22 +506,20 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
 #pragma unroll
         for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bh[ut]), O[ct][ut]);
     }
-
     // residual of the encoder epilogue, loaded after the aggregation (register pressure)
     float4 R[use_res ? 4 : 1][use_res ? NUT : 1];
     if constexpr (use_res) {
+      const auto rr = rsrc(a.xres + cbase, col_bytes);
 #pragma unroll
-      for (int ut = 0; ut < NUT; ++ut) {
-        const float* p = a.xres + (((size_t)n * T + min(16 * ut + cl, T - 1)) * V + v) * 64 + 4 * kl;
+      for (int ut = 0; ut < NUT; ++ut)
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) R[ct][ut] = ld4(p + 16 * ct);
-      }
+        for (int ct = 0; ct < 4; ++ct) R[ct][ut] = bld4(rr, uoff[ut] + 64 * ct);
     }
+
     // ---- epilogue ----
+    const auto ry = rsrc(a.y + cbase, col_bytes);
 #pragma unroll
     for (int ut = 0; ut < NUT; ++ut) {
-      const int uo = 16 * ut + cl;
-      float* py = a.y + (((size_t)n * T + min(uo, T - 1)) * V + v) * 64 + 4 * kl;
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         f32x4& o = O[ct][ut];
@@ -498,7 +536,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
           o[2] = prelu_f(fmaf(o[2], sc.z, sh.z), pw);
           o[3] = prelu_f(fmaf(o[3], sc.w, sh.w), pw);
         }
-        if (uo < T) st4(py + 16 * ct, make_float4(o[0], o[1], o[2], o[3]));
+        bst4(ry, uoff[ut] + 64 * ct, make_float4(o[0], o[1], o[2], o[3]));
       }
     }
     // ---- next block's P_s/Q_s (8 channels) of the output ----
@@ -509,25 +547,24 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const f16x8 qh = as_h8(pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(pql[(ks * 2 + 1) * 64 + lz]);
+        f16x8 hh[NUT], hl[NUT];
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) {
-          f16x8 hh, hl;
-          split_acc(O[2 * ks][ut], O[2 * ks + 1][ut], hh, hl);
-          acc[ut] = mfma32(qo, hh, acc[ut]);
-          acc[ut] = mfma32(qh, hl, acc[ut]);
-          acc[ut] = mfma32(qh, hh, acc[ut]);
-        }
+        for (int ut = 0; ut < NUT; ++ut) split_acc(O[2 * ks][ut], O[2 * ks + 1][ut], hh[ut], hl[ut]);
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma32(qo, hh[ut], acc[ut]);
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma32(qh, hl[ut], acc[ut]);
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma32(qh, hh[ut], acc[ut]);
       }
-      if (kl < 2) {
-        const float s = scl[1];
+      const float s = scl[1];
+      const auto rp = rsrc(a.pq + (size_t)u * T * 8, T * 32);
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) {
-          const int uo = 16 * ut + cl;
-          if (uo < T)
-            st4(a.pq + ((size_t)u * T + uo) * 8 + 4 * kl,
-                make_float4(fmaf(acc[ut][0], s, bql[4 * kl]), fmaf(acc[ut][1], s, bql[4 * kl + 1]),
-                            fmaf(acc[ut][2], s, bql[4 * kl + 2]), fmaf(acc[ut][3], s, bql[4 * kl + 3])));
-        }
+      for (int ut = 0; ut < NUT; ++ut) {
+        const int b4 = 4 * (kl & 1);
+        bst4(rp, upq[ut],
+             make_float4(fmaf(acc[ut][0], s, bql[b4]), fmaf(acc[ut][1], s, bql[b4 + 1]), fmaf(acc[ut][2], s, bql[b4 + 2]),
+                         fmaf(acc[ut][3], s, bql[b4 + 3])));
       }
     }
     u = un;
