@@ -87,7 +87,9 @@ struct BlockFold {
   uint4* hl_pqs;    // conv_t.conv_m1/m2 (P/Q written by the spatial kernel)
   uint4* hl_wt;     // conv_t.conv_f
   uint4* hl_pqt;    // next block's conv_s[*].conv_m1/m2 (P/Q written by the temporal kernel)
-  float* hl_scale;  // [5]: 2^-s of ws0, ws1, pqs, wt, pqt
+  uint4* hl_rms[2]; // conv_s[g].conv_rm (spatial adjacency)
+  uint4* hl_rmt;    // conv_t.conv_rm (temporal adjacency)
+  float* hl_scale;  // [8]: 2^-s of ws0, ws1, pqs, wt, pqt, rms0, rms1, rmt
 };
 
 // Split-f16 GC kernels (dstd_hilo.hip) where the shape has them: 1 (default),
@@ -127,6 +129,9 @@ void carve_fold(Carver& cv, BlockFold& f, int T, int V, int cout, bool res) {
   f.hl_pqs = img(kHLPQImg);
   f.hl_wt = img(kHLConvImg);
   f.hl_pqt = img(kHLPQImg);
+  f.hl_rms[0] = img(hl_rm_img(T, 2 * T));
+  f.hl_rms[1] = img(hl_rm_img(T, 2 * T));
+  f.hl_rmt = img(hl_rm_img(V, 2 * V));
   f.hl_scale = cv.take(8);
 }
 
@@ -216,6 +221,17 @@ void add_hl_conv(HLList& l, const float* w, uint4* img, float* sc) {
   j.inv_scale = sc;
   l.push_back(j);
 }
+void add_hl_rm(HLList& l, const float* w, int rows, int cols, uint4* img, float* sc) {
+  HLJob j{};
+  j.kind = HLJ_RM;
+  j.w[0] = w;
+  j.nblk = 1;
+  j.rows = rows;
+  j.cols = cols;
+  j.img = img;
+  j.inv_scale = sc;
+  l.push_back(j);
+}
 void add_hl_pq(HLList& l, const float* const* w, int nblk, uint4* img, float* sc) {
   HLJob j{};
   j.kind = HLJ_PQ;
@@ -248,14 +264,17 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V
 
 // Weight images of the block's split-f16 launches.
 void add_block_hl_jobs(HLList& l, const dstd_block_params* p, const BlockFold& f, const BlockTail& tail,
-                       const BlockHL& hl) {
+                       const BlockHL& hl, int T, int V) {
   if (hl.s) {
+    add_hl_rm(l, p->conv_s[0].wrm, T, 2 * T, f.hl_rms[0], f.hl_scale + 5);
+    add_hl_rm(l, p->conv_s[1].wrm, T, 2 * T, f.hl_rms[1], f.hl_scale + 6);
     add_hl_conv(l, p->conv_s[0].wf, f.hl_ws[0], f.hl_scale + 0);
     add_hl_conv(l, p->conv_s[1].wf, f.hl_ws[1], f.hl_scale + 1);
     const float* w[2] = {p->conv_t.wm1, p->conv_t.wm2};
     add_hl_pq(l, w, 2, f.hl_pqs, f.hl_scale + 2);
   }
   if (hl.t) {
+    add_hl_rm(l, p->conv_t.wrm, V, 2 * V, f.hl_rmt, f.hl_scale + 7);
     add_hl_conv(l, p->conv_t.wf, f.hl_wt, f.hl_scale + 3);
     if (tail.next) {
       const dstd_block_params* q = tail.next;
@@ -306,7 +325,28 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     aa.out_sG = (long)T * aa.ldo;
   }
   pf.begin(DSTD_KIND_ADJ_S, s);
-  hipError_t e = launch_adj(aa, s);
+  hipError_t e;
+  if (hl.s) {
+    AdjHLArgs ah{};
+    ah.pq = aa.pq;
+    ah.pql = aa.pql;
+    ah.B = B;
+    ah.ngroups = 2;
+    for (int g = 0; g < 2; ++g) {
+      ah.p_ch[g] = aa.p_ch[g];
+      ah.wimg[g] = f.hl_rms[g];
+      ah.wscale[g] = f.hl_scale + 5 + g;
+      ah.bias[g] = aa.bias[g];
+      ah.astat[g] = aa.astat[g];
+    }
+    ah.alpha = aa.alpha;
+    ah.out = reinterpret_cast<uint16_t*>(aa.out);
+    ah.out_sN = 2 * aa.out_sN;  // halves
+    ah.out_sG = 2 * aa.out_sG;
+    e = launch_adj_hl(ah, 0, T, V, s);
+  } else {
+    e = launch_adj(aa, s);
+  }
   pf.end(s);
   if (e != hipSuccess) return e;
 
@@ -406,7 +446,25 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ta.out_sN = (long)V * ta.ldo;
   }
   pf.begin(DSTD_KIND_ADJ_T, s);
-  e = launch_adj(ta, s);
+  if (hl.t) {
+    AdjHLArgs ah{};
+    ah.pq = ta.pq;
+    ah.pql = ta.pql;
+    ah.B = B;
+    ah.ngroups = 1;
+    ah.p_ch[0] = ta.p_ch[0];
+    ah.wimg[0] = f.hl_rmt;
+    ah.wscale[0] = f.hl_scale + 7;
+    ah.bias[0] = ta.bias[0];
+    ah.astat[0] = ta.astat[0];
+    ah.alpha = ta.alpha;
+    ah.out = reinterpret_cast<uint16_t*>(ta.out);
+    ah.out_sN = 2 * ta.out_sN;
+    ah.out_sG = 0;
+    e = launch_adj_hl(ah, 1, T, V, s);
+  } else {
+    e = launch_adj(ta, s);
+  }
   pf.end(s);
   if (e != hipSuccess) return e;
 
@@ -710,7 +768,7 @@ int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int
   BlockTail tail{TEPI_RAW, nullptr, nullptr, nullptr, nullptr, nullptr};
   const BlockHL hl = block_hl(p, tail, T, V);
   HLList hj;
-  add_block_hl_jobs(hj, p, L.f, tail, hl);
+  add_block_hl_jobs(hj, p, L.f, tail, hl, T, V);
   DSTD_TRY(run_hl_prep(hj, s));
   Prof pf;
   DSTD_TRY(run_block(p, L.f, L.sc, B, T, V, L.xin, L.h, L.yout, tail, s, pf, hl));
@@ -826,7 +884,7 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
   HLList hj;
   for (int b = 0; b < NB; ++b) {
     hls[b] = block_hl(blk[b], tails[b], T, V);
-    add_block_hl_jobs(hj, blk[b], *fold[b], tails[b], hls[b]);
+    add_block_hl_jobs(hj, blk[b], *fold[b], tails[b], hls[b], T, V);
   }
   pf.begin(DSTD_KIND_FOLD, s);
   DSTD_TRY(run_hl_prep(hj, s));

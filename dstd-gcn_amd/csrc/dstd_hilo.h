@@ -29,6 +29,7 @@
 // in slot order: one 16-byte load per lane gives a B fragment.
 #pragma once
 #include "dstd_common.h"
+#include "dstd_kernels.h"
 
 namespace dstd {
 
@@ -143,14 +144,20 @@ inline int hl_sl_temporal(int T) {
 // HLJ_PQ: A fragments of the P/Q conv of the next DSTDGC(s): row ch = 2*blk + rr
 //   of w[blk][rr*64 + c], slot (kg, e = 4mm + r) of K-step ks <-> c = 16*(2ks+mm) + 4kg + r:
 //   img[(ks*2 + plane)*64 + lane], 4 KiB.
-enum HLJobKind { HLJ_CONV = 0, HLJ_PQ = 1 };
+// HLJ_RM: A fragments of conv_rm, W[row][k] (rows x cols = T x 2T spatial,
+//   V x 2V temporal): img[((rt*NS + s)*2 + plane)*64 + lane] = 8 halves of
+//   2^s * W[16rt + i][32s + 8kg + e] (i = lane&15, kg = lane>>4, zero outside),
+//   NS = cdiv(cols, 32).
+enum HLJobKind { HLJ_CONV = 0, HLJ_PQ = 1, HLJ_RM = 2 };
 struct HLJob {
   int kind;
-  const float* w[4];  // HLJ_CONV: w[0] = [64][64]; HLJ_PQ: nblk two-row blocks [2][64]
+  const float* w[4];  // HLJ_CONV: w[0] = [64][64]; HLJ_PQ: nblk two-row blocks [2][64]; HLJ_RM: w[0]
   int nblk;
+  int rows, cols;     // HLJ_RM
   uint4* img;
   float* inv_scale;   // 2^-s
 };
+inline int hl_rm_img(int rows, int cols) { return cdiv(rows, 16) * cdiv(cols, 32) * 2 * 64; }  // uint4
 constexpr int kMaxHLJobs = 48;
 struct HLPrepArgs {
   HLJob jobs[kMaxHLJobs];
@@ -196,7 +203,28 @@ struct TemporalHLArgs {
   float* pq;                 // [B][V][T][8]
 };
 
+// ---- dynamic adjacency in split-f16 planes ---------------------------------
+// Adj = alpha * (W_rm . tanh(P - Q) + b_rm) + Astat as a GEMM on
+// v_mfma_f32_16x16x32_f16 (three products): rows t (spatial) / v (temporal),
+// K = 2T / 2V, columns (q, slot) in the slot order above; output planes as
+// AdjArgs.hl documents.  Shapes: hl_shape() of dstd_hilo.hip.
+struct AdjHLArgs {
+  const float* pq;          // channel-innermost P/Q planes (PQLayout sch == 1)
+  PQLayout pql;
+  int p_ch[2];              // first channel (P_0, P_1, Q_0, Q_1) of each graph
+  int B, ngroups;
+  const uint4* wimg[2];     // HLJ_RM images of conv_rm
+  const float* wscale[2];
+  const float* bias[2];
+  const float* alpha;
+  const float* astat[2];    // [NA][NA]
+  uint16_t* out;
+  long out_sN, out_sG;      // halves
+};
+
 hipError_t launch_hl_prep(const HLPrepArgs& a, hipStream_t s);
+// mode 0 spatial, 1 temporal
+hipError_t launch_adj_hl(const AdjHLArgs& a, int mode, int T, int V, hipStream_t s);
 // hipErrorNotSupported when the shape has no instantiation
 hipError_t launch_spatial_hl(const SpatialHLArgs& a, hipStream_t s);
 hipError_t launch_temporal_hl(const TemporalHLArgs& a, hipStream_t s);

@@ -24,6 +24,17 @@
 #include "dstd_hilo.h"
 #include "dstd_kernels.h"
 
+// Workgroup timeline of the split adjacency kernel (debug builds,
+// -DDSTD_STAMPS; scripts/timeline.py --hl): s_memrealtime at entry, prologue
+// done, tiles done, exit.
+#ifdef DSTD_STAMPS
+__device__ unsigned long long g_tl_hl[2][2048][4];
+#define TLH(m, i) \
+  if (threadIdx.x == 0 && blockIdx.x < 2048) g_tl_hl[m][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();
+#else
+#define TLH(m, i)
+#endif
+
 namespace dstd {
 
 namespace {
@@ -36,7 +47,12 @@ __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<floa
 __device__ __forceinline__ f16x8 as_h8(const uint4& v) { return __builtin_bit_cast(f16x8, v); }
 
 __device__ __forceinline__ f32x4 mfma32(const f16x8& a, const f16x8& b, f32x4 c) {
+#ifdef DSTD_ABL_MFMA
+  c[0] += (float)a[0] * (float)b[0];
+  return c;
+#else
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#endif
 }
 
 // hi/lo pair of an f32x4 quartet from two accumulator tiles (slots e = 0..3
@@ -80,6 +96,10 @@ __device__ __forceinline__ uint4 bldu4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
+#ifdef DSTD_ABL_STORE
+  if (v.x == 12345.f) off = 0;  // keep the value alive; store only lanes with nothing to store
+  else off = OOB;
+#endif
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
 }
 
@@ -99,9 +119,9 @@ __device__ __forceinline__ void stage_bn64(float4* dst, const float* src, int V,
 __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
   const HLJob& j = a.jobs[blockIdx.x];
   const int tid = threadIdx.x;
-  const int n = j.kind == HLJ_CONV ? 64 * 64 : 128 * j.nblk;
+  const int n = j.kind == HLJ_CONV ? 64 * 64 : j.kind == HLJ_RM ? j.rows * j.cols : 128 * j.nblk;
   float m = 0.f;
-  for (int i = tid; i < n; i += 256) m = fmaxf(m, fabsf(j.kind == HLJ_CONV ? j.w[0][i] : j.w[i >> 7][i & 127]));
+  for (int i = tid; i < n; i += 256) m = fmaxf(m, fabsf(j.kind != HLJ_PQ ? j.w[0][i] : j.w[i >> 7][i & 127]));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   __shared__ float red[4];
@@ -126,6 +146,19 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
              make_float4(w[4] * scale, w[5] * scale, w[6] * scale, w[7] * scale), hi, lo);
       j.img[((ct * 2 + ks) * 2 + 0) * 64 + lane] = hi;
       j.img[((ct * 2 + ks) * 2 + 1) * 64 + lane] = lo;
+    }
+  } else if (j.kind == HLJ_RM) {
+    const int NS = cdiv(j.cols, 32), nimg = cdiv(j.rows, 16) * NS * 64;
+    for (int i = tid; i < nimg; i += 256) {
+      const int lane = i & 63, s = (i >> 6) % NS, rt = (i >> 6) / NS;
+      const int r = 16 * rt + (lane & 15), k0 = 32 * s + 8 * (lane >> 4);
+      float v[8];
+#pragma unroll
+      for (int e8 = 0; e8 < 8; ++e8) v[e8] = r < j.rows && k0 + e8 < j.cols ? j.w[0][r * j.cols + k0 + e8] * scale : 0.f;
+      uint4 hi, lo;
+      split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), hi, lo);
+      j.img[((rt * NS + s) * 2 + 0) * 64 + lane] = hi;
+      j.img[((rt * NS + s) * 2 + 1) * 64 + lane] = lo;
     }
   } else {
     for (int i = tid; i < 2 * 64; i += 256) {
@@ -187,15 +220,12 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
   const uint32_t xo1 = (uint32_t)(min(SM::row_idx(1, cl), V - 1) * 64 + 8 * kl) * 4;
   constexpr uint32_t unit_bytes = V * 64 * 4;     // one frame of x / y
   constexpr uint32_t adj_bytes = 2 * V * SL * 2;  // one (n, g, t) adjacency: 2 planes of V x SL halves
-  // per output tile wt: this lane's joint w = 16wt + cl (OOB past V)
-  uint32_t wro[NWT], wadj[NWT], wpq[NWT];
-#pragma unroll
-  for (int wt = 0; wt < NWT; ++wt) {
-    const int w = 16 * wt + cl;
-    wro[wt] = w < V ? (uint32_t)(w * 64 + 4 * kl) * 4 : OOB;
-    wadj[wt] = w < V && kl < NG ? (uint32_t)(w * SL + 8 * kl) * 2 : OOB;
-    wpq[wt] = w < V && kl == 0 ? (uint32_t)w * 16 : OOB;
-  }
+  // per output tile wt: this lane's joint w = 16wt + cl.  Joints past V fall
+  // outside the unit's buffer range by themselves (w * row >= V * row); only
+  // the adjacency lane groups past NG need an explicit out-of-range offset.
+  const uint32_t wro0 = (uint32_t)(cl * 64 + 4 * kl) * 4;                    // + wt * 4096
+  const uint32_t wadj0 = kl < NG ? (uint32_t)(cl * SL + 8 * kl) * 2 : OOB;  // + wt * 32 * SL
+  const uint32_t wpq0 = kl == 0 ? (uint32_t)cl * 16 : OOB;                  // + wt * 256
 
   float4 xr[2][2][2];  // [tile][k-step][half]: channels 32ks + 8kl .. +7 of the tile row
   auto load_x = [&](int uu) {
@@ -213,11 +243,12 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     const int n = uu / T, t = uu - n * T;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-      const auto r = rsrc(a.adj + ((size_t)(n * 2 + g) * T + t) * (adj_bytes / 2), adj_bytes);
+      const uint16_t* base = a.adj + ((size_t)(n * 2 + g) * T + t) * (adj_bytes / 2);
+      const auto rh = rsrc(base, adj_bytes / 2), rl = rsrc(base + V * SL, adj_bytes / 2);  // one plane each
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt) {
-        ab[g][wt][0] = bldu4(r, wadj[wt]);
-        ab[g][wt][1] = bldu4(r, wadj[wt] + V * SL * 2);
+        ab[g][wt][0] = bldu4(rh, wadj0 + wt * 32 * SL);
+        ab[g][wt][1] = bldu4(rl, wadj0 + wt * 32 * SL);
       }
     }
   };
@@ -234,12 +265,19 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
     for (int wt = 0; wt < NWT; ++wt)
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) R[ct][wt] = bld4(rx, wro[wt] + 64 * ct);
+      for (int ct = 0; ct < 4; ++ct) R[ct][wt] = bld4(rx, wro0 + wt * 4096 + 64 * ct);
     f16x8 xh[2][2], xo[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) split8(xr[m][ks][0], xr[m][ks][1], xh[m][ks], xo[m][ks]);
+      for (int ks = 0; ks < 2; ++ks) {
+#ifdef DSTD_ABL_SPLITX
+        xh[m][ks] = __builtin_bit_cast(f16x8, xr[m][ks][0]);
+        xo[m][ks] = __builtin_bit_cast(f16x8, xr[m][ks][1]);
+#else
+        split8(xr[m][ks][0], xr[m][ks][1], xh[m][ks], xo[m][ks]);
+#endif
+      }
 
     f32x4 O[4][NWT];
 #pragma unroll
@@ -278,7 +316,13 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
             for (int m = 0; m < 2; ++m) D[m][c2 + q] = mfma32(xh[m][ks], wh[q], D[m][c2 + q]);
         }
       // x is dead after the second conv: prefetch the next unit's rows
-      if (g == 1 && un < uend) load_x(un);
+      // (unconditionally -- the last unit reloads itself -- so that no
+      // branch hides the loads from hipcc's vmcnt bookkeeping)
+      if (g == 1) {
+        __builtin_amdgcn_sched_barrier(0);  // keep the prefetch here: its registers free up only now
+        load_x(min(un, uend - 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
       // ---- aggregation: O[c][w] += sum_v D[v][c] Adj[v][w] ----
       const float s = scl[g];
       f16x8 dh[4], dl[4];
@@ -289,7 +333,12 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int r = 0; r < 4; ++r) D[m][ct][r] = fmaf(D[m][ct][r], s, b);
+#ifdef DSTD_ABL_SPLITD
+        dh[ct] = __builtin_bit_cast(f16x8, make_float4(D[0][ct][0], D[0][ct][1], D[0][ct][2], D[0][ct][3]));
+        dl[ct] = __builtin_bit_cast(f16x8, make_float4(D[1][ct][0], D[1][ct][1], D[1][ct][2], D[1][ct][3]));
+#else
         split_acc(D[0][ct], D[1][ct], dh[ct], dl[ct]);
+#endif
       }
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct)
@@ -304,7 +353,9 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
         for (int wt = 0; wt < NWT; ++wt) O[ct][wt] = mfma32(dh[ct], as_h8(ab[g][wt][0]), O[ct][wt]);
     }
-    if (un < uend) load_adj(un);
+    __builtin_amdgcn_sched_barrier(0);
+    load_adj(min(un, uend - 1));
+    __builtin_amdgcn_sched_barrier(0);
 
     // ---- epilogue: h = prelu(bn(y) + x) -> NTVC ----
     const auto ry = rsrc(a.y + (size_t)u * V * 64, unit_bytes);
@@ -314,18 +365,24 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         f32x4& o = O[ct][wt];
+#ifndef DSTD_ABL_EPI
         const float4 sc = bnl[0][(4 * ct + kl) * V + wc], sh = bnl[1][(4 * ct + kl) * V + wc];
         o[0] = prelu_f(fmaf(o[0], sc.x, sh.x) + R[ct][wt].x, pw);
         o[1] = prelu_f(fmaf(o[1], sc.y, sh.y) + R[ct][wt].y, pw);
         o[2] = prelu_f(fmaf(o[2], sc.z, sh.z) + R[ct][wt].z, pw);
         o[3] = prelu_f(fmaf(o[3], sc.w, sh.w) + R[ct][wt].w, pw);
-        bst4(ry, wro[wt] + 64 * ct, make_float4(o[0], o[1], o[2], o[3]));
+#else
+        (void)wc;
+        o[0] += R[ct][wt].x;
+#endif
+        bst4(ry, wro0 + wt * 4096 + 64 * ct, make_float4(o[0], o[1], o[2], o[3]));
       }
     }
     // ---- P_t/Q_t of h: out[ch][w] = sum_c wq[ch][c] h[c][w] + b ----
     f32x4 acc[NWT];
 #pragma unroll
     for (int wt = 0; wt < NWT; ++wt) acc[wt] = zero4();
+#ifndef DSTD_ABL_PQ
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const f16x8 qh = as_h8(pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(pql[(ks * 2 + 1) * 64 + lz]);
@@ -339,12 +396,13 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt) acc[wt] = mfma32(qh, hh[wt], acc[wt]);
     }
+#endif
     {
       const float s = scl[2];
       const auto rp = rsrc(a.pq + (size_t)u * V * 4, V * 16);
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt)
-        bst4(rp, wpq[wt],
+        bst4(rp, wpq0 + wt * 256,
              make_float4(fmaf(acc[wt][0], s, bql[0]), fmaf(acc[wt][1], s, bql[1]), fmaf(acc[wt][2], s, bql[2]),
                          fmaf(acc[wt][3], s, bql[3])));
     }
@@ -435,6 +493,24 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
     const int un = u + 1;
     const int lz = lane + opaque_zero();
     const size_t cbase = ((size_t)n * T * V + v) * 64;
+    // Issue order matters: vmcnt retires in order, so every load this unit
+    // waits for (adjacency, residual) is issued before the next unit's h-row
+    // prefetch, which lands behind them.
+    uint4 bh[NS][NUT], bo[NS][NUT];  // adjacency B fragments [K-step][u tile]
+    {
+      const auto rh = rsrc(a.adj + (size_t)u * (adj_bytes / 2), adj_bytes / 2);  // hi plane
+      const auto rl = rsrc(a.adj + (size_t)u * (adj_bytes / 2) + T * SL, adj_bytes / 2);
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) {
+          const int uo = 16 * ut + cl;
+          const uint32_t off = uo < T && kl < SM::ng(s) ? (uint32_t)(uo * SL + 8 * (SM::goff(s) + kl)) * 2 : OOB;
+          bh[s][ut] = bldu4(rh, off);
+          bo[s][ut] = bldu4(rl, off);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
     f16x8 xh[MT][2], xo[MT][2];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -461,7 +537,6 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
         for (int m = 0; m < MT; ++m) D[m][ct] = mfma32(xh[m][ks], wh, D[m][ct]);
       }
     }
-    if (un < uend) load_x(un);  // h rows are dead after the conv
     {
       const float s = scl[0];
 #pragma unroll
@@ -473,41 +548,9 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
           for (int r = 0; r < 4; ++r) D[m][ct][r] = fmaf(D[m][ct][r], s, b);
       }
     }
-    // ---- aggregation: O[c][u] = sum_t D[t][c] Adj[v][t][u] ----
-    f32x4 O[4][NUT];
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = zero4();
-    const auto radj = rsrc(a.adj + (size_t)u * (adj_bytes / 2), adj_bytes);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      uint4 bh[NUT], bo[NUT];
-#pragma unroll
-      for (int ut = 0; ut < NUT; ++ut) {
-        const int uo = 16 * ut + cl;
-        const uint32_t off = uo < T && kl < SM::ng(s) ? (uint32_t)(uo * SL + 8 * (SM::goff(s) + kl)) * 2 : OOB;
-        bh[ut] = bldu4(radj, off);
-        bo[ut] = bldu4(radj, off + T * SL * 2);
-      }
-      f16x8 dh[4], dl[4];
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) split_acc(D[2 * s][ct], 2 * s + 1 < MT ? D[2 * s + 1][ct] : zero4(), dh[ct], dl[ct]);
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dl[ct], as_h8(bh[ut]), O[ct][ut]);
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bo[ut]), O[ct][ut]);
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bh[ut]), O[ct][ut]);
-    }
-    // residual of the encoder epilogue, loaded after the aggregation (register pressure)
+    // residual of the encoder epilogue
     float4 R[use_res ? 4 : 1][use_res ? NUT : 1];
+    __builtin_amdgcn_sched_barrier(0);
     if constexpr (use_res) {
       const auto rr = rsrc(a.xres + cbase, col_bytes);
 #pragma unroll
@@ -515,6 +558,36 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct) R[ct][ut] = bld4(rr, uoff[ut] + 64 * ct);
     }
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- aggregation: O[c][u] = sum_t D[t][c] Adj[v][t][u] ----
+    f32x4 O[4][NUT];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = zero4();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      f16x8 dh[4], dl[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) split_acc(D[2 * s][ct], 2 * s + 1 < MT ? D[2 * s + 1][ct] : zero4(), dh[ct], dl[ct]);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dl[ct], as_h8(bh[s][ut]), O[ct][ut]);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bo[s][ut]), O[ct][ut]);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bh[s][ut]), O[ct][ut]);
+    }
+    // next unit's h rows (unconditional -- the last unit reloads itself -- so
+    // that no branch hides the loads from hipcc's vmcnt bookkeeping)
+    __builtin_amdgcn_sched_barrier(0);
+    load_x(min(un, uend - 1));
+    __builtin_amdgcn_sched_barrier(0);
 
     // ---- epilogue ----
     const auto ry = rsrc(a.y + cbase, col_bytes);
@@ -569,6 +642,218 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
     }
     u = un;
   }
+}
+
+
+// ===========================================================================
+// Dynamic adjacency in split-f16 planes (DSTDGC.forward model/dstdgcn.py:
+// 83-87 spatial, 88-93 temporal: tanh(P - Q), conv_rm, * alpha + A):
+//   out[row][q][slot] = alpha * (sum_k W[row][k] tanh(P[k][p] - Q[k][q]) + b[row]) + Astat[p][q]
+// with p = slot_idx(slot).  MODE 0 (spatial): row = t, (p, q) = joints,
+// k = r*T + t'.  MODE 1 (temporal): row = v, (p, q) = frames, k = r*V + v'.
+// tanh separably, as in dstd_fast.hip: E = 2^(c P), F = 2^(-c Q) once per
+// workgroup in LDS ([p][k] rows, k contiguous so a lane's 8 k of a K-step are
+// two 16-byte reads), tanh = 1 - 2 / (E F + 1); a sample with |cP| or |cQ|
+// above 120 takes the direct tanh(P - Q) path.  The B fragments (tanh
+// values) are split into hi/lo in registers and meet the conv_rm A
+// fragments (HLJ_RM image in LDS) in three 16x16x32 f16 MFMAs.
+// Workgroup = (sample, graph, column chunk), 8 waves over 16-column tiles.
+// ===========================================================================
+
+template <int MODE, int NROW, int K, int NA>
+struct AdjHLGeom {
+  static constexpr int RT = cdiv(NROW, 16), NS = cdiv(K, 32), KP = 32 * NS, KH = K / 2;
+  static constexpr int SE = KP + 4;  // LDS row stride of E / F (16-byte aligned, rows spread over banks)
+  using SM = SlotMap<NA, MODE == 0>;
+  static constexpr int SL = SM::SL, NCOL = NA * SL, NCT = cdiv(NCOL, 16);
+  static constexpr int NCHUNK = MODE == 0 ? 1 : 2;
+  static constexpr int CPC = cdiv(NCT, NCHUNK);
+  static constexpr int OS = 20;  // staging row stride (floats)
+  static constexpr int T = MODE == 0 ? NROW : NA, V = MODE == 0 ? NA : NROW;
+  static_assert(2 * KH == K, "K = 2 * (T or V)");
+  // waves per workgroup: every wave gets the same number of column tiles
+  // (33 spatial tiles at V = 22 -> 11 waves x 3; the old 8 waves left a
+  // 5-vs-4 tail in every workgroup)
+  static constexpr int ROUNDS = cdiv(CPC, 12);
+  static constexpr int AW = cdiv(CPC, ROUNDS);
+  static constexpr int AT = AW * 64;
+};
+
+template <int MODE, int NROW, int K, int NA>
+__global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(AdjHLArgs a) {
+  using Gm = AdjHLGeom<MODE, NROW, K, NA>;
+  using SM = typename Gm::SM;
+  constexpr int RT = Gm::RT, NS = Gm::NS, KP = Gm::KP, KH = Gm::KH, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
+  constexpr int AW = Gm::AW, AT = Gm::AT;
+  constexpr int OS = Gm::OS, T = Gm::T, V = Gm::V;
+  constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
+  __shared__ float El[(NA + 1) * SE];
+  __shared__ float Fl[(NA + 1) * SE];
+  __shared__ uint4 wl[RT * NS * 2 * 64];
+  __shared__ float asl[NA * NA + 1];
+  __shared__ float bsl[RT * 16];
+  __shared__ float stg[AW][32 * OS];  // two row tiles at a time
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int kg = lane >> 4, cl = lane & 15;
+  const int chunk = blockIdx.x % Gm::NCHUNK;
+  const int g = (blockIdx.x / Gm::NCHUNK) % a.ngroups;
+  const int n = blockIdx.x / (Gm::NCHUNK * a.ngroups);
+  if (n >= a.B) return;
+  TLH(MODE, 0)
+
+  // ---- prologue: P/Q -> E/F rows, conv_rm fragments, A-stat, bias.  Every
+  // global load is issued before the first LDS write (one memory round
+  // trip instead of one per loop iteration) ----
+  const PQLayout L = a.pql;
+  const float* pqb = a.pq + (size_t)n * L.sn + a.p_ch[g];
+  constexpr int NPQ = cdiv(T * V, AT), NW = cdiv(RT * NS * 2 * 64, AT), NAS = cdiv(NA * NA, AT);
+  float4 q4[NPQ];
+  uint4 wv[NW];
+  float av[NAS];
+#pragma unroll
+  for (int it = 0; it < NPQ; ++it) {
+    const int i = min(tid + it * AT, T * V - 1);                              // clamped: no branch
+    const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;  // memory order
+    q4[it] = ld4(pqb + t * L.st + v * L.sv);                                  // (P_0, P_1, Q_0, Q_1)
+  }
+#pragma unroll
+  for (int it = 0; it < NW; ++it) wv[it] = a.wimg[g][min(tid + it * AT, RT * NS * 2 * 64 - 1)];
+#pragma unroll
+  for (int it = 0; it < NAS; ++it) av[it] = a.astat[g][min(tid + it * AT, NA * NA - 1)];
+  const float bv = tid < NROW ? a.bias[g][tid] : 0.f;
+  // padding: k in [K, KP) and the row p = q = NA: E = F = 1 (tanh 0)
+  for (int i = tid; i < (NA + 1) * (KP - K); i += AT) {
+    const int r = i / (KP - K), k = K + i % (KP - K);
+    El[r * SE + k] = 1.f;
+    Fl[r * SE + k] = 1.f;
+  }
+  for (int i = tid; i < K; i += AT) {
+    El[NA * SE + i] = 1.f;
+    Fl[NA * SE + i] = 1.f;
+  }
+  int bad = 0;
+#pragma unroll
+  for (int it = 0; it < NPQ; ++it) {
+    const int i = tid + it * AT;
+    if (i < T * V) {
+      const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;
+      const int pr = MODE == 0 ? v : t, ki = MODE == 0 ? t : v;
+      const float ep0 = C2 * q4[it].x, ep1 = C2 * q4[it].y, eq0 = -C2 * q4[it].z, eq1 = -C2 * q4[it].w;
+      bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
+      El[pr * SE + ki] = __builtin_amdgcn_exp2f(ep0);
+      El[pr * SE + KH + ki] = __builtin_amdgcn_exp2f(ep1);
+      Fl[pr * SE + ki] = __builtin_amdgcn_exp2f(eq0);
+      Fl[pr * SE + KH + ki] = __builtin_amdgcn_exp2f(eq1);
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < NW; ++it)
+    if (tid + it * AT < RT * NS * 2 * 64) wl[tid + it * AT] = wv[it];
+#pragma unroll
+  for (int it = 0; it < NAS; ++it)
+    if (tid + it * AT < NA * NA) asl[tid + it * AT] = av[it];
+  if (tid == 0) asl[NA * NA] = 0.f;
+  if (tid < RT * 16) bsl[tid] = bv;
+  const bool sep = __syncthreads_or(bad) == 0;
+  if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0)
+    for (int i = tid; i < T * V; i += AT) {
+      const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;
+      const float4 q4 = ld4(pqb + t * L.st + v * L.sv);
+      const int pr = MODE == 0 ? v : t, ki = MODE == 0 ? t : v;
+      El[pr * SE + ki] = q4.x;
+      El[pr * SE + KH + ki] = q4.y;
+      Fl[pr * SE + ki] = q4.z;
+      Fl[pr * SE + KH + ki] = q4.w;
+    }
+    for (int i = tid; i < (NA + 1) * (KP - K); i += AT) {
+      const int r = i / (KP - K), k = K + i % (KP - K);
+      El[r * SE + k] = 0.f;
+      Fl[r * SE + k] = 0.f;
+    }
+    for (int i = tid; i < K; i += AT) {
+      El[NA * SE + i] = 0.f;
+      Fl[NA * SE + i] = 0.f;
+    }
+    __syncthreads();
+  }
+  const float alpha = *a.alpha, inv = *a.wscale[g];
+  TLH(MODE, 1)
+
+  float* so = stg[wave];
+  uint16_t* out = a.out + (size_t)n * a.out_sN + (size_t)g * a.out_sG;
+  const int ct_end = min(Gm::NCT, (chunk + 1) * Gm::CPC);
+  for (int ct = chunk * Gm::CPC + wave; ct < ct_end; ct += AW) {
+    // this lane's column (B operand column j = cl)
+    const int col = ct * 16 + cl;
+    const int q = col / SL, pi = SM::slot_idx(col - q * SL);
+    const bool valid = col < NCOL && pi < NA;
+    const int pr = valid ? pi : NA, qr = col < NCOL ? q : NA;
+    // ---- B fragments: tanh(P[k][p] - Q[k][q]) for k = 32s + 8kg + e ----
+    f16x8 bh[NS], bo[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const float* ep = El + pr * SE + 32 * s + 8 * kg;
+      const float* fq = Fl + qr * SE + 32 * s + 8 * kg;
+      const float4 e0 = ld4(ep), e1 = ld4(ep + 4), f0 = ld4(fq), f1 = ld4(fq + 4);
+      float tv[8];
+      const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+      const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      if (sep) {
+#pragma unroll
+        for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fmaf(-2.f, __builtin_amdgcn_rcpf(fmaf(ev[e8], fv[e8], 1.f)), 1.f);
+      } else {
+#pragma unroll
+        for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fast_tanh(ev[e8] - fv[e8]);
+      }
+      split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
+    }
+    // ---- conv_rm: acc[row][col] = sum_k W'[row][k] B[k][col] ----
+    f32x4 acc[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = zero4();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      f16x8 ah[RT], ao[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        ah[rt] = as_h8(wl[((rt * NS + s) * 2 + 0) * 64 + lane]);
+        ao[rt] = as_h8(wl[((rt * NS + s) * 2 + 1) * 64 + lane]);
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ao[rt], bh[s], acc[rt]);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bo[s], acc[rt]);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bh[s], acc[rt]);
+    }
+    // ---- epilogue: alpha * (acc + b) + Astat, 0 on padding slots; staged
+    // through this wave's LDS slot so a lane stores 8 consecutive slots ----
+    const float as = asl[valid ? pr * NA + qr : NA * NA];
+#pragma unroll
+    for (int r2 = 0; r2 < RT; r2 += 2) {
+#pragma unroll
+      for (int dr = 0; dr < 2; ++dr) {
+        if (r2 + dr >= RT) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = (r2 + dr) * 16 + 4 * kg + r;
+          so[(dr * 16 + 4 * kg + r) * OS + cl] = valid ? fmaf(alpha, fmaf(acc[r2 + dr][r], inv, bsl[row]), as) : 0.f;
+        }
+      }
+      // lane -> (row of the pair, 8-column half)
+      const int rl = lane >> 1, h = lane & 1, row = r2 * 16 + rl, c8 = ct * 16 + 8 * h;
+      if (row < NROW && c8 < NCOL) {
+        const float4 v0 = ld4(so + rl * OS + 8 * h), v1 = ld4(so + rl * OS + 8 * h + 4);
+        uint4 hi, lo;
+        split8(v0, v1, hi, lo);
+        *reinterpret_cast<uint4*>(out + (size_t)row * (2 * NCOL) + c8) = hi;
+        *reinterpret_cast<uint4*>(out + (size_t)row * (2 * NCOL) + NCOL + c8) = lo;
+      }
+    }
+  }
+  TLH(MODE, 2)
+  TLH(MODE, 3)
 }
 
 // ===========================================================================
@@ -628,6 +913,33 @@ static bool hl_shape(int T, int V) {
   return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23) || (T == 75 && V == 22);
 }
 bool spatial_hl_supported(int T, int V) { return hl_shape(T, V); }
+
+template <int MODE, int NROW, int K, int NA>
+hipError_t adj_hl_run(const AdjHLArgs& a, hipStream_t s) {
+  using Gm = AdjHLGeom<MODE, NROW, K, NA>;
+  const int grid = a.B * a.ngroups * Gm::NCHUNK;
+  hipLaunchKernelGGL((k_adj_hl<MODE, NROW, K, NA>), dim3(grid), dim3(Gm::AT), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_adj_hl(const AdjHLArgs& a, int mode, int T, int V, hipStream_t s) {
+  if (a.pql.sch != 1 || ((uintptr_t)a.pq & 15) || (a.pql.st & 3) || (a.pql.sv & 3) || (a.pql.sn & 3))
+    return hipErrorNotSupported;
+  for (int g = 0; g < a.ngroups; ++g)
+    if (a.p_ch[g] & 3) return hipErrorNotSupported;
+  if (mode == 0) {
+    if (T == 35 && V == 22) return adj_hl_run<0, 35, 70, 22>(a, s);
+    if (T == 35 && V == 25) return adj_hl_run<0, 35, 70, 25>(a, s);
+    if (T == 40 && V == 23) return adj_hl_run<0, 40, 80, 23>(a, s);
+    if (T == 75 && V == 22) return adj_hl_run<0, 75, 150, 22>(a, s);
+  } else {
+    if (T == 35 && V == 22) return adj_hl_run<1, 22, 44, 35>(a, s);
+    if (T == 35 && V == 25) return adj_hl_run<1, 25, 50, 35>(a, s);
+    if (T == 40 && V == 23) return adj_hl_run<1, 23, 46, 40>(a, s);
+    if (T == 75 && V == 22) return adj_hl_run<1, 22, 44, 75>(a, s);
+  }
+  return hipErrorNotSupported;
+}
 bool temporal_hl_supported(int T, int V) { return hl_shape(T, V); }
 
 hipError_t launch_spatial_hl(const SpatialHLArgs& a, hipStream_t s) {
@@ -651,3 +963,11 @@ hipError_t launch_temporal_hl(const TemporalHLArgs& a, hipStream_t s) {
 }
 
 }  // namespace dstd
+
+#ifdef DSTD_STAMPS
+extern "C" int dstd_debug_timeline_hl(int mode, unsigned long long* host, int n) {
+  if (mode < 0 || mode > 1 || n > 2048 * 4) return 1;
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tl_hl), n * sizeof(unsigned long long),
+                                  mode * 2048 * 4 * sizeof(unsigned long long));
+}
+#endif

@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """Workgroup timeline of the adjacency kernels (library built with -DDSTD_STAMPS).
 
-  python scripts/timeline.py dstd-gcn_amd/libdstd_gcn_stamps.so
-Runs one forward, then reads the last launch's per-workgroup s_memrealtime
+  python scripts/timeline.py dstd-gcn_amd/libdstd_gcn_stamps.so [--hl]
+(--hl: the split-f16 adjacency kernels of dstd_hilo.hip).  Runs one forward, then reads the last launch's per-workgroup s_memrealtime
 stamps (entry, staging done, compute done, exit; 100 MHz) for each mode.
 """
 import ctypes
@@ -25,7 +25,7 @@ def main():
     os.environ["DSTD_LIB"] = lib
     native.LIB_PATH = lib
     L = native.lib()
-    fn = L.dstd_debug_timeline
+    fn = L.dstd_debug_timeline_hl if "--hl" in sys.argv else L.dstd_debug_timeline
     fn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
     dev = torch.device("cuda", 0)
     model, opts, _ = bench.load_model("h36m", dev)
