@@ -13,11 +13,16 @@ calibrated), so activations stay finite; values do not change the work.
           collective; the per-rank elapsed time is MAX-reduced over RCCL)
 
 One JSON line on rank 0.  Besides the driver's fields it carries
-  roofline     : the dominant kernel family, timed with HIP events around its
-                 launches inside the timed region; achieved = its algorithmic
-                 FLOPs / its summed launch time, against the
-                 fp32 MFMA peak.  traffic = HBM bytes per launch from
-                 profiles/pmc_traffic.json (rocprofv3 PMC run) when present.
+  roofline     : the dominant kernel family (largest summed time per step in
+                 an untimed profiled pass), its launch in DSTDGCB 1 (the first
+                 encoder, a 64->64 split-f16 launch) bracketed by two HIP events
+                 in every timed step; achieved = that launch's algorithmic HBM
+                 bytes (each input read once, each output written once, in the
+                 layouts of DESIGN.md §3; block_bytes below) / its average
+                 duration, against the 8 TB/s HBM3E peak.  The split-f16
+                 kernels are not MFMA-bound, so HBM is the
+                 roofline.  traffic = measured HBM bytes per launch of that
+                 kernel from profiles/pmc_traffic.json (rocprofv3 PMC passes).
   cpu_baseline : the CPU oracle (op-for-op restatement of the reference
                  forward, torch fp32) timed on this host's cores, N=1 only.
 """
@@ -86,6 +91,54 @@ def block_flops(cin, cout, T, V, tail):
             native.KIND_TEMPORAL: temporal}
 
 
+def hl_sl_spatial(V):
+    return 8 * ((V + 7) // 8)
+
+
+def hl_sl_temporal(T):
+    g = 0
+    for s in range((T + 31) // 32):
+        n = 0
+        for kg in range(4):
+            for e in range(8):
+                if 32 * s + 16 * (e >> 2) + 4 * kg + (e & 3) < T:
+                    n = kg + 1
+        g += n
+    return 8 * g
+
+
+def block_bytes(cin, cout, T, V, tail, split):
+    """Algorithmic HBM bytes per sample of each kernel family of one DSTDGCB:
+    inputs read once, outputs written once, in the stored layouts (NTVC fp32
+    activations, channel-innermost P/Q, adjacencies as fp32 rows or split-f16
+    planes).  split: (spatial, temporal) launches run the
+    split-f16 kernels."""
+    TV = T * V
+    adj_s = 2 * T * (2 * V * hl_sl_spatial(V) * 2 if split[0] else 4 * ((V * V + 3) // 4 * 4))
+    adj_t = V * (2 * T * hl_sl_temporal(T) * 2 if split[1] else 4 * ((T * T + 3) // 4 * 4))
+    pq_s, pq_t = TV * 8 * 4, TV * 4 * 4
+    spatial = TV * cin * 4 + adj_s + TV * cout * 4 + pq_t
+    temporal = TV * cout * 4 + adj_t + (TV * cout * 4 if tail == "enc" else 0) + TV * (cout if tail != "out" else 3) * 4
+    if tail == "out":
+        temporal += V * 3 * 4  # last observed frame of the model input
+    else:
+        temporal += pq_s
+    return {native.KIND_ADJ_S: pq_s + adj_s, native.KIND_SPATIAL: spatial, native.KIND_ADJ_T: pq_t + adj_t,
+            native.KIND_TEMPORAL: temporal}
+
+
+def model_block_bytes(opts, split_on):
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    V, C, L = opts["joints_to_consider"], opts["num_feature"], opts["num_layers"]
+    cin0, cout_last = opts["input_channels"], opts["input_channels"] // 2
+    spec = [(cin0, C, "in")] + [(C, C, "enc")] * L + [(C, cout_last, "out")]
+    out = []
+    for cin, cout, tail in spec:
+        split = (split_on and cin == 64 and cout == 64, split_on and cout == 64)
+        out.append(block_bytes(cin, cout, T, V, tail, split))
+    return out
+
+
 def model_block_flops(opts):
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V, C, L = opts["joints_to_consider"], opts["num_feature"], opts["num_layers"]
@@ -105,7 +158,7 @@ class Profiler:
         native.check(L.dstd_events_create(self.n, self.events), "dstd_events_create")
         self.kinds = (ctypes.c_int * pairs)()
         self.block = (ctypes.c_int * pairs)()
-        self.prof = native.Profile(kind_mask, pairs, 0, self.events, self.kinds, self.block)
+        self.prof = native.Profile(kind_mask, pairs, 0, self.events, self.kinds, self.block, -1)
 
     def elapsed(self):
         out = []
@@ -219,8 +272,10 @@ def main():
         prof.close()
         dominant = max((k for k in per_kind if k in fl[0]), key=lambda k: per_kind[k])
 
-        # timed region: exactly K steps, events only around the dominant family
-        prof = Profiler(L, args.steps * nb, 1 << dominant)
+        # timed region: exactly K steps; two events per step around the
+        # dominant family's launch in DSTDGCB 1 (an encoder)
+        prof = Profiler(L, args.steps, 1 << dominant)
+        prof.prof.only_block = 1
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -240,12 +295,16 @@ def main():
         # partials (the forward itself has no exchange)
         D.reduce_partials(y.double().abs().sum().reshape(1), torch.tensor([B], device=device))
 
+    split_on = L.dstd_get_gc_precision() == 1
+    bb = model_block_bytes(opts, split_on)
     kernel_ms = sum(ms for _, _, ms in launches)
-    kernel_flop = sum(fl[blk][dominant] for _, blk, _ in launches) * B
-    achieved = kernel_flop / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+    kernel_bytes = sum(bb[blk][dominant] for _, blk, _ in launches) * B
+    achieved = kernel_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     kname = native.KIND_NAMES[dominant]
-    traffic = load_traffic(kname)
+    split_blk = split_on and opts["num_layers"] > 0
+    traffic = load_traffic(kname + "_split" if split_blk else kname)
     total_flop_per_seq = sum(sum(b.values()) for b in fl)
+    total_bytes_per_seq = sum(sum(b.values()) for b in bb)
 
     if rank == 0:
         out = {
@@ -260,13 +319,19 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "arithmetic": ("split-f16 MFMA for the 64->64 GC contractions (fp32 operands as f16 hi/lo pairs, three "
+                           "v_mfma_f32_16x16x32_f16, fp32 accumulate), exact-fp32 MFMA elsewhere") if split_on
+                          else "exact-fp32 MFMA (v_mfma_f32_16x16x4_f32)",
             "data": "synthetic (N(0,1) poses, future frames padded with the last observed; fixture weights)",
             "config": {"workload": CONFIGS[args.config][1] + f", B={B}/GPU, eval forward", "global_batch": B * world,
                        "seq_len": T, "joints": V, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3),
-                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": traffic, "launches": len(launches),
+            "roofline": {"bound": "hbm", "kernel": kname + (" (split-f16, DSTDGCB 1)" if split_blk else " (DSTDGCB 1)"),
+                         "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": int(bb[1][dominant] * B) if launches else None,
+                         "launches": len(launches),
                          "avg_launch_us": round(kernel_ms / max(len(launches), 1) * 1e3, 2),
+                         "whole_forward_gbs": round(total_bytes_per_seq * B * args.steps / elapsed / 1e9, 1),
                          "whole_forward_tflops": round(total_flop_per_seq * B * args.steps / elapsed / 1e12, 3)},
             "kernel_ms_per_step": {native.KIND_NAMES[k]: round(v / args.steps, 4) for k, v in sorted(per_kind.items())},
         }

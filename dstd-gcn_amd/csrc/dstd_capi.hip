@@ -63,6 +63,7 @@ struct Prof {
   void begin(int kind, hipStream_t s) {
     open = -1;
     if (!p || !(p->kind_mask & (1u << kind)) || p->count >= p->capacity) return;
+    if (p->only_block >= 0 && p->only_block != block) return;
     open = p->count++;
     p->kinds[open] = kind;
     if (p->block) p->block[open] = block;

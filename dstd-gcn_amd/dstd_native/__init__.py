@@ -49,7 +49,7 @@ class ModelParams(ctypes.Structure):
 class Profile(ctypes.Structure):
     _fields_ = [("kind_mask", ctypes.c_uint), ("capacity", ctypes.c_int), ("count", ctypes.c_int),
                 ("events", ctypes.POINTER(ctypes.c_void_p)), ("kinds", ctypes.POINTER(ctypes.c_int)),
-                ("block", ctypes.POINTER(ctypes.c_int))]
+                ("block", ctypes.POINTER(ctypes.c_int)), ("only_block", ctypes.c_int)]
 
 
 class GCGrads(ctypes.Structure):

@@ -147,6 +147,8 @@ typedef struct dstd_profile {
   void** events;
   int* kinds;
   int* block;
+  int only_block; /* >= 0: bracket only launches of that DSTDGCB (two events per
+                     forward keep the timed region close to an unprofiled one) */
 } dstd_profile;
 
 int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,

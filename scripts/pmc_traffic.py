@@ -18,6 +18,18 @@ from collections import defaultdict
 
 
 def family(name):
+    # split-f16 kernels (dstd_hilo.hip) are families of their own: the
+    # 64->64 launches whose bytes bench.py's roofline divides
+    if "k_spatial_hl" in name:
+        return "spatial_gc_split"
+    if "k_temporal_hl" in name:
+        return "temporal_gc_split"
+    if "k_adj_hl<0" in name:
+        return "adj_spatial_split"
+    if "k_adj_hl<1" in name:
+        return "adj_temporal_split"
+    if "k_hl_prep" in name:
+        return "hl_prep"
     if "k_spatial" in name:
         return "spatial_gc"
     if "k_temporal" in name:
