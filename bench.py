@@ -174,14 +174,9 @@ class Profiler:
 
 
 def forward_profiled(model, x, y, prof):
-    L = native.lib()
-    p = model._native_params()
-    B, T, V = x.shape[0], x.shape[1], x.shape[2]
-    nbytes = L.dstd_model_workspace_bytes(B, T, V, model.num_feature, model.num_layers)
-    ws = native.workspace(x.device, nbytes)
-    code = L.dstd_model_fwd_profiled(p, x.data_ptr(), B, y.data_ptr(), ws.data_ptr(), ws.numel(),
-                                     native.stream_handle(x.device), ctypes.byref(prof.prof))
-    native.check(code, "dstd_model_fwd_profiled")
+    """The model's own eval forward (DSTDGCN._forward_native: constants reused
+    across steps as in production) with event brackets."""
+    model._forward_native(x, y, ctypes.byref(prof.prof))
 
 
 def load_traffic(kernel):

@@ -779,11 +779,17 @@ int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int
 
 int dstd_model_fwd(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                    size_t workspace_bytes, void* stream) {
-  return dstd_model_fwd_profiled(p, x, B, y, workspace, workspace_bytes, stream, nullptr);
+  return dstd_model_fwd_ex(p, x, B, y, workspace, workspace_bytes, stream, 0u, nullptr);
 }
 
 int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                             size_t workspace_bytes, void* stream, dstd_profile* prof) {
+  return dstd_model_fwd_ex(p, x, B, y, workspace, workspace_bytes, stream, 0u, prof);
+}
+
+int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
+                      size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof) {
+  const bool reuse = (flags & DSTD_FWD_REUSE_CONSTANTS) != 0;
   if (!p || !x || !y || !workspace) return DSTD_EINVAL;
   if (prof && (prof->capacity < 0 || (prof->capacity > 0 && (!prof->events || !prof->kinds)))) return DSTD_EINVAL;
   Prof pf;
@@ -811,9 +817,11 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
     add_block_jobs(fa, &p->enc[i], L.f_enc[i], T, V);
     add_bn_job(fa, p->enc_bn[i], C, V, L.ebn_s[i], L.ebn_h[i]);
   }
-  pf.begin(DSTD_KIND_FOLD, s);
-  DSTD_TRY(run_fold(fa, s));
-  pf.end(s);
+  if (!reuse) {
+    pf.begin(DSTD_KIND_FOLD, s);
+    DSTD_TRY(run_fold(fa, s));
+    pf.end(s);
+  }
 
   // input prep: x6 = cat(x, x - x[:, -1]) and block-0 spatial P/Q (:298-305)
   PQArgs pa{};
@@ -887,9 +895,11 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
     hls[b] = block_hl(blk[b], tails[b], T, V);
     add_block_hl_jobs(hj, blk[b], *fold[b], tails[b], hls[b], T, V);
   }
-  pf.begin(DSTD_KIND_FOLD, s);
-  DSTD_TRY(run_hl_prep(hj, s));
-  pf.end(s);
+  if (!reuse) {
+    pf.begin(DSTD_KIND_FOLD, s);
+    DSTD_TRY(run_hl_prep(hj, s));
+    pf.end(s);
+  }
   for (int b = 0; b < NB; ++b) {
     pf.block = b;
     DSTD_TRY(run_block(blk[b], *fold[b], L.sc, B, T, V, xin[b], hbuf[b], ybuf[b], tails[b], s, pf, hls[b]));

@@ -90,9 +90,16 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+#ifdef DSTD_ABL_LOAD
+  const float f = (float)(off & 255) * 1e-3f;
+  return make_float4(f, f, f, f);
+#endif
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 __device__ __forceinline__ uint4 bldu4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+#ifdef DSTD_ABL_LOAD
+  return make_uint4(off & 0x3c003c00u, off, off, off);
+#endif
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
@@ -185,7 +192,11 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
 //   h = prelu(bn(y) + x)  ->  NTVC, and P_t/Q_t of h ([B][T][V][4])
 // ===========================================================================
 template <int V>
-__global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_spatial_hl(SpatialHLArgs a) {
+#ifndef DSTD_HL_WPE
+#define DSTD_HL_WPE 2
+#endif
+__global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE, DSTD_HL_WPE))) void k_spatial_hl(
+    SpatialHLArgs a) {
   using SM = SlotMap<V, true>;
   constexpr int SL = SM::SL, NG = SM::NG, NWT = cdiv(V, 16);
   static_assert(SM::MT == 2 && SM::NS == 1, "one K-step of two tiles per frame");
@@ -239,10 +250,9 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     }
   };
   uint4 ab[2][NWT][2];  // adjacency B fragments [graph][w tile][plane]
-  auto load_adj = [&](int uu) {
+  auto load_adj_g = [&](int uu, int g) {
     const int n = uu / T, t = uu - n * T;
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    {
       const uint16_t* base = a.adj + ((size_t)(n * 2 + g) * T + t) * (adj_bytes / 2);
       const auto rh = rsrc(base, adj_bytes / 2), rl = rsrc(base + V * SL, adj_bytes / 2);  // one plane each
 #pragma unroll
@@ -252,10 +262,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
       }
     }
   };
-  if (u < uend) {
-    load_x(u);
-    load_adj(u);
-  }
+  if (u < uend) load_x(u);
   while (u < uend) {
     const int un = u + 1;
     const int lz = lane + opaque_zero();
@@ -266,6 +273,10 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
     for (int wt = 0; wt < NWT; ++wt)
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) R[ct][wt] = bld4(rx, wro0 + wt * 4096 + 64 * ct);
+    // this unit's graph-0 adjacency now, graph 1 after the first conv (a
+    // whole-unit-ahead prefetch of both measured 6% slower: registers)
+    load_adj_g(u, 0);
+    __builtin_amdgcn_sched_barrier(0);
     f16x8 xh[2][2], xo[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -315,6 +326,11 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
             for (int m = 0; m < 2; ++m) D[m][c2 + q] = mfma32(xh[m][ks], wh[q], D[m][c2 + q]);
         }
+      if (g == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        load_adj_g(u, 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       // x is dead after the second conv: prefetch the next unit's rows
       // (unconditionally -- the last unit reloads itself -- so that no
       // branch hides the loads from hipcc's vmcnt bookkeeping)
@@ -353,9 +369,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(2, 2))) void
 #pragma unroll
         for (int wt = 0; wt < NWT; ++wt) O[ct][wt] = mfma32(dh[ct], as_h8(ab[g][wt][0]), O[ct][wt]);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    load_adj(min(un, uend - 1));
-    __builtin_amdgcn_sched_barrier(0);
+
 
     // ---- epilogue: h = prelu(bn(y) + x) -> NTVC ----
     const auto ry = rsrc(a.y + (size_t)u * V * 64, unit_bytes);

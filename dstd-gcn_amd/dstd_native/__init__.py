@@ -73,6 +73,7 @@ class ModelGrads(ctypes.Structure):
                 ("enc_prelu", ctypes.c_void_p * MAX_LAYERS), ("st_out", BlockGrads)]
 
 
+FWD_REUSE_CONSTANTS = 1  # include/dstd_gcn.h DSTD_FWD_REUSE_CONSTANTS
 KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL = range(6)
 KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temporal_gc")
 
@@ -102,6 +103,9 @@ def lib():
         L.dstd_block_fwd.argtypes = [ctypes.POINTER(BlockParams), vp, ci, ci, ci, vp, vp, sz, vp]
         L.dstd_model_fwd.restype = ci
         L.dstd_model_fwd.argtypes = [ctypes.POINTER(ModelParams), vp, ci, vp, vp, sz, vp]
+        L.dstd_model_fwd_ex.restype = ci
+        L.dstd_model_fwd_ex.argtypes = [ctypes.POINTER(ModelParams), vp, ci, vp, vp, sz, vp, ctypes.c_uint,
+                                        ctypes.POINTER(Profile)]
         L.dstd_model_fwd_profiled.restype = ci
         L.dstd_model_fwd_profiled.argtypes = [ctypes.POINTER(ModelParams), vp, ci, vp, vp, sz, vp,
                                               ctypes.POINTER(Profile)]
@@ -166,7 +170,7 @@ def lib():
 EXPORTS = ("dstd_version", "dstd_error_string", "dstd_dstdgc_workspace_bytes", "dstd_block_workspace_bytes",
            "dstd_model_workspace_bytes", "dstd_dstdgc_fwd", "dstd_block_fwd", "dstd_model_fwd",
            "dstd_model_fwd_profiled", "dstd_events_create", "dstd_events_destroy", "dstd_event_elapsed_ms",
-           "dstd_set_gc_precision", "dstd_get_gc_precision")
+           "dstd_set_gc_precision", "dstd_get_gc_precision", "dstd_model_fwd_ex")
 TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_bytes", "dstd_dstdgc_train_fwd",
                  "dstd_dstdgc_train_bwd", "dstd_block_train_saved_bytes", "dstd_block_train_workspace_bytes",
                  "dstd_block_train_fwd", "dstd_block_train_bwd", "dstd_model_train_saved_bytes",
@@ -221,12 +225,20 @@ _ws_cache = {}
 def workspace(device, nbytes):
     """Caller-owned scratch (torch caching allocator), grown on demand and kept
     per (device, stream) so graph capture and steady state reuse one buffer."""
+    return workspace_claim(device, nbytes, None)[0]
+
+
+def workspace_claim(device, nbytes, tag):
+    """workspace() for a caller that can reuse what its previous call left in
+    the buffer: returns (buf, reused), reused = True iff the last claim of this
+    buffer carried the same (non-None) tag and nothing else used it since."""
     key = (str(device), torch.cuda.current_stream(device).cuda_stream)
-    buf = _ws_cache.get(key)
+    buf, last = _ws_cache.get(key, (None, None))
+    reused = buf is not None and buf.numel() >= nbytes and tag is not None and last == tag
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
-        _ws_cache[key] = buf
-    return buf
+    _ws_cache[key] = (buf, tag)
+    return buf, reused
 
 
 def gc_weights(dstdgc):

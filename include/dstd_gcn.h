@@ -153,6 +153,16 @@ typedef struct dstd_profile {
 
 int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                             size_t workspace_bytes, void* stream, dstd_profile* prof);
+
+/* dstd_model_fwd with flags (and an optional profile, as _profiled).
+ * DSTD_FWD_REUSE_CONSTANTS: the workspace still holds the folded constants
+ * and split-f16 weight images of a previous forward of the SAME parameters
+ * (same pointers, unmodified values), batch size and workspace, so the two
+ * parameter-preparation launches are skipped.  The caller vouches for it
+ * (the Python layer checks torch's per-tensor version counters). */
+#define DSTD_FWD_REUSE_CONSTANTS 1u
+int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
+                      size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof);
 int dstd_events_create(int n, void** events);
 int dstd_events_destroy(int n, void** events);
 int dstd_event_elapsed_ms(void* start, void* stop, float* ms);

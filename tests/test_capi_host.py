@@ -22,7 +22,7 @@ def header_symbols(name="dstd_gcn.h"):
 def test_library_exports_every_header_symbol():
     L = native.lib()
     syms = header_symbols()
-    assert len(syms) == 14, syms
+    assert len(syms) == 15, syms
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(native.EXPORTS)

@@ -162,6 +162,29 @@ def test_split_vs_fp32_bench_batch():
     assert rel_err(y32[picks].numpy(), y64) <= tol
 
 
+def test_constant_reuse_tracks_parameter_updates():
+    """Repeated forwards reuse the folded constants / weight images left in
+    the workspace (DSTD_FWD_REUSE_CONSTANTS); an in-place parameter update or
+    another user of the workspace in between must force a refold."""
+    m, d, sd, opts = load_model("h36m")
+    x = t(d["x"])
+    with torch.no_grad():
+        y0 = m(x)
+        y1 = m(x)  # reuse path
+        assert torch.equal(y0, y1)
+        m.encoders[0][1].bn.weight.mul_(1.5)  # in place: version counter moves
+        y2 = m(x)
+        m2, _, _, _ = load_model("h36m")
+        m2.encoders[0][1].bn.weight.data.mul_(1.5)
+        y_ref = m2(x)  # fresh model, fresh fold
+        assert torch.equal(y2, y_ref)
+        assert not torch.equal(y2, y0)
+        # another workspace user in between (a block forward), then the model again
+        blk = m.encoders[1][0].stgcn[0][0]
+        blk(torch.randn(2, 64, 35, 22, device=DEV))
+        assert torch.equal(m(x), y2)
+
+
 def test_deterministic_repeat():
     m, d, _, _ = load_model("cmu")
     x = t(d["x"])
