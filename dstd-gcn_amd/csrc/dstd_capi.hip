@@ -84,13 +84,13 @@ struct BlockFold {
   float* astat_s;  // [2][V][V]
   float* astat_t;  // [T][T]
   // split-f16 weight images (k_hl_prep, dstd_hilo.h) of the 64 -> 64 GC kernels
-  uint4* hl_ws[2];  // conv_s[g].conv_f
+  uint4* hl_ws[3];  // conv_s[g].conv_f, [2]: residual conv (cin != cout)
   uint4* hl_pqs;    // conv_t.conv_m1/m2 (P/Q written by the spatial kernel)
   uint4* hl_wt;     // conv_t.conv_f
   uint4* hl_pqt;    // next block's conv_s[*].conv_m1/m2 (P/Q written by the temporal kernel)
   uint4* hl_rms[2]; // conv_s[g].conv_rm (spatial adjacency)
   uint4* hl_rmt;    // conv_t.conv_rm (temporal adjacency)
-  float* hl_scale;  // [8]: 2^-s of ws0, ws1, pqs, wt, pqt, rms0, rms1, rmt
+  float* hl_scale;  // [9]: 2^-s of ws0, ws1, pqs, wt, pqt, rms0, rms1, rmt, ws2
 };
 
 // Split-f16 GC kernels (dstd_hilo.hip) where the shape has them: 1 (default),
@@ -127,13 +127,14 @@ void carve_fold(Carver& cv, BlockFold& f, int T, int V, int cout, bool res) {
   auto img = [&](int n) { return reinterpret_cast<uint4*>(cv.take((size_t)4 * n)); };
   f.hl_ws[0] = img(kHLConvImg);
   f.hl_ws[1] = img(kHLConvImg);
+  f.hl_ws[2] = img(kHLConvImg);
   f.hl_pqs = img(kHLPQImg);
   f.hl_wt = img(kHLConvImg);
   f.hl_pqt = img(kHLPQImg);
   f.hl_rms[0] = img(hl_rm_img(T, 2 * T));
   f.hl_rms[1] = img(hl_rm_img(T, 2 * T));
   f.hl_rmt = img(hl_rm_img(V, 2 * V));
-  f.hl_scale = cv.take(8);
+  f.hl_scale = cv.take(12);
 }
 
 // adjacency scratch: the larger of the fp32 rows and the split-f16 planes
@@ -213,11 +214,13 @@ hipError_t run_hl_prep(const HLList& jobs, hipStream_t s) {
   return hipSuccess;
 }
 
-void add_hl_conv(HLList& l, const float* w, uint4* img, float* sc) {
+void add_hl_conv(HLList& l, const float* w, int rows, int cols, uint4* img, float* sc) {
   HLJob j{};
   j.kind = HLJ_CONV;
   j.w[0] = w;
   j.nblk = 1;
+  j.rows = rows;
+  j.cols = cols;
   j.img = img;
   j.inv_scale = sc;
   l.push_back(j);
@@ -233,11 +236,12 @@ void add_hl_rm(HLList& l, const float* w, int rows, int cols, uint4* img, float*
   j.inv_scale = sc;
   l.push_back(j);
 }
-void add_hl_pq(HLList& l, const float* const* w, int nblk, uint4* img, float* sc) {
+void add_hl_pq(HLList& l, const float* const* w, int nblk, int cols, uint4* img, float* sc) {
   HLJob j{};
   j.kind = HLJ_PQ;
   for (int i = 0; i < nblk; ++i) j.w[i] = w[i];
   j.nblk = nblk;
+  j.cols = cols;
   j.img = img;
   j.inv_scale = sc;
   l.push_back(j);
@@ -256,7 +260,8 @@ struct BlockTail {
 BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V) {
   BlockHL r{false, false};
   if (!hl_on()) return r;
-  r.s = p->cin == 64 && p->cout == 64 && spatial_hl_supported(T, V);
+  r.s = spatial_hl_supported(T, V) &&
+        ((p->cin == 64 && p->cout == 64) || (p->cin == 6 && p->cout == 64) || (p->cin == 64 && p->cout == 3));
   r.t = p->cout == 64 && temporal_hl_supported(T, V) &&
         (tail.epi == TEPI_ENC || tail.epi == TEPI_IN || tail.epi == TEPI_RAW) &&
         (!tail.next || tail.next->cin == 64);
@@ -269,18 +274,19 @@ void add_block_hl_jobs(HLList& l, const dstd_block_params* p, const BlockFold& f
   if (hl.s) {
     add_hl_rm(l, p->conv_s[0].wrm, T, 2 * T, f.hl_rms[0], f.hl_scale + 5);
     add_hl_rm(l, p->conv_s[1].wrm, T, 2 * T, f.hl_rms[1], f.hl_scale + 6);
-    add_hl_conv(l, p->conv_s[0].wf, f.hl_ws[0], f.hl_scale + 0);
-    add_hl_conv(l, p->conv_s[1].wf, f.hl_ws[1], f.hl_scale + 1);
+    add_hl_conv(l, p->conv_s[0].wf, p->cout, p->cin, f.hl_ws[0], f.hl_scale + 0);
+    add_hl_conv(l, p->conv_s[1].wf, p->cout, p->cin, f.hl_ws[1], f.hl_scale + 1);
+    if (p->cin != p->cout) add_hl_conv(l, p->res_w, p->cout, p->cin, f.hl_ws[2], f.hl_scale + 8);
     const float* w[2] = {p->conv_t.wm1, p->conv_t.wm2};
-    add_hl_pq(l, w, 2, f.hl_pqs, f.hl_scale + 2);
+    add_hl_pq(l, w, 2, p->cout, f.hl_pqs, f.hl_scale + 2);
   }
   if (hl.t) {
     add_hl_rm(l, p->conv_t.wrm, V, 2 * V, f.hl_rmt, f.hl_scale + 7);
-    add_hl_conv(l, p->conv_t.wf, f.hl_wt, f.hl_scale + 3);
+    add_hl_conv(l, p->conv_t.wf, 64, 64, f.hl_wt, f.hl_scale + 3);
     if (tail.next) {
       const dstd_block_params* q = tail.next;
       const float* w[4] = {q->conv_s[0].wm1, q->conv_s[0].wm2, q->conv_s[1].wm1, q->conv_s[1].wm2};
-      add_hl_pq(l, w, 4, f.hl_pqt, f.hl_scale + 4);
+      add_hl_pq(l, w, 4, 64, f.hl_pqt, f.hl_scale + 4);
     }
   }
 }
@@ -358,11 +364,20 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ha.B = B;
     ha.T = T;
     ha.V = V;
+    ha.Cin = p->cin;
+    ha.Cout = p->cout;
     ha.adj = reinterpret_cast<const uint16_t*>(sc.adj_s);
     for (int g = 0; g < 2; ++g) {
       ha.wimg[g] = f.hl_ws[g];
       ha.wscale[g] = f.hl_scale + g;
       ha.bf[g] = p->conv_s[g].bf;
+    }
+    if (res) {
+      ha.wimg[2] = f.hl_ws[2];
+      ha.wscale[2] = f.hl_scale + 8;
+      ha.bf[2] = p->res_b;
+      ha.rbn_s = f.rbn_s;
+      ha.rbn_h = f.rbn_h;
     }
     ha.bn_s = f.bn_s;
     ha.bn_h = f.bn_h;

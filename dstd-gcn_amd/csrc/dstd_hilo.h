@@ -138,12 +138,14 @@ inline int hl_sl_temporal(int T) {
 }
 
 // ---- weight images (one k_hl_prep launch per forward) --------------------
-// HLJ_CONV: B fragments of a transposed 64 -> 64 conv, W[c][k] (c out, k in):
-//   img[((ct*2 + ks)*2 + plane)*64 + lane] = 8 halves of 2^s * W[16ct + j][32ks + 8kg + e]
-//   (j = lane&15, kg = lane>>4), 16 KiB.
-// HLJ_PQ: A fragments of the P/Q conv of the next DSTDGC(s): row ch = 2*blk + rr
-//   of w[blk][rr*64 + c], slot (kg, e = 4mm + r) of K-step ks <-> c = 16*(2ks+mm) + 4kg + r:
-//   img[(ks*2 + plane)*64 + lane], 4 KiB.
+// HLJ_CONV: fragments of a 1x1 conv W[c][k] (rows = c out, cols = k in):
+//   img[((ct*KSI + ks)*2 + plane)*64 + lane] = 8 halves of 2^s * W[16ct + j][32ks + 8kg + e]
+//   (j = lane&15, kg = lane>>4, KSI = cdiv(cols, 32), zero outside) -- the B
+//   operand of the transposed conv and the A operand of a conv in output
+//   layout alike; <= 16 KiB.
+// HLJ_PQ: A fragments of the P/Q conv of the next DSTDGC(s) over cols input
+//   channels: row ch = 2*blk + rr of w[blk][rr*cols + c], slot (kg, e = 4mm + r)
+//   of K-step ks <-> c = 16*(2ks+mm) + 4kg + r: img[(ks*2 + plane)*64 + lane], <= 4 KiB.
 // HLJ_RM: A fragments of conv_rm, W[row][k] (rows x cols = T x 2T spatial,
 //   V x 2V temporal): img[((rt*NS + s)*2 + plane)*64 + lane] = 8 halves of
 //   2^s * W[16rt + i][32s + 8kg + e] (i = lane&15, kg = lane>>4, zero outside),
@@ -151,9 +153,9 @@ inline int hl_sl_temporal(int T) {
 enum HLJobKind { HLJ_CONV = 0, HLJ_PQ = 1, HLJ_RM = 2 };
 struct HLJob {
   int kind;
-  const float* w[4];  // HLJ_CONV: w[0] = [64][64]; HLJ_PQ: nblk two-row blocks [2][64]; HLJ_RM: w[0]
+  const float* w[4];  // HLJ_CONV / HLJ_RM: w[0] = [rows][cols]; HLJ_PQ: nblk two-row blocks [2][cols]
   int nblk;
-  int rows, cols;     // HLJ_RM
+  int rows, cols;
   uint4* img;
   float* inv_scale;   // 2^-s
 };
@@ -168,16 +170,18 @@ constexpr int kHLPQImg = 2 * 2 * 64;        // uint4 per HLJ_PQ image
 
 // ---- GC kernel arguments --------------------------------------------------
 struct SpatialHLArgs {
-  const float* x;            // NTVC [B][T][V][64]
-  int B, T, V;
+  const float* x;            // NTVC [B][T][V][Cin]
+  int B, T, V, Cin, Cout;    // (Cin, Cout) in {(64, 64), (6, 64), (64, 3)}
   const uint16_t* adj;       // [B][2][T][2 planes][V][SL] halves
-  const uint4* wimg[2];      // HLJ_CONV images of conv_s[g].conv_f
-  const float* wscale[2];
-  const float* bf[2];        // conv_f biases
-  const float* bn_s;         // folded BN [V][64]
+  const uint4* wimg[3];      // HLJ_CONV images of conv_s[g].conv_f, [2]: residual conv (Cin != Cout)
+  const float* wscale[3];
+  const float* bf[3];        // conv_f biases, [2]: residual conv bias
+  const float* bn_s;         // folded BN [V][Cout]
   const float* bn_h;
+  const float* rbn_s;        // folded residual BN [V][Cout] (Cin != Cout)
+  const float* rbn_h;
   const float* prelu;
-  float* y;                  // NTVC [B][T][V][64]
+  float* y;                  // NTVC [B][T][V][Cout]
   const uint4* pqimg;        // HLJ_PQ image of conv_t.conv_m1/m2 (4 channels)
   const float* pqscale;
   const float* pqb[2];

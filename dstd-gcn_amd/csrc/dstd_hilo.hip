@@ -126,9 +126,11 @@ __device__ __forceinline__ void stage_bn64(float4* dst, const float* src, int V,
 __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
   const HLJob& j = a.jobs[blockIdx.x];
   const int tid = threadIdx.x;
-  const int n = j.kind == HLJ_CONV ? 64 * 64 : j.kind == HLJ_RM ? j.rows * j.cols : 128 * j.nblk;
+  // HLJ_CONV / HLJ_RM: w[0] is rows x cols; HLJ_PQ: nblk blocks of 2 x cols
+  const int n = j.kind != HLJ_PQ ? j.rows * j.cols : 2 * j.cols * j.nblk;
   float m = 0.f;
-  for (int i = tid; i < n; i += 256) m = fmaxf(m, fabsf(j.kind != HLJ_PQ ? j.w[0][i] : j.w[i >> 7][i & 127]));
+  for (int i = tid; i < n; i += 256)
+    m = fmaxf(m, fabsf(j.kind != HLJ_PQ ? j.w[0][i] : j.w[i / (2 * j.cols)][i % (2 * j.cols)]));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   __shared__ float red[4];
@@ -144,15 +146,17 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
   }
   if (tid == 0) *j.inv_scale = 1.f / scale;
   if (j.kind == HLJ_CONV) {
-    for (int i = tid; i < 4 * 2 * 64; i += 256) {
-      const int lane = i & 63, ks = (i >> 6) & 1, ct = i >> 7;
+    const int NCT = cdiv(j.rows, 16), KSI = cdiv(j.cols, 32);
+    for (int i = tid; i < NCT * KSI * 64; i += 256) {
+      const int lane = i & 63, ks = (i >> 6) % KSI, ct = (i >> 6) / KSI;
       const int c = 16 * ct + (lane & 15), k0 = 32 * ks + 8 * (lane >> 4);
-      const float* w = j.w[0] + c * 64 + k0;
+      float v[8];
+#pragma unroll
+      for (int e8 = 0; e8 < 8; ++e8) v[e8] = c < j.rows && k0 + e8 < j.cols ? j.w[0][c * j.cols + k0 + e8] * scale : 0.f;
       uint4 hi, lo;
-      split8(make_float4(w[0] * scale, w[1] * scale, w[2] * scale, w[3] * scale),
-             make_float4(w[4] * scale, w[5] * scale, w[6] * scale, w[7] * scale), hi, lo);
-      j.img[((ct * 2 + ks) * 2 + 0) * 64 + lane] = hi;
-      j.img[((ct * 2 + ks) * 2 + 1) * 64 + lane] = lo;
+      split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), hi, lo);
+      j.img[((ct * KSI + ks) * 2 + 0) * 64 + lane] = hi;
+      j.img[((ct * KSI + ks) * 2 + 1) * 64 + lane] = lo;
     }
   } else if (j.kind == HLJ_RM) {
     const int NS = cdiv(j.cols, 32), nimg = cdiv(j.rows, 16) * NS * 64;
@@ -168,14 +172,15 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
       j.img[((rt * NS + s) * 2 + 1) * 64 + lane] = lo;
     }
   } else {
-    for (int i = tid; i < 2 * 64; i += 256) {
+    const int KSO = cdiv(cdiv(j.cols, 16), 2);
+    for (int i = tid; i < KSO * 64; i += 256) {
       const int lane = i & 63, ks = i >> 6;
       const int ch = lane & 15, kg = lane >> 4;
       float v[8];
 #pragma unroll
       for (int e8 = 0; e8 < 8; ++e8) {
         const int c = 16 * (2 * ks + (e8 >> 2)) + 4 * kg + (e8 & 3);
-        v[e8] = ch < 2 * j.nblk ? j.w[ch >> 1][(ch & 1) * 64 + c] * scale : 0.f;
+        v[e8] = ch < 2 * j.nblk && c < j.cols ? j.w[ch >> 1][(ch & 1) * j.cols + c] * scale : 0.f;
       }
       uint4 hi, lo;
       split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), hi, lo);
@@ -186,143 +191,192 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
 }
 
 // ===========================================================================
-// Spatial GC, 64 -> 64, two graphs (DSTDGCB.forward model/dstdgcn.py:141-154
-// with DSTDGC.forward spatial :80-87), unit = (sample n, frame t):
+// Spatial GC, two graphs (DSTDGCB.forward model/dstdgcn.py:141-154 with
+// DSTDGC.forward spatial :80-87), unit = (sample n, frame t):
 //   y[c][w] = sum_g sum_v (W_g x + b_g)[v][c] Adj_g[t][v][w]
-//   h = prelu(bn(y) + x)  ->  NTVC, and P_t/Q_t of h ([B][T][V][4])
+//   h = prelu(bn(y) + r)  ->  NTVC, and P_t/Q_t of h ([B][T][V][4]);
+//   r = x (64 -> 64) or bn_r(W_r x + b_r) (the residual conv of conv_st_in
+//   6 -> 64 and conv_st_out 64 -> 3, :117-121), computed in output layout
+//   (A = W_r fragments, B = x rows of the output joints).
 // ===========================================================================
-template <int V>
 #ifndef DSTD_HL_WPE
 #define DSTD_HL_WPE 2
 #endif
+
+// 8 consecutive channels k0 .. k0+7 of row `row` of a unit (C channels per
+// row, zero past C; C % 8 == 0 or C == 6 / 3)
+template <int C>
+__device__ __forceinline__ void load_row8(__amdgpu_buffer_rsrc_t r, int row, int k0, float4& lo4, float4& hi4) {
+  if constexpr (C % 8 == 0) {
+    const uint32_t off = (uint32_t)(row * C + k0) * 4;
+    lo4 = bld4(r, off);
+    hi4 = bld4(r, off + 16);
+  } else {
+    // C < 8: only k0 == 0 has data; rows are 4-byte aligned (dword loads)
+    const uint32_t off = k0 == 0 ? (uint32_t)(row * C) * 4 : OOB;
+    float e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+      e[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * i, 0, 0));
+    lo4 = make_float4(e[0], e[1], e[2], e[3]);
+    hi4 = make_float4(e[4], e[5], e[6], e[7]);
+  }
+}
+
+// folded BN vectors [V][C] -> LDS [c/4][v] for NCT*4 channel quads (zero past C)
+template <int C, int NCT>
+__device__ __forceinline__ void stage_bnC(float4* dst, const float* src, int V, int tid) {
+  for (int i = tid; i < V * 4 * NCT; i += HT) {
+    const int v = i / (4 * NCT), c4 = i % (4 * NCT);
+    float e[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) e[q] = 4 * c4 + q < C ? src[v * C + 4 * c4 + q] : 0.f;
+    dst[c4 * V + v] = make_float4(e[0], e[1], e[2], e[3]);
+  }
+}
+
+template <int V, int CIN, int COUT>
 __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE, DSTD_HL_WPE))) void k_spatial_hl(
     SpatialHLArgs a) {
   using SM = SlotMap<V, true>;
+  constexpr bool RES = CIN != COUT;
   constexpr int SL = SM::SL, NG = SM::NG, NWT = cdiv(V, 16);
+  constexpr int KSI = cdiv(CIN, 32);   // conv k-steps
+  constexpr int NCT = cdiv(COUT, 16);  // output channel tiles
+  constexpr int KSO = cdiv(NCT, 2);    // P/Q k-steps
+  constexpr int WIMG = NCT * KSI * 2 * 64, PIMG = KSO * 2 * 64;
   static_assert(SM::MT == 2 && SM::NS == 1, "one K-step of two tiles per frame");
-  __shared__ uint4 wl[2][kHLConvImg];
-  __shared__ uint4 pql[kHLPQImg];
-  __shared__ float4 bnl[2][16 * V];
-  __shared__ float bfl[2][64];
+  __shared__ uint4 wl[RES ? 3 : 2][WIMG];  // conv (graphs 0, 1), residual conv
+  __shared__ uint4 pql[PIMG];
+  __shared__ float4 bnl[RES ? 4 : 2][4 * NCT * V];
+  __shared__ float bfl[3][16 * NCT];
   __shared__ float bql[4];
-  __shared__ float scl[3];
+  __shared__ float scl[4];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int kl = lane >> 4, cl = lane & 15;
   const int T = a.T;
-  for (int i = tid; i < 2 * kHLConvImg; i += HT) wl[i / kHLConvImg][i % kHLConvImg] = a.wimg[i / kHLConvImg][i % kHLConvImg];
-  for (int i = tid; i < kHLPQImg; i += HT) pql[i] = a.pqimg[i];
-  stage_bn64(bnl[0], a.bn_s, V, tid);
-  stage_bn64(bnl[1], a.bn_h, V, tid);
-  if (tid < 128) bfl[tid >> 6][tid & 63] = a.bf[tid >> 6][tid & 63];
+  for (int i = tid; i < (RES ? 3 : 2) * WIMG; i += HT) wl[i / WIMG][i % WIMG] = a.wimg[i / WIMG][i % WIMG];
+  for (int i = tid; i < PIMG; i += HT) pql[i] = a.pqimg[i];
+  stage_bnC<COUT, NCT>(bnl[0], a.bn_s, V, tid);
+  stage_bnC<COUT, NCT>(bnl[1], a.bn_h, V, tid);
+  if constexpr (RES) {
+    stage_bnC<COUT, NCT>(bnl[2], a.rbn_s, V, tid);
+    stage_bnC<COUT, NCT>(bnl[3], a.rbn_h, V, tid);
+  }
+  for (int i = tid; i < (RES ? 3 : 2) * 16 * NCT; i += HT) {
+    const int g = i / (16 * NCT), c = i % (16 * NCT);
+    bfl[g][c] = c < COUT ? a.bf[g][c] : 0.f;
+  }
   if (tid < 4) bql[tid] = a.pqb[tid >> 1][tid & 1];
   if (tid == 0) {
     scl[0] = *a.wscale[0];
     scl[1] = *a.wscale[1];
     scl[2] = *a.pqscale;
+    scl[3] = RES ? *a.wscale[2] : 0.f;
   }
   __syncthreads();
 
   int uend;
   int u = unit_range(a.B * T, uend);
   const float pw = *a.prelu;
-  // x rows of the two conv tiles: joint of tile m, row cl; k-step ks, lane group kl
-  const uint32_t xo0 = (uint32_t)(min(SM::row_idx(0, cl), V - 1) * 64 + 8 * kl) * 4;
-  const uint32_t xo1 = (uint32_t)(min(SM::row_idx(1, cl), V - 1) * 64 + 8 * kl) * 4;
-  constexpr uint32_t unit_bytes = V * 64 * 4;     // one frame of x / y
+  // conv rows: joint of tile m, row cl
+  const int jr0 = min(SM::row_idx(0, cl), V - 1), jr1 = min(SM::row_idx(1, cl), V - 1);
+  constexpr uint32_t xunit = V * CIN * 4;         // one frame of x
+  constexpr uint32_t yunit = V * COUT * 4;        // one frame of y
   constexpr uint32_t adj_bytes = 2 * V * SL * 2;  // one (n, g, t) adjacency: 2 planes of V x SL halves
-  // per output tile wt: this lane's joint w = 16wt + cl.  Joints past V fall
-  // outside the unit's buffer range by themselves (w * row >= V * row); only
-  // the adjacency lane groups past NG need an explicit out-of-range offset.
-  const uint32_t wro0 = (uint32_t)(cl * 64 + 4 * kl) * 4;                    // + wt * 4096
+  // this lane's output joint w = 16wt + cl: joints past V fall outside the
+  // unit's buffer range by themselves; adjacency lane groups past NG and
+  // P/Q lanes other than kl == 0 get an explicit out-of-range offset
   const uint32_t wadj0 = kl < NG ? (uint32_t)(cl * SL + 8 * kl) * 2 : OOB;  // + wt * 32 * SL
   const uint32_t wpq0 = kl == 0 ? (uint32_t)cl * 16 : OOB;                  // + wt * 256
 
-  float4 xr[2][2][2];  // [tile][k-step][half]: channels 32ks + 8kl .. +7 of the tile row
+  float4 xr[2][KSI][2];  // [tile][k-step][half]: channels 32ks + 8kl .. +7 of the tile row
   auto load_x = [&](int uu) {
-    const auto r = rsrc(a.x + (size_t)uu * V * 64, unit_bytes);
+    const auto r = rsrc(a.x + (size_t)uu * V * CIN, xunit);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      xr[0][ks][0] = bld4(r, xo0 + 128 * ks);
-      xr[0][ks][1] = bld4(r, xo0 + 128 * ks + 16);
-      xr[1][ks][0] = bld4(r, xo1 + 128 * ks);
-      xr[1][ks][1] = bld4(r, xo1 + 128 * ks + 16);
+    for (int ks = 0; ks < KSI; ++ks) {
+      load_row8<CIN>(r, jr0, 32 * ks + 8 * kl, xr[0][ks][0], xr[0][ks][1]);
+      load_row8<CIN>(r, jr1, 32 * ks + 8 * kl, xr[1][ks][0], xr[1][ks][1]);
     }
   };
   uint4 ab[2][NWT][2];  // adjacency B fragments [graph][w tile][plane]
   auto load_adj_g = [&](int uu, int g) {
     const int n = uu / T, t = uu - n * T;
-    {
-      const uint16_t* base = a.adj + ((size_t)(n * 2 + g) * T + t) * (adj_bytes / 2);
-      const auto rh = rsrc(base, adj_bytes / 2), rl = rsrc(base + V * SL, adj_bytes / 2);  // one plane each
+    const uint16_t* base = a.adj + ((size_t)(n * 2 + g) * T + t) * (adj_bytes / 2);
+    const auto rh = rsrc(base, adj_bytes / 2), rl = rsrc(base + V * SL, adj_bytes / 2);  // one plane each
 #pragma unroll
-      for (int wt = 0; wt < NWT; ++wt) {
-        ab[g][wt][0] = bldu4(rh, wadj0 + wt * 32 * SL);
-        ab[g][wt][1] = bldu4(rl, wadj0 + wt * 32 * SL);
-      }
+    for (int wt = 0; wt < NWT; ++wt) {
+      ab[g][wt][0] = bldu4(rh, wadj0 + wt * 32 * SL);
+      ab[g][wt][1] = bldu4(rl, wadj0 + wt * 32 * SL);
     }
   };
   if (u < uend) load_x(u);
   while (u < uend) {
     const int un = u + 1;
     const int lz = lane + opaque_zero();
-    const auto rx = rsrc(a.x + (size_t)u * V * 64, unit_bytes);
-    // identity residual at the output positions (w = 16wt + cl, channels 16ct + 4kl ..)
-    float4 R[4][NWT];
+    const auto rx = rsrc(a.x + (size_t)u * V * CIN, xunit);
+    // residual: identity -> x at the output positions (w, channels 16ct + 4kl ..);
+    // residual conv -> x rows of the output joints as B fragments
+    float4 R[RES ? 1 : 4][RES ? 1 : NWT];
+    float4 xw[RES ? NWT : 1][RES ? KSI : 1][2];
+    if constexpr (RES) {
 #pragma unroll
-    for (int wt = 0; wt < NWT; ++wt)
+      for (int wt = 0; wt < NWT; ++wt)
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) R[ct][wt] = bld4(rx, wro0 + wt * 4096 + 64 * ct);
+        for (int ks = 0; ks < KSI; ++ks) load_row8<CIN>(rx, 16 * wt + cl, 32 * ks + 8 * kl, xw[wt][ks][0], xw[wt][ks][1]);
+    } else {
+#pragma unroll
+      for (int wt = 0; wt < NWT; ++wt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) R[ct][wt] = bld4(rx, (uint32_t)((16 * wt + cl) * 64 + 4 * kl) * 4 + 64 * ct);
+    }
     // this unit's graph-0 adjacency now, graph 1 after the first conv (a
     // whole-unit-ahead prefetch of both measured 6% slower: registers)
     load_adj_g(u, 0);
     __builtin_amdgcn_sched_barrier(0);
-    f16x8 xh[2][2], xo[2][2];
+    f16x8 xh[2][KSI], xo[2][KSI];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-#ifdef DSTD_ABL_SPLITX
-        xh[m][ks] = __builtin_bit_cast(f16x8, xr[m][ks][0]);
-        xo[m][ks] = __builtin_bit_cast(f16x8, xr[m][ks][1]);
-#else
-        split8(xr[m][ks][0], xr[m][ks][1], xh[m][ks], xo[m][ks]);
-#endif
-      }
+      for (int ks = 0; ks < KSI; ++ks) split8(xr[m][ks][0], xr[m][ks][1], xh[m][ks], xo[m][ks]);
 
-    f32x4 O[4][NWT];
+    f32x4 O[NCT][NWT];
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt) O[ct][wt] = zero4();
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
       // ---- conv (transposed): D[p][c] = sum_k x[p][k] W'[c][k] ----
-      f32x4 D[2][4];
+      f32x4 D[2][NCT];
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) D[m][ct] = zero4();
+        for (int ct = 0; ct < NCT; ++ct) D[m][ct] = zero4();
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < KSI; ++ks)
 #pragma unroll
-        for (int c2 = 0; c2 < 4; c2 += 2) {
-          f16x8 wh[2], wo[2];
+        for (int c2 = 0; c2 < NCT; c2 += 2) {
+          constexpr int Q2 = NCT < 2 ? NCT : 2;
+          f16x8 wh[Q2], wo[Q2];
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            wh[q] = as_h8(wl[g][(((c2 + q) * 2 + ks) * 2 + 0) * 64 + lz]);
-            wo[q] = as_h8(wl[g][(((c2 + q) * 2 + ks) * 2 + 1) * 64 + lz]);
+          for (int q = 0; q < Q2; ++q) {
+            wh[q] = as_h8(wl[g][(((c2 + q) * KSI + ks) * 2 + 0) * 64 + lz]);
+            wo[q] = as_h8(wl[g][(((c2 + q) * KSI + ks) * 2 + 1) * 64 + lz]);
           }
 #pragma unroll
-          for (int q = 0; q < 2; ++q)
+          for (int q = 0; q < Q2; ++q)
 #pragma unroll
             for (int m = 0; m < 2; ++m) D[m][c2 + q] = mfma32(xo[m][ks], wh[q], D[m][c2 + q]);
 #pragma unroll
-          for (int q = 0; q < 2; ++q)
+          for (int q = 0; q < Q2; ++q)
 #pragma unroll
             for (int m = 0; m < 2; ++m) D[m][c2 + q] = mfma32(xh[m][ks], wo[q], D[m][c2 + q]);
 #pragma unroll
-          for (int q = 0; q < 2; ++q)
+          for (int q = 0; q < Q2; ++q)
 #pragma unroll
             for (int m = 0; m < 2; ++m) D[m][c2 + q] = mfma32(xh[m][ks], wh[q], D[m][c2 + q]);
         }
@@ -341,68 +395,112 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
       }
       // ---- aggregation: O[c][w] += sum_v D[v][c] Adj[v][w] ----
       const float s = scl[g];
-      f16x8 dh[4], dl[4];
+      f16x8 dh[NCT], dl[NCT];
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
+      for (int ct = 0; ct < NCT; ++ct) {
         const float b = bfl[g][16 * ct + cl];
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int r = 0; r < 4; ++r) D[m][ct][r] = fmaf(D[m][ct][r], s, b);
-#ifdef DSTD_ABL_SPLITD
-        dh[ct] = __builtin_bit_cast(f16x8, make_float4(D[0][ct][0], D[0][ct][1], D[0][ct][2], D[0][ct][3]));
-        dl[ct] = __builtin_bit_cast(f16x8, make_float4(D[1][ct][0], D[1][ct][1], D[1][ct][2], D[1][ct][3]));
-#else
         split_acc(D[0][ct], D[1][ct], dh[ct], dl[ct]);
-#endif
       }
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
         for (int wt = 0; wt < NWT; ++wt) O[ct][wt] = mfma32(dl[ct], as_h8(ab[g][wt][0]), O[ct][wt]);
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
         for (int wt = 0; wt < NWT; ++wt) O[ct][wt] = mfma32(dh[ct], as_h8(ab[g][wt][1]), O[ct][wt]);
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
         for (int wt = 0; wt < NWT; ++wt) O[ct][wt] = mfma32(dh[ct], as_h8(ab[g][wt][0]), O[ct][wt]);
     }
 
+    // ---- residual conv in output layout: rc[c][w] = sum_k W_r[c][k] x[w][k] ----
+    f32x4 rc[RES ? NCT : 1][RES ? NWT : 1];
+    if constexpr (RES) {
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int wt = 0; wt < NWT; ++wt) rc[ct][wt] = zero4();
+#pragma unroll
+      for (int ks = 0; ks < KSI; ++ks) {
+        f16x8 bh[NWT], bo[NWT];
+#pragma unroll
+        for (int wt = 0; wt < NWT; ++wt) split8(xw[wt][ks][0], xw[wt][ks][1], bh[wt], bo[wt]);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct) {
+          const f16x8 ah = as_h8(wl[2][((ct * KSI + ks) * 2 + 0) * 64 + lz]);
+          const f16x8 ao = as_h8(wl[2][((ct * KSI + ks) * 2 + 1) * 64 + lz]);
+#pragma unroll
+          for (int wt = 0; wt < NWT; ++wt) rc[ct][wt] = mfma32(ao, bh[wt], rc[ct][wt]);
+#pragma unroll
+          for (int wt = 0; wt < NWT; ++wt) rc[ct][wt] = mfma32(ah, bo[wt], rc[ct][wt]);
+#pragma unroll
+          for (int wt = 0; wt < NWT; ++wt) rc[ct][wt] = mfma32(ah, bh[wt], rc[ct][wt]);
+        }
+      }
+    }
 
-    // ---- epilogue: h = prelu(bn(y) + x) -> NTVC ----
-    const auto ry = rsrc(a.y + (size_t)u * V * 64, unit_bytes);
+    // ---- epilogue: h = prelu(bn(y) + r) -> NTVC ----
+    const auto ry = rsrc(a.y + (size_t)u * V * COUT, yunit);
 #pragma unroll
     for (int wt = 0; wt < NWT; ++wt) {
       const int wc = min(16 * wt + cl, V - 1);
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
+      for (int ct = 0; ct < NCT; ++ct) {
         f32x4& o = O[ct][wt];
-#ifndef DSTD_ABL_EPI
-        const float4 sc = bnl[0][(4 * ct + kl) * V + wc], sh = bnl[1][(4 * ct + kl) * V + wc];
-        o[0] = prelu_f(fmaf(o[0], sc.x, sh.x) + R[ct][wt].x, pw);
-        o[1] = prelu_f(fmaf(o[1], sc.y, sh.y) + R[ct][wt].y, pw);
-        o[2] = prelu_f(fmaf(o[2], sc.z, sh.z) + R[ct][wt].z, pw);
-        o[3] = prelu_f(fmaf(o[3], sc.w, sh.w) + R[ct][wt].w, pw);
-#else
-        (void)wc;
-        o[0] += R[ct][wt].x;
-#endif
-        bst4(ry, wro0 + wt * 4096 + 64 * ct, make_float4(o[0], o[1], o[2], o[3]));
+        const int c4 = (4 * ct + kl) * V + wc;
+        const float4 sc = bnl[0][c4], sh = bnl[1][c4];
+        float r[4];
+        if constexpr (RES) {
+          const float4 rs = bnl[2][c4], rh = bnl[3][c4];
+          const float s3 = scl[3];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float b = bfl[2][16 * ct + 4 * kl + q];
+            const float rv = fmaf(rc[ct][wt][q], s3, b);
+            r[q] = fmaf(rv, q == 0 ? rs.x : q == 1 ? rs.y : q == 2 ? rs.z : rs.w,
+                        q == 0 ? rh.x : q == 1 ? rh.y : q == 2 ? rh.z : rh.w);
+          }
+        } else {
+          r[0] = R[ct][wt].x;
+          r[1] = R[ct][wt].y;
+          r[2] = R[ct][wt].z;
+          r[3] = R[ct][wt].w;
+        }
+        o[0] = prelu_f(fmaf(o[0], sc.x, sh.x) + r[0], pw);
+        o[1] = prelu_f(fmaf(o[1], sc.y, sh.y) + r[1], pw);
+        o[2] = prelu_f(fmaf(o[2], sc.z, sh.z) + r[2], pw);
+        o[3] = prelu_f(fmaf(o[3], sc.w, sh.w) + r[3], pw);
+        if constexpr (COUT % 4 == 0) {
+          bst4(ry, (uint32_t)((16 * wt + cl) * COUT + 16 * ct + 4 * kl) * 4, make_float4(o[0], o[1], o[2], o[3]));
+        } else {
+          static_assert(COUT == 3, "thin output: 3 channels");
+          const uint32_t off = kl == 0 ? (uint32_t)(16 * wt + cl) * 12 : OOB;
+          // (a whole f32x3 bit_cast: hipcc 7.2 folds __builtin_bit_cast of
+          // single vector elements o[1], o[2] to o[0]'s bits -- measured)
+          typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+          typedef float f32x3 __attribute__((ext_vector_type(3)));
+          const f32x3 o3 = {o[0], o[1], o[2]};
+          __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(u32x3, o3), ry, off, 0, 0);
+        }
       }
     }
     // ---- P_t/Q_t of h: out[ch][w] = sum_c wq[ch][c] h[c][w] + b ----
     f32x4 acc[NWT];
 #pragma unroll
     for (int wt = 0; wt < NWT; ++wt) acc[wt] = zero4();
-#ifndef DSTD_ABL_PQ
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KSO; ++ks) {
       const f16x8 qh = as_h8(pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(pql[(ks * 2 + 1) * 64 + lz]);
       f16x8 hh[NWT], hl[NWT];
 #pragma unroll
-      for (int wt = 0; wt < NWT; ++wt) split_acc(O[2 * ks][wt], O[2 * ks + 1][wt], hh[wt], hl[wt]);
+      for (int wt = 0; wt < NWT; ++wt)
+        split_acc(O[2 * ks][wt], 2 * ks + 1 < NCT ? O[2 * ks + 1][wt] : zero4(), hh[wt], hl[wt]);
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt) acc[wt] = mfma32(qo, hh[wt], acc[wt]);
 #pragma unroll
@@ -410,7 +508,6 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt) acc[wt] = mfma32(qh, hh[wt], acc[wt]);
     }
-#endif
     {
       const float s = scl[2];
       const auto rp = rsrc(a.pq + (size_t)u * V * 4, V * 16);
@@ -956,12 +1053,20 @@ hipError_t launch_adj_hl(const AdjHLArgs& a, int mode, int T, int V, hipStream_t
 }
 bool temporal_hl_supported(int T, int V) { return hl_shape(T, V); }
 
+template <int V>
+hipError_t spatial_hl_v(const SpatialHLArgs& a, hipStream_t s) {
+  if (a.Cin == 64 && a.Cout == 64) return launch_units<k_spatial_hl<V, 64, 64>>(a.B * a.T, a, s);
+  if (a.Cin == 6 && a.Cout == 64) return launch_units<k_spatial_hl<V, 6, 64>>(a.B * a.T, a, s);
+  if (a.Cin == 64 && a.Cout == 3) return launch_units<k_spatial_hl<V, 64, 3>>(a.B * a.T, a, s);
+  return hipErrorNotSupported;
+}
+
 hipError_t launch_spatial_hl(const SpatialHLArgs& a, hipStream_t s) {
   if (!spatial_hl_supported(a.T, a.V)) return hipErrorNotSupported;
   switch (a.V) {
-    case 22: return launch_units<k_spatial_hl<22>>(a.B * a.T, a, s);
-    case 23: return launch_units<k_spatial_hl<23>>(a.B * a.T, a, s);
-    case 25: return launch_units<k_spatial_hl<25>>(a.B * a.T, a, s);
+    case 22: return spatial_hl_v<22>(a, s);
+    case 23: return spatial_hl_v<23>(a, s);
+    case 25: return spatial_hl_v<25>(a, s);
     default: return hipErrorNotSupported;
   }
 }
