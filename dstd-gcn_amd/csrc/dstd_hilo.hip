@@ -283,7 +283,9 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
   int u = unit_range(a.B * T, uend);
   const float pw = *a.prelu;
   // conv rows: joint of tile m, row cl
-  const int jr0 = min(SM::row_idx(0, cl), V - 1), jr1 = min(SM::row_idx(1, cl), V - 1);
+  // (padding slots read past the unit's range: zero rows, no memory traffic)
+  const int jr0 = SM::row_idx(0, cl) < V ? SM::row_idx(0, cl) : 1 << 20;
+  const int jr1 = SM::row_idx(1, cl) < V ? SM::row_idx(1, cl) : 1 << 20;
   constexpr uint32_t xunit = V * CIN * 4;         // one frame of x
   constexpr uint32_t yunit = V * COUT * 4;        // one frame of y
   constexpr uint32_t adj_bytes = 2 * V * SL * 2;  // one (n, g, t) adjacency: 2 planes of V x SL halves
@@ -577,7 +579,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
   constexpr uint32_t adj_bytes = 2 * T * SL * 2;  // one (n, v): 2 planes of T x SL halves
   uint32_t xoff[MT];  // conv rows: frame 16m + cl, channels 8kl ..
 #pragma unroll
-  for (int m = 0; m < MT; ++m) xoff[m] = (uint32_t)min(16 * m + cl, T - 1) * frame_bytes + 32 * kl;
+  for (int m = 0; m < MT; ++m) xoff[m] = 16 * m + cl < T ? (uint32_t)(16 * m + cl) * frame_bytes + 32 * kl : OOB;
   uint32_t uoff[NUT], upq[NUT];  // output frame uo = 16ut + cl (OOB past T), channels 4kl ..
 #pragma unroll
   for (int ut = 0; ut < NUT; ++ut) {
@@ -964,7 +966,12 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
     }
   }
   TLH(MODE, 2)
-  TLH(MODE, 3)
+#ifdef DSTD_STAMPS
+  // slot 3: HW_ID (cu / se) and XCC_ID of the workgroup's placement
+  if (threadIdx.x == 0 && blockIdx.x < 2048)
+    g_tl_hl[MODE][blockIdx.x][3] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                                   (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+#endif
 }
 
 // ===========================================================================

@@ -38,8 +38,13 @@ def main():
     buf = np.zeros(2048 * 4, dtype=np.uint64)
     for mode in (0, 1):
         fn(mode, buf.ctypes.data, buf.size)
-        tl = buf.reshape(2048, 4).astype(np.float64)
-        tl = tl[tl[:, 0] > 0]
+        raw = buf.reshape(2048, 4).copy()
+        raw = raw[raw[:, 0] > 0]
+        hw = None
+        if "--hl" in sys.argv:  # slot 3 holds (XCC_ID << 32) | HW_ID: placement per workgroup
+            hw = raw[:, 3].copy()
+            raw[:, 3] = raw[:, 2]
+        tl = raw.astype(np.float64)
         t0 = tl[:, 0].min()
         us = (tl - t0) / 100.0  # 100 MHz -> us
         print(f"mode {mode}: {len(tl)} workgroups, span {us[:, 3].max():.2f} us")
@@ -48,6 +53,25 @@ def main():
             print(f"   {name:9s} min {c.min():6.2f}  p50 {np.median(c):6.2f}  p90 {np.percentile(c, 90):6.2f}  max {c.max():6.2f}")
         d = us[:, 2] - us[:, 1]
         print(f"   compute   p50 {np.median(d):6.2f} us; staging p50 {np.median(us[:, 1] - us[:, 0]):6.2f} us")
+        if hw is not None:
+            hwid = (hw & 0xffffffff).astype(np.int64)
+            xcc = (hw >> 32).astype(np.int64) & 0xf
+            cu = (hwid >> 8) & 0xf
+            sh = (hwid >> 12) & 0x1
+            se = (hwid >> 13) & 0x7
+            key = xcc * 1000 + se * 100 + sh * 16 + cu
+            uniq, cnt = np.unique(key, return_counts=True)
+            print(f"   placement: {len(uniq)} distinct CUs, workgroups per CU histogram "
+                  f"{dict(zip(*np.unique(cnt, return_counts=True)))}")
+            per = {k: c for k, c in zip(uniq, cnt)}
+            shared = np.array([per[k] for k in key])
+            for x in sorted(set(xcc)):
+                sel = xcc == x
+                print(f"     XCC {x}: {sel.sum()} WGs, compute p50 {np.median(d[sel]):6.2f} p90 {np.percentile(d[sel], 90):6.2f}"
+                      f" max {d[sel].max():6.2f}, staged p50 {np.median(us[sel, 1]):6.2f}")
+            for c in sorted(set(shared)):
+                sel = shared == c
+                print(f"     {c} WG/CU: {sel.sum()} WGs, compute p50 {np.median(d[sel]):6.2f} us, max {d[sel].max():6.2f}")
 
 
 if __name__ == "__main__":
