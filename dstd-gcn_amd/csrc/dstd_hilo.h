@@ -147,9 +147,14 @@ inline int hl_sl_temporal(int T) {
 //   channels: row ch = 2*blk + rr of w[blk][rr*cols + c], slot (kg, e = 4mm + r)
 //   of K-step ks <-> c = 16*(2ks+mm) + 4kg + r: img[(ks*2 + plane)*64 + lane], <= 4 KiB.
 // HLJ_RM: A fragments of conv_rm, W[row][k] (rows x cols = T x 2T spatial,
-//   V x 2V temporal): img[((rt*NS + s)*2 + plane)*64 + lane] = 8 halves of
-//   2^s * W[16rt + i][32s + 8kg + e] (i = lane&15, kg = lane>>4, zero outside),
-//   NS = cdiv(cols, 32).
+//   V x 2V temporal), K-steps as hl_rm_ksteps(): NSF full steps of 32 for the
+//   16x16x32 MFMA, img[((rt*NSF + s)*2 + plane)*64 + lane] = 8 halves of
+//   2^s * W[16rt + i][32s + 8kg + e], then (when the remainder fits 16) one
+//   16x16x16 tail step, img16[(rt*2 + plane)*64 + lane] = 4 halves of
+//   W[16rt + i][32 NSF + 4kg + e] as uint2 after the full steps
+//   (i = lane&15, kg = lane>>4, zero outside).
+__host__ __device__ constexpr inline int hl_rm_nsf(int K) { return K % 32 > 16 ? K / 32 + 1 : K / 32; }
+__host__ __device__ constexpr inline int hl_rm_tail(int K) { return K % 32 != 0 && K % 32 <= 16 ? 1 : 0; }
 enum HLJobKind { HLJ_CONV = 0, HLJ_PQ = 1, HLJ_RM = 2 };
 struct HLJob {
   int kind;
@@ -159,7 +164,9 @@ struct HLJob {
   uint4* img;
   float* inv_scale;   // 2^-s
 };
-inline int hl_rm_img(int rows, int cols) { return cdiv(rows, 16) * cdiv(cols, 32) * 2 * 64; }  // uint4
+inline int hl_rm_img(int rows, int cols) {  // uint4
+  return cdiv(rows, 16) * (hl_rm_nsf(cols) * 2 * 64 + hl_rm_tail(cols) * 64);
+}
 constexpr int kMaxHLJobs = 48;
 struct HLPrepArgs {
   HLJob jobs[kMaxHLJobs];

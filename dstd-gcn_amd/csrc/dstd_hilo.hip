@@ -45,6 +45,7 @@ constexpr int HT = HW * 64;  // threads per workgroup
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 __device__ __forceinline__ f16x8 as_h8(const uint4& v) { return __builtin_bit_cast(f16x8, v); }
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x4 mfma32(const f16x8& a, const f16x8& b, f32x4 c) {
 #ifdef DSTD_ABL_MFMA
@@ -159,17 +160,31 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
       j.img[((ct * KSI + ks) * 2 + 1) * 64 + lane] = lo;
     }
   } else if (j.kind == HLJ_RM) {
-    const int NS = cdiv(j.cols, 32), nimg = cdiv(j.rows, 16) * NS * 64;
-    for (int i = tid; i < nimg; i += 256) {
-      const int lane = i & 63, s = (i >> 6) % NS, rt = (i >> 6) / NS;
+    const int NSF = hl_rm_nsf(j.cols), RT = cdiv(j.rows, 16);
+    for (int i = tid; i < RT * NSF * 64; i += 256) {
+      const int lane = i & 63, s = (i >> 6) % NSF, rt = (i >> 6) / NSF;
       const int r = 16 * rt + (lane & 15), k0 = 32 * s + 8 * (lane >> 4);
       float v[8];
 #pragma unroll
       for (int e8 = 0; e8 < 8; ++e8) v[e8] = r < j.rows && k0 + e8 < j.cols ? j.w[0][r * j.cols + k0 + e8] * scale : 0.f;
       uint4 hi, lo;
       split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), hi, lo);
-      j.img[((rt * NS + s) * 2 + 0) * 64 + lane] = hi;
-      j.img[((rt * NS + s) * 2 + 1) * 64 + lane] = lo;
+      j.img[((rt * NSF + s) * 2 + 0) * 64 + lane] = hi;
+      j.img[((rt * NSF + s) * 2 + 1) * 64 + lane] = lo;
+    }
+    if (hl_rm_tail(j.cols)) {  // 16x16x16 tail step: 4 halves per lane and plane
+      uint2* img16 = reinterpret_cast<uint2*>(j.img + RT * NSF * 2 * 64);
+      for (int i = tid; i < RT * 64; i += 256) {
+        const int lane = i & 63, rt = i >> 6;
+        const int r = 16 * rt + (lane & 15), k0 = 32 * NSF + 4 * (lane >> 4);
+        float v[4];
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) v[e4] = r < j.rows && k0 + e4 < j.cols ? j.w[0][r * j.cols + k0 + e4] * scale : 0.f;
+        uint4 hi, lo;
+        split8(make_float4(v[0], v[1], v[2], v[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+        img16[(rt * 2 + 0) * 64 + lane] = make_uint2(hi.x, hi.y);
+        img16[(rt * 2 + 1) * 64 + lane] = make_uint2(lo.x, lo.y);
+      }
     }
   } else {
     const int KSO = cdiv(cdiv(j.cols, 16), 2);
@@ -775,7 +790,12 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
 
 template <int MODE, int NROW, int K, int NA>
 struct AdjHLGeom {
-  static constexpr int RT = cdiv(NROW, 16), NS = cdiv(K, 32), KP = 32 * NS, KH = K / 2;
+  // K-steps: NS full 16x16x32 steps, then (TAIL) one 16x16x16 step when the
+  // remainder fits 16 -- K = 70 -> 64 + 16 instead of 96 (17% fewer tanh),
+  // K = 44 -> 32 + 16 instead of 64 (25% fewer)
+  static constexpr int NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL;
+  static constexpr int RT = cdiv(NROW, 16), KH = K / 2;
+  static constexpr int WIMG = RT * (NS * 2 * 64 + TAIL * 64);  // uint4 of the HLJ_RM image
   static constexpr int SE = KP + 4;  // LDS row stride of E / F (16-byte aligned, rows spread over banks)
   using SM = SlotMap<NA, MODE == 0>;
   static constexpr int SL = SM::SL, NCOL = NA * SL, NCT = cdiv(NCOL, 16);
@@ -797,12 +817,12 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   using Gm = AdjHLGeom<MODE, NROW, K, NA>;
   using SM = typename Gm::SM;
   constexpr int RT = Gm::RT, NS = Gm::NS, KP = Gm::KP, KH = Gm::KH, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
-  constexpr int AW = Gm::AW, AT = Gm::AT;
+  constexpr int AW = Gm::AW, AT = Gm::AT, TAIL = Gm::TAIL, WIMG = Gm::WIMG;
   constexpr int OS = Gm::OS, T = Gm::T, V = Gm::V;
   constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
   __shared__ float El[(NA + 1) * SE];
   __shared__ float Fl[(NA + 1) * SE];
-  __shared__ uint4 wl[RT * NS * 2 * 64];
+  __shared__ uint4 wl[WIMG];
   __shared__ float asl[NA * NA + 1];
   __shared__ float bsl[RT * 16];
   __shared__ float stg[AW][32 * OS];  // two row tiles at a time
@@ -820,7 +840,7 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   // trip instead of one per loop iteration) ----
   const PQLayout L = a.pql;
   const float* pqb = a.pq + (size_t)n * L.sn + a.p_ch[g];
-  constexpr int NPQ = cdiv(T * V, AT), NW = cdiv(RT * NS * 2 * 64, AT), NAS = cdiv(NA * NA, AT);
+  constexpr int NPQ = cdiv(T * V, AT), NW = cdiv(WIMG, AT), NAS = cdiv(NA * NA, AT);
   float4 q4[NPQ];
   uint4 wv[NW];
   float av[NAS];
@@ -831,7 +851,7 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
     q4[it] = ld4(pqb + t * L.st + v * L.sv);                                  // (P_0, P_1, Q_0, Q_1)
   }
 #pragma unroll
-  for (int it = 0; it < NW; ++it) wv[it] = a.wimg[g][min(tid + it * AT, RT * NS * 2 * 64 - 1)];
+  for (int it = 0; it < NW; ++it) wv[it] = a.wimg[g][min(tid + it * AT, WIMG - 1)];
 #pragma unroll
   for (int it = 0; it < NAS; ++it) av[it] = a.astat[g][min(tid + it * AT, NA * NA - 1)];
   const float bv = tid < NROW ? a.bias[g][tid] : 0.f;
@@ -862,7 +882,7 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   }
 #pragma unroll
   for (int it = 0; it < NW; ++it)
-    if (tid + it * AT < RT * NS * 2 * 64) wl[tid + it * AT] = wv[it];
+    if (tid + it * AT < WIMG) wl[tid + it * AT] = wv[it];
 #pragma unroll
   for (int it = 0; it < NAS; ++it)
     if (tid + it * AT < NA * NA) asl[tid + it * AT] = av[it];
@@ -921,6 +941,24 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       }
       split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
     }
+    // tail K-step (16x16x16): k = 32 NS + 4kg + e, e < 4
+    f16x4 th, to;
+    if constexpr (TAIL) {
+      const float4 e0 = ld4(El + pr * SE + 32 * NS + 4 * kg), f0 = ld4(Fl + qr * SE + 32 * NS + 4 * kg);
+      const float ev[4] = {e0.x, e0.y, e0.z, e0.w}, fv[4] = {f0.x, f0.y, f0.z, f0.w};
+      float tv[4];
+      if (sep) {
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fmaf(-2.f, __builtin_amdgcn_rcpf(fmaf(ev[e4], fv[e4], 1.f)), 1.f);
+      } else {
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fast_tanh(ev[e4] - fv[e4]);
+      }
+      uint4 hi, lo;
+      split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+      th = __builtin_bit_cast(f16x4, make_uint2(hi.x, hi.y));
+      to = __builtin_bit_cast(f16x4, make_uint2(lo.x, lo.y));
+    }
     // ---- conv_rm: acc[row][col] = sum_k W'[row][k] B[k][col] ----
     f32x4 acc[RT];
 #pragma unroll
@@ -939,6 +977,21 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bo[s], acc[rt]);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bh[s], acc[rt]);
+    }
+    if constexpr (TAIL) {
+      const uint2* w16 = reinterpret_cast<const uint2*>(wl + RT * NS * 2 * 64);
+      f16x4 ah[RT], ao[RT];
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        ah[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
+        ao[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ao[rt], th, acc[rt], 0, 0, 0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], to, acc[rt], 0, 0, 0);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], th, acc[rt], 0, 0, 0);
     }
     // ---- epilogue: alpha * (acc + b) + Astat, 0 on padding slots; staged
     // through this wave's LDS slot so a lane stores 8 consecutive slots ----
