@@ -262,9 +262,10 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V
   if (!hl_on()) return r;
   r.s = spatial_hl_supported(T, V) &&
         ((p->cin == 64 && p->cout == 64) || (p->cin == 6 && p->cout == 64) || (p->cin == 64 && p->cout == 3));
-  r.t = p->cout == 64 && temporal_hl_supported(T, V) &&
-        (tail.epi == TEPI_ENC || tail.epi == TEPI_IN || tail.epi == TEPI_RAW) &&
-        (!tail.next || tail.next->cin == 64);
+  r.t = temporal_hl_supported(T, V) &&
+        ((p->cout == 64 && (tail.epi == TEPI_ENC || tail.epi == TEPI_IN || tail.epi == TEPI_RAW) &&
+          (!tail.next || tail.next->cin == 64)) ||
+         (p->cout == 3 && (tail.epi == TEPI_OUT || tail.epi == TEPI_RAW) && !tail.next));
   return r;
 }
 
@@ -282,7 +283,7 @@ void add_block_hl_jobs(HLList& l, const dstd_block_params* p, const BlockFold& f
   }
   if (hl.t) {
     add_hl_rm(l, p->conv_t.wrm, V, 2 * V, f.hl_rmt, f.hl_scale + 7);
-    add_hl_conv(l, p->conv_t.wf, 64, 64, f.hl_wt, f.hl_scale + 3);
+    add_hl_conv(l, p->conv_t.wf, p->cout, p->cout, f.hl_wt, f.hl_scale + 3);
     if (tail.next) {
       const dstd_block_params* q = tail.next;
       const float* w[4] = {q->conv_s[0].wm1, q->conv_s[0].wm2, q->conv_s[1].wm1, q->conv_s[1].wm2};
@@ -491,6 +492,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ht.B = B;
     ht.T = T;
     ht.V = V;
+    ht.C = p->cout;
     ht.adj = reinterpret_cast<const uint16_t*>(sc.adj_t);
     ht.wimg = f.hl_wt;
     ht.wscale = f.hl_scale + 3;

@@ -196,14 +196,14 @@ struct SpatialHLArgs {
 };
 
 struct TemporalHLArgs {
-  const float* h;            // NTVC [B][T][V][64]
-  int B, T, V;
+  const float* h;            // NTVC [B][T][V][C]
+  int B, T, V, C;            // C = 64, or 3 (conv_st_out: OUT / RAW epilogue, no P/Q)
   const uint16_t* adj;       // [B][V][2 planes][T][SL] halves
   const uint4* wimg;
   const float* wscale;
   const float* bf;
-  int epi;                   // TemporalEpi: ENC, IN or RAW
-  const float* xres;
+  int epi;                   // TemporalEpi: ENC, IN, RAW (C = 64); OUT, RAW (C = 3)
+  const float* xres;         // ENC: block input; OUT: model input [B][T][V][3]
   const float* bn_s;
   const float* bn_h;
   const float* prelu;

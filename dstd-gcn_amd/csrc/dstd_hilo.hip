@@ -539,30 +539,57 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
 }
 
 // ===========================================================================
-// Temporal GC, 64 -> 64 (DSTDGC.forward temporal, model/dstdgcn.py:88-93) with
-// the DSTDGCB tail epilogues (:161-163, DSTDGCN.forward :306-311), unit =
+// Temporal GC, C -> C, C = 64 (every encoder and conv_st_in) or 3 (the
+// conv_st_out tail) (DSTDGC.forward temporal, model/dstdgcn.py:88-93) with the
+// DSTDGCB tail epilogues (:161-163, DSTDGCN.forward :306-315), unit =
 // (sample n, joint v):
 //   y[c][u] = sum_t (W h + b)[t][c] Adj[v][t][u]
-//   ENC: prelu(bn(y + xres));  IN: prelu(bn(y));  RAW: y
+//   ENC: prelu(bn(y + xres));  IN: prelu(bn(y));  RAW: y;
+//   OUT: y + x_model[n][T-1][v][c] (the model output, C = 3)
 //   + P_s/Q_s (8 channels, [B][V][T][8]) of the output for the next block
 // ===========================================================================
-// two waves per SIMD up to 48 frames; the 75-frame units need one SIMD each
-template <int T>
+// waves per SIMD: 64 channels two up to 48 frames (one at 75); the 3-channel
+// tail is light enough for twice as many
+template <int T, int C>
 constexpr int temporal_hl_wpe() {
-  return T <= 48 ? 2 : 1;
+  return (T <= 48 ? 2 : 1) * (C == 3 ? 2 : 1);
 }
-template <int T, int EPI>
-__global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_wpe<T>(), temporal_hl_wpe<T>()))) void k_temporal_hl(
+
+// 8 channels k0 .. k0+7 of the row at byte offset `row_off` (C per row; zero
+// past C, and an out-of-range row_off reads zeros)
+template <int C>
+__device__ __forceinline__ void load_row8_at(__amdgpu_buffer_rsrc_t r, uint32_t row_off, int k0, float4& lo4, float4& hi4) {
+  if constexpr (C % 8 == 0) {
+    lo4 = bld4(r, row_off + 4 * k0);
+    hi4 = bld4(r, row_off + 4 * k0 + 16);
+  } else {
+    const uint32_t off = k0 == 0 ? row_off : OOB;
+    float e[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < C; ++i)
+      e[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * i, 0, 0));
+    lo4 = make_float4(e[0], e[1], e[2], e[3]);
+    hi4 = make_float4(e[4], e[5], e[6], e[7]);
+  }
+}
+
+template <int T, int EPI, int C>
+__global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_wpe<T, C>(), temporal_hl_wpe<T, C>()))) void k_temporal_hl(
     TemporalHLArgs a) {
   using SM = SlotMap<T, false>;
   constexpr int SL = SM::SL, MT = SM::MT, NS = SM::NS, NUT = cdiv(T, 16);
+  constexpr int KSI = cdiv(C, 32), NCT = cdiv(C, 16), KSO = cdiv(NCT, 2);
+  constexpr int WIMG = NCT * KSI * 2 * 64, PIMG = KSO * 2 * 64;
   constexpr int VMAX = 32;
   constexpr bool use_bn = EPI == TEPI_ENC || EPI == TEPI_IN;
-  constexpr bool use_res = EPI == TEPI_ENC;
-  __shared__ uint4 wl[kHLConvImg];
-  __shared__ uint4 pql[kHLPQImg];
-  __shared__ float4 bnl[2][use_bn ? 16 * VMAX : 1];
-  __shared__ float bfl[64];
+  constexpr bool use_res = EPI == TEPI_ENC || EPI == TEPI_OUT;
+  static_assert(C == 64 || (C == 3 && (EPI == TEPI_OUT || EPI == TEPI_RAW)), "shapes of the forward");
+  __shared__ uint4 wl[WIMG];
+  __shared__ uint4 pql[PIMG];
+  __shared__ float4 bnl[2][use_bn ? 4 * NCT * VMAX : 1];
+  __shared__ float bfl[16 * NCT];
   __shared__ float bql[8];
   __shared__ float scl[2];
 
@@ -570,14 +597,14 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
   const int kl = lane >> 4, cl = lane & 15;
   const int V = a.V;
   const bool has_pq = a.pq != nullptr;
-  for (int i = tid; i < kHLConvImg; i += HT) wl[i] = a.wimg[i];
+  for (int i = tid; i < WIMG; i += HT) wl[i] = a.wimg[i];
   if (has_pq)
-    for (int i = tid; i < kHLPQImg; i += HT) pql[i] = a.pqimg[i];
+    for (int i = tid; i < PIMG; i += HT) pql[i] = a.pqimg[i];
   if constexpr (use_bn) {
-    stage_bn64(bnl[0], a.bn_s, V, tid);
-    stage_bn64(bnl[1], a.bn_h, V, tid);
+    stage_bnC<C, NCT>(bnl[0], a.bn_s, V, tid);
+    stage_bnC<C, NCT>(bnl[1], a.bn_h, V, tid);
   }
-  if (tid < 64) bfl[tid] = a.bf[tid];
+  if (tid < 16 * NCT) bfl[tid] = tid < C ? a.bf[tid] : 0.f;
   if (tid < 8) bql[tid] = has_pq ? a.pqb[tid >> 1][tid & 1] : 0.f;
   if (tid == 0) {
     scl[0] = *a.wscale;
@@ -588,39 +615,38 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
   int uend;
   int u = unit_range(a.B * V, uend);
   const float pw = use_bn ? *a.prelu : 0.f;
-  // a unit's rows: frame t of joint v at t * V * 64 floats from the unit base
-  const uint32_t col_bytes = (uint32_t)((T - 1) * V + 1) * 64 * 4;
-  const uint32_t frame_bytes = (uint32_t)V * 64 * 4;
+  // a unit's rows: frame t of joint v at t * V * C floats from the unit base
+  const uint32_t col_bytes = (uint32_t)((T - 1) * V + 1) * C * 4;
+  const uint32_t frame_bytes = (uint32_t)V * C * 4;
   constexpr uint32_t adj_bytes = 2 * T * SL * 2;  // one (n, v): 2 planes of T x SL halves
-  uint32_t xoff[MT];  // conv rows: frame 16m + cl, channels 8kl ..
+  uint32_t xoff[MT];  // conv rows: frame 16m + cl (OOB past T)
 #pragma unroll
-  for (int m = 0; m < MT; ++m) xoff[m] = 16 * m + cl < T ? (uint32_t)(16 * m + cl) * frame_bytes + 32 * kl : OOB;
-  uint32_t uoff[NUT], upq[NUT];  // output frame uo = 16ut + cl (OOB past T), channels 4kl ..
+  for (int m = 0; m < MT; ++m) xoff[m] = 16 * m + cl < T ? (uint32_t)(16 * m + cl) * frame_bytes : OOB;
+  // output frame uo = 16ut + cl (OOB past T), channels 4kl .. (C = 64) or the
+  // 3 channels on lanes kl == 0 (C = 3)
+  uint32_t uoff[NUT], upq[NUT];
 #pragma unroll
   for (int ut = 0; ut < NUT; ++ut) {
     const int uo = 16 * ut + cl;
-    uoff[ut] = uo < T ? (uint32_t)uo * frame_bytes + 16 * kl : OOB;
+    uoff[ut] = uo < T && (C % 4 == 0 || kl == 0) ? (uint32_t)uo * frame_bytes + (C % 4 == 0 ? 16 * kl : 0) : OOB;
     upq[ut] = uo < T && kl < 2 ? (uint32_t)(uo * 8 + 4 * kl) * 4 : OOB;
   }
 
-  float4 xr[MT][2][2];  // tile m row cl = frame 16m + cl
+  float4 xr[MT][KSI][2];  // tile m row cl = frame 16m + cl
   auto load_x = [&](int uu) {
     const int n = uu / V, v = uu - n * V;
-    const auto r = rsrc(a.h + ((size_t)n * T * V + v) * 64, col_bytes);
+    const auto r = rsrc(a.h + ((size_t)n * T * V + v) * C, col_bytes);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        xr[m][ks][0] = bld4(r, xoff[m] + 128 * ks);
-        xr[m][ks][1] = bld4(r, xoff[m] + 128 * ks + 16);
-      }
+      for (int ks = 0; ks < KSI; ++ks) load_row8_at<C>(r, xoff[m], 32 * ks + 8 * kl, xr[m][ks][0], xr[m][ks][1]);
   };
   if (u < uend) load_x(u);
   while (u < uend) {
     const int n = u / V, v = u - n * V;
     const int un = u + 1;
     const int lz = lane + opaque_zero();
-    const size_t cbase = ((size_t)n * T * V + v) * 64;
+    const size_t cbase = ((size_t)n * T * V + v) * C;
     // Issue order matters: vmcnt retires in order, so every load this unit
     // waits for (adjacency, residual) is issued before the next unit's h-row
     // prefetch, which lands behind them.
@@ -639,24 +665,24 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
         }
     }
     __builtin_amdgcn_sched_barrier(0);
-    f16x8 xh[MT][2], xo[MT][2];
+    f16x8 xh[MT][KSI], xo[MT][KSI];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) split8(xr[m][ks][0], xr[m][ks][1], xh[m][ks], xo[m][ks]);
+      for (int ks = 0; ks < KSI; ++ks) split8(xr[m][ks][0], xr[m][ks][1], xh[m][ks], xo[m][ks]);
 
     // ---- conv (transposed): D[t][c] = sum_k h[t][k] W'[c][k] ----
-    f32x4 D[MT][4];
+    f32x4 D[MT][NCT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) D[m][ct] = zero4();
+      for (int ct = 0; ct < NCT; ++ct) D[m][ct] = zero4();
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KSI; ++ks) {
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const f16x8 wh = as_h8(wl[((ct * 2 + ks) * 2 + 0) * 64 + lz]);
-        const f16x8 wo = as_h8(wl[((ct * 2 + ks) * 2 + 1) * 64 + lz]);
+      for (int ct = 0; ct < NCT; ++ct) {
+        const f16x8 wh = as_h8(wl[((ct * KSI + ks) * 2 + 0) * 64 + lz]);
+        const f16x8 wo = as_h8(wl[((ct * KSI + ks) * 2 + 1) * 64 + lz]);
 #pragma unroll
         for (int m = 0; m < MT; ++m) D[m][ct] = mfma32(xo[m][ks], wh, D[m][ct]);
 #pragma unroll
@@ -668,7 +694,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
     {
       const float s = scl[0];
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
+      for (int ct = 0; ct < NCT; ++ct) {
         const float b = bfl[16 * ct + cl];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
@@ -676,38 +702,48 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
           for (int r = 0; r < 4; ++r) D[m][ct][r] = fmaf(D[m][ct][r], s, b);
       }
     }
-    // residual of the encoder epilogue
-    float4 R[use_res ? 4 : 1][use_res ? NUT : 1];
+    // residual of the epilogue: the encoder input (ENC) or the model input's
+    // last observed frame (OUT)
+    float4 R[use_res ? NCT : 1][use_res ? NUT : 1];
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (use_res) {
+    if constexpr (EPI == TEPI_ENC) {
       const auto rr = rsrc(a.xres + cbase, col_bytes);
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut)
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) R[ct][ut] = bld4(rr, uoff[ut] + 64 * ct);
+        for (int ct = 0; ct < NCT; ++ct) R[ct][ut] = bld4(rr, uoff[ut] + 64 * ct);
+    } else if constexpr (EPI == TEPI_OUT) {
+      // x_model [B][T][V][C]: frame T-1 of joint v, 3 channels on lanes kl == 0
+      const auto rr = rsrc(a.xres + (((size_t)n * T + T - 1) * V + v) * C, C * 4);
+      float e[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < C && i < 4; ++i)
+        e[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, kl == 0 ? 4 * i : OOB, 0, 0));
+#pragma unroll
+      for (int ut = 0; ut < NUT; ++ut) R[0][ut] = make_float4(e[0], e[1], e[2], e[3]);
     }
     __builtin_amdgcn_sched_barrier(0);
     // ---- aggregation: O[c][u] = sum_t D[t][c] Adj[v][t][u] ----
-    f32x4 O[4][NUT];
+    f32x4 O[NCT][NUT];
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = zero4();
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
-      f16x8 dh[4], dl[4];
+      f16x8 dh[NCT], dl[NCT];
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) split_acc(D[2 * s][ct], 2 * s + 1 < MT ? D[2 * s + 1][ct] : zero4(), dh[ct], dl[ct]);
+      for (int ct = 0; ct < NCT; ++ct) split_acc(D[2 * s][ct], 2 * s + 1 < MT ? D[2 * s + 1][ct] : zero4(), dh[ct], dl[ct]);
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
         for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dl[ct], as_h8(bh[s][ut]), O[ct][ut]);
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
         for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bo[s][ut]), O[ct][ut]);
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
         for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bh[s][ut]), O[ct][ut]);
     }
@@ -722,7 +758,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
 #pragma unroll
     for (int ut = 0; ut < NUT; ++ut) {
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
+      for (int ct = 0; ct < NCT; ++ct) {
         f32x4& o = O[ct][ut];
         if constexpr (use_res) {
           o[0] += R[ct][ut].x;
@@ -737,7 +773,16 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
           o[2] = prelu_f(fmaf(o[2], sc.z, sh.z), pw);
           o[3] = prelu_f(fmaf(o[3], sc.w, sh.w), pw);
         }
-        bst4(ry, uoff[ut] + 64 * ct, make_float4(o[0], o[1], o[2], o[3]));
+        if constexpr (C % 4 == 0) {
+          bst4(ry, uoff[ut] + 64 * ct, make_float4(o[0], o[1], o[2], o[3]));
+        } else {
+          // (a whole f32x3 bit_cast: hipcc 7.2 folds __builtin_bit_cast of
+          // single vector elements to element 0's bits -- measured)
+          typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+          typedef float f32x3 __attribute__((ext_vector_type(3)));
+          const f32x3 o3 = {o[0], o[1], o[2]};
+          __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(u32x3, o3), ry, uoff[ut], 0, 0);
+        }
       }
     }
     // ---- next block's P_s/Q_s (8 channels) of the output ----
@@ -746,11 +791,12 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut) acc[ut] = zero4();
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
+      for (int ks = 0; ks < KSO; ++ks) {
         const f16x8 qh = as_h8(pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(pql[(ks * 2 + 1) * 64 + lz]);
         f16x8 hh[NUT], hl[NUT];
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) split_acc(O[2 * ks][ut], O[2 * ks + 1][ut], hh[ut], hl[ut]);
+        for (int ut = 0; ut < NUT; ++ut)
+          split_acc(O[2 * ks][ut], 2 * ks + 1 < NCT ? O[2 * ks + 1][ut] : zero4(), hh[ut], hl[ut]);
 #pragma unroll
         for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma32(qo, hh[ut], acc[ut]);
 #pragma unroll
@@ -771,7 +817,6 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
     u = un;
   }
 }
-
 
 // ===========================================================================
 // Dynamic adjacency in split-f16 planes (DSTDGC.forward model/dstdgcn.py:
@@ -1062,10 +1107,19 @@ hipError_t launch_units(int units, const A& a, hipStream_t s) {
 
 template <int T>
 hipError_t temporal_hl_t(const TemporalHLArgs& a, hipStream_t s) {
+  if (a.C == 3) {
+    if (a.pq) return hipErrorNotSupported;
+    switch (a.epi) {
+      case TEPI_OUT: return launch_units<k_temporal_hl<T, TEPI_OUT, 3>>(a.B * a.V, a, s);
+      case TEPI_RAW: return launch_units<k_temporal_hl<T, TEPI_RAW, 3>>(a.B * a.V, a, s);
+      default: return hipErrorNotSupported;
+    }
+  }
+  if (a.C != 64) return hipErrorNotSupported;
   switch (a.epi) {
-    case TEPI_ENC: return launch_units<k_temporal_hl<T, TEPI_ENC>>(a.B * a.V, a, s);
-    case TEPI_IN: return launch_units<k_temporal_hl<T, TEPI_IN>>(a.B * a.V, a, s);
-    case TEPI_RAW: return launch_units<k_temporal_hl<T, TEPI_RAW>>(a.B * a.V, a, s);
+    case TEPI_ENC: return launch_units<k_temporal_hl<T, TEPI_ENC, 64>>(a.B * a.V, a, s);
+    case TEPI_IN: return launch_units<k_temporal_hl<T, TEPI_IN, 64>>(a.B * a.V, a, s);
+    case TEPI_RAW: return launch_units<k_temporal_hl<T, TEPI_RAW, 64>>(a.B * a.V, a, s);
     default: return hipErrorNotSupported;
   }
 }
