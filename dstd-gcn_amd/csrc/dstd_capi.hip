@@ -295,10 +295,14 @@ void add_block_hl_jobs(HLList& l, const dstd_block_params* p, const BlockFold& f
 // One DSTDGCB on NTVC activations.  pq_s must already hold P/Q of x for the
 // block's two spatial DSTDGCs; the block's weight images (add_block_hl_jobs)
 // must be prepared when hl says so.
+// xmodel (conv_st_in of the model, split spatial only): the model input
+// [B][T][V][3]; the kernels build x6 and block-0's spatial P/Q from it, x is
+// not read.
 hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const BlockScratch& sc, int B, int T, int V,
                      const float* x, float* h, float* y, const BlockTail& tail, hipStream_t s, Prof& pf,
-                     const BlockHL& hl) {
+                     const BlockHL& hl, const float* xmodel = nullptr) {
   const bool res = p->cin != p->cout;
+  const bool from_model = xmodel && hl.s && p->cin == 6;
   // (1) spatial adjacency for both graphs
   AdjArgs aa{};
   aa.pq = sc.pq_s;
@@ -351,6 +355,15 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ah.out = reinterpret_cast<uint16_t*>(aa.out);
     ah.out_sN = 2 * aa.out_sN;  // halves
     ah.out_sG = 2 * aa.out_sG;
+    if (from_model) {
+      ah.xin = xmodel;
+      for (int g = 0; g < 2; ++g) {
+        ah.mw[g][0] = p->conv_s[g].wm1;
+        ah.mw[g][1] = p->conv_s[g].wm2;
+        ah.mb[g][0] = p->conv_s[g].bm1;
+        ah.mb[g][1] = p->conv_s[g].bm2;
+      }
+    }
     e = launch_adj_hl(ah, 0, T, V, s);
   } else {
     e = launch_adj(aa, s);
@@ -361,7 +374,8 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   // (2) spatial GC + bn + residual + prelu, P_t/Q_t of h
   if (hl.s) {
     SpatialHLArgs ha{};
-    ha.x = x;
+    ha.x = from_model ? xmodel : x;
+    ha.xmodel = from_model ? 1 : 0;
     ha.B = B;
     ha.T = T;
     ha.V = V;
@@ -840,31 +854,6 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
     pf.end(s);
   }
 
-  // input prep: x6 = cat(x, x - x[:, -1]) and block-0 spatial P/Q (:298-305)
-  PQArgs pa{};
-  pa.x = x;
-  pa.B = B;
-  pa.T = T;
-  pa.V = V;
-  pa.Cin = 6;
-  pa.make_x6 = 1;
-  pa.x6 = L.act[0];
-  const dstd_block_params* b0 = &p->st_in;
-  pa.w[0] = b0->conv_s[0].wm1;
-  pa.w[1] = b0->conv_s[0].wm2;
-  pa.w[2] = b0->conv_s[1].wm1;
-  pa.w[3] = b0->conv_s[1].wm2;
-  pa.b[0] = b0->conv_s[0].bm1;
-  pa.b[1] = b0->conv_s[0].bm2;
-  pa.b[2] = b0->conv_s[1].bm1;
-  pa.b[3] = b0->conv_s[1].bm2;
-  pa.nw = 4;
-  pa.pq = L.sc.pq_s;
-  pa.pql = pq_layout_vt(8, T, V);
-  pf.begin(DSTD_KIND_PREP, s);
-  DSTD_TRY(launch_pq(pa, s));
-  pf.end(s);
-
   // conv_st_in -> bn_in -> prelu (dropout is identity in eval); encoders
   // x = prelu_e(bn_e(DSTDGCB(x) + x)); conv_st_out + output residual written
   // straight into y [B][T][V][3].  Buffers rotate over act[0..2].
@@ -912,6 +901,34 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
     hls[b] = block_hl(blk[b], tails[b], T, V);
     add_block_hl_jobs(hj, blk[b], *fold[b], tails[b], hls[b], T, V);
   }
+
+  // input prep: x6 = cat(x, x - x[:, -1]) and block-0 spatial P/Q (:298-305)
+  PQArgs pa{};
+  pa.x = x;
+  pa.B = B;
+  pa.T = T;
+  pa.V = V;
+  pa.Cin = 6;
+  pa.make_x6 = 1;
+  pa.x6 = L.act[0];
+  const dstd_block_params* b0 = &p->st_in;
+  pa.w[0] = b0->conv_s[0].wm1;
+  pa.w[1] = b0->conv_s[0].wm2;
+  pa.w[2] = b0->conv_s[1].wm1;
+  pa.w[3] = b0->conv_s[1].wm2;
+  pa.b[0] = b0->conv_s[0].bm1;
+  pa.b[1] = b0->conv_s[0].bm2;
+  pa.b[2] = b0->conv_s[1].bm1;
+  pa.b[3] = b0->conv_s[1].bm2;
+  pa.nw = 4;
+  pa.pq = L.sc.pq_s;
+  pa.pql = pq_layout_vt(8, T, V);
+  if (!hls[0].s) {  // the split kernels build x6 and these P/Q from x themselves
+    pf.begin(DSTD_KIND_PREP, s);
+    DSTD_TRY(launch_pq(pa, s));
+    pf.end(s);
+  }
+
   if (!reuse) {
     pf.begin(DSTD_KIND_FOLD, s);
     DSTD_TRY(run_hl_prep(hj, s));
@@ -919,7 +936,8 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
   }
   for (int b = 0; b < NB; ++b) {
     pf.block = b;
-    DSTD_TRY(run_block(blk[b], *fold[b], L.sc, B, T, V, xin[b], hbuf[b], ybuf[b], tails[b], s, pf, hls[b]));
+    DSTD_TRY(run_block(blk[b], *fold[b], L.sc, B, T, V, xin[b], hbuf[b], ybuf[b], tails[b], s, pf, hls[b],
+                       b == 0 ? x : nullptr));
   }
   return DSTD_OK;
 }

@@ -177,7 +177,8 @@ constexpr int kHLPQImg = 2 * 2 * 64;        // uint4 per HLJ_PQ image
 
 // ---- GC kernel arguments --------------------------------------------------
 struct SpatialHLArgs {
-  const float* x;            // NTVC [B][T][V][Cin]
+  const float* x;            // NTVC [B][T][V][Cin]; xmodel: the model input [B][T][V][3]
+  int xmodel;                // Cin == 6 only: build x6 = cat(x, x - x[:, -1]) rows on the fly
   int B, T, V, Cin, Cout;    // (Cin, Cout) in {(64, 64), (6, 64), (64, 3)}
   const uint16_t* adj;       // [B][2][T][2 planes][V][SL] halves
   const uint4* wimg[3];      // HLJ_CONV images of conv_s[g].conv_f, [2]: residual conv (Cin != Cout)
@@ -220,6 +221,11 @@ struct TemporalHLArgs {
 // K = 2T / 2V, columns (q, slot) in the slot order above; output planes as
 // AdjArgs.hl documents.  Shapes: hl_shape() of dstd_hilo.hip.
 struct AdjHLArgs {
+  const float* xin;         // spatial, conv_st_in of the model: the model input [B][T][V][3]; P/Q
+                            // of x6 = cat(x, x - x[:, -1]) are formed in the prologue from mw/mb
+                            // (no prep launch); null: read pq
+  const float* mw[2][2];    // [graph][conv_m1, conv_m2] weights [2][6]
+  const float* mb[2][2];
   const float* pq;          // channel-innermost P/Q planes (PQLayout sch == 1)
   PQLayout pql;
   int p_ch[2];              // first channel (P_0, P_1, Q_0, Q_1) of each graph

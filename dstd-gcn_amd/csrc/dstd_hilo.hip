@@ -240,6 +240,22 @@ __device__ __forceinline__ void load_row8(__amdgpu_buffer_rsrc_t r, int row, int
   }
 }
 
+// conv_st_in's 6-channel input row built on the fly from the model input
+// (model/dstdgcn.py:298-303): x6 = (x[t][v], x[t][v] - x[T-1][v]); rf / rl:
+// the unit's frame and the last frame ([V][3] each); only k0 == 0 has data
+__device__ __forceinline__ void load_x6row(__amdgpu_buffer_rsrc_t rf, __amdgpu_buffer_rsrc_t rl, int row, int k0,
+                                           float4& lo4, float4& hi4) {
+  const uint32_t off = k0 == 0 ? (uint32_t)row * 12 : OOB;
+  float c[3], l[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    c[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rf, off + 4 * i, 0, 0));
+    l[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rl, off + 4 * i, 0, 0));
+  }
+  lo4 = make_float4(c[0], c[1], c[2], c[0] - l[0]);
+  hi4 = make_float4(c[1] - l[1], c[2] - l[2], 0.f, 0.f);
+}
+
 // folded BN vectors [V][C] -> LDS [c/4][v] for NCT*4 channel quads (zero past C)
 template <int C, int NCT>
 __device__ __forceinline__ void stage_bnC(float4* dst, const float* src, int V, int tid) {
@@ -310,13 +326,22 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
   const uint32_t wadj0 = kl < NG ? (uint32_t)(cl * SL + 8 * kl) * 2 : OOB;  // + wt * 32 * SL
   const uint32_t wpq0 = kl == 0 ? (uint32_t)cl * 16 : OOB;                  // + wt * 256
 
+  // xmodel (CIN == 6 only): x is the model input [B][T][V][3] and the rows
+  // are x6 = cat(x, x - x[:, -1]) built on the fly (no x6 tensor, no prep launch)
+  const bool x6 = CIN == 6 && a.xmodel;
+  auto frame_rsrc = [&](int uu) { return x6 ? rsrc(a.x + (size_t)uu * V * 3, V * 12) : rsrc(a.x + (size_t)uu * V * CIN, xunit); };
+  auto last_rsrc = [&](int uu) { return rsrc(a.x + ((size_t)(uu / T) * T + T - 1) * V * 3, V * 12); };
+  auto row8 = [&](__amdgpu_buffer_rsrc_t rf, __amdgpu_buffer_rsrc_t rl, int row, int k0, float4& lo4, float4& hi4) {
+    if (x6) load_x6row(rf, rl, row, k0, lo4, hi4);
+    else load_row8<CIN>(rf, row, k0, lo4, hi4);
+  };
   float4 xr[2][KSI][2];  // [tile][k-step][half]: channels 32ks + 8kl .. +7 of the tile row
   auto load_x = [&](int uu) {
-    const auto r = rsrc(a.x + (size_t)uu * V * CIN, xunit);
+    const auto r = frame_rsrc(uu), rl = last_rsrc(uu);
 #pragma unroll
     for (int ks = 0; ks < KSI; ++ks) {
-      load_row8<CIN>(r, jr0, 32 * ks + 8 * kl, xr[0][ks][0], xr[0][ks][1]);
-      load_row8<CIN>(r, jr1, 32 * ks + 8 * kl, xr[1][ks][0], xr[1][ks][1]);
+      row8(r, rl, jr0, 32 * ks + 8 * kl, xr[0][ks][0], xr[0][ks][1]);
+      row8(r, rl, jr1, 32 * ks + 8 * kl, xr[1][ks][0], xr[1][ks][1]);
     }
   };
   uint4 ab[2][NWT][2];  // adjacency B fragments [graph][w tile][plane]
@@ -334,7 +359,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
   while (u < uend) {
     const int un = u + 1;
     const int lz = lane + opaque_zero();
-    const auto rx = rsrc(a.x + (size_t)u * V * CIN, xunit);
+    const auto rx = frame_rsrc(u), rxl = last_rsrc(u);
     // residual: identity -> x at the output positions (w, channels 16ct + 4kl ..);
     // residual conv -> x rows of the output joints as B fragments
     float4 R[RES ? 1 : 4][RES ? 1 : NWT];
@@ -343,7 +368,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt)
 #pragma unroll
-        for (int ks = 0; ks < KSI; ++ks) load_row8<CIN>(rx, 16 * wt + cl, 32 * ks + 8 * kl, xw[wt][ks][0], xw[wt][ks][1]);
+        for (int ks = 0; ks < KSI; ++ks) row8(rx, rxl, 16 * wt + cl, 32 * ks + 8 * kl, xw[wt][ks][0], xw[wt][ks][1]);
     } else {
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt)
@@ -889,11 +914,41 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   float4 q4[NPQ];
   uint4 wv[NW];
   float av[NAS];
+  if (MODE == 0 && a.xin) {
+    // conv_st_in (model/dstdgcn.py:298-305): P/Q of x6 = cat(x, x - x[:, -1])
+    // straight from the model input [B][T][V][3]; this graph's conv_m1/m2 rows
+    float wm[4][6], bm[4];
 #pragma unroll
-  for (int it = 0; it < NPQ; ++it) {
-    const int i = min(tid + it * AT, T * V - 1);                              // clamped: no branch
-    const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;  // memory order
-    q4[it] = ld4(pqb + t * L.st + v * L.sv);                                  // (P_0, P_1, Q_0, Q_1)
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) wm[r][c] = a.mw[g][r >> 1][(r & 1) * 6 + c];
+      bm[r] = a.mb[g][r >> 1][r & 1];
+    }
+    const float* xn = a.xin + (size_t)n * T * V * 3;
+#pragma unroll
+    for (int it = 0; it < NPQ; ++it) {
+      const int i = min(tid + it * AT, T * V - 1);
+      const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;
+      const float* xc = xn + (t * V + v) * 3;
+      const float* xl = xn + ((T - 1) * V + v) * 3;
+      const float x6v[6] = {xc[0], xc[1], xc[2], xc[0] - xl[0], xc[1] - xl[1], xc[2] - xl[2]};
+      float pq[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float acc = bm[r];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) acc = fmaf(wm[r][c], x6v[c], acc);
+        pq[r] = acc;
+      }
+      q4[it] = make_float4(pq[0], pq[1], pq[2], pq[3]);
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < NPQ; ++it) {
+      const int i = min(tid + it * AT, T * V - 1);                              // clamped: no branch
+      const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;  // memory order
+      q4[it] = ld4(pqb + t * L.st + v * L.sv);                                  // (P_0, P_1, Q_0, Q_1)
+    }
   }
 #pragma unroll
   for (int it = 0; it < NW; ++it) wv[it] = a.wimg[g][min(tid + it * AT, WIMG - 1)];
@@ -935,14 +990,18 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   if (tid < RT * 16) bsl[tid] = bv;
   const bool sep = __syncthreads_or(bad) == 0;
   if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0)
-    for (int i = tid; i < T * V; i += AT) {
-      const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;
-      const float4 q4 = ld4(pqb + t * L.st + v * L.sv);
-      const int pr = MODE == 0 ? v : t, ki = MODE == 0 ? t : v;
-      El[pr * SE + ki] = q4.x;
-      El[pr * SE + KH + ki] = q4.y;
-      Fl[pr * SE + ki] = q4.z;
-      Fl[pr * SE + KH + ki] = q4.w;
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < NPQ; ++it) {
+      const int i = tid + it * AT;
+      if (i < T * V) {
+        const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;
+        const int pr = MODE == 0 ? v : t, ki = MODE == 0 ? t : v;
+        El[pr * SE + ki] = q4[it].x;
+        El[pr * SE + KH + ki] = q4[it].y;
+        Fl[pr * SE + ki] = q4[it].z;
+        Fl[pr * SE + KH + ki] = q4[it].w;
+      }
     }
     for (int i = tid; i < (NA + 1) * (KP - K); i += AT) {
       const int r = i / (KP - K), k = K + i % (KP - K);
