@@ -179,16 +179,26 @@ def forward_profiled(model, x, y, prof):
     model._forward_native(x, y, ctypes.byref(prof.prof))
 
 
-def load_traffic(kernel):
+def load_traffic(kernel, instance=None):
+    """Measured HBM bytes per launch (profiles/pmc_traffic.json): the exact
+    kernel instantiation when profiled, else the family average."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
+        if instance and instance in d.get("by_kernel", {}):
+            return d["by_kernel"][instance].get("hbm_bytes_per_launch")
         return d.get(kernel, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+
+
+def split_instance(kind, T, V):
+    """Kernel instantiation of DSTDGCB 1 (an encoder) for kind."""
+    return {native.KIND_SPATIAL: f"k_spatial_hl<{V}, 64, 64>", native.KIND_TEMPORAL: f"k_temporal_hl<{T}, 1, 64>",
+            native.KIND_ADJ_S: f"k_adj_hl<0, {T}, {2 * T}, {V}>", native.KIND_ADJ_T: f"k_adj_hl<1, {V}, {2 * V}, {T}>"}.get(kind)
 
 
 def cpu_baseline(opts, sd, x_cpu, min_s, max_s):
@@ -297,7 +307,7 @@ def main():
     achieved = kernel_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
     kname = native.KIND_NAMES[dominant]
     split_blk = split_on and opts["num_layers"] > 0
-    traffic = load_traffic(kname + "_split" if split_blk else kname)
+    traffic = load_traffic(kname + "_split" if split_blk else kname, split_instance(dominant, T, V) if split_blk else None)
     total_flop_per_seq = sum(sum(b.values()) for b in fl)
     total_bytes_per_seq = sum(sum(b.values()) for b in bb)
 
@@ -314,8 +324,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "arithmetic": ("split-f16 MFMA for the 64->64 GC contractions (fp32 operands as f16 hi/lo pairs, three "
-                           "v_mfma_f32_16x16x32_f16, fp32 accumulate), exact-fp32 MFMA elsewhere") if split_on
+            "arithmetic": ("split-f16 MFMA for every contraction of the forward (fp32 operands as f16 hi/lo pairs, "
+                           "three v_mfma_f32_16x16x32_f16 per product, fp32 accumulate; fp32 storage, VALU and "
+                           "epilogues)") if split_on
                           else "exact-fp32 MFMA (v_mfma_f32_16x16x4_f32)",
             "data": "synthetic (N(0,1) poses, future frames padded with the last observed; fixture weights)",
             "config": {"workload": CONFIGS[args.config][1] + f", B={B}/GPU, eval forward", "global_batch": B * world,

@@ -47,12 +47,18 @@ def family(name):
     return None
 
 
-def per_launch(path, counter):
+def short(name):
+    """'void dstd::k_spatial_hl<22, 64, 64>(dstd::SpatialHLArgs)' -> 'k_spatial_hl<22, 64, 64>'"""
+    name = name.split("(")[0].replace("void ", "")
+    return name.split("::")[-1] if "<" not in name else name[name.index("k_"):] if "k_" in name else name
+
+
+def per_launch(path, counter, key=family):
     tot, ids = defaultdict(float), defaultdict(set)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        f = family(r["Kernel_Name"])
+        f = key(r["Kernel_Name"])
         if f is None:
             continue
         tot[f] += float(r["Counter_Value"])
@@ -64,6 +70,7 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), dst + "_kernel_stats.csv")
     fetch = write = None
+    fetch_k = write_k = {}
     for d in sorted(os.listdir(src)):
         p = os.path.join(src, d, "run_counter_collection.csv")
         if not d.startswith("pmc") or not os.path.exists(p):
@@ -71,8 +78,10 @@ def main():
         names = {r["Counter_Name"] for r in csv.DictReader(open(p))}
         if "FETCH_SIZE" in names:
             fetch = per_launch(p, "FETCH_SIZE")
+            fetch_k = per_launch(p, "FETCH_SIZE", short)
         if "WRITE_SIZE" in names:
             write = per_launch(p, "WRITE_SIZE")
+            write_k = per_launch(p, "WRITE_SIZE", short)
     out = {"_note": "HBM bytes per launch, averaged over every launch of the family in the profiled bench run; "
                     "FETCH_SIZE doubled (gfx950 half-count of wide reads), WRITE_SIZE as reported; KB = 1024 B",
            "_source": os.path.basename(dst)}
@@ -81,6 +90,12 @@ def main():
         wb = 1024 * (write or {}).get(f, 0.0)
         out[f] = {"fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb),
                   "hbm_bytes_per_launch": round(fb + wb)}
+    out["by_kernel"] = {}
+    for k in sorted(set(fetch_k) | set(write_k)):
+        fb = 2 * 1024 * fetch_k.get(k, 0.0)
+        wb = 1024 * write_k.get(k, 0.0)
+        out["by_kernel"][k] = {"fetch_bytes_per_launch": round(fb), "write_bytes_per_launch": round(wb),
+                               "hbm_bytes_per_launch": round(fb + wb)}
     with open(os.path.join(os.path.dirname(dst) or ".", "pmc_traffic.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
