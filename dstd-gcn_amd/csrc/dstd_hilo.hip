@@ -20,6 +20,8 @@
 //    epilogue, stores are 16 bytes per lane.
 // Weights come as fragment images (k_hl_prep) copied into LDS with 16-byte
 // loads.  Units are contiguous ranges per wave, no barrier after the prologue.
+#include <type_traits>
+
 #include "dstd_common.h"
 #include "dstd_hilo.h"
 #include "dstd_kernels.h"
@@ -1019,109 +1021,117 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
 
   float* so = stg[wave];
   uint16_t* out = a.out + (size_t)n * a.out_sN + (size_t)g * a.out_sG;
+  const auto ro = rsrc(out, 2u * NROW * 2 * NCOL);
   const int ct_end = min(Gm::NCT, (chunk + 1) * Gm::CPC);
-  for (int ct = chunk * Gm::CPC + wave; ct < ct_end; ct += AW) {
-    // this lane's column (B operand column j = cl)
-    const int col = ct * 16 + cl;
-    const int q = col / SL, pi = SM::slot_idx(col - q * SL);
-    const bool valid = col < NCOL && pi < NA;
-    const int pr = valid ? pi : NA, qr = col < NCOL ? q : NA;
-    // ---- B fragments: tanh(P[k][p] - Q[k][q]) for k = 32s + 8kg + e ----
-    f16x8 bh[NS], bo[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const float* ep = El + pr * SE + 32 * s + 8 * kg;
-      const float* fq = Fl + qr * SE + 32 * s + 8 * kg;
-      const float4 e0 = ld4(ep), e1 = ld4(ep + 4), f0 = ld4(fq), f1 = ld4(fq + 4);
-      float tv[8];
-      const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-      const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-      if (sep) {
-#pragma unroll
-        for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fmaf(-2.f, __builtin_amdgcn_rcpf(fmaf(ev[e8], fv[e8], 1.f)), 1.f);
-      } else {
-#pragma unroll
-        for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fast_tanh(ev[e8] - fv[e8]);
-      }
-      split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
-    }
-    // tail K-step (16x16x16): k = 32 NS + 4kg + e, e < 4
-    f16x4 th, to;
-    if constexpr (TAIL) {
-      const float4 e0 = ld4(El + pr * SE + 32 * NS + 4 * kg), f0 = ld4(Fl + qr * SE + 32 * NS + 4 * kg);
-      const float ev[4] = {e0.x, e0.y, e0.z, e0.w}, fv[4] = {f0.x, f0.y, f0.z, f0.w};
-      float tv[4];
-      if (sep) {
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fmaf(-2.f, __builtin_amdgcn_rcpf(fmaf(ev[e4], fv[e4], 1.f)), 1.f);
-      } else {
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fast_tanh(ev[e4] - fv[e4]);
-      }
-      uint4 hi, lo;
-      split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
-      th = __builtin_bit_cast(f16x4, make_uint2(hi.x, hi.y));
-      to = __builtin_bit_cast(f16x4, make_uint2(lo.x, lo.y));
-    }
-    // ---- conv_rm: acc[row][col] = sum_k W'[row][k] B[k][col] ----
-    f32x4 acc[RT];
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc[rt] = zero4();
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      f16x8 ah[RT], ao[RT];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        ah[rt] = as_h8(wl[((rt * NS + s) * 2 + 0) * 64 + lane]);
-        ao[rt] = as_h8(wl[((rt * NS + s) * 2 + 1) * 64 + lane]);
-      }
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ao[rt], bh[s], acc[rt]);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bo[s], acc[rt]);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bh[s], acc[rt]);
-    }
-    if constexpr (TAIL) {
-      const uint2* w16 = reinterpret_cast<const uint2*>(wl + RT * NS * 2 * 64);
-      f16x4 ah[RT], ao[RT];
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        ah[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
-        ao[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
-      }
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ao[rt], th, acc[rt], 0, 0, 0);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], to, acc[rt], 0, 0, 0);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], th, acc[rt], 0, 0, 0);
-    }
-    // ---- epilogue: alpha * (acc + b) + Astat, 0 on padding slots; staged
-    // through this wave's LDS slot so a lane stores 8 consecutive slots ----
-    const float as = asl[valid ? pr * NA + qr : NA * NA];
-#pragma unroll
-    for (int r2 = 0; r2 < RT; r2 += 2) {
-#pragma unroll
-      for (int dr = 0; dr < 2; ++dr) {
-        if (r2 + dr >= RT) continue;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = (r2 + dr) * 16 + 4 * kg + r;
-          so[(dr * 16 + 4 * kg + r) * OS + cl] = valid ? fmaf(alpha, fmaf(acc[r2 + dr][r], inv, bsl[row]), as) : 0.f;
+  auto tiles = [&](auto sep_c) {
+    constexpr bool SEP = decltype(sep_c)::value;
+    for (int ct = chunk * Gm::CPC + wave; ct < ct_end; ct += AW) {
+      // this lane's column (B operand column j = cl)
+      const int col = ct * 16 + cl;
+      const int q = col / SL, pi = SM::slot_idx(col - q * SL);
+      const bool valid = col < NCOL && pi < NA;
+      const int pr = valid ? pi : NA, qr = col < NCOL ? q : NA;
+      // ---- B fragments: tanh(P[k][p] - Q[k][q]) for k = 32s + 8kg + e ----
+      f16x8 bh[NS], bo[NS];
+  #pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        const float* ep = El + pr * SE + 32 * s + 8 * kg;
+        const float* fq = Fl + qr * SE + 32 * s + 8 * kg;
+        const float4 e0 = ld4(ep), e1 = ld4(ep + 4), f0 = ld4(fq), f1 = ld4(fq + 4);
+        float tv[8];
+        const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+        const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+        if constexpr (SEP) {
+  #pragma unroll
+          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fmaf(-2.f, __builtin_amdgcn_rcpf(fmaf(ev[e8], fv[e8], 1.f)), 1.f);
+        } else {
+  #pragma unroll
+          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fast_tanh(ev[e8] - fv[e8]);
         }
+        split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
       }
-      // lane -> (row of the pair, 8-column half)
-      const int rl = lane >> 1, h = lane & 1, row = r2 * 16 + rl, c8 = ct * 16 + 8 * h;
-      if (row < NROW && c8 < NCOL) {
+      // tail K-step (16x16x16): k = 32 NS + 4kg + e, e < 4
+      f16x4 th, to;
+      if constexpr (TAIL) {
+        const float4 e0 = ld4(El + pr * SE + 32 * NS + 4 * kg), f0 = ld4(Fl + qr * SE + 32 * NS + 4 * kg);
+        const float ev[4] = {e0.x, e0.y, e0.z, e0.w}, fv[4] = {f0.x, f0.y, f0.z, f0.w};
+        float tv[4];
+        if constexpr (SEP) {
+  #pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fmaf(-2.f, __builtin_amdgcn_rcpf(fmaf(ev[e4], fv[e4], 1.f)), 1.f);
+        } else {
+  #pragma unroll
+          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fast_tanh(ev[e4] - fv[e4]);
+        }
+        uint4 hi, lo;
+        split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+        th = __builtin_bit_cast(f16x4, make_uint2(hi.x, hi.y));
+        to = __builtin_bit_cast(f16x4, make_uint2(lo.x, lo.y));
+      }
+      // ---- conv_rm: acc[row][col] = sum_k W'[row][k] B[k][col] ----
+      f32x4 acc[RT];
+  #pragma unroll
+      for (int rt = 0; rt < RT; ++rt) acc[rt] = zero4();
+  #pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        f16x8 ah[RT], ao[RT];
+  #pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          ah[rt] = as_h8(wl[((rt * NS + s) * 2 + 0) * 64 + lane]);
+          ao[rt] = as_h8(wl[((rt * NS + s) * 2 + 1) * 64 + lane]);
+        }
+  #pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ao[rt], bh[s], acc[rt]);
+  #pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bo[s], acc[rt]);
+  #pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bh[s], acc[rt]);
+      }
+      if constexpr (TAIL) {
+        const uint2* w16 = reinterpret_cast<const uint2*>(wl + RT * NS * 2 * 64);
+        f16x4 ah[RT], ao[RT];
+  #pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+          ah[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
+          ao[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
+        }
+  #pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ao[rt], th, acc[rt], 0, 0, 0);
+  #pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], to, acc[rt], 0, 0, 0);
+  #pragma unroll
+        for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], th, acc[rt], 0, 0, 0);
+      }
+      // ---- epilogue: alpha * (acc + b) + Astat, 0 on padding slots; staged
+      // through this wave's LDS slot so a lane stores 8 consecutive slots ----
+      // padding slots: alpha -> 0 and Astat[NA*NA] = 0, so the value is 0 without a select
+      const float as = asl[valid ? pr * NA + qr : NA * NA], al = valid ? alpha : 0.f;
+  #pragma unroll
+      for (int r2 = 0; r2 < RT; r2 += 2) {
+  #pragma unroll
+        for (int dr = 0; dr < 2; ++dr) {
+          if (r2 + dr >= RT) continue;
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = (r2 + dr) * 16 + 4 * kg + r;
+            so[(dr * 16 + 4 * kg + r) * OS + cl] = fmaf(al, fmaf(acc[r2 + dr][r], inv, bsl[row]), as);
+          }
+        }
+        // lane -> (row of the pair, 8-column half)
+        const int rl = lane >> 1, h = lane & 1, row = r2 * 16 + rl, c8 = ct * 16 + 8 * h;
         const float4 v0 = ld4(so + rl * OS + 8 * h), v1 = ld4(so + rl * OS + 8 * h + 4);
         uint4 hi, lo;
         split8(v0, v1, hi, lo);
-        *reinterpret_cast<uint4*>(out + (size_t)row * (2 * NCOL) + c8) = hi;
-        *reinterpret_cast<uint4*>(out + (size_t)row * (2 * NCOL) + NCOL + c8) = lo;
+        // rows / columns past the plane: out-of-range offset, the store is dropped
+        const uint32_t off = row < NROW && c8 < NCOL ? 2u * (uint32_t)(row * (2 * NCOL) + c8) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), ro, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), ro, off + 2u * NCOL, 0, 0);
       }
     }
-  }
+  };
+  // separable-exp path or the direct tanh fallback, chosen once per workgroup
+  if (sep) tiles(std::true_type{});
+  else tiles(std::false_type{});
   TLH(MODE, 2)
 #ifdef DSTD_STAMPS
   // slot 3: HW_ID (cu / se) and XCC_ID of the workgroup's placement
