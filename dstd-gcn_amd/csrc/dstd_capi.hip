@@ -91,6 +91,7 @@ struct BlockFold {
   uint4* hl_rms[2]; // conv_s[g].conv_rm (spatial adjacency)
   uint4* hl_rmt;    // conv_t.conv_rm (temporal adjacency)
   float* hl_scale;  // [9]: 2^-s of ws0, ws1, pqs, wt, pqt, rms0, rms1, rmt, ws2
+  float* hl_rbias;  // [2T + V]: fused conv_rm biases (HLJob::bias_out) of rms0, rms1, rmt
 };
 
 // Split-f16 GC kernels (dstd_hilo.hip) where the shape has them: 1 (default),
@@ -135,6 +136,7 @@ void carve_fold(Carver& cv, BlockFold& f, int T, int V, int cout, bool res) {
   f.hl_rms[1] = img(hl_rm_img(T, 2 * T));
   f.hl_rmt = img(hl_rm_img(V, 2 * V));
   f.hl_scale = cv.take(12);
+  f.hl_rbias = cv.take((size_t)2 * T + V);
 }
 
 // adjacency scratch: the larger of the fp32 rows and the split-f16 planes
@@ -225,10 +227,12 @@ void add_hl_conv(HLList& l, const float* w, int rows, int cols, uint4* img, floa
   j.inv_scale = sc;
   l.push_back(j);
 }
-void add_hl_rm(HLList& l, const float* w, int rows, int cols, uint4* img, float* sc) {
+void add_hl_rm(HLList& l, const float* w, const float* b, int rows, int cols, uint4* img, float* sc, float* bout) {
   HLJob j{};
   j.kind = HLJ_RM;
   j.w[0] = w;
+  j.bias = b;
+  j.bias_out = bout;
   j.nblk = 1;
   j.rows = rows;
   j.cols = cols;
@@ -273,8 +277,8 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V
 void add_block_hl_jobs(HLList& l, const dstd_block_params* p, const BlockFold& f, const BlockTail& tail,
                        const BlockHL& hl, int T, int V) {
   if (hl.s) {
-    add_hl_rm(l, p->conv_s[0].wrm, T, 2 * T, f.hl_rms[0], f.hl_scale + 5);
-    add_hl_rm(l, p->conv_s[1].wrm, T, 2 * T, f.hl_rms[1], f.hl_scale + 6);
+    add_hl_rm(l, p->conv_s[0].wrm, p->conv_s[0].brm, T, 2 * T, f.hl_rms[0], f.hl_scale + 5, f.hl_rbias);
+    add_hl_rm(l, p->conv_s[1].wrm, p->conv_s[1].brm, T, 2 * T, f.hl_rms[1], f.hl_scale + 6, f.hl_rbias + T);
     add_hl_conv(l, p->conv_s[0].wf, p->cout, p->cin, f.hl_ws[0], f.hl_scale + 0);
     add_hl_conv(l, p->conv_s[1].wf, p->cout, p->cin, f.hl_ws[1], f.hl_scale + 1);
     if (p->cin != p->cout) add_hl_conv(l, p->res_w, p->cout, p->cin, f.hl_ws[2], f.hl_scale + 8);
@@ -282,7 +286,7 @@ void add_block_hl_jobs(HLList& l, const dstd_block_params* p, const BlockFold& f
     add_hl_pq(l, w, 2, p->cout, f.hl_pqs, f.hl_scale + 2);
   }
   if (hl.t) {
-    add_hl_rm(l, p->conv_t.wrm, V, 2 * V, f.hl_rmt, f.hl_scale + 7);
+    add_hl_rm(l, p->conv_t.wrm, p->conv_t.brm, V, 2 * V, f.hl_rmt, f.hl_scale + 7, f.hl_rbias + 2 * T);
     add_hl_conv(l, p->conv_t.wf, p->cout, p->cout, f.hl_wt, f.hl_scale + 3);
     if (tail.next) {
       const dstd_block_params* q = tail.next;
@@ -348,7 +352,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
       ah.p_ch[g] = aa.p_ch[g];
       ah.wimg[g] = f.hl_rms[g];
       ah.wscale[g] = f.hl_scale + 5 + g;
-      ah.bias[g] = aa.bias[g];
+      ah.bias[g] = f.hl_rbias + g * T;
       ah.astat[g] = aa.astat[g];
     }
     ah.alpha = aa.alpha;
@@ -486,7 +490,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ah.p_ch[0] = ta.p_ch[0];
     ah.wimg[0] = f.hl_rmt;
     ah.wscale[0] = f.hl_scale + 7;
-    ah.bias[0] = ta.bias[0];
+    ah.bias[0] = f.hl_rbias + 2 * T;
     ah.astat[0] = ta.astat[0];
     ah.alpha = ta.alpha;
     ah.out = reinterpret_cast<uint16_t*>(ta.out);

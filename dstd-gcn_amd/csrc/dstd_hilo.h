@@ -163,6 +163,8 @@ struct HLJob {
   int rows, cols;
   uint4* img;
   float* inv_scale;   // 2^-s
+  const float* bias;  // HLJ_RM: conv_rm bias; bias_out[r] = bias[r] + sum_k W[r][k]
+  float* bias_out;    //   (the adjacency kernel contracts W with 1/(E F + 1), see k_adj_hl)
 };
 inline int hl_rm_img(int rows, int cols) {  // uint4
   return cdiv(rows, 16) * (hl_rm_nsf(cols) * 2 * 64 + hl_rm_tail(cols) * 64);
@@ -232,7 +234,7 @@ struct AdjHLArgs {
   int B, ngroups;
   const uint4* wimg[2];     // HLJ_RM images of conv_rm
   const float* wscale[2];
-  const float* bias[2];
+  const float* bias[2];     // HLJob::bias_out of the conv_rm image (bias + row sums of W)
   const float* alpha;
   const float* astat[2];    // [NA][NA]
   uint16_t* out;

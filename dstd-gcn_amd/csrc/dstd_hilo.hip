@@ -148,6 +148,13 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
     scale = ldexpf(1.f, 14 - e);
   }
   if (tid == 0) *j.inv_scale = 1.f / scale;
+  if (j.kind == HLJ_RM) {  // fused bias: b[r] + sum_k W[r][k] (fixed order)
+    for (int r = tid; r < j.rows; r += 256) {
+      float acc = 0.f;
+      for (int k = 0; k < j.cols; ++k) acc += j.w[0][r * j.cols + k];
+      j.bias_out[r] = j.bias[r] + acc;
+    }
+  }
   if (j.kind == HLJ_CONV) {
     const int NCT = cdiv(j.rows, 16), KSI = cdiv(j.cols, 32);
     for (int i = tid; i < NCT * KSI * 64; i += 256) {
@@ -579,6 +586,9 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
 // tail is light enough for twice as many
 template <int T, int C>
 constexpr int temporal_hl_wpe() {
+#ifdef DSTD_T_WPE
+  return DSTD_T_WPE * (C == 3 ? 2 : 1);
+#endif
   return (T <= 48 ? 2 : 1) * (C == 3 ? 2 : 1);
 }
 
@@ -1016,7 +1026,9 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
     }
     __syncthreads();
   }
-  const float alpha = *a.alpha, inv = *a.wscale[g];
+  // tanh(P - Q) = 1 - 2 r with r = 1 / (E F + 1): the B fragments carry r,
+  // the accumulator is scaled by -2 / 2^s and the bias holds b + sum_k W[.][k]
+  const float alpha = *a.alpha, inv = -2.f * *a.wscale[g];
   TLH(MODE, 1)
 
   float* so = stg[wave];
@@ -1043,10 +1055,10 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
         const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
         if constexpr (SEP) {
   #pragma unroll
-          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fmaf(-2.f, __builtin_amdgcn_rcpf(fmaf(ev[e8], fv[e8], 1.f)), 1.f);
+          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = __builtin_amdgcn_rcpf(fmaf(ev[e8], fv[e8], 1.f));
         } else {
   #pragma unroll
-          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fast_tanh(ev[e8] - fv[e8]);
+          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fmaf(-0.5f, fast_tanh(ev[e8] - fv[e8]), 0.5f);
         }
         split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
       }
@@ -1058,10 +1070,10 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
         float tv[4];
         if constexpr (SEP) {
   #pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fmaf(-2.f, __builtin_amdgcn_rcpf(fmaf(ev[e4], fv[e4], 1.f)), 1.f);
+          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = __builtin_amdgcn_rcpf(fmaf(ev[e4], fv[e4], 1.f));
         } else {
   #pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fast_tanh(ev[e4] - fv[e4]);
+          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fmaf(-0.5f, fast_tanh(ev[e4] - fv[e4]), 0.5f);
         }
         uint4 hi, lo;
         split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
