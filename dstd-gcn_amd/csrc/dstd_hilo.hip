@@ -1055,7 +1055,11 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
         const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
         if constexpr (SEP) {
   #pragma unroll
-          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = __builtin_amdgcn_rcpf(fmaf(ev[e8], fv[e8], 1.f));
+          for (int e2 = 0; e2 < 8; e2 += 2) {  // E F + 1 as packed fp32 (v_pk_fma_f32)
+            const f32x2_t d = __builtin_elementwise_fma(f32x2_t{ev[e2], ev[e2 + 1]}, f32x2_t{fv[e2], fv[e2 + 1]}, f32x2_t{1.f, 1.f});
+            tv[e2] = __builtin_amdgcn_rcpf(d.x);
+            tv[e2 + 1] = __builtin_amdgcn_rcpf(d.y);
+          }
         } else {
   #pragma unroll
           for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fmaf(-0.5f, fast_tanh(ev[e8] - fv[e8]), 0.5f);
@@ -1070,7 +1074,11 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
         float tv[4];
         if constexpr (SEP) {
   #pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = __builtin_amdgcn_rcpf(fmaf(ev[e4], fv[e4], 1.f));
+          for (int e2 = 0; e2 < 4; e2 += 2) {
+            const f32x2_t d = __builtin_elementwise_fma(f32x2_t{ev[e2], ev[e2 + 1]}, f32x2_t{fv[e2], fv[e2 + 1]}, f32x2_t{1.f, 1.f});
+            tv[e2] = __builtin_amdgcn_rcpf(d.x);
+            tv[e2 + 1] = __builtin_amdgcn_rcpf(d.y);
+          }
         } else {
   #pragma unroll
           for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fmaf(-0.5f, fast_tanh(ev[e4] - fv[e4]), 0.5f);
@@ -1124,9 +1132,15 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
         for (int dr = 0; dr < 2; ++dr) {
           if (r2 + dr >= RT) continue;
   #pragma unroll
-          for (int r = 0; r < 4; ++r) {
+          for (int r = 0; r < 4; r += 2) {  // row pairs as packed fp32
             const int row = (r2 + dr) * 16 + 4 * kg + r;
-            so[(dr * 16 + 4 * kg + r) * OS + cl] = fmaf(al, fmaf(acc[r2 + dr][r], inv, bsl[row]), as);
+            const f32x2_t v = __builtin_elementwise_fma(
+                f32x2_t{al, al},
+                __builtin_elementwise_fma(f32x2_t{acc[r2 + dr][r], acc[r2 + dr][r + 1]}, f32x2_t{inv, inv},
+                                          f32x2_t{bsl[row], bsl[row + 1]}),
+                f32x2_t{as, as});
+            so[(dr * 16 + 4 * kg + r) * OS + cl] = v.x;
+            so[(dr * 16 + 4 * kg + r + 1) * OS + cl] = v.y;
           }
         }
         // lane -> (row of the pair, 8-column half)
