@@ -105,12 +105,24 @@ __device__ __forceinline__ uint4 bldu4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 #endif
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
+// cache policy of the activation / P-Q stores (GC kernels) and of the
+// adjacency plane stores (buffer aux bits: 1 sc0, 2 nt, 16 sc1).  GC
+// outputs go write-through (sc1): the next launch reads them from other
+// XCDs anyway, and no dirty L2 lines are left for the kernel boundary to
+// write back (forward 2% faster; sc1 on the adjacency planes measured 3%
+// slower, nt 30% slower -- scripts/ab_kernels.py)
+#ifndef DSTD_GC_ST_AUX
+#define DSTD_GC_ST_AUX 16
+#endif
+#ifndef DSTD_ADJ_ST_AUX
+#define DSTD_ADJ_ST_AUX 0
+#endif
 __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
 #ifdef DSTD_ABL_STORE
   if (v.x == 12345.f) off = 0;  // keep the value alive; store only lanes with nothing to store
   else off = OOB;
 #endif
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, DSTD_GC_ST_AUX);
 }
 
 // folded BN vectors [V][64] -> LDS [c/4][v]
@@ -537,7 +549,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
           typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
           typedef float f32x3 __attribute__((ext_vector_type(3)));
           const f32x3 o3 = {o[0], o[1], o[2]};
-          __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(u32x3, o3), ry, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(u32x3, o3), ry, off, 0, DSTD_GC_ST_AUX);
         }
       }
     }
@@ -818,7 +830,7 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
           typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
           typedef float f32x3 __attribute__((ext_vector_type(3)));
           const f32x3 o3 = {o[0], o[1], o[2]};
-          __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(u32x3, o3), ry, uoff[ut], 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(u32x3, o3), ry, uoff[ut], 0, DSTD_GC_ST_AUX);
         }
       }
     }
@@ -1150,8 +1162,8 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
         split8(v0, v1, hi, lo);
         // rows / columns past the plane: out-of-range offset, the store is dropped
         const uint32_t off = row < NROW && c8 < NCOL ? 2u * (uint32_t)(row * (2 * NCOL) + c8) : OOB;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), ro, off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), ro, off + 2u * NCOL, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), ro, off, 0, DSTD_ADJ_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), ro, off + 2u * NCOL, 0, DSTD_ADJ_ST_AUX);
       }
     }
   };

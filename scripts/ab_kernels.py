@@ -9,6 +9,7 @@ import argparse
 import ctypes
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -59,10 +60,18 @@ def main():
                 prof.close()
                 for k, v in per.items():
                     res[p].setdefault(k, []).append(v)
+                # wall clock of unbracketed forwards (kernel-boundary costs included)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(5 * a.steps):
+                    model._forward_native(x, y)
+                torch.cuda.synchronize()
+                res[p].setdefault("wall", []).append((time.perf_counter() - t0) * 1e3 / (5 * a.steps))
     for p in a.libs:
-        tot = sum(np.median(v) for v in res[p].values())
-        print(os.path.basename(p), f"total {tot:.4f} ms/step",
-              {k: round(float(np.median(v)), 4) for k, v in res[p].items()})
+        tot = sum(np.median(v) for k, v in res[p].items() if k != "wall")
+        print(os.path.basename(p), f"wall {np.median(res[p]['wall']):.4f} (min {min(res[p]['wall']):.4f}) "
+              f"kernels {tot:.4f} ms/step",
+              {k: round(float(np.median(v)), 4) for k, v in res[p].items() if k != "wall"})
 
 
 if __name__ == "__main__":
