@@ -221,6 +221,29 @@ def cpu_baseline(opts, sd, x_cpu, min_s, max_s):
                       f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
 
 
+def variant_throughput(config, B, device, steps, warmup):
+    """Side measurement at N=1 (not `value`): the same eval forward on another
+    shape of the H36M model -- BASELINE.json's metric names "22J x 50T" while
+    the shipped yaml (dstdgcn_h36m.yaml:137-138) runs 10 + 25 frames; the
+    '50 in / 25 out' T=75 variant is timed here so both are on the line."""
+    model, opts, _ = load_model(config, device)
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    V = opts["joints_to_consider"]
+    x = synth_input(B, T, V, opts["input_time_frame"], 1234).to(device)
+    y = torch.empty_like(x)
+    with torch.no_grad():
+        for _ in range(max(warmup, 2)):
+            model._forward_native(x, y)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            model._forward_native(x, y)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    return {"workload": CONFIGS[config][1] + f", B={B}, eval forward", "seq_len": T,
+            "value": round(B * steps / el, 2), "unit": "seq/s", "ms_per_step": round(el / steps * 1e3, 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -230,6 +253,8 @@ def main():
     ap.add_argument("--config", default="h36m", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variant", action="store_true",
+                    help="skip the side measurement of the '50 in / 25 out' (T=75) H36M variant at N=1")
     ap.add_argument("--probe-every", type=int, default=5,
                     help="bracket the dominant launch with HIP events in one of every P timed steps "
                          "(an event pair costs ~5%% of a step)")
@@ -349,6 +374,8 @@ def main():
                          "whole_forward_tflops": round(total_flop_per_seq * B * args.steps / elapsed / 1e12, 3)},
             "kernel_ms_per_step": {native.KIND_NAMES[k]: round(v / args.steps, 4) for k, v in sorted(per_kind.items())},
         }
+        if world == 1 and args.config == "h36m" and not args.no_variant:
+            out["variant_t75"] = variant_throughput("h36m75", B, device, args.steps, args.warmup)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(opts, sd, x_cpu, args.cpu_seconds, 30.0)
         else:

@@ -288,6 +288,8 @@ class DSTDGC(nn.Module):
         x = x.contiguous()
         native.require_device(x, "x")
         dev = x.device
+        if B == 0:  # empty batch: empty output, as the reference's torch ops give
+            return _mark(x.new_empty(0, self.out_channels, T, V), x)
         A = A.reshape(A.shape[-2], A.shape[-1]).contiguous()
         if not torch.is_tensor(alpha_m):
             alpha_m = torch.full((1,), float(alpha_m), dtype=torch.float32, device=dev)
@@ -351,6 +353,8 @@ class DSTDGCB(nn.Module):
         B, cin, T, V = x.shape
         x = x.contiguous()
         native.require_device(x, "x")
+        if B == 0 and not self.training:  # empty batch: empty output (reference torch semantics)
+            return _mark(x.new_empty(0, self.out_channels, T, V), x, *self.parameters())
         if self.training:
             return _BlockTrain.apply(self, x, *self.parameters())
         dev = x.device
@@ -594,6 +598,8 @@ class DSTDGCN(nn.Module):
         L = native.lib()
         x = x.contiguous()
         native.require_device(x, "x")
+        if n == 0 and not self.training:  # empty batch: empty output (reference torch semantics)
+            return _mark(torch.empty_like(x), x, *self.parameters())
         if self.training:
             return _ModelTrain.apply(self, x, *self.parameters())
         y = torch.empty_like(x)

@@ -136,6 +136,21 @@ def test_ragged_batches(B, precision):
     assert rel_err(y[:k].numpy(), y64) <= max(1e-4, 4 * float(d["ref32_err"]))
 
 
+def test_empty_batch():
+    """B = 0 (edge case of the reference's torch ops): an empty output of the
+    right shape from the model, a block and an op, no kernel launched."""
+    m, d, sd, opts = load_model("h36m")
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    with torch.no_grad():
+        y = m(torch.empty(0, T, 22, 3, device=DEV))
+        assert y.shape == (0, T, 22, 3) and y.device.type == "cuda"
+        blk = DSTDGCB(64, 3, T, 22, "h36m").to(DEV).eval()
+        assert blk(torch.empty(0, 64, T, 22, device=DEV)).shape == (0, 3, T, 22)
+        op = DSTDGC(64, 64, T, 22, mode="spatial").to(DEV)
+        A = torch.rand(1, 22, 22, device=DEV)
+        assert op(torch.empty(0, 64, T, 22, device=DEV), A, 1.0).shape == (0, 64, T, 22)
+
+
 def test_split_vs_fp32_bench_batch():
     """The bench workload (H36M B=256) under both arithmetics: each against
     the fp64 oracle on a sample subset, and against each other on the whole
