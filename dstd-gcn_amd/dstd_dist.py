@@ -103,6 +103,13 @@ def allreduce_grads(params, group=None):
     grads = [p.grad for p in params if p.grad is not None]
     if world == 1 or not grads:
         return
+    base = grads[0]._base
+    if base is not None and base.dim() == 1 and all(g._base is base for g in grads):
+        # the gradients are slices of one arena (dstd_native.grad_sink): reduce
+        # it in place, padding gaps included (zeros on every rank)
+        dist.all_reduce(base, op=dist.ReduceOp.SUM, group=group)
+        base.div_(world)
+        return
     flat = torch.cat([g.reshape(-1) for g in grads])
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     flat.div_(world)

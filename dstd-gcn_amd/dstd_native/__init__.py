@@ -305,6 +305,41 @@ class GradArena:
         return out
 
 
+def grad_sink(owner, params, device):
+    """Where a native backward writes the parameters' gradients.
+
+    Returns (arena, direct).  direct=True: the parameters' ``.grad`` ARE
+    slices of ``owner``'s persistent arena and the backward kernels, which
+    always accumulate (+=), add into them in place -- the caller returns None
+    to autograd for the parameters.  That is torch's accumulate semantics
+    without a per-parameter clone / add kernel per backward (a training step
+    with the inverse pass runs two backwards into the same gradients:
+    engine/prediction.py:267-287).  It holds when every trainable parameter's
+    ``.grad`` is None (the arena is zeroed and the views installed) or is
+    still the view installed earlier.  Otherwise (gradients set by someone
+    else) a fresh zeroed arena is returned with direct=False and the caller
+    hands its views to autograd as before."""
+    params = params if isinstance(params, list) else list(params)
+    dev = torch.device(device)
+    arena = getattr(owner, "_dstd_grad_arena", None)
+    if (arena is None or len(arena.params) != len(params) or arena.buf.device != dev
+            or any(a is not b for a, b in zip(arena.params, params))):
+        arena = GradArena(params, device)
+        # (parameter, its slice) for every trainable parameter, built once
+        arena.pairs = [(q, v) for q, v in zip(arena.params, arena.views()) if v is not None]
+        owner._dstd_grad_arena = arena
+    pairs = arena.pairs
+    grads = [q.grad for q, _ in pairs]
+    if all(g is None for g in grads):
+        arena.buf.zero_()
+        for q, v in pairs:
+            q.grad = v
+        return arena, True
+    if all(g is v for g, (_, v) in zip(grads, pairs)):
+        return arena, True
+    return GradArena(params, device), False
+
+
 def gc_grads(dstdgc, arena):
     g = GCGrads()
     for f, conv in (("f", dstdgc.conv_f), ("m1", dstdgc.conv_m1), ("m2", dstdgc.conv_m2), ("rm", dstdgc.conv_rm)):

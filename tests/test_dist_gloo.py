@@ -169,3 +169,31 @@ def test_allreduce_grads_averages_one_bucket():
         for m, a in zip(mean, avg):
             assert torch.allclose(m, a)
     assert not torch.allclose(res[0][0][0], res[1][0][0])
+
+
+def _allreduce_arena_body(rank, world):
+    import dstd_native as N
+    torch.manual_seed(7)
+    lin = torch.nn.Linear(4, 3)
+    holder = torch.nn.Module()
+    arena, direct = N.grad_sink(holder, list(lin.parameters()), "cpu")  # installs the arena views
+    x = torch.full((5, 4), float(rank + 1))
+    with torch.no_grad():  # what a native backward does: += into the views
+        lin.weight.grad += torch.ones(3, 5) @ x
+        lin.bias.grad += torch.ones(3) * 5
+    local = [p.grad.clone() for p in lin.parameters()]
+    D.allreduce_grads(list(lin.parameters()))
+    same_base = all(p.grad._base is arena.buf for p in lin.parameters())
+    return direct, local, [p.grad.clone() for p in lin.parameters()], same_base
+
+
+def test_allreduce_grads_reduces_the_arena_in_place():
+    """Gradients that are slices of one arena (dstd_native.grad_sink) are
+    averaged by one all-reduce of the arena itself and stay views of it."""
+    res = run_world("_allreduce_arena_body")
+    mean = [(a + b) / 2 for a, b in zip(res[0][1], res[1][1])]
+    for r in (0, 1):
+        direct, local, avg, same_base = res[r]
+        assert direct and same_base
+        for m, a in zip(mean, avg):
+            assert torch.allclose(m, a)

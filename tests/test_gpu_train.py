@@ -213,6 +213,45 @@ def test_model_step_gradients_vs_reference_fp64():
     assert named["conv_st_in.stgcn.0.0.A_s"].grad is None
 
 
+def test_gradient_sink_paths_agree():
+    """The model backward accumulates into the parameters' .grad in place
+    (dstd_native.grad_sink) when they are its own arena views, and hands
+    fresh views to autograd otherwise: both give the same gradients, a second
+    backward without zero_grad accumulates (torch semantics), and the
+    gradients of a step with the inverse pass are slices of one buffer."""
+    from engine import mpjpe_error_3d
+    m, d = _model_3dpw()
+    inp, inv, seq = (torch.from_numpy(d[f"train/{n}0"]).to(DEV) for n in ("inp", "inv", "seq"))
+    B, T, VC = inp.shape
+
+    def step():
+        out = m(inp.view(B, T, 23, 3)).view(B, T, VC)
+        out_i = m(inv.view(B, T, 23, 3)).view(B, T, VC)
+        ((mpjpe_error_3d(out, seq) + mpjpe_error_3d(out_i, seq.flip(1))) / 2).backward()
+
+    # the paths differ only in summation order (arena += vs autograd's sum of
+    # two arenas): 1e-4 of a tensor's max covers the global-sum scalars
+    # (alphas, PReLU slopes, ~1e-5 measured), far inside their fp32 noise
+    TOL = 1e-4
+    params = [p for p in m.parameters() if p.requires_grad]
+    step()  # direct: .grad were None
+    g_direct = [p.grad.clone() for p in params]
+    bases = {p.grad._base.data_ptr() for p in params}
+    assert len(bases) == 1 and all(p.grad._base is not None for p in params)
+    step()  # no zero_grad: accumulates into the same views
+    for p, g in zip(params, g_direct):
+        assert float((p.grad - 2 * g).abs().max()) <= TOL * float(g.abs().max()) + 1e-12
+    for p in params:  # user-owned gradients: the autograd path
+        p.grad = torch.zeros_like(p)
+    step()
+    for p, g in zip(params, g_direct):
+        assert p.grad._base is None
+        assert float((p.grad - g).abs().max()) <= TOL * float(g.abs().max()) + 1e-12
+    m.zero_grad(set_to_none=True)
+    step()  # back to the in-place arena
+    assert all(p.grad._base is not None for p in params)
+
+
 def test_training_curve_matches_reference():
     """PredictionEngine.train, 5 one-batch epochs on the engine.npz 3DPW run."""
     from engine import PredictionEngine

@@ -1,0 +1,36 @@
+"""Host-side logic of the model drop-in (no GPU): the cached walk of the
+module tree that replaces ``parameters()`` / ``buffers()`` on the hot path
+(model/dstdgcn.py:_TensorTree) must always equal torch's own walk."""
+import copy
+
+import torch
+
+from model import get_model
+
+OPTS = dict(input_channels=6, input_time_frame=10, output_time_frame=25, st_gcnn_dropout=0.0,
+            joints_to_consider=22, num_feature=64, num_layers=7, layout="h36m")
+
+
+def same(m):
+    p, b = m._tree.get(m)
+    tp, tb = list(m.parameters()), list(m.buffers())
+    return len(p) == len(tp) and len(b) == len(tb) and all(x is y for x, y in zip(p, tp)) and all(
+        x is y for x, y in zip(b, tb))
+
+
+def test_tensor_tree_matches_torch_walk_and_invalidates():
+    m = get_model("dstdgcn", dstdgcn=OPTS)
+    assert same(m) and same(m)  # built, then reused
+    m.prelu.weight = torch.nn.Parameter(torch.ones(1))  # replaced parameter
+    assert same(m)
+    m.bn_in.bn.running_mean = torch.zeros_like(m.bn_in.bn.running_mean)  # replaced buffer
+    assert same(m)
+    m.encoders[0] = copy.deepcopy(m.encoders[0])  # replaced submodule
+    assert same(m)
+    m.encoders[1].register_parameter("extra", torch.nn.Parameter(torch.ones(2)))  # added parameter
+    assert same(m)
+    m.encoders[2].add_module("extra", torch.nn.Linear(2, 2))  # added submodule
+    assert same(m)
+    m2 = copy.deepcopy(m)
+    assert same(m2)
+    assert not any(x is y for x, y in zip(m2._tree.get(m2)[0], m.parameters()))
