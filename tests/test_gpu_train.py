@@ -252,6 +252,30 @@ def test_gradient_sink_paths_agree():
     assert all(p.grad._base is not None for p in params)
 
 
+def test_autocast_bf16_runs_the_fp32_path():
+    """Config 5 names a bf16 training loop: under torch.autocast(bf16) the
+    native model computes in fp32 (arithmetic >= bf16; autocast does not
+    retype custom autograd Functions), so loss and gradients equal the plain
+    fp32 step bit for bit."""
+    from engine import mpjpe_error_3d
+    m, d = _model_3dpw()
+    inp, seq = (torch.from_numpy(d[f"train/{n}0"]).to(DEV) for n in ("inp", "seq"))
+    B, T, VC = inp.shape
+    res = []
+    for ac in (False, True):
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in group(d, "train/sd0/").items()})
+        _realias(m)
+        m.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=ac):
+            out = m(inp.view(B, T, 23, 3)).view(B, T, VC)
+            loss = mpjpe_error_3d(out, seq)
+        assert out.dtype == torch.float32
+        loss.backward()
+        res.append((float(loss), [p.grad.clone() for p in m.parameters() if p.requires_grad]))
+    assert res[0][0] == res[1][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
+
+
 def test_training_curve_matches_reference():
     """PredictionEngine.train, 5 one-batch epochs on the engine.npz 3DPW run."""
     from engine import PredictionEngine
