@@ -215,10 +215,38 @@ def cpu_baseline(opts, sd, x_cpu, min_s, max_s):
             el = time.perf_counter() - t0
             if el >= min_s or el >= max_s:
                 break
-    return {"value": n * x_cpu.shape[0] / el, "unit": "seq/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n} x B={x_cpu.shape[0]} forwards of the fp32 CPU oracle (oracle/dstdgcn_oracle.py, "
-                      f"op-for-op restatement of model/dstdgcn.py:293-317), {el:.1f} s, "
-                      f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads"}
+    out = {"value": n * x_cpu.shape[0] / el, "unit": "seq/s", "cores": torch.get_num_threads(), "kind": "port",
+           "sample": f"{n} x B={x_cpu.shape[0]} forwards of the fp32 CPU oracle (oracle/dstdgcn_oracle.py, "
+                     f"op-for-op restatement of model/dstdgcn.py:293-317), {el:.1f} s, "
+                     f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads",
+           "nproc": os.cpu_count(), "cpu_model": cpu_model()}
+    # SURVEY §8(d) also asks for one thread: a B=16 slice of the same batch, ~3 s
+    torch.set_num_threads(1)
+    xs = x_cpu[:16]
+    with torch.no_grad():
+        O.dstdgcn(xs, sd32, opts["num_layers"], dtype=torch.float32)
+        n1, t0 = 0, time.perf_counter()
+        while True:
+            O.dstdgcn(xs, sd32, opts["num_layers"], dtype=torch.float32)
+            n1 += 1
+            el1 = time.perf_counter() - t0
+            if el1 >= min(3.0, min_s):
+                break
+    torch.set_num_threads(threads)
+    out["single_thread"] = {"value": n1 * xs.shape[0] / el1, "unit": "seq/s", "cores": 1,
+                            "sample": f"{n1} x B={xs.shape[0]} forwards, {el1:.1f} s"}
+    return out
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def variant_throughput(config, B, device, steps, warmup):
