@@ -1155,8 +1155,11 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
             so[(dr * 16 + 4 * kg + r + 1) * OS + cl] = v.y;
           }
         }
-        // lane -> (row of the pair, 8-column half)
-        const int rl = lane >> 1, h = lane & 1, row = r2 * 16 + rl, c8 = ct * 16 + 8 * h;
+        // lane -> (row of the pair, 8-column half); rows on consecutive lanes
+        // (lane & 31), halves on the wave halves: with OS = 20 every 16-lane
+        // group of the ds_read_b128 hits 16 distinct 4-bank chunks (the
+        // (lane >> 1, lane & 1) map was 2-way conflicted; -0.6% per launch)
+        const int rl = lane & 31, h = lane >> 5, row = r2 * 16 + rl, c8 = ct * 16 + 8 * h;
         const float4 v0 = ld4(so + rl * OS + 8 * h), v1 = ld4(so + rl * OS + 8 * h + 4);
         uint4 hi, lo;
         split8(v0, v1, hi, lo);
