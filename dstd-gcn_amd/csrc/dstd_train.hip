@@ -76,8 +76,10 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
     const float* Ab = g.A + b1 * g.a_b1 + b2 * g.a_b2;
     const float* Bb = g.B + b1 * g.b_b1 + b2 * g.b_b2;
     const int k_end = min(g.K, (kc + 1) * kc_len);
-    for (int k0 = kc * kc_len; k0 < k_end; k0 += KT) {
-      float ra[EA], rb[EB];
+    // register-staged k-tiles: the next tile's global loads are issued before
+    // the current tile's MFMAs, so their latency hides behind the compute
+    float ra[EA], rb[EB];
+    auto gload = [&](int k0) {
 #pragma unroll
       for (int e = 0; e < EA; ++e) {
         const int idx = tid + 256 * e;
@@ -95,7 +97,11 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
         rb[e] = (gn < g.N && gk < k_end) ? ((g.b_ones_last && gn == g.N - 1) ? 1.f : Bb[gk * g.b_k + gn * g.b_n])
                                          : 0.f;
       }
-      __syncthreads();
+    };
+    int k0 = kc * kc_len;
+    if (k0 < k_end) gload(k0);
+    for (; k0 < k_end; k0 += KT) {
+      __syncthreads();  // the previous tile's fragment reads are done
 #pragma unroll
       for (int e = 0; e < EA; ++e) {
         const int idx = tid + 256 * e;
@@ -111,6 +117,7 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
         Bs[k * LB + n] = rb[e];
       }
       __syncthreads();
+      if (k0 + KT < k_end) gload(k0 + KT);
 #pragma unroll
       for (int kk = 0; kk < KT / 4; ++kk) {
         const int kr = kk * 4 + (lane >> 4);
