@@ -658,7 +658,7 @@ hipError_t to_layout(const float* src, float* dst, int B, int C, int TV, int to_
 
 extern "C" {
 
-const char* dstd_version(void) { return "dstd-gcn-mi355x 0.1 (gfx950, fp32 MFMA 16x16x4)"; }
+const char* dstd_version(void) { return "dstd-gcn-mi355x 0.2 (gfx950; forward: split-f16 MFMA 16x16x32, fp32 storage / accumulate; training: fp32 MFMA 16x16x4)"; }
 
 const char* dstd_error_string(int code) {
   switch (code) {
