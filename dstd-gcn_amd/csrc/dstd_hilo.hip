@@ -41,7 +41,10 @@ namespace dstd {
 
 namespace {
 
-constexpr int HW = 4;        // waves per workgroup
+#ifndef DSTD_HW
+#define DSTD_HW 8  // one 8-wave workgroup per CU at two waves per SIMD: one copy of the weight images per CU (A/B: -2.3% per forward vs 4 waves)
+#endif
+constexpr int HW = DSTD_HW;  // waves per workgroup
 constexpr int HT = HW * 64;  // threads per workgroup
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
