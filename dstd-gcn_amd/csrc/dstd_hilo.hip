@@ -41,11 +41,6 @@ namespace dstd {
 
 namespace {
 
-#ifndef DSTD_HW
-#define DSTD_HW 8  // one 8-wave workgroup per CU at two waves per SIMD: one copy of the weight images per CU (A/B: -2.3% per forward vs 4 waves)
-#endif
-constexpr int HW = DSTD_HW;  // waves per workgroup
-constexpr int HT = HW * 64;  // threads per workgroup
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
@@ -78,8 +73,9 @@ __device__ __forceinline__ int opaque_zero() {
 
 __device__ __forceinline__ int unit_range(int nunits, int& uend) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int gw = blockIdx.x * HW + wave;
-  const long nw = (long)gridDim.x * HW;
+  const int hw = blockDim.x >> 6;  // waves per workgroup (per kernel: spatial_nt / temporal_nt)
+  const int gw = blockIdx.x * hw + wave;
+  const long nw = (long)gridDim.x * hw;
   uend = (int)(((long)(gw + 1) * nunits) / nw);
   return (int)(((long)gw * nunits) / nw);
 }
@@ -126,14 +122,6 @@ __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, flo
   else off = OOB;
 #endif
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, DSTD_GC_ST_AUX);
-}
-
-// folded BN vectors [V][64] -> LDS [c/4][v]
-__device__ __forceinline__ void stage_bn64(float4* dst, const float* src, int V, int tid) {
-  for (int i = tid; i < V * 16; i += HT) {
-    const int v = i >> 4, c4 = i & 15;
-    dst[c4 * V + v] = ld4(src + v * 64 + 4 * c4);
-  }
 }
 
 }  // namespace
@@ -241,6 +229,10 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
 #ifndef DSTD_HL_WPE
 #define DSTD_HL_WPE 2
 #endif
+// threads per workgroup: one workgroup of 4 x (waves per SIMD) waves per CU,
+// so a CU stages one copy of the weight images (A/B against two 4-wave
+// workgroups: forward -2.3%); at most 8 waves
+constexpr int spatial_nt() { return 64 * (4 * DSTD_HL_WPE < 8 ? 4 * DSTD_HL_WPE : 8); }
 
 // 8 consecutive channels k0 .. k0+7 of row `row` of a unit (C channels per
 // row, zero past C; C % 8 == 0 or C == 6 / 3)
@@ -283,7 +275,7 @@ __device__ __forceinline__ void load_x6row(__amdgpu_buffer_rsrc_t rf, __amdgpu_b
 // folded BN vectors [V][C] -> LDS [c/4][v] for NCT*4 channel quads (zero past C)
 template <int C, int NCT>
 __device__ __forceinline__ void stage_bnC(float4* dst, const float* src, int V, int tid) {
-  for (int i = tid; i < V * 4 * NCT; i += HT) {
+  for (int i = tid; i < V * 4 * NCT; i += (int)blockDim.x) {
     const int v = i / (4 * NCT), c4 = i % (4 * NCT);
     float e[4];
 #pragma unroll
@@ -293,7 +285,7 @@ __device__ __forceinline__ void stage_bnC(float4* dst, const float* src, int V, 
 }
 
 template <int V, int CIN, int COUT>
-__global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE, DSTD_HL_WPE))) void k_spatial_hl(
+__global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE, DSTD_HL_WPE))) void k_spatial_hl(
     SpatialHLArgs a) {
   using SM = SlotMap<V, true>;
   constexpr bool RES = CIN != COUT;
@@ -313,15 +305,16 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE,
   const int tid = threadIdx.x, lane = tid & 63;
   const int kl = lane >> 4, cl = lane & 15;
   const int T = a.T;
-  for (int i = tid; i < (RES ? 3 : 2) * WIMG; i += HT) wl[i / WIMG][i % WIMG] = a.wimg[i / WIMG][i % WIMG];
-  for (int i = tid; i < PIMG; i += HT) pql[i] = a.pqimg[i];
+  constexpr int NT = spatial_nt();
+  for (int i = tid; i < (RES ? 3 : 2) * WIMG; i += NT) wl[i / WIMG][i % WIMG] = a.wimg[i / WIMG][i % WIMG];
+  for (int i = tid; i < PIMG; i += NT) pql[i] = a.pqimg[i];
   stage_bnC<COUT, NCT>(bnl[0], a.bn_s, V, tid);
   stage_bnC<COUT, NCT>(bnl[1], a.bn_h, V, tid);
   if constexpr (RES) {
     stage_bnC<COUT, NCT>(bnl[2], a.rbn_s, V, tid);
     stage_bnC<COUT, NCT>(bnl[3], a.rbn_h, V, tid);
   }
-  for (int i = tid; i < (RES ? 3 : 2) * 16 * NCT; i += HT) {
+  for (int i = tid; i < (RES ? 3 : 2) * 16 * NCT; i += NT) {
     const int g = i / (16 * NCT), c = i % (16 * NCT);
     bfl[g][c] = c < COUT ? a.bf[g][c] : 0.f;
   }
@@ -606,6 +599,12 @@ constexpr int temporal_hl_wpe() {
 #endif
   return (T <= 48 ? 2 : 1) * (C == 3 ? 2 : 1);
 }
+// one workgroup per CU at the kernel's waves per SIMD (4 waves at one per
+// SIMD: an 8-wave workgroup would force two per SIMD and spill), at most 8
+template <int T, int C>
+constexpr int temporal_nt() {
+  return 64 * (4 * temporal_hl_wpe<T, C>() < 8 ? 4 * temporal_hl_wpe<T, C>() : 8);
+}
 
 // 8 channels k0 .. k0+7 of the row at byte offset `row_off` (C per row; zero
 // past C, and an out-of-range row_off reads zeros)
@@ -628,7 +627,7 @@ __device__ __forceinline__ void load_row8_at(__amdgpu_buffer_rsrc_t r, uint32_t 
 }
 
 template <int T, int EPI, int C>
-__global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_wpe<T, C>(), temporal_hl_wpe<T, C>()))) void k_temporal_hl(
+__global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_per_eu(temporal_hl_wpe<T, C>(), temporal_hl_wpe<T, C>()))) void k_temporal_hl(
     TemporalHLArgs a) {
   using SM = SlotMap<T, false>;
   constexpr int SL = SM::SL, MT = SM::MT, NS = SM::NS, NUT = cdiv(T, 16);
@@ -649,9 +648,10 @@ __global__ __launch_bounds__(HT) __attribute__((amdgpu_waves_per_eu(temporal_hl_
   const int kl = lane >> 4, cl = lane & 15;
   const int V = a.V;
   const bool has_pq = a.pq != nullptr;
-  for (int i = tid; i < WIMG; i += HT) wl[i] = a.wimg[i];
+  constexpr int NT = temporal_nt<T, C>();
+  for (int i = tid; i < WIMG; i += NT) wl[i] = a.wimg[i];
   if (has_pq)
-    for (int i = tid; i < PIMG; i += HT) pql[i] = a.pqimg[i];
+    for (int i = tid; i < PIMG; i += NT) pql[i] = a.pqimg[i];
   if constexpr (use_bn) {
     stage_bnC<C, NCT>(bnl[0], a.bn_s, V, tid);
     stage_bnC<C, NCT>(bnl[1], a.bn_h, V, tid);
@@ -1202,19 +1202,19 @@ int hl_num_cus() {
 }
 
 template <typename K>
-int hl_occupancy(K k) {
+int hl_occupancy(K k, int nt) {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k, HT, 0) != hipSuccess || nb < 1) nb = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k, nt, 0) != hipSuccess || nb < 1) nb = 1;
   (void)hipGetLastError();
   return nb;
 }
 
-template <auto K, typename A>
+template <auto K, int NT, typename A>
 hipError_t launch_units(int units, const A& a, hipStream_t s) {
-  static const int occ = hl_occupancy(K);  // one per kernel instantiation
+  static const int occ = hl_occupancy(K, NT);  // one per kernel instantiation
   int grid = hl_num_cus() * occ;
-  grid = min(grid, cdiv(units, HW));
-  hipLaunchKernelGGL(K, dim3(grid), dim3(HT), 0, s, a);
+  grid = min(grid, cdiv(units, NT / 64));
+  hipLaunchKernelGGL(K, dim3(grid), dim3(NT), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1223,16 +1223,16 @@ hipError_t temporal_hl_t(const TemporalHLArgs& a, hipStream_t s) {
   if (a.C == 3) {
     if (a.pq) return hipErrorNotSupported;
     switch (a.epi) {
-      case TEPI_OUT: return launch_units<k_temporal_hl<T, TEPI_OUT, 3>>(a.B * a.V, a, s);
-      case TEPI_RAW: return launch_units<k_temporal_hl<T, TEPI_RAW, 3>>(a.B * a.V, a, s);
+      case TEPI_OUT: return launch_units<k_temporal_hl<T, TEPI_OUT, 3>, temporal_nt<T, 3>()>(a.B * a.V, a, s);
+      case TEPI_RAW: return launch_units<k_temporal_hl<T, TEPI_RAW, 3>, temporal_nt<T, 3>()>(a.B * a.V, a, s);
       default: return hipErrorNotSupported;
     }
   }
   if (a.C != 64) return hipErrorNotSupported;
   switch (a.epi) {
-    case TEPI_ENC: return launch_units<k_temporal_hl<T, TEPI_ENC, 64>>(a.B * a.V, a, s);
-    case TEPI_IN: return launch_units<k_temporal_hl<T, TEPI_IN, 64>>(a.B * a.V, a, s);
-    case TEPI_RAW: return launch_units<k_temporal_hl<T, TEPI_RAW, 64>>(a.B * a.V, a, s);
+    case TEPI_ENC: return launch_units<k_temporal_hl<T, TEPI_ENC, 64>, temporal_nt<T, 64>()>(a.B * a.V, a, s);
+    case TEPI_IN: return launch_units<k_temporal_hl<T, TEPI_IN, 64>, temporal_nt<T, 64>()>(a.B * a.V, a, s);
+    case TEPI_RAW: return launch_units<k_temporal_hl<T, TEPI_RAW, 64>, temporal_nt<T, 64>()>(a.B * a.V, a, s);
     default: return hipErrorNotSupported;
   }
 }
@@ -1282,9 +1282,9 @@ bool temporal_hl_supported(int T, int V) { return hl_shape(T, V); }
 
 template <int V>
 hipError_t spatial_hl_v(const SpatialHLArgs& a, hipStream_t s) {
-  if (a.Cin == 64 && a.Cout == 64) return launch_units<k_spatial_hl<V, 64, 64>>(a.B * a.T, a, s);
-  if (a.Cin == 6 && a.Cout == 64) return launch_units<k_spatial_hl<V, 6, 64>>(a.B * a.T, a, s);
-  if (a.Cin == 64 && a.Cout == 3) return launch_units<k_spatial_hl<V, 64, 3>>(a.B * a.T, a, s);
+  if (a.Cin == 64 && a.Cout == 64) return launch_units<k_spatial_hl<V, 64, 64>, spatial_nt()>(a.B * a.T, a, s);
+  if (a.Cin == 6 && a.Cout == 64) return launch_units<k_spatial_hl<V, 6, 64>, spatial_nt()>(a.B * a.T, a, s);
+  if (a.Cin == 64 && a.Cout == 3) return launch_units<k_spatial_hl<V, 64, 3>, spatial_nt()>(a.B * a.T, a, s);
   return hipErrorNotSupported;
 }
 
