@@ -7,24 +7,34 @@ already resident in HBM.  Weights are the committed H36M fixture state dict
 (tests/golden/model_h36m.npz: random init, dynamic terms randomised, BN
 calibrated), so activations stay finite; values do not change the work.
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W] [--global-batch G]
   N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-         (weak scaling: every rank runs its own B=256 shard, no data-path
-          collective; the per-rank elapsed time is MAX-reduced over RCCL)
+         weak scaling (default): every rank runs its own B=256 shard;
+         --global-batch G: strong scaling, G sequences split over the ranks
+         (SURVEY §8(d) config 4: 2048).  No data-path collective either way;
+         the per-rank elapsed time is MAX-reduced over RCCL.
+
+Timing: barrier + synchronize, t0, exactly K steps, synchronize, t1, barrier
+(the barriers bracket the region but are not inside it).
 
 One JSON line on rank 0.  Besides the driver's fields it carries
   roofline     : the dominant kernel family (largest summed time per step in
-                 an untimed profiled pass), its launch in DSTDGCB 1 (the first
-                 encoder, a 64->64 split-f16 launch) bracketed by two HIP events
-                 in one of every --probe-every timed steps; achieved = that launch's algorithmic HBM
-                 bytes (each input read once, each output written once, in the
-                 layouts of DESIGN.md §3; block_bytes below) / its average
-                 duration, against the 8 TB/s HBM3E peak.  The split-f16
-                 kernels are not MFMA-bound, so HBM is the
-                 roofline.  traffic = measured HBM bytes per launch of that
-                 kernel from profiles/pmc_traffic.json (rocprofv3 PMC passes).
+                 an untimed profiled pass) and its launch in DSTDGCB 1 (the
+                 first encoder, a 64->64 split-f16 launch), bracketed by two
+                 HIP events on the launch stream in one of every --probe-every
+                 timed steps.  achieved = the launch's COMPULSORY bytes (SURVEY
+                 §8(d): one 64->64 DSTDGC reads its input and writes its output
+                 once, 394,240 B per H36M sequence, x B sequences) / its average
+                 duration, against the 8 TB/s HBM3E peak.  layout_bytes: what the
+                 launch moves by design in this build's stored layouts (the
+                 adjacency planes and P/Q it reads on top).  traffic: measured HBM
+                 bytes per launch of that kernel (profiles/pmc_traffic.json,
+                 rocprofv3 PMC passes).  whole_forward: compulsory bytes of the
+                 whole forward (2.393 MB per H36M sequence, each block's input
+                 read and output written once) and FLOPs over the step time.
   cpu_baseline : the CPU oracle (op-for-op restatement of the reference
-                 forward, torch fp32) timed on this host's cores, N=1 only.
+                 forward, torch fp32) timed on this host's cores, N=1 only; the
+                 thread-count sweep is on the line, the best count is `value`.
 """
 import argparse
 import ctypes
@@ -127,6 +137,21 @@ def block_bytes(cin, cout, T, V, tail, split):
             native.KIND_TEMPORAL: temporal}
 
 
+def op_compulsory_bytes(cin, cout, T, V):
+    """one DSTDGC reads its input and writes its output once
+    (fp32; weights excluded)."""
+    return T * V * (cin + cout) * 4
+
+
+def model_compulsory_bytes(opts):
+    """per sequence, every DSTDGCB reads its input activation and
+    writes its output once (fp32): 2.393 MB for H36M T=35 V=22."""
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    V, C, L = opts["joints_to_consider"], opts["num_feature"], opts["num_layers"]
+    cin0, cout_last = opts["input_channels"], opts["input_channels"] // 2
+    return sum(T * V * (a + b) * 4 for a, b in [(cin0, C)] + [(C, C)] * L + [(C, cout_last)])
+
+
 def model_block_bytes(opts, split_on):
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V, C, L = opts["joints_to_consider"], opts["num_feature"], opts["num_layers"]
@@ -202,40 +227,42 @@ def split_instance(kind, T, V):
 
 
 def cpu_baseline(opts, sd, x_cpu, min_s, max_s):
+    """The fp32 CPU oracle on this host, on the bench's own B=256 batch: one
+    forward per thread count (1, 16, 32, 64), then the best count timed for
+    ~min_s seconds (`value`).  os.cpu_count() threads (256 on the MI355X box)
+    is left out of the default run: it measured 0.8 seq/s (80 s per B=64
+    forward; torch's intra-op pool on these small ops, profiles/r02_bench.json)."""
     from oracle import dstdgcn_oracle as O  # baseline leg only
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
     sd32 = {k: torch.from_numpy(v).float() for k, v in sd.items()}
+    ncpu = os.cpu_count() or 1
+
+    def fwd(xs):
+        O.dstdgcn(xs, sd32, opts["num_layers"], dtype=torch.float32)
+
+    sweep = {}
     with torch.no_grad():
-        O.dstdgcn(x_cpu, sd32, opts["num_layers"], dtype=torch.float32)  # warm-up
+        for th in sorted({1, min(16, ncpu), min(32, ncpu), min(64, ncpu)}):
+            torch.set_num_threads(th)
+            fwd(x_cpu[:8])  # warm-up at this count
+            t0 = time.perf_counter()
+            fwd(x_cpu)
+            sweep[th] = round(x_cpu.shape[0] / (time.perf_counter() - t0), 1)
+        best = max(sweep, key=sweep.get)
+        torch.set_num_threads(best)
         n, t0 = 0, time.perf_counter()
         while True:
-            O.dstdgcn(x_cpu, sd32, opts["num_layers"], dtype=torch.float32)
+            fwd(x_cpu)
             n += 1
             el = time.perf_counter() - t0
             if el >= min_s or el >= max_s:
                 break
-    out = {"value": n * x_cpu.shape[0] / el, "unit": "seq/s", "cores": torch.get_num_threads(), "kind": "port",
-           "sample": f"{n} x B={x_cpu.shape[0]} forwards of the fp32 CPU oracle (oracle/dstdgcn_oracle.py, "
-                     f"op-for-op restatement of model/dstdgcn.py:293-317), {el:.1f} s, "
-                     f"torch {torch.__version__} CPU, {torch.get_num_threads()} threads",
-           "nproc": os.cpu_count(), "cpu_model": cpu_model()}
-    # SURVEY §8(d) also asks for one thread: a B=16 slice of the same batch, ~3 s
-    torch.set_num_threads(1)
-    xs = x_cpu[:16]
-    with torch.no_grad():
-        O.dstdgcn(xs, sd32, opts["num_layers"], dtype=torch.float32)
-        n1, t0 = 0, time.perf_counter()
-        while True:
-            O.dstdgcn(xs, sd32, opts["num_layers"], dtype=torch.float32)
-            n1 += 1
-            el1 = time.perf_counter() - t0
-            if el1 >= min(3.0, min_s):
-                break
-    torch.set_num_threads(threads)
-    out["single_thread"] = {"value": n1 * xs.shape[0] / el1, "unit": "seq/s", "cores": 1,
-                            "sample": f"{n1} x B={xs.shape[0]} forwards, {el1:.1f} s"}
-    return out
+    torch.set_num_threads(min(16, ncpu))
+    return {"value": n * x_cpu.shape[0] / el, "unit": "seq/s", "cores": best, "kind": "port",
+            "sample": f"{n} x B={x_cpu.shape[0]} forwards of the fp32 CPU oracle (oracle/dstdgcn_oracle.py, "
+                      f"op-for-op restatement of model/dstdgcn.py:293-317), {el:.1f} s, torch {torch.__version__} "
+                      f"CPU, {best} threads (the best of the sweep)",
+            "thread_sweep_seq_s": sweep, "sweep_sample": f"one B={x_cpu.shape[0]} forward per thread count",
+            "nproc": ncpu, "cpu_model": cpu_model()}
 
 
 def cpu_model():
@@ -277,7 +304,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="strong scaling: this many sequences in total, split over the ranks")
     ap.add_argument("--config", default="h36m", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -304,9 +333,11 @@ def main():
         D.broadcast_module(model, src=0)  # weights once, rank 0 -> all
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V = opts["joints_to_consider"]
-    B = args.batch
-    # one global batch of B x world sequences, contiguous shard per rank
-    x_cpu = D.shard(synth_input(B * world, T, V, opts["input_time_frame"], 1234), world, rank).contiguous()
+    strong = args.global_batch > 0
+    G = args.global_batch if strong else args.batch * world
+    # one global batch, contiguous shard per rank (dstd_dist.shard_bounds)
+    x_cpu = D.shard(synth_input(G, T, V, opts["input_time_frame"], 1234), world, rank).contiguous()
+    B = x_cpu.shape[0]
     x = x_cpu.to(device)
     y = torch.empty_like(x)
     L = native.lib()
@@ -348,8 +379,8 @@ def main():
             else:
                 model._forward_native(x, y)
         torch.cuda.synchronize()
-        barrier()
         elapsed = time.perf_counter() - t0
+        barrier()
         launches = prof.elapsed()
         prof.close()
 
@@ -361,28 +392,32 @@ def main():
         # partials (the forward itself has no exchange)
         D.reduce_partials(y.double().abs().sum().reshape(1), torch.tensor([B], device=device))
 
-    split_on = L.dstd_get_gc_precision() == 1
+    split_on = model.gc_arithmetic == "split"
     bb = model_block_bytes(opts, split_on)
     kernel_ms = sum(ms for _, _, ms in launches)
-    kernel_bytes = sum(bb[blk][dominant] for _, blk, _ in launches) * B
-    achieved = kernel_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    avg_launch_s = kernel_ms * 1e-3 / max(len(launches), 1)
+    C = opts["num_feature"]
+    # compulsory bytes of the probed launch: DSTDGCB 1 is a 64 -> 64 block; its
+    # spatial / temporal GC launch is one DSTDGC's input read + output write
+    comp = op_compulsory_bytes(C, C, T, V) * B
+    achieved = comp / avg_launch_s / 1e9 if kernel_ms > 0 else 0.0
     kname = native.KIND_NAMES[dominant]
     split_blk = split_on and opts["num_layers"] > 0
     traffic = load_traffic(kname + "_split" if split_blk else kname, split_instance(dominant, T, V) if split_blk else None)
     total_flop_per_seq = sum(sum(b.values()) for b in fl)
-    total_bytes_per_seq = sum(sum(b.values()) for b in bb)
+    whole_bytes = model_compulsory_bytes(opts) * G * args.steps / elapsed / 1e9
 
     if rank == 0:
         out = {
             "metric": METRIC,
-            "value": round(B * world * args.steps / elapsed, 2),
+            "value": round(G * args.steps / elapsed, 2),
             "unit": "seq/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "arithmetic": ("split-f16 MFMA for every contraction of the forward (fp32 operands as f16 hi/lo pairs, "
@@ -390,17 +425,26 @@ def main():
                            "epilogues)") if split_on
                           else "exact-fp32 MFMA (v_mfma_f32_16x16x4_f32)",
             "data": "synthetic (N(0,1) poses, future frames padded with the last observed; fixture weights)",
-            "config": {"workload": CONFIGS[args.config][1] + f", B={B}/GPU, eval forward", "global_batch": B * world,
-                       "seq_len": T, "joints": V, "parallelism": f"dp{world}"},
+            "config": {"workload": CONFIGS[args.config][1] + (f", {G} sequences over {world} GPU(s)" if strong else
+                                                              f", B={B}/GPU") + ", eval forward",
+                       "global_batch": G, "seq_len": T, "joints": V, "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "kernel": kname + (" (split-f16, DSTDGCB 1)" if split_blk else " (DSTDGCB 1)"),
                          "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": int(bb[1][dominant] * B) if launches else None,
+                         "compulsory_bytes_per_launch": comp,
+                         "compulsory_basis": f"SURVEY §8(d): {op_compulsory_bytes(C, C, T, V)} B/seq (one 64->64 "
+                                             f"DSTDGC: input read + output written once) x {B} seq",
+                         "layout_bytes_per_launch": int(bb[1][dominant] * B) if launches else None,
                          "launches": len(launches), "probe_every": every,
-                         "avg_launch_us": round(kernel_ms / max(len(launches), 1) * 1e3, 2),
-                         "whole_forward_gbs": round(total_bytes_per_seq * B * args.steps / elapsed / 1e9, 1),
-                         "whole_forward_tflops": round(total_flop_per_seq * B * args.steps / elapsed / 1e12, 3)},
-            "kernel_ms_per_step": {native.KIND_NAMES[k]: round(v / args.steps, 4) for k, v in sorted(per_kind.items())},
+                         "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                         "whole_forward": {"compulsory_bytes_per_seq": model_compulsory_bytes(opts),
+                                           "achieved_gbs": round(whole_bytes, 1),
+                                           "frac_hbm": round(whole_bytes / PEAK_HBM_GBS, 4),
+                                           "flop_per_seq": total_flop_per_seq,
+                                           "achieved_tflops": round(total_flop_per_seq * G * args.steps / elapsed / 1e12,
+                                                                    3)}},
+            "kernel_ms_per_step_event_bracketed": {native.KIND_NAMES[k]: round(v / args.steps, 4)
+                                                   for k, v in sorted(per_kind.items())},
         }
         if world == 1 and args.config == "h36m" and not args.no_variant:
             out["variant_t75"] = variant_throughput("h36m75", B, device, args.steps, args.warmup)

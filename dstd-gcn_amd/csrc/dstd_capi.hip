@@ -90,21 +90,9 @@ struct BlockFold {
   uint4* hl_pqt;    // next block's conv_s[*].conv_m1/m2 (P/Q written by the temporal kernel)
   uint4* hl_rms[2]; // conv_s[g].conv_rm (spatial adjacency)
   uint4* hl_rmt;    // conv_t.conv_rm (temporal adjacency)
-  float* hl_scale;  // [9]: 2^-s of ws0, ws1, pqs, wt, pqt, rms0, rms1, rmt, ws2
+  float* hl_scale;  // 9 scale slots (kHLSlot floats each, dstd_hilo.h): ws0, ws1, pqs, wt, pqt, rms0, rms1, rmt, ws2
   float* hl_rbias;  // [2T + V]: fused conv_rm biases (HLJob::bias_out) of rms0, rms1, rmt
 };
-
-// Split-f16 GC kernels (dstd_hilo.hip) where the shape has them: 1 (default),
-// or 0 for the exact-fp32 kernels everywhere (env DSTD_HILO=0 or
-// dstd_set_gc_precision).
-int g_hl_mode = -1;
-bool hl_on() {
-  if (g_hl_mode < 0) {
-    const char* e = getenv("DSTD_HILO");
-    g_hl_mode = (e && e[0] == '0') ? 0 : 1;
-  }
-  return g_hl_mode == 1;
-}
 
 // Which GC launches of a block run the split-f16 kernels.
 struct BlockHL {
@@ -135,7 +123,7 @@ void carve_fold(Carver& cv, BlockFold& f, int T, int V, int cout, bool res) {
   f.hl_rms[0] = img(hl_rm_img(T, 2 * T));
   f.hl_rms[1] = img(hl_rm_img(T, 2 * T));
   f.hl_rmt = img(hl_rm_img(V, 2 * V));
-  f.hl_scale = cv.take(12);
+  f.hl_scale = cv.take(9 * kHLSlot);
   f.hl_rbias = cv.take((size_t)2 * T + V);
 }
 
@@ -216,10 +204,11 @@ hipError_t run_hl_prep(const HLList& jobs, hipStream_t s) {
   return hipSuccess;
 }
 
-void add_hl_conv(HLList& l, const float* w, int rows, int cols, uint4* img, float* sc) {
+void add_hl_conv(HLList& l, const float* w, const float* b, int rows, int cols, uint4* img, float* sc) {
   HLJob j{};
   j.kind = HLJ_CONV;
   j.w[0] = w;
+  j.bias = b;
   j.nblk = 1;
   j.rows = rows;
   j.cols = cols;
@@ -227,10 +216,14 @@ void add_hl_conv(HLList& l, const float* w, int rows, int cols, uint4* img, floa
   j.inv_scale = sc;
   l.push_back(j);
 }
-void add_hl_rm(HLList& l, const float* w, const float* b, int rows, int cols, uint4* img, float* sc, float* bout) {
+void add_hl_rm(HLList& l, const float* w, const float* b, int rows, int cols, uint4* img, float* sc, float* bout,
+               const float* alpha, const float* astat, int nastat) {
   HLJob j{};
   j.kind = HLJ_RM;
   j.w[0] = w;
+  j.alpha = alpha;
+  j.astat = astat;
+  j.nastat = nastat;
   j.bias = b;
   j.bias_out = bout;
   j.nblk = 1;
@@ -261,9 +254,11 @@ struct BlockTail {
   const dstd_block_params* next;  // next block: its spatial P/Q are produced here
 };
 
-BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V) {
+// Split-f16 GC kernels (dstd_hilo.hip) where the shape has them, unless the
+// call asks for exact fp32 (DSTD_FWD_EXACT_FP32).
+BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V, bool exact) {
   BlockHL r{false, false};
-  if (!hl_on()) return r;
+  if (exact) return r;
   r.s = spatial_hl_supported(T, V) &&
         ((p->cin == 64 && p->cout == 64) || (p->cin == 6 && p->cout == 64) || (p->cin == 64 && p->cout == 3));
   r.t = temporal_hl_supported(T, V) &&
@@ -273,25 +268,31 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V
   return r;
 }
 
+// scale slot i of a block's weight images (BlockFold::hl_scale)
+float* hls(const BlockFold& f, int i) { return f.hl_scale + kHLSlot * i; }
+
 // Weight images of the block's split-f16 launches.
 void add_block_hl_jobs(HLList& l, const dstd_block_params* p, const BlockFold& f, const BlockTail& tail,
                        const BlockHL& hl, int T, int V) {
   if (hl.s) {
-    add_hl_rm(l, p->conv_s[0].wrm, p->conv_s[0].brm, T, 2 * T, f.hl_rms[0], f.hl_scale + 5, f.hl_rbias);
-    add_hl_rm(l, p->conv_s[1].wrm, p->conv_s[1].brm, T, 2 * T, f.hl_rms[1], f.hl_scale + 6, f.hl_rbias + T);
-    add_hl_conv(l, p->conv_s[0].wf, p->cout, p->cin, f.hl_ws[0], f.hl_scale + 0);
-    add_hl_conv(l, p->conv_s[1].wf, p->cout, p->cin, f.hl_ws[1], f.hl_scale + 1);
-    if (p->cin != p->cout) add_hl_conv(l, p->res_w, p->cout, p->cin, f.hl_ws[2], f.hl_scale + 8);
+    add_hl_rm(l, p->conv_s[0].wrm, p->conv_s[0].brm, T, 2 * T, f.hl_rms[0], hls(f, 5), f.hl_rbias, p->alpha_sm,
+              f.astat_s, V * V);
+    add_hl_rm(l, p->conv_s[1].wrm, p->conv_s[1].brm, T, 2 * T, f.hl_rms[1], hls(f, 6), f.hl_rbias + T, p->alpha_sm,
+              f.astat_s + V * V, V * V);
+    add_hl_conv(l, p->conv_s[0].wf, p->conv_s[0].bf, p->cout, p->cin, f.hl_ws[0], hls(f, 0));
+    add_hl_conv(l, p->conv_s[1].wf, p->conv_s[1].bf, p->cout, p->cin, f.hl_ws[1], hls(f, 1));
+    if (p->cin != p->cout) add_hl_conv(l, p->res_w, p->res_b, p->cout, p->cin, f.hl_ws[2], hls(f, 8));
     const float* w[2] = {p->conv_t.wm1, p->conv_t.wm2};
-    add_hl_pq(l, w, 2, p->cout, f.hl_pqs, f.hl_scale + 2);
+    add_hl_pq(l, w, 2, p->cout, f.hl_pqs, hls(f, 2));
   }
   if (hl.t) {
-    add_hl_rm(l, p->conv_t.wrm, p->conv_t.brm, V, 2 * V, f.hl_rmt, f.hl_scale + 7, f.hl_rbias + 2 * T);
-    add_hl_conv(l, p->conv_t.wf, p->cout, p->cout, f.hl_wt, f.hl_scale + 3);
+    add_hl_rm(l, p->conv_t.wrm, p->conv_t.brm, V, 2 * V, f.hl_rmt, hls(f, 7), f.hl_rbias + 2 * T, p->alpha_tm,
+              f.astat_t, T * T);
+    add_hl_conv(l, p->conv_t.wf, p->conv_t.bf, p->cout, p->cout, f.hl_wt, hls(f, 3));
     if (tail.next) {
       const dstd_block_params* q = tail.next;
       const float* w[4] = {q->conv_s[0].wm1, q->conv_s[0].wm2, q->conv_s[1].wm1, q->conv_s[1].wm2};
-      add_hl_pq(l, w, 4, 64, f.hl_pqt, f.hl_scale + 4);
+      add_hl_pq(l, w, 4, 64, f.hl_pqt, hls(f, 4));
     }
   }
 }
@@ -351,7 +352,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     for (int g = 0; g < 2; ++g) {
       ah.p_ch[g] = aa.p_ch[g];
       ah.wimg[g] = f.hl_rms[g];
-      ah.wscale[g] = f.hl_scale + 5 + g;
+      ah.wscale[g] = hls(f, 5 + g);
       ah.bias[g] = f.hl_rbias + g * T;
       ah.astat[g] = aa.astat[g];
     }
@@ -388,12 +389,13 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ha.adj = reinterpret_cast<const uint16_t*>(sc.adj_s);
     for (int g = 0; g < 2; ++g) {
       ha.wimg[g] = f.hl_ws[g];
-      ha.wscale[g] = f.hl_scale + g;
+      ha.wscale[g] = hls(f, g);
+      ha.adjb[g] = hls(f, 5 + g);
       ha.bf[g] = p->conv_s[g].bf;
     }
     if (res) {
       ha.wimg[2] = f.hl_ws[2];
-      ha.wscale[2] = f.hl_scale + 8;
+      ha.wscale[2] = hls(f, 8);
       ha.bf[2] = p->res_b;
       ha.rbn_s = f.rbn_s;
       ha.rbn_h = f.rbn_h;
@@ -403,7 +405,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ha.prelu = p->prelu;
     ha.y = h;
     ha.pqimg = f.hl_pqs;
-    ha.pqscale = f.hl_scale + 2;
+    ha.pqscale = hls(f, 2);
     ha.pqb[0] = p->conv_t.bm1;
     ha.pqb[1] = p->conv_t.bm2;
     ha.pq = sc.pq_t;
@@ -489,7 +491,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ah.ngroups = 1;
     ah.p_ch[0] = ta.p_ch[0];
     ah.wimg[0] = f.hl_rmt;
-    ah.wscale[0] = f.hl_scale + 7;
+    ah.wscale[0] = hls(f, 7);
     ah.bias[0] = f.hl_rbias + 2 * T;
     ah.astat[0] = ta.astat[0];
     ah.alpha = ta.alpha;
@@ -513,7 +515,8 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ht.C = p->cout;
     ht.adj = reinterpret_cast<const uint16_t*>(sc.adj_t);
     ht.wimg = f.hl_wt;
-    ht.wscale = f.hl_scale + 3;
+    ht.wscale = hls(f, 3);
+    ht.adjb = hls(f, 7);
     ht.bf = p->conv_t.bf;
     ht.epi = tail.epi;
     ht.xres = tail.xres;
@@ -524,7 +527,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     if (tail.next) {
       const dstd_block_params* q = tail.next;
       ht.pqimg = f.hl_pqt;
-      ht.pqscale = f.hl_scale + 4;
+      ht.pqscale = hls(f, 4);
       ht.pqb[0] = q->conv_s[0].bm1;
       ht.pqb[1] = q->conv_s[0].bm2;
       ht.pqb[2] = q->conv_s[1].bm1;
@@ -789,6 +792,12 @@ int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, i
 
 int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float* y, void* workspace,
                    size_t workspace_bytes, void* stream) {
+  return dstd_block_fwd_ex(p, x, B, T, V, y, workspace, workspace_bytes, stream, 0u);
+}
+
+int dstd_block_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float* y, void* workspace,
+                      size_t workspace_bytes, void* stream, unsigned flags) {
+  if (flags & ~DSTD_FWD_EXACT_FP32) return DSTD_EINVAL;
   if (!x || !y || !workspace || !block_ok(p) || !shape_ok(B, T, V)) return DSTD_EINVAL;
   if (!limits_ok(T, V, p->cin, p->cout)) return DSTD_ELIMIT;
   if (workspace_bytes < dstd_block_workspace_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
@@ -802,7 +811,7 @@ int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int
   DSTD_TRY(to_layout(x, L.xin, B, p->cin, T * V, 1, s));
   DSTD_TRY(spatial_pq(p, L.xin, B, T, V, L.sc.pq_s, s));
   BlockTail tail{TEPI_RAW, nullptr, nullptr, nullptr, nullptr, nullptr};
-  const BlockHL hl = block_hl(p, tail, T, V);
+  const BlockHL hl = block_hl(p, tail, T, V, (flags & DSTD_FWD_EXACT_FP32) != 0);
   HLList hj;
   add_block_hl_jobs(hj, p, L.f, tail, hl, T, V);
   DSTD_TRY(run_hl_prep(hj, s));
@@ -825,6 +834,8 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
 int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof) {
   const bool reuse = (flags & DSTD_FWD_REUSE_CONSTANTS) != 0;
+  const bool exact = (flags & DSTD_FWD_EXACT_FP32) != 0;
+  if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32)) return DSTD_EINVAL;
   if (!p || !x || !y || !workspace) return DSTD_EINVAL;
   if (prof && (prof->capacity < 0 || (prof->capacity > 0 && (!prof->events || !prof->kinds)))) return DSTD_EINVAL;
   Prof pf;
@@ -902,7 +913,7 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
   }
   HLList hj;
   for (int b = 0; b < NB; ++b) {
-    hls[b] = block_hl(blk[b], tails[b], T, V);
+    hls[b] = block_hl(blk[b], tails[b], T, V, exact);
     add_block_hl_jobs(hj, blk[b], *fold[b], tails[b], hls[b], T, V);
   }
 
@@ -946,13 +957,6 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
   return DSTD_OK;
 }
 
-int dstd_set_gc_precision(int mode) {
-  if (mode != 0 && mode != 1) return DSTD_EINVAL;
-  g_hl_mode = mode;
-  return DSTD_OK;
-}
-
-int dstd_get_gc_precision(void) { return hl_on() ? 1 : 0; }
 
 int dstd_events_create(int n, void** events) {
   if (n < 0 || (n > 0 && !events)) return DSTD_EINVAL;

@@ -7,8 +7,10 @@
 //   a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi     (three MFMAs, fp32 accumulate)
 // -- 5.3x fewer MFMA cycles than fp32.  Weights are pre-scaled by a power of
 // two (max|w| * 2^s < 2^14) so that their low halves stay normal f16 numbers;
-// the accumulator is scaled back by 2^-s (exact).  Activations, adjacency
-// entries and tanh values are O(1) and split unscaled.  Emulated on the
+// the accumulator is scaled back by 2^-s (exact).  Activations and adjacency
+// entries are split under a power-of-two RANGE SCALE (below) so that no half
+// can overflow f16 whatever the fp32 magnitudes; tanh values are in [0, 1].
+// Emulated on the
 // fixtures (scripts/split_precision.py) the whole-model error against the
 // fp64 reference stays at the level of an fp32 run (0.6-1.1x the reference's
 // own fp32 error), per op 0.5-0.9x.
@@ -137,6 +139,33 @@ inline int hl_sl_temporal(int T) {
   return 8 * g;
 }
 
+// ---- range scaling (the split path over the whole fp32 range) -------------
+// An f16 half holds at most 65504, so an fp32 activation above that would split
+// into inf.  Every split operand is therefore brought below 2^14 by an exact
+// power of two, chosen where it is split and undone on the fp32 accumulator:
+//  * a GC unit's input rows x (spatial (sample, frame), temporal (sample,
+//    joint)): x_s = 2^-sx x with the smallest sx >= 0 such that
+//    max|x| * max(1, |W_f|_inf) < 2^(14 + sx) and max|b_f| < 2^(14 + sx), so
+//    both x_s and the conv output F_s = W_f x_s + 2^-sx b_f (split again as
+//    the aggregation operand) stay below 2^15; the aggregation result is
+//    scaled back by 2^sx.  |W_f|_inf (max row L1 norm) and max|b_f| come from
+//    k_hl_prep, max|x| is a wave reduction over the unit;
+//  * the unit's output h before the next P/Q conv: h_s = 2^-sh h, max|h_s| < 2^14;
+//  * the adjacency planes: 2^-sa Adj with |Adj| <= |alpha| max_r(sum_k |W_rm| +
+//    |b_rm|) + max|Astat| < 2^(14 + sa) (a bound from the weights alone,
+//    computed by k_hl_prep; both graphs of a spatial launch share one sa).
+// sx = sh = sa = 0 whenever the values are in range, which leaves the
+// arithmetic bit-identical to an unscaled split; every scale is exact, so the
+// only cost of a shift is the dynamic range of the low halves (relative to
+// the unit's largest value, 2^-24).
+constexpr int kHLSlot = 4;  // floats per weight-image scale slot:
+enum HLSlotField {
+  HLS_INV = 0,    // 2^-s of the image
+  HLS_BOUND = 1,  // HLJ_CONV: |W|_inf (max row L1 norm, unscaled); HLJ_RM: the adjacency bound
+  HLS_BMAX = 2,   // HLJ_CONV: max|bias| (0 without a bias)
+};
+__host__ __device__ constexpr inline int hl_range_shift(int e) { return e - 14 < 0 ? 0 : e - 14 > 120 ? 120 : e - 14; }
+
 // ---- weight images (one k_hl_prep launch per forward) --------------------
 // HLJ_CONV: fragments of a 1x1 conv W[c][k] (rows = c out, cols = k in):
 //   img[((ct*KSI + ks)*2 + plane)*64 + lane] = 8 halves of 2^s * W[16ct + j][32ks + 8kg + e]
@@ -162,9 +191,12 @@ struct HLJob {
   int nblk;
   int rows, cols;
   uint4* img;
-  float* inv_scale;   // 2^-s
-  const float* bias;  // HLJ_RM: conv_rm bias; bias_out[r] = bias[r] + sum_k W[r][k]
-  float* bias_out;    //   (the adjacency kernel contracts W with 1/(E F + 1), see k_adj_hl)
+  float* inv_scale;   // scale slot (kHLSlot floats, HLSlotField)
+  const float* bias;  // HLJ_RM: conv_rm bias, copied to bias_out; HLJ_CONV: the conv bias or null (HLS_BMAX)
+  float* bias_out;
+  const float* alpha; // HLJ_RM: alpha and the static adjacency [nastat] of the bound
+  const float* astat;
+  int nastat;
 };
 inline int hl_rm_img(int rows, int cols) {  // uint4
   return cdiv(rows, 16) * (hl_rm_nsf(cols) * 2 * 64 + hl_rm_tail(cols) * 64);
@@ -191,6 +223,7 @@ struct SpatialHLArgs {
   const float* rbn_s;        // folded residual BN [V][Cout] (Cin != Cout)
   const float* rbn_h;
   const float* prelu;
+  const float* adjb[2];      // scale slots of the two spatial conv_rm images (HLS_BOUND: range of the planes)
   float* y;                  // NTVC [B][T][V][Cout]
   const uint4* pqimg;        // HLJ_PQ image of conv_t.conv_m1/m2 (4 channels)
   const float* pqscale;
@@ -205,6 +238,7 @@ struct TemporalHLArgs {
   const uint4* wimg;
   const float* wscale;
   const float* bf;
+  const float* adjb;         // scale slot of the temporal conv_rm image (HLS_BOUND)
   int epi;                   // TemporalEpi: ENC, IN, RAW (C = 64); OUT, RAW (C = 3)
   const float* xres;         // ENC: block input; OUT: model input [B][T][V][3]
   const float* bn_s;
@@ -234,7 +268,7 @@ struct AdjHLArgs {
   int B, ngroups;
   const uint4* wimg[2];     // HLJ_RM images of conv_rm
   const float* wscale[2];
-  const float* bias[2];     // HLJob::bias_out of the conv_rm image (bias + row sums of W)
+  const float* bias[2];     // HLJob::bias_out of the conv_rm image (the conv_rm bias)
   const float* alpha;
   const float* astat[2];    // [NA][NA]
   uint16_t* out;

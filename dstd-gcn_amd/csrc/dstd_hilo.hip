@@ -124,6 +124,38 @@ __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, flo
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, DSTD_GC_ST_AUX);
 }
 
+// ---- range scaling helpers (dstd_hilo.h "range scaling") ----
+// 2^e as a float, e in [-126, 127]
+__device__ __forceinline__ float pow2f(int e) { return __uint_as_float((uint32_t)(127 + e) << 23); }
+// e with v < 2^e for the bits of a non-negative float v (frexp's exponent;
+// zero and denormals -> -126)
+__device__ __forceinline__ int fexp_bits(uint32_t b) { return (int)(b >> 23) - 126; }
+// max over the wave of non-negative floats, as bits (the bit patterns of
+// non-negative floats order like the values): DPP within rows of 16, then
+// the four row maxima through SGPRs -- a wave-uniform result
+__device__ __forceinline__ uint32_t wave_max_bits(float v) {
+  uint32_t b = __float_as_uint(v);
+  b = max(b, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  b = max(b, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  b = max(b, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  b = max(b, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, 0x140, 0xF, 0xF, false));  // row_mirror
+  const uint32_t r0 = __builtin_amdgcn_readlane(b, 0), r1 = __builtin_amdgcn_readlane(b, 16);
+  const uint32_t r2 = __builtin_amdgcn_readlane(b, 32), r3 = __builtin_amdgcn_readlane(b, 48);
+  return max(max(r0, r1), max(r2, r3));
+}
+__device__ __forceinline__ float amax4(float m, const float4& v) {
+  return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
+}
+__device__ __forceinline__ float amax4(float m, const f32x4& v) {
+  return fmaxf(fmaxf(m, fmaxf(fabsf(v[0]), fabsf(v[1]))), fmaxf(fabsf(v[2]), fabsf(v[3])));
+}
+__device__ __forceinline__ float4 mul4(const float4& v, float s) { return make_float4(v.x * s, v.y * s, v.z * s, v.w * s); }
+// input shift of a GC unit: the smallest sx >= 0 with max|x| * max(1, |W|_inf)
+// < 2^(14 + sx) and max|b| < 2^(14 + sx); efb / eb: fexp of max(1, |W|_inf) / max|b|
+__device__ __forceinline__ int input_shift(uint32_t xmax_bits, int efb, int eb) {
+  return hl_range_shift(max(fexp_bits(xmax_bits) + efb, eb));
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -132,17 +164,21 @@ __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, flo
 __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
   const HLJob& j = a.jobs[blockIdx.x];
   const int tid = threadIdx.x;
+  __shared__ float red[4];
+  auto block_max = [&](float m) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    __syncthreads();  // red[] is reused
+    if ((tid & 63) == 0) red[tid >> 6] = m;
+    __syncthreads();
+    return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  };
   // HLJ_CONV / HLJ_RM: w[0] is rows x cols; HLJ_PQ: nblk blocks of 2 x cols
   const int n = j.kind != HLJ_PQ ? j.rows * j.cols : 2 * j.cols * j.nblk;
   float m = 0.f;
   for (int i = tid; i < n; i += 256)
     m = fmaxf(m, fabsf(j.kind != HLJ_PQ ? j.w[0][i] : j.w[i / (2 * j.cols)][i % (2 * j.cols)]));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-  __shared__ float red[4];
-  if ((tid & 63) == 0) red[tid >> 6] = m;
-  __syncthreads();
-  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  m = block_max(m);
   // 2^s with max|w| * 2^s < 2^14: low halves of the scaled weights stay normal
   int e = 0;
   float scale = 1.f;
@@ -150,14 +186,36 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
     frexpf(m, &e);  // m = f * 2^e, f in [0.5, 1)
     scale = ldexpf(1.f, 14 - e);
   }
-  if (tid == 0) *j.inv_scale = 1.f / scale;
-  if (j.kind == HLJ_RM) {  // fused bias: b[r] + sum_k W[r][k] (fixed order)
+  if (tid == 0) j.inv_scale[HLS_INV] = 1.f / scale;
+  // range bounds of the split operands (dstd_hilo.h "range scaling")
+  if (j.kind == HLJ_CONV) {  // |W|_inf and max|b|
+    float nrm = 0.f, bm = 0.f;
     for (int r = tid; r < j.rows; r += 256) {
       float acc = 0.f;
-      for (int k = 0; k < j.cols; ++k) acc += j.w[0][r * j.cols + k];
-      j.bias_out[r] = j.bias[r] + acc;
+      for (int k = 0; k < j.cols; ++k) acc += fabsf(j.w[0][r * j.cols + k]);
+      nrm = fmaxf(nrm, acc);
+      if (j.bias) bm = fmaxf(bm, fabsf(j.bias[r]));
     }
+    nrm = block_max(nrm);
+    bm = block_max(bm);
+    if (tid == 0) {
+      j.inv_scale[HLS_BOUND] = nrm;
+      j.inv_scale[HLS_BMAX] = bm;
+    }
+  } else if (j.kind == HLJ_RM) {  // |alpha| max_r (sum_k |W[r][k]| + |b[r]|) + max|Astat|
+    float rb = 0.f, am = 0.f;
+    for (int r = tid; r < j.rows; r += 256) {
+      float acc = fabsf(j.bias[r]);
+      for (int k = 0; k < j.cols; ++k) acc += fabsf(j.w[0][r * j.cols + k]);
+      rb = fmaxf(rb, acc);
+    }
+    for (int i = tid; i < j.nastat; i += 256) am = fmaxf(am, fabsf(j.astat[i]));
+    rb = block_max(rb);
+    am = block_max(am);
+    if (tid == 0) j.inv_scale[HLS_BOUND] = fabsf(*j.alpha) * rb + am;
   }
+  if (j.kind == HLJ_RM)  // the conv_rm bias as the adjacency kernel reads it (LDS-staged per workgroup)
+    for (int r = tid; r < j.rows; r += 256) j.bias_out[r] = j.bias[r];
   if (j.kind == HLJ_CONV) {
     const int NCT = cdiv(j.rows, 16), KSI = cdiv(j.cols, 32);
     for (int i = tid; i < NCT * KSI * 64; i += 256) {
@@ -301,6 +359,7 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
   __shared__ float bfl[3][16 * NCT];
   __shared__ float bql[4];
   __shared__ float scl[4];
+  __shared__ int rng[3];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int kl = lane >> 4, cl = lane & 15;
@@ -324,8 +383,14 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
     scl[1] = *a.wscale[1];
     scl[2] = *a.pqscale;
     scl[3] = RES ? *a.wscale[2] : 0.f;
+    // range: |W_f|_inf and max|b_f| over both graphs, the planes' shared shift
+    rng[0] = fexp_bits(__float_as_uint(fmaxf(1.f, fmaxf(a.wscale[0][HLS_BOUND], a.wscale[1][HLS_BOUND]))));
+    rng[1] = fexp_bits(__float_as_uint(fmaxf(a.wscale[0][HLS_BMAX], a.wscale[1][HLS_BMAX])));
+    rng[2] = hl_range_shift(fexp_bits(__float_as_uint(fmaxf(a.adjb[0][HLS_BOUND], a.adjb[1][HLS_BOUND]))));
   }
   __syncthreads();
+  const int efb = __builtin_amdgcn_readfirstlane(rng[0]), eb = __builtin_amdgcn_readfirstlane(rng[1]);
+  const int sa = __builtin_amdgcn_readfirstlane(rng[2]);
 
   int uend;
   int u = unit_range(a.B * T, uend);
@@ -396,6 +461,23 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
     // whole-unit-ahead prefetch of both measured 6% slower: registers)
     load_adj_g(u, 0);
     __builtin_amdgcn_sched_barrier(0);
+    // range shift of the unit's rows (0 unless a half could overflow)
+    float xm = 0.f;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int ks = 0; ks < KSI; ++ks) xm = amax4(amax4(xm, xr[m][ks][0]), xr[m][ks][1]);
+    const int sx = input_shift(wave_max_bits(xm), efb, eb);
+    const float dnx = pow2f(-sx);
+    if (sx) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int ks = 0; ks < KSI; ++ks) {
+          xr[m][ks][0] = mul4(xr[m][ks][0], dnx);
+          xr[m][ks][1] = mul4(xr[m][ks][1], dnx);
+        }
+    }
     f16x8 xh[2][KSI], xo[2][KSI];
 #pragma unroll
     for (int m = 0; m < 2; ++m)
@@ -457,7 +539,7 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
       f16x8 dh[NCT], dl[NCT];
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
-        const float b = bfl[g][16 * ct + cl];
+        const float b = bfl[g][16 * ct + cl] * dnx;  // F_s = 2^-sx F
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -489,7 +571,13 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
       for (int ks = 0; ks < KSI; ++ks) {
         f16x8 bh[NWT], bo[NWT];
 #pragma unroll
-        for (int wt = 0; wt < NWT; ++wt) split8(xw[wt][ks][0], xw[wt][ks][1], bh[wt], bo[wt]);
+        for (int wt = 0; wt < NWT; ++wt) {
+          if (sx) {
+            xw[wt][ks][0] = mul4(xw[wt][ks][0], dnx);
+            xw[wt][ks][1] = mul4(xw[wt][ks][1], dnx);
+          }
+          split8(xw[wt][ks][0], xw[wt][ks][1], bh[wt], bo[wt]);
+        }
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) {
           const f16x8 ah = as_h8(wl[2][((ct * KSI + ks) * 2 + 0) * 64 + lz]);
@@ -505,6 +593,14 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
     }
 
     // ---- epilogue: h = prelu(bn(y) + r) -> NTVC ----
+    // y = 2^(sx + sa) O (the aggregation ran on 2^-sx F and 2^-sa Adj)
+    if (const int su = min(sx + sa, 127)) {
+      const float up = pow2f(su);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int wt = 0; wt < NWT; ++wt) O[ct][wt] *= up;
+    }
     const auto ry = rsrc(a.y + (size_t)u * V * COUT, yunit);
 #pragma unroll
     for (int wt = 0; wt < NWT; ++wt) {
@@ -517,7 +613,7 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
         float r[4];
         if constexpr (RES) {
           const float4 rs = bnl[2][c4], rh = bnl[3][c4];
-          const float s3 = scl[3];
+          const float s3 = scl[3] * pow2f(sx);  // the residual conv ran on 2^-sx x
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float b = bfl[2][16 * ct + 4 * kl + q];
@@ -550,6 +646,20 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
       }
     }
     // ---- P_t/Q_t of h: out[ch][w] = sum_c wq[ch][c] h[c][w] + b ----
+    // on h_s = 2^-sh h (range shift of the unit's output)
+    float hm = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+      for (int wt = 0; wt < NWT; ++wt) hm = amax4(hm, O[ct][wt]);
+    const int sh = hl_range_shift(fexp_bits(wave_max_bits(hm)));
+    if (sh) {
+      const float dn = pow2f(-sh);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int wt = 0; wt < NWT; ++wt) O[ct][wt] *= dn;
+    }
     f32x4 acc[NWT];
 #pragma unroll
     for (int wt = 0; wt < NWT; ++wt) acc[wt] = zero4();
@@ -568,7 +678,7 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
       for (int wt = 0; wt < NWT; ++wt) acc[wt] = mfma32(qh, hh[wt], acc[wt]);
     }
     {
-      const float s = scl[2];
+      const float s = scl[2] * pow2f(sh);
       const auto rp = rsrc(a.pq + (size_t)u * V * 4, V * 16);
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt)
@@ -643,6 +753,7 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
   __shared__ float bfl[16 * NCT];
   __shared__ float bql[8];
   __shared__ float scl[2];
+  __shared__ int rng[3];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int kl = lane >> 4, cl = lane & 15;
@@ -661,8 +772,14 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
   if (tid == 0) {
     scl[0] = *a.wscale;
     scl[1] = has_pq ? *a.pqscale : 0.f;
+    // range: |W_f|_inf, max|b_f| and the planes' shift
+    rng[0] = fexp_bits(__float_as_uint(fmaxf(1.f, a.wscale[HLS_BOUND])));
+    rng[1] = fexp_bits(__float_as_uint(a.wscale[HLS_BMAX]));
+    rng[2] = hl_range_shift(fexp_bits(__float_as_uint(a.adjb[HLS_BOUND])));
   }
   __syncthreads();
+  const int efb = __builtin_amdgcn_readfirstlane(rng[0]), eb = __builtin_amdgcn_readfirstlane(rng[1]);
+  const int sa = __builtin_amdgcn_readfirstlane(rng[2]);
 
   int uend;
   int u = unit_range(a.B * V, uend);
@@ -717,6 +834,23 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
         }
     }
     __builtin_amdgcn_sched_barrier(0);
+    // range shift of the unit's rows (0 unless a half could overflow)
+    float xm = 0.f;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int ks = 0; ks < KSI; ++ks) xm = amax4(amax4(xm, xr[m][ks][0]), xr[m][ks][1]);
+    const int sx = input_shift(wave_max_bits(xm), efb, eb);
+    const float dnx = pow2f(-sx);
+    if (sx) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int ks = 0; ks < KSI; ++ks) {
+          xr[m][ks][0] = mul4(xr[m][ks][0], dnx);
+          xr[m][ks][1] = mul4(xr[m][ks][1], dnx);
+        }
+    }
     f16x8 xh[MT][KSI], xo[MT][KSI];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -747,7 +881,7 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
       const float s = scl[0];
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
-        const float b = bfl[16 * ct + cl];
+        const float b = bfl[16 * ct + cl] * dnx;  // F_s = 2^-sx F
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -806,6 +940,14 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- epilogue ----
+    // y = 2^(sx + sa) O (the aggregation ran on 2^-sx F and 2^-sa Adj)
+    if (const int su = min(sx + sa, 127)) {
+      const float up = pow2f(su);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] *= up;
+    }
     const auto ry = rsrc(a.y + cbase, col_bytes);
 #pragma unroll
     for (int ut = 0; ut < NUT; ++ut) {
@@ -839,6 +981,20 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
     }
     // ---- next block's P_s/Q_s (8 channels) of the output ----
     if (has_pq) {
+      // on h_s = 2^-sh h (range shift of the unit's output)
+      float hm = 0.f;
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) hm = amax4(hm, O[ct][ut]);
+      const int sh = hl_range_shift(fexp_bits(wave_max_bits(hm)));
+      if (sh) {
+        const float dn = pow2f(-sh);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+          for (int ut = 0; ut < NUT; ++ut) O[ct][ut] *= dn;
+      }
       f32x4 acc[NUT];
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut) acc[ut] = zero4();
@@ -856,7 +1012,7 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
 #pragma unroll
         for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma32(qh, hh[ut], acc[ut]);
       }
-      const float s = scl[1];
+      const float s = scl[1] * pow2f(sh);
       const auto rp = rsrc(a.pq + (size_t)u * T * 8, T * 32);
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut) {
@@ -1041,9 +1197,16 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
     }
     __syncthreads();
   }
-  // tanh(P - Q) = 1 - 2 r with r = 1 / (E F + 1): the B fragments carry r,
-  // the accumulator is scaled by -2 / 2^s and the bias holds b + sum_k W[.][k]
-  const float alpha = *a.alpha, inv = -2.f * *a.wscale[g];
+  // tanh(P - Q) = 1 - 2 / (E F + 1) formed per element (contracting W with
+  // r = 1 / (E F + 1) and folding b + sum_k W into the bias saves one packed
+  // FMA per element but cancels in the accumulator: the whole-model error
+  // tail measured 1.7x the reference's fp32 error at the 90th percentile
+  // against 1.2x this way -- scripts/parity_stats.py)
+  // planes stored as 2^-sa Adj (dstd_hilo.h "range scaling"; one sa for both
+  // spatial graphs, the GC kernel scales its aggregation back)
+  const float bnd = a.ngroups == 2 ? fmaxf(a.wscale[0][HLS_BOUND], a.wscale[1][HLS_BOUND]) : a.wscale[0][HLS_BOUND];
+  const float dna = pow2f(-hl_range_shift(fexp_bits(__float_as_uint(bnd))));
+  const float alpha = *a.alpha * dna, inv = *a.wscale[g];
   TLH(MODE, 1)
 
   float* so = stg[wave];
@@ -1070,14 +1233,16 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
         const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
         if constexpr (SEP) {
   #pragma unroll
-          for (int e2 = 0; e2 < 8; e2 += 2) {  // E F + 1 as packed fp32 (v_pk_fma_f32)
+          for (int e2 = 0; e2 < 8; e2 += 2) {  // E F + 1 and 1 - 2 r as packed fp32 (v_pk_fma_f32)
             const f32x2_t d = __builtin_elementwise_fma(f32x2_t{ev[e2], ev[e2 + 1]}, f32x2_t{fv[e2], fv[e2 + 1]}, f32x2_t{1.f, 1.f});
-            tv[e2] = __builtin_amdgcn_rcpf(d.x);
-            tv[e2 + 1] = __builtin_amdgcn_rcpf(d.y);
+            const f32x2_t t = __builtin_elementwise_fma(
+                f32x2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}, f32x2_t{-2.f, -2.f}, f32x2_t{1.f, 1.f});
+            tv[e2] = t.x;
+            tv[e2 + 1] = t.y;
           }
         } else {
   #pragma unroll
-          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fmaf(-0.5f, fast_tanh(ev[e8] - fv[e8]), 0.5f);
+          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fast_tanh(ev[e8] - fv[e8]);
         }
         split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
       }
@@ -1091,12 +1256,14 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   #pragma unroll
           for (int e2 = 0; e2 < 4; e2 += 2) {
             const f32x2_t d = __builtin_elementwise_fma(f32x2_t{ev[e2], ev[e2 + 1]}, f32x2_t{fv[e2], fv[e2 + 1]}, f32x2_t{1.f, 1.f});
-            tv[e2] = __builtin_amdgcn_rcpf(d.x);
-            tv[e2 + 1] = __builtin_amdgcn_rcpf(d.y);
+            const f32x2_t t = __builtin_elementwise_fma(
+                f32x2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}, f32x2_t{-2.f, -2.f}, f32x2_t{1.f, 1.f});
+            tv[e2] = t.x;
+            tv[e2 + 1] = t.y;
           }
         } else {
   #pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fmaf(-0.5f, fast_tanh(ev[e4] - fv[e4]), 0.5f);
+          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fast_tanh(ev[e4] - fv[e4]);
         }
         uint4 hi, lo;
         split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
@@ -1140,7 +1307,7 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       // ---- epilogue: alpha * (acc + b) + Astat, 0 on padding slots; staged
       // through this wave's LDS slot so a lane stores 8 consecutive slots ----
       // padding slots: alpha -> 0 and Astat[NA*NA] = 0, so the value is 0 without a select
-      const float as = asl[valid ? pr * NA + qr : NA * NA], al = valid ? alpha : 0.f;
+      const float as = asl[valid ? pr * NA + qr : NA * NA] * dna, al = valid ? alpha : 0.f;
   #pragma unroll
       for (int r2 = 0; r2 < RT; r2 += 2) {
   #pragma unroll

@@ -42,7 +42,10 @@ def shard(x, world, rank, dim=0):
 def broadcast_module(module, src=0, group=None):
     """Broadcast every parameter and buffer of ``module`` from ``src`` in place.
     Tensors sharing storage (the reference's ``A_s``/``R_s`` alias,
-    ``model/dstdgcn.py:107-109``) are sent once, so the alias survives."""
+    ``model/dstdgcn.py:107-109``) are sent once, so the alias survives.  The
+    collectives write the tensors outside autograd's version counters, so the
+    native modules' cached folded constants are invalidated explicitly."""
+    from model.dstdgcn import invalidate_native_cache
     seen = set()
     for t in list(module.parameters()) + list(module.buffers()):
         key = (t.untyped_storage().data_ptr(), t.storage_offset(), tuple(t.shape))
@@ -50,7 +53,8 @@ def broadcast_module(module, src=0, group=None):
             continue
         seen.add(key)
         with torch.no_grad():
-            dist.broadcast(t.data, src=src, group=group)
+            dist.broadcast(t, src=src, group=group)
+    invalidate_native_cache(module)
 
 
 def gather_batch(y_local, n_total, group=None):

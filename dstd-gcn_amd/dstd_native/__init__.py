@@ -74,6 +74,7 @@ class ModelGrads(ctypes.Structure):
 
 
 FWD_REUSE_CONSTANTS = 1  # include/dstd_gcn.h DSTD_FWD_REUSE_CONSTANTS
+FWD_EXACT_FP32 = 2  # include/dstd_gcn.h DSTD_FWD_EXACT_FP32
 KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL = range(6)
 KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temporal_gc")
 
@@ -101,6 +102,8 @@ def lib():
         L.dstd_dstdgc_fwd.argtypes = [ci, vp, ci, ci, ci, ci, ci, ctypes.POINTER(GCWeights), vp, vp, vp, vp, sz, vp]
         L.dstd_block_fwd.restype = ci
         L.dstd_block_fwd.argtypes = [ctypes.POINTER(BlockParams), vp, ci, ci, ci, vp, vp, sz, vp]
+        L.dstd_block_fwd_ex.restype = ci
+        L.dstd_block_fwd_ex.argtypes = [ctypes.POINTER(BlockParams), vp, ci, ci, ci, vp, vp, sz, vp, ctypes.c_uint]
         L.dstd_model_fwd.restype = ci
         L.dstd_model_fwd.argtypes = [ctypes.POINTER(ModelParams), vp, ci, vp, vp, sz, vp]
         L.dstd_model_fwd_ex.restype = ci
@@ -115,10 +118,6 @@ def lib():
         L.dstd_events_destroy.argtypes = [ci, ctypes.POINTER(ctypes.c_void_p)]
         L.dstd_event_elapsed_ms.restype = ci
         L.dstd_event_elapsed_ms.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_float)]
-        L.dstd_set_gc_precision.restype = ci
-        L.dstd_set_gc_precision.argtypes = [ci]
-        L.dstd_get_gc_precision.restype = ci
-        L.dstd_get_gc_precision.argtypes = []
         # training path (include/dstd_gcn_train.h)
         u64, f32 = ctypes.c_ulonglong, ctypes.c_float
         for n, k in (("dstd_dstdgc_train_saved_bytes", 6), ("dstd_dstdgc_train_workspace_bytes", 6),
@@ -170,7 +169,7 @@ def lib():
 EXPORTS = ("dstd_version", "dstd_error_string", "dstd_dstdgc_workspace_bytes", "dstd_block_workspace_bytes",
            "dstd_model_workspace_bytes", "dstd_dstdgc_fwd", "dstd_block_fwd", "dstd_model_fwd",
            "dstd_model_fwd_profiled", "dstd_events_create", "dstd_events_destroy", "dstd_event_elapsed_ms",
-           "dstd_set_gc_precision", "dstd_get_gc_precision", "dstd_model_fwd_ex")
+           "dstd_block_fwd_ex", "dstd_model_fwd_ex")
 TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_bytes", "dstd_dstdgc_train_fwd",
                  "dstd_dstdgc_train_bwd", "dstd_block_train_saved_bytes", "dstd_block_train_workspace_bytes",
                  "dstd_block_train_fwd", "dstd_block_train_bwd", "dstd_model_train_saved_bytes",
@@ -180,15 +179,16 @@ AUX_EXPORTS = ("dstd_ctg_workspace_bytes", "dstd_ctg_fwd", "dstd_ctg_bwd", "dstd
                "dstd_conv2d_fwd", "dstd_conv2d_bwd")
 
 
-def set_gc_precision(mode):
-    """Arithmetic of the 64->64 graph convolutions (include/dstd_gcn.h):
-    "split" (split-f16 MFMA, default) or "fp32" (exact-fp32 MFMA).  Returns the
-    previous mode."""
-    modes = {"fp32": 0, "split": 1}
-    L = lib()
-    prev = "split" if L.dstd_get_gc_precision() == 1 else "fp32"
-    check(L.dstd_set_gc_precision(modes[mode]), "dstd_set_gc_precision")
-    return prev
+ARITHMETICS = ("split", "fp32")
+
+
+def arith_flags(mode):
+    """Per-call flag of the graph-convolution arithmetic (include/dstd_gcn.h
+    DSTD_FWD_EXACT_FP32): "split" (split-f16 MFMA where the shape has kernels,
+    the default) or "fp32" (exact-fp32 MFMA everywhere)."""
+    if mode not in ARITHMETICS:
+        raise ValueError(f"gc arithmetic must be one of {ARITHMETICS}, got {mode!r}")
+    return FWD_EXACT_FP32 if mode == "fp32" else 0
 
 
 def check(code, what):

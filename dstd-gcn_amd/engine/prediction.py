@@ -8,14 +8,24 @@ format as the reference, driving the MI355X model:
   backward, Adam step, StepLR at epoch end.  Losses accumulate on the GPU; the
   epoch synchronises once when it reports its average.  Under
   ``torch.distributed`` (one process per GPU) gradients are averaged with one
-  flat all-reduce per step (dstd_dist.allreduce_grads).
+  flat all-reduce per step (dstd_dist.allreduce_grads) and the reported
+  epoch losses are the global averages (one all-reduce of the loss sums and
+  sample counts).  The engine opts the model into the in-place gradient arena
+  (dstd_native.grad_sink); other callers get plain autograd gradients.
 * ``test`` (:319-430): eval forward, then the per-frame MPJPE of every batch
   in one kernel (dstd_frame_mpjpe) accumulating on the device; one
   synchronisation per call instead of one ``.item()`` per frame and batch.
+  Under ``torch.distributed`` with more than one rank the batches are sharded
+  round-robin over the ranks (unless the loader already shards through a
+  DistributedSampler) and the per-frame sums and sample counts are
+  all-reduced (dstd_dist.reduce_partials), so every rank returns the metric of
+  the whole loader.
 * ``save`` / ``recover`` (:159-182): the same ``{"lr", "err", "model",
   "optimizer", "scheduler", "epoch"}`` dict with ``model.``-prefixed keys;
   recover loads with ``weights_only=True``.
 """
+import warnings
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -65,6 +75,13 @@ class ModelWrapper(nn.Module):
                 loss = loss + w * fn(pred, gt, wgts)
             return loss
         return self.loss_funcs[loss_type]
+
+
+def _world():
+    """(rank, world size) of the default process group, (0, 1) without one."""
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
 
 
 def _to_dev(x, dev):
@@ -140,7 +157,9 @@ class PredictionEngine:
         dev = self.device
         t_l = {key_loss: DeviceAccum(dev) for key_loss in self.config["loss"]}
         self.model.train()
-        distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+        # backward accumulates straight into .grad (dstd_native.grad_sink)
+        self.model.model._dstd_inplace_grads = True
+        distributed = _world()[1] > 1
         num_iter = len(train_loader) if max_iter == -1 else min(len(train_loader), max_iter)
         for i, (inputs, inputs_inv, targets, all_seqs) in enumerate(train_loader):
             inputs, inputs_inv, targets = _to_dev(inputs, dev), _to_dev(inputs_inv, dev), _to_dev(targets, dev)
@@ -186,25 +205,40 @@ class PredictionEngine:
             self.optimizer.step()
             if i >= num_iter - 1:
                 break
-        desc = f"epoch: {epoch + 1}|train|" + "".join("{}:{:.2f}|".format(ls, t_l[ls].avg) for ls in t_l)
+        if distributed:  # global averages: one all-reduce of (loss sums, sample counts)
+            from dstd_dist import reduce_partials
+            sums = torch.stack([t_l[ls].sum for ls in t_l])
+            counts = torch.tensor([float(t_l[ls].count) for ls in t_l], dtype=torch.float64, device=sums.device)
+            sums, counts = reduce_partials(sums, counts)
+            avg = {ls: float(s) / float(c) if c else 0.0 for ls, s, c in zip(t_l, sums.tolist(), counts.tolist())}
+        else:
+            avg = {ls: t_l[ls].avg for ls in t_l}
+        desc = f"epoch: {epoch + 1}|train|" + "".join("{}:{:.2f}|".format(ls, avg[ls]) for ls in t_l)
         self.logger.info(desc)
         self.scheduler.step()
-        self.lr = self.scheduler.get_last_lr()[0]
-        return sum(t_l[ls].avg for ls in t_l)
+        # the reference reads get_lr() here (:311): on a StepLR boundary that is
+        # the decayed rate decayed once more -- the value its checkpoints store
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)
+            self.lr = self.scheduler.get_lr()[0]
+        return sum(avg.values())
 
     # ------------------------------------------------------------------
     def test(self, test_loader, input_n=10, eval_frame=None, dim_used=None, joint_to_ignore=None, joint_equal=None,
              time_tsfm=None, scale_tsfm=None, action=None, save_path=None):
         assert eval_frame is not None
         dev = self.device
-        L = native.lib()
         sums = torch.zeros(len(eval_frame), dtype=torch.float32, device=dev)
         N = 0
         save_results = dict() if save_path is not None else None
         index_cache = {}
+        rank, world = _world()
+        presharded = isinstance(getattr(test_loader, "sampler", None), torch.utils.data.DistributedSampler)
         self.model.eval()
         with torch.no_grad():
             for i, (inputs, _, _, all_seqs) in enumerate(test_loader):
+                if world > 1 and not presharded and i % world != rank:
+                    continue  # round-robin batch sharding over the ranks
                 inputs = _to_dev(inputs, dev)
                 all_seqs = all_seqs.float().to(dev, non_blocking=True).contiguous()
                 outputs = self.inverse(self.model(self.transform(inputs), False))
@@ -224,11 +258,7 @@ class PredictionEngine:
                     index_cache[key] = self._metric_indices(D, outputs.shape[2], seq_len, input_n, eval_frame,
                                                             dim_used, joint_to_ignore, joint_equal)
                 used_pos, joint_src, frames = index_cache[key]
-                code = L.dstd_frame_mpjpe(native.ptr(all_seqs, "all_seqs"), native.ptr(outputs, "outputs"), n,
-                                          seq_len, D, t_out0, used_pos.data_ptr(), outputs.shape[2],
-                                          joint_src.data_ptr(), frames.data_ptr(), len(eval_frame), sums.data_ptr(),
-                                          native.stream_handle(dev))
-                native.check(code, "dstd_frame_mpjpe")
+                self._frame_metric(all_seqs, outputs, t_out0, used_pos, joint_src, frames, sums)
                 N += n
                 if save_results is not None:
                     pred = self._fill_pred(all_seqs, outputs, used_pos, joint_src, t_out0)[:, input_n:]
@@ -238,12 +268,26 @@ class PredictionEngine:
                         save_results[k] = a if k not in save_results else np.concatenate((save_results[k], a), 0)
             if action is None:
                 action = "NA"
+            if world > 1:  # per-frame sums and sample counts of every rank
+                from dstd_dist import reduce_partials
+                sums, n_all = reduce_partials(sums, torch.tensor([float(N)], dtype=torch.float64, device=sums.device))
+                N = float(n_all[0])
             t_metric = sums.double().cpu().numpy() / N  # the one synchronisation
             self.logger.info(f"action: {action}|test|loss:{t_metric.mean():.2f}")
             if save_results is not None:
                 np.savez(save_path + ".npz", target=save_results["target"], result=save_results["result"])
         # t_l.avg of the reference = sum over (batch, frame) of metric_k / (N * frames)
         return float(t_metric.mean()), t_metric
+
+    def _frame_metric(self, all_seqs, outputs, t_out0, used_pos, joint_src, frames, sums):
+        """sums[k] += sum over the batch of the MPJPE at frames[k] (:366-404),
+        one kernel on the device (dstd_frame_mpjpe)."""
+        n, seq_len, D = all_seqs.shape
+        code = native.lib().dstd_frame_mpjpe(native.ptr(all_seqs, "all_seqs"), native.ptr(outputs, "outputs"), n,
+                                             seq_len, D, t_out0, used_pos.data_ptr(), outputs.shape[2],
+                                             joint_src.data_ptr(), frames.data_ptr(), len(frames), sums.data_ptr(),
+                                             native.stream_handle(all_seqs.device))
+        native.check(code, "dstd_frame_mpjpe")
 
     def _metric_indices(self, D, n_out_dims, seq_len, input_n, eval_frame, dim_used, joint_to_ignore, joint_equal):
         """Device index tables of the metric: used_pos[d] (position of dim d in

@@ -27,6 +27,7 @@ grad_fn whose backward raises (the reference would back-propagate through
 running-statistics BN there; no shipped recipe does), so a silent wrong
 gradient is impossible.
 """
+import itertools
 import math
 
 import numpy as np
@@ -72,6 +73,23 @@ class _ForwardOnly(torch.autograd.Function):
     def backward(ctx, *grads):
         raise NotImplementedError("backward through an eval-mode DSTDGCB / DSTDGCN (running-statistics BN) is not "
                                   "built; call .train() for the native training path")
+
+
+# Native modules that cache folded constants in the workspace between
+# forwards (DSTDGCN) carry an instance token that is never reused (unlike id())
+# and a generation counter, both part of the reuse tag.
+_UIDS = itertools.count(1)
+
+
+def invalidate_native_cache(module):
+    """Force the next eval forward of every native module in ``module``'s tree
+    to refold its constants.  Needed after writes the version counters do not
+    see: through ``.data``, by collectives (dstd_dist.broadcast_module calls
+    it), or by foreign kernels.  In-place torch ops, optimizer steps,
+    ``load_state_dict`` and ``.to()`` are detected without it."""
+    for m in module.modules():
+        if hasattr(m, "_dstd_gen"):
+            m._dstd_gen += 1
 
 
 def _mark(y, *deps):
@@ -280,8 +298,15 @@ class _ModelTrain(torch.autograd.Function):
         dev = x.device
         dy = dy.contiguous()
         # gradients accumulate straight into the parameters' .grad (one arena,
-        # native +=) when they are ours; else into a fresh arena handed to autograd
-        arena, direct = native.grad_sink(model, ctx.params, dev)
+        # native +=) when the caller opted in (engine.PredictionEngine.train
+        # sets model._dstd_inplace_grads) and no parameter carries hooks; else
+        # into a fresh arena whose views autograd accumulates (hooks, DDP and
+        # torch.autograd.grad see ordinary gradients)
+        if getattr(model, "_dstd_inplace_grads", False) and not any(
+                p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None) for p in ctx.params):
+            arena, direct = native.grad_sink(model, ctx.params, dev)
+        else:
+            arena, direct = native.GradArena(ctx.params, dev), False
         g = getattr(arena, "model_grads", None) if direct else None
         if g is None:
             g = model._native_grads(arena)
@@ -405,6 +430,9 @@ class DSTDGCB(nn.Module):
         self.alpha_tm = nn.Parameter(torch.zeros(1))
         self.prelu = nn.PReLU()
         self.do = nn.Dropout(0.1)  # constructed but never applied (reference :133)
+        # arithmetic of the eval forward's graph convolutions, per call
+        # (include/dstd_gcn.h DSTD_FWD_EXACT_FP32): "split" or "fp32"
+        self.gc_arithmetic = "split"
 
     def init_parameter(self):
         stdt = 1.0 / math.sqrt(self.R_t.size(1))
@@ -426,9 +454,9 @@ class DSTDGCB(nn.Module):
         nbytes = L.dstd_block_workspace_bytes(B, cin, self.out_channels, T, V)
         ws = native.workspace(dev, nbytes)
         p = native.block_struct(self)
-        code = L.dstd_block_fwd(p, native.ptr(x, "x"), B, T, V, native.ptr(y, "y"), ws.data_ptr(), ws.numel(),
-                                native.stream_handle(dev))
-        native.check(code, "dstd_block_fwd")
+        code = L.dstd_block_fwd_ex(p, native.ptr(x, "x"), B, T, V, native.ptr(y, "y"), ws.data_ptr(), ws.numel(),
+                                   native.stream_handle(dev), native.arith_flags(self.gc_arithmetic))
+        native.check(code, "dstd_block_fwd_ex")
         return _mark(y, x, *self.parameters())
 
 
@@ -615,6 +643,19 @@ class DSTDGCN(nn.Module):
         self.prelu = nn.PReLU()
         self._native = None
         self._tree = _TensorTree()
+        self.gc_arithmetic = "split"  # see DSTDGCB; set_gc_arithmetic() sets the whole tree
+        self._dstd_uid = next(_UIDS)
+        self._dstd_gen = 0
+        self.register_load_state_dict_post_hook(lambda mod, incompatible: invalidate_native_cache(mod))
+
+    def set_gc_arithmetic(self, mode):
+        """"split" (default) or "fp32" for this model's eval forward and every
+        DSTDGCB in it (include/dstd_gcn.h DSTD_FWD_EXACT_FP32)."""
+        native.arith_flags(mode)  # validates
+        for m in self.modules():
+            if isinstance(m, (DSTDGCN, DSTDGCB)):
+                m.gc_arithmetic = mode
+        return self
 
     # -- native parameter block ---------------------------------------------
     def _native_params(self):
@@ -675,17 +716,25 @@ class DSTDGCN(nn.Module):
     def _forward_native(self, x, y, prof=None):
         """One eval forward through dstd_model_fwd_ex.  The folded constants
         and split-f16 weight images a forward leaves in the workspace are
-        reused when nothing changed since (same parameter storage, torch
-        version counters unchanged -- no in-place update --, batch size,
-        arithmetic mode, and no other user of the workspace in between)."""
+        reused when nothing changed since: same model instance (a token never
+        reused) and cache generation (invalidate_native_cache), same parameter
+        storage, torch version counters unchanged (no in-place update), batch
+        size, arithmetic, and no other user of the workspace in between.
+        Tensors without version counters (inference tensors) never reuse."""
         L = native.lib()
         n, t, v, _ = x.shape
         dev = x.device
         p = self._native_params()
-        tensors = self._native_tensors
-        tag = (id(self), id(p), n, L.dstd_get_gc_precision(), tuple(tt._version for tt in tensors))
+        flags = native.arith_flags(self.gc_arithmetic)
+        try:
+            versions = tuple(tt._version for tt in self._native_tensors)
+            tag = (self._dstd_uid, self._dstd_gen, tuple(self._native[0]), n, flags, versions)
+        except RuntimeError:  # "Inference tensors do not track version counter"
+            tag = None
         nbytes = L.dstd_model_workspace_bytes(n, t, v, self.num_feature, self.num_layers)
         ws, reuse = native.workspace_claim(dev, nbytes, tag)
+        if reuse:
+            flags |= native.FWD_REUSE_CONSTANTS
         code = L.dstd_model_fwd_ex(p, native.ptr(x, "x"), n, native.ptr(y, "y"), ws.data_ptr(), ws.numel(),
-                                   native.stream_handle(dev), native.FWD_REUSE_CONSTANTS if reuse else 0, prof)
+                                   native.stream_handle(dev), flags, prof)
         native.check(code, "dstd_model_fwd_ex")

@@ -118,6 +118,9 @@ int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, i
 /* y = DSTDGCB(x) in eval mode; x [B][cin][T][V] -> y [B][cout][T][V]. */
 int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float* y,
                    void* workspace, size_t workspace_bytes, void* stream);
+/* dstd_block_fwd with flags (DSTD_FWD_EXACT_FP32 only). */
+int dstd_block_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float* y,
+                      void* workspace, size_t workspace_bytes, void* stream, unsigned flags);
 
 /* y = DSTDGCN(x) in eval mode; x, y [B][T][V][in_channels/2]. */
 int dstd_model_fwd(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
@@ -161,24 +164,23 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
  * parameter-preparation launches are skipped.  The caller vouches for it
  * (the Python layer checks torch's per-tensor version counters). */
 #define DSTD_FWD_REUSE_CONSTANTS 1u
+/* Arithmetic of the graph convolutions, per call (no process-wide state).
+ * Default (flag clear): split-f16 MFMA -- each fp32 operand as an f16 hi/lo
+ * pair under a power-of-two range scale, three v_mfma_f32_16x16x32_f16 per
+ * product, fp32 accumulation -- where the shape has kernels: (T, V) in
+ * {(35,22), (35,25), (40,23), (75,22)}, Cin/Cout 64 (6 -> 64 and 64 -> 3 at
+ * the model's ends); everything else exact fp32.  DSTD_FWD_EXACT_FP32: the
+ * exact-fp32 MFMA kernels (v_mfma_f32_16x16x4_f32) everywhere.  Both stay
+ * within the reference parity bars over the whole fp32 range
+ * (tests/test_gpu_parity.py).  No counterpart in the reference (pure fp32
+ * ATen, model/dstdgcn.py:80-94). */
+#define DSTD_FWD_EXACT_FP32 2u
 int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof);
 int dstd_events_create(int n, void** events);
 int dstd_events_destroy(int n, void** events);
 int dstd_event_elapsed_ms(void* start, void* stop, float* ms);
 
-/* Arithmetic of the 64 -> 64 graph convolutions of dstd_block_fwd /
- * dstd_model_fwd (process-wide; default from env DSTD_HILO, else 1):
- *   1  split-f16 MFMA (each fp32 operand as an f16 hi/lo pair, three
- *      v_mfma_f32_16x16x32_f16 per product, fp32 accumulation; 22-bit
- *      operands) where the shape has kernels: (T, V) in {(35,22), (35,25),
- *      (40,23), (75,22)};
- *   0  exact-fp32 MFMA (v_mfma_f32_16x16x4_f32) everywhere.
- * Outputs of both stay within the parity bar against the reference
- * (tests/test_gpu_parity.py).  No counterpart in the reference (pure fp32
- * ATen, model/dstdgcn.py:80-94).  Returns DSTD_EINVAL for other modes. */
-int dstd_set_gc_precision(int mode);
-int dstd_get_gc_precision(void);
 
 #ifdef __cplusplus
 }

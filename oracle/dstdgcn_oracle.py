@@ -23,10 +23,10 @@ BN_EPS = 1e-5  # nn.BatchNorm1d default, model/dstdgcn.py:42
 BN_RECORD = None
 
 
-def _t(a, dtype):
+def _t(a, dtype, device="cpu"):
     if torch.is_tensor(a):
-        return a.detach().to("cpu", dtype)
-    return torch.as_tensor(a, dtype=dtype)
+        return a.detach().to(device, dtype)
+    return torch.as_tensor(a, dtype=dtype, device=device)
 
 
 def conv1x1(x, w, b):
@@ -112,12 +112,14 @@ def dstdgcb(x, p, training=False):
     return dstdgc(h, sub(p, "conv_t.0."), a_t, p["alpha_tm"], "temporal")
 
 
-def dstdgcn(x, sd, num_layers, dtype=torch.float64, training=False):
+def dstdgcn(x, sd, num_layers, dtype=torch.float64, training=False, device="cpu"):
     """DSTDGCN.forward (model/dstdgcn.py:293-317), dropout treated as eval.
 
-    x: [N, T, V, 3]; sd: reference state dict (numpy or tensors)."""
-    sd = {k: _t(v, dtype) for k, v in sd.items() if not k.endswith("num_batches_tracked")}
-    return dstdgcn_fn(_t(x, dtype), sd, num_layers, training)
+    x: [N, T, V, 3]; sd: reference state dict (numpy or tensors).  ``device``
+    other than the CPU only serves scripts/parity_report.py (the reference
+    forward's own fp32 error on the GPU box, torch-ROCm ops)."""
+    sd = {k: _t(v, dtype, device) for k, v in sd.items() if not k.endswith("num_batches_tracked")}
+    return dstdgcn_fn(_t(x, dtype, device), sd, num_layers, training)
 
 
 def dstdgcn_fn(x, sd, num_layers, training=False):

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.." || exit 2
 mkdir -p gpurun_out
 ok_status() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 
-timeout -k 10 ${PYTEST_TIMEOUT:-600} python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 st=$?; echo "pytest exit $st"; tail -25 gpurun_out/pytest_gpu.log
 ok_status $st || exit $st
 

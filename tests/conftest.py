@@ -31,6 +31,12 @@ def rel_err(y, ref):
     return float(np.abs(y - ref).max() / max(np.abs(ref).max(), 1e-30))
 
 
+def model_tol(ref32_err):
+    """Whole-model parity bar of SURVEY §8(c): max|y - y64| / max|y64| <=
+    max(1e-4, 2 x the reference's own fp32-vs-fp64 error on the same input)."""
+    return max(1e-4, 2.0 * float(ref32_err))
+
+
 @pytest.fixture(scope="session")
 def golden():
     return load_npz

@@ -22,23 +22,26 @@ def header_symbols(name="dstd_gcn.h"):
 def test_library_exports_every_header_symbol():
     L = native.lib()
     syms = header_symbols()
-    assert len(syms) == 15, syms
+    assert len(syms) == 14, syms
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(native.EXPORTS)
 
 
-def test_gc_precision_switch_without_gpu():
-    """The arithmetic switch of the 64->64 GC kernels is host state only."""
+def test_arithmetic_is_a_per_call_flag():
+    """No process-wide arithmetic state: the choice travels with each call
+    (DSTD_FWD_EXACT_FP32); unknown flag bits are rejected before any GPU work."""
     L = native.lib()
-    prev = L.dstd_get_gc_precision()
-    assert prev in (0, 1)
-    assert L.dstd_set_gc_precision(2) == -1  # DSTD_EINVAL
-    assert native.set_gc_precision("fp32") in ("fp32", "split")
-    assert L.dstd_get_gc_precision() == 0
-    assert native.set_gc_precision("split") == "fp32"
-    assert L.dstd_get_gc_precision() == 1
-    L.dstd_set_gc_precision(prev)
+    assert not hasattr(L, "dstd_set_gc_precision")
+    assert native.arith_flags("split") == 0 and native.arith_flags("fp32") == native.FWD_EXACT_FP32
+    with pytest.raises(ValueError):
+        native.arith_flags("bf16")
+    assert L.dstd_block_fwd_ex(None, None, 4, 35, 22, None, None, 0, None, 4) == -1  # DSTD_EINVAL
+    assert L.dstd_model_fwd_ex(None, None, 4, None, None, 0, None, 8, None) == -1
+    m = get_model("dstdgcn", dstdgcn=H36M)
+    assert m.gc_arithmetic == "split"
+    m.set_gc_arithmetic("fp32")
+    assert all(b.gc_arithmetic == "fp32" for b in m.modules() if isinstance(b, DSTDGCB))
 
 
 def test_library_exports_every_training_header_symbol():

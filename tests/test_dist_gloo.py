@@ -197,3 +197,62 @@ def test_allreduce_grads_reduces_the_arena_in_place():
         assert direct and same_base
         for m, a in zip(mean, avg):
             assert torch.allclose(m, a)
+
+
+# ---- sharded test metric of the engine (engine/prediction.py:391-404) -------
+def _engine_metric_body(rank, world):
+    """PredictionEngine.test under torch.distributed: each rank evaluates its
+    round-robin share of the loader's batches and the per-frame sums / counts
+    are all-reduced.  No GPU in this leg: the model is the fp64 oracle and the
+    per-batch metric the oracle's restatement of :366-404 (the native forward
+    and the dstd_frame_mpjpe kernel are checked on the GPU,
+    tests/test_gpu_train.py::test_engine_test_metric_matches_reference)."""
+    from engine import PredictionEngine
+    from oracle import dstdgcn_oracle as O
+    d = load_npz("engine.npz")
+    sd = group(d, "test/sd/")
+
+    class OracleModel(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.anchor = torch.nn.Parameter(torch.zeros(1))  # gives the engine a device
+
+        def forward(self, x):
+            return O.dstdgcn(x, sd, 5).float()
+
+    class CPUEngine(PredictionEngine):
+        seen = []
+
+        def _frame_metric(self, all_seqs, outputs, t_out0, used_pos, joint_src, frames, sums):
+            self.seen.append(all_seqs.shape[0])
+            pred = self._fill_pred(all_seqs, outputs, used_pos, joint_src, t_out0).double()
+            targ = all_seqs.view(pred.shape).double()
+            for k, f in enumerate(frames.tolist()):
+                sums[k] += float((targ[:, f] - pred[:, f]).norm(dim=-1).mean(dim=1).sum())
+
+    class _Log:
+        def info(self, *a, **k):
+            pass
+
+    cfg = dict(learn=dict(opt="adam", lr=3e-3, weight_decay=0, gamma=0.9, step_size=5),
+               loss=dict(joint=["jl2", 1]), n_out=1, transform="tsc", use_weight=False, inverse=True)
+    eng = CPUEngine(cfg, OracleModel(), _Log())
+    inputs = torch.from_numpy(d["test/inputs"])
+    all_seqs = torch.from_numpy(d["test/all_seqs"])
+    # three batches (2, 1, 1): rank 0 takes batches 0 and 2, rank 1 batch 1
+    loader = [(inputs[:2], None, None, all_seqs[:2]), (inputs[2:3], None, None, all_seqs[2:3]),
+              (inputs[3:], None, None, all_seqs[3:])]
+    avg, metric = eng.test(loader, input_n=10, eval_frame=list(d["test/eval_frame"]), dim_used=d["test/dim_used"],
+                           joint_to_ignore=d["test/joint_to_ignore"], joint_equal=d["test/joint_equal"])
+    return avg, metric, list(CPUEngine.seen)
+
+
+def test_engine_test_metric_sharded_equals_reference():
+    d = load_npz("engine.npz")
+    res = run_world("_engine_metric_body")
+    ref, ref_avg = d["test/metric"], float(d["test/avg"])
+    assert res[0][2] == [2, 1] and res[1][2] == [1]  # the batches each rank evaluated
+    for r in (0, 1):
+        avg, metric, _ = res[r]
+        assert float((torch.as_tensor(metric) - torch.from_numpy(ref)).abs().max()) <= 2e-4 * float(abs(ref).max())
+        assert abs(avg - ref_avg) <= 2e-4 * ref_avg

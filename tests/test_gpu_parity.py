@@ -1,23 +1,30 @@
 """MI355X parity: the HIP path vs the reference's own outputs (golden fixtures,
 fp64) and vs the CPU oracle.  Tolerance:
   per op / block : max|y - y64| / max|y64| <= 1e-4
-  whole model    : <= max(1e-4, 4 * ref32_err) where ref32_err is the
-                   reference's own fp32-vs-fp64 error on that fixture.
-The 21-op stack amplifies a 1e-7 rounding difference ~10^3x:
-any fp32 summation order lands at ~0.5-2x ref32_err (measured, see
-scripts/parity_report.py), while every op and block stays at ~1x.
+  whole model    : <= max(1e-4, 2 * ref32_err) (conftest.model_tol) where
+                   ref32_err is the reference's own fp32-vs-fp64 error on
+                   that input (the fixture's, or the fp32 oracle's live).
+The 21-op stack amplifies a 1e-7 rounding difference ~10^3x;
+per-fixture ratios of both arithmetics: profiles/r02_parity_report.json
+(scripts/parity_report.py).
 
-Blocks and whole models run under both GC arithmetics of the library
-(dstd_set_gc_precision): "split" (split-f16 MFMA, 22-bit operands, the
-default) and "fp32" (exact-fp32 MFMA); both must meet the same bars.
+Blocks and whole models run under both GC arithmetics of the library (a
+per-call flag, DSTDGCN.set_gc_arithmetic / DSTDGCB.gc_arithmetic): "split"
+(split-f16 MFMA under a power-of-two range scale, the default) and "fp32"
+(exact-fp32 MFMA).  The fixture models hold the 2x bar in the default
+arithmetic; for both arithmetics the error ratio err / ref32 is also checked
+over 8 synthetic inputs per layout (test_model_error_distribution): one
+input is one draw of a chaotic amplification, and the exact
+path's draw on the T=75 fixture lands at 2.4x while its distribution has
+median 1.0x, max 1.6x (scripts/parity_stats.py).
 """
 import numpy as np
 import pytest
 import torch
 
-from conftest import group, load_npz, rel_err
-import dstd_native
+from conftest import group, load_npz, model_tol, rel_err
 from model import DSTDGC, DSTDGCB, DSTDGCN, get_model
+from model.dstdgcn import invalidate_native_cache
 from oracle import dstdgcn_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -48,18 +55,16 @@ def t(a):
 
 @pytest.fixture(params=["split", "fp32"])
 def precision(request):
-    prev = dstd_native.set_gc_precision(request.param)
-    yield request.param
-    dstd_native.set_gc_precision(prev)
+    return request.param
 
 
-def load_model(tag):
+def load_model(tag, arith="split"):
     d = load_npz(f"model_{tag}.npz")
     opts = {k[4:]: d[k].item() for k in d.files if k.startswith("opt/")}
     m = get_model("dstdgcn", dstdgcn=opts)
     sd = group(d, "sd/")
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    return m.to(DEV).eval(), d, sd, opts
+    return m.to(DEV).eval().set_gc_arithmetic(arith), d, sd, opts
 
 
 @pytest.mark.parametrize("name", list(OPS))
@@ -83,19 +88,39 @@ def test_dstdgcb_block(name, precision):
     blk = DSTDGCB(cin, cout, T, V, layout)
     blk.load_state_dict({k: torch.from_numpy(v) for k, v in group(d, f"{name}/sd/").items()})
     blk = blk.to(DEV).eval()
+    blk.gc_arithmetic = precision
     with torch.no_grad():
         y = blk(t(d[f"{name}/x"]))
     assert rel_err(y.cpu().numpy(), d[f"{name}/y64"]) <= 1e-4
 
 
 @pytest.mark.parametrize("tag", MODELS)
-def test_dstdgcn_model(tag, precision):
+def test_dstdgcn_model(tag):
     m, d, _, _ = load_model(tag)
     with torch.no_grad():
         y = m(t(d["x"]))
-    tol = max(1e-4, 4 * float(d["ref32_err"]))
+    tol = model_tol(d["ref32_err"])
     err = rel_err(y.cpu().numpy(), d["y64"])
     assert err <= tol, (err, tol)
+
+
+@pytest.mark.parametrize("tag", MODELS)
+def test_model_error_distribution(tag, precision):
+    """err / ref32 over 8 synthetic B=4 inputs (ref32: the reference's own
+    fp32 error on the same input, from the fp32 oracle): median <= 1.25 and
+    every input within the 2x bar."""
+    m, d, sd, opts = load_model(tag, precision)
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    ratios = []
+    for i in range(8):
+        x = synth(4, T, opts["joints_to_consider"], opts["input_time_frame"], 1000 + i)
+        with torch.no_grad():
+            y = m(x.to(DEV)).cpu().numpy()
+        y64 = O.dstdgcn(x, sd, opts["num_layers"]).numpy()
+        ref32 = rel_err(O.dstdgcn(x, sd, opts["num_layers"], dtype=torch.float32).numpy(), y64)
+        ratios.append(rel_err(y, y64) / ref32)
+        assert rel_err(y, y64) <= model_tol(ref32), (i, ratios)
+    assert float(np.median(ratios)) <= 1.25, ratios
 
 
 def synth(B, T, V, Tin, seed):
@@ -109,7 +134,7 @@ def test_large_batch_vs_oracle_and_sample_independence(precision):
     """B=256 (the bench workload): samples checked against the fp64 oracle,
     and every sample equals its own B=1 run bit for bit (no cross-sample
     coupling in eval; the property behind data-parallel sharding)."""
-    m, d, sd, opts = load_model("h36m")
+    m, d, sd, opts = load_model("h36m", precision)
     T = opts["input_time_frame"] + opts["output_time_frame"]
     x = synth(256, T, 22, opts["input_time_frame"], 7)
     with torch.no_grad():
@@ -119,13 +144,13 @@ def test_large_batch_vs_oracle_and_sample_independence(precision):
             yi = m(x[i:i + 1].to(DEV)).cpu()
             assert torch.equal(yi[0], y[i]), i
     y64 = O.dstdgcn(x[picks], sd, opts["num_layers"]).numpy()
-    tol = max(1e-4, 4 * float(d["ref32_err"]))
+    tol = model_tol(d["ref32_err"])
     assert rel_err(y[picks].numpy(), y64) <= tol
 
 
 @pytest.mark.parametrize("B", [1, 3, 257])
 def test_ragged_batches(B, precision):
-    m, d, sd, opts = load_model("3dpw")
+    m, d, sd, opts = load_model("3dpw", precision)
     T = opts["input_time_frame"] + opts["output_time_frame"]
     x = synth(B, T, 23, opts["input_time_frame"], B)
     with torch.no_grad():
@@ -133,7 +158,7 @@ def test_ragged_batches(B, precision):
     assert torch.isfinite(y).all()
     k = min(B, 3)
     y64 = O.dstdgcn(x[:k], sd, opts["num_layers"]).numpy()
-    assert rel_err(y[:k].numpy(), y64) <= max(1e-4, 4 * float(d["ref32_err"]))
+    assert rel_err(y[:k].numpy(), y64) <= model_tol(d["ref32_err"])
 
 
 def test_empty_batch():
@@ -159,16 +184,10 @@ def test_split_vs_fp32_bench_batch():
     m, d, sd, opts = load_model("h36m")
     T = opts["input_time_frame"] + opts["output_time_frame"]
     x = synth(256, T, 22, opts["input_time_frame"], 21).to(DEV)
-    prev = dstd_native.set_gc_precision("fp32")
-    try:
-        with torch.no_grad():
-            y32 = m(x).cpu()
-        dstd_native.set_gc_precision("split")
-        with torch.no_grad():
-            ys = m(x).cpu()
-    finally:
-        dstd_native.set_gc_precision(prev)
-    tol = max(1e-4, 4 * float(d["ref32_err"]))
+    with torch.no_grad():
+        y32 = m.set_gc_arithmetic("fp32")(x).cpu()
+        ys = m.set_gc_arithmetic("split")(x).cpu()
+    tol = model_tol(d["ref32_err"])
     assert torch.isfinite(ys).all()
     assert rel_err(ys.numpy(), y32.numpy()) <= tol
     picks = [0, 100, 255]
@@ -198,6 +217,25 @@ def test_constant_reuse_tracks_parameter_updates():
         blk = m.encoders[1][0].stgcn[0][0]
         blk(torch.randn(2, 64, 35, 22, device=DEV))
         assert torch.equal(m(x), y2)
+        # a write through .data is invisible to the version counters:
+        # invalidate_native_cache (what dstd_dist.broadcast_module calls)
+        m.conv_st_out.stgcn[0][0].conv_t[0].conv_f.weight.data.mul_(0.5)
+        invalidate_native_cache(m)
+        y3 = m(x)
+        m3, _, _, _ = load_model("h36m")
+        m3.encoders[0][1].bn.weight.data.mul_(1.5)
+        m3.conv_st_out.stgcn[0][0].conv_t[0].conv_f.weight.data.mul_(0.5)
+        assert torch.equal(y3, m3(x))
+        # a new model on the same workspace after the old one is gone (id()
+        # reuse must not alias the two): fresh instance token, fresh fold
+        del m, m2, m3
+        m4, _, _, _ = load_model("h36m")
+        assert torch.equal(m4(x), y0)
+    # parameters created in inference mode carry no version counter: no reuse, still right
+    with torch.inference_mode():
+        m5, _, _, _ = load_model("h36m")
+        xi = t(d["x"])
+        assert torch.equal(m5(xi), y0) and torch.equal(m5(xi), y0)
 
 
 def test_deterministic_repeat():
@@ -274,7 +312,7 @@ def test_dstdgcn_generic_T30():
     m = m.to(DEV).eval()
     with torch.no_grad():
         y = m(x.to(DEV)).cpu().numpy()
-    assert rel_err(y, y64) <= max(1e-4, 4 * ref32), ref32
+    assert rel_err(y, y64) <= model_tol(ref32), ref32
 
 
 @pytest.mark.parametrize("cin,cout", [(64, 64), (6, 64), (64, 3)])
@@ -299,4 +337,104 @@ def test_dstdgcb_generic_T30(cin, cout):
     blk = blk.to(DEV).eval()
     with torch.no_grad():
         y = blk(x.to(DEV)).cpu().numpy()
+    assert rel_err(y, y64) <= 1e-4
+
+
+# ---- B=256 (the bench batch size) for every layout: the persistent unit loop
+# (several units per wave, next-unit prefetch) against the oracle -----------
+@pytest.mark.parametrize("tag,V", [("cmu", 25), ("h36m75", 22), ("3dpw", 23)])
+def test_large_batch_layouts_vs_oracle(tag, V, precision):
+    m, d, sd, opts = load_model(tag, precision)
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    x = synth(256, T, V, opts["input_time_frame"], 31)
+    picks = [0, 131, 255]
+    with torch.no_grad():
+        y = m(x.to(DEV)).cpu()
+        y1 = m(x[131:132].to(DEV)).cpu()
+    assert torch.isfinite(y).all()
+    assert torch.equal(y1[0], y[131])  # sample independence at this shape
+    y64 = O.dstdgcn(x[picks], sd, opts["num_layers"]).numpy()
+    ref32 = rel_err(O.dstdgcn(x[picks], sd, opts["num_layers"], dtype=torch.float32).numpy(), y64)
+    assert rel_err(y[picks].numpy(), y64) <= model_tol(ref32), ref32
+
+
+# ---- range: the split arithmetic over the whole fp32 range ------------------
+# (dstd_hilo.h "range scaling").  A freshly constructed
+# model with untouched BatchNorm statistics drives activations to ~1e5-1e6
+# inside the stack and mm-scale poses put ~1e3 into the input;
+# both exceed what an unscaled f16 half holds (65504).
+H36M_YAML = dict(input_channels=6, input_time_frame=10, output_time_frame=25, st_gcnn_dropout=0.1,
+                 joints_to_consider=22, num_feature=64, num_layers=5, layout="h36m")  # dstdgcn_h36m.yaml:136-143
+
+
+def fresh_h36m(seed):
+    torch.manual_seed(seed)
+    return get_model("dstdgcn", dstdgcn=H36M_YAML)
+
+
+@pytest.mark.parametrize("B,scale", [(4, 1.0), (256, 1.0), (4, 1000.0)])
+def test_fresh_model_untouched_bn(B, scale, precision):
+    """config 1's "construct and forward" model: dynamic terms zero, BN at
+    its initial statistics; N(0,1) poses (activations reach ~1e6) and the
+    same in millimetres (~1e9)."""
+    m = fresh_h36m(5 + B)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    x = synth(B, 35, 22, 10, 40 + B) * scale
+    m = m.to(DEV).eval().set_gc_arithmetic(precision)
+    with torch.no_grad():
+        y = m(x.to(DEV)).cpu()
+    assert torch.isfinite(y).all()
+    picks = list(range(B)) if B <= 4 else [0, 97, 255]
+    y64 = O.dstdgcn(x[picks], sd, 5).numpy()
+    assert np.abs(y64).max() > 1e6 * scale  # the regime this test is about
+    ref32 = rel_err(O.dstdgcn(x[picks], sd, 5, dtype=torch.float32).numpy(), y64)
+    assert rel_err(y[picks].numpy(), y64) <= model_tol(ref32), ref32
+
+
+@pytest.mark.parametrize("tag", MODELS)
+def test_mm_scale_inputs(tag, precision):
+    """Poses in millimetres (the reference's H36M / CMU data after expmap ->
+    xyz): the fixture poses x1000 into the fixture model whose first-layer
+    weights that read the input (conv_st_in's conv_f, conv_m1/m2 and residual
+    conv) are /1000, i.e. a model trained on mm data.  (The fixture model
+    itself on x1000 inputs is chaotic in fp32 -- the reference's own fp32
+    output is off its fp64 one by ~100% -- so it pins nothing.)"""
+    m, d, sd, opts = load_model(tag, precision)
+    sd = {k: torch.from_numpy(v).clone() for k, v in sd.items()}
+    for k in sd:
+        if k.startswith("conv_st_in.stgcn.0.0.") and k.endswith("weight") and (
+                ".conv_f." in k or ".conv_m1." in k or ".conv_m2." in k or ".residual.0." in k) and ".conv_t." not in k:
+            sd[k] = sd[k] / 1000.0
+    m.load_state_dict(sd)
+    x = torch.from_numpy(d["x"]) * 1000.0
+    with torch.no_grad():
+        y = m(x.to(DEV)).cpu().numpy()
+    assert np.isfinite(y).all()
+    y64 = O.dstdgcn(x, sd, opts["num_layers"]).numpy()
+    ref32 = rel_err(O.dstdgcn(x, sd, opts["num_layers"], dtype=torch.float32).numpy(), y64)
+    assert rel_err(y, y64) <= model_tol(ref32), ref32
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 64), (6, 64), (64, 3)])
+def test_block_large_adjacency_and_activations(cin, cout, precision):
+    """|alpha * D + A| far above 2^14 (range-shifted adjacency planes) and
+    activations ~1e6 on one block, per-block bar 1e-4."""
+    torch.manual_seed(100 + cin + cout)
+    blk = DSTDGCB(cin, cout, 35, 22, "h36m")
+    with torch.no_grad():
+        blk.alpha_sm.fill_(3.0e4)
+        blk.alpha_tm.fill_(-2.0e4)
+        blk.W_s.copy_(0.2 * torch.randn(blk.W_s.shape))
+        blk.R_t.copy_(0.1 * torch.randn(blk.R_t.shape))
+        for mod in blk.modules():
+            if isinstance(mod, torch.nn.Conv2d):
+                mod.bias.copy_(0.1 * torch.randn(mod.bias.shape))
+    x = 1.0e6 * torch.randn(2, cin, 35, 22)
+    sd = {k: v.clone() for k, v in blk.state_dict().items()}
+    y64 = O.dstdgcb_forward(x, sd).numpy()
+    blk = blk.to(DEV).eval()
+    blk.gc_arithmetic = precision
+    with torch.no_grad():
+        y = blk(x.to(DEV)).cpu().numpy()
+    assert np.isfinite(y).all()
     assert rel_err(y, y64) <= 1e-4

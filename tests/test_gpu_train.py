@@ -234,6 +234,7 @@ def test_gradient_sink_paths_agree():
     # (alphas, PReLU slopes, ~1e-5 measured), far inside their fp32 noise
     TOL = 1e-4
     params = [p for p in m.parameters() if p.requires_grad]
+    m._dstd_inplace_grads = True  # what engine.PredictionEngine.train opts into
     step()  # direct: .grad were None
     g_direct = [p.grad.clone() for p in params]
     bases = {p.grad._base.data_ptr() for p in params}
@@ -250,6 +251,22 @@ def test_gradient_sink_paths_agree():
     m.zero_grad(set_to_none=True)
     step()  # back to the in-place arena
     assert all(p.grad._base is not None for p in params)
+    # a parameter hook (DDP, user hooks) turns the in-place path off ...
+    m.zero_grad(set_to_none=True)
+    h = params[0].register_hook(lambda g: g)
+    step()
+    h.remove()
+    assert all(p.grad._base is None for p in params)
+    for p, g in zip(params, g_direct):
+        assert float((p.grad - g).abs().max()) <= TOL * float(g.abs().max()) + 1e-12
+    # ... and so does not opting in (the default for every caller but the engine)
+    m._dstd_inplace_grads = False
+    m.zero_grad(set_to_none=True)
+    step()
+    assert all(p.grad._base is None for p in params)
+    grads = torch.autograd.grad(  # autograd.grad sees the gradients and leaves .grad alone
+        mpjpe_error_3d(m(inp.view(B, T, 23, 3)).view(B, T, VC), seq), params)
+    assert all(g is not None for g in grads)
 
 
 def test_autocast_bf16_runs_the_fp32_path():

@@ -37,7 +37,7 @@ def test_oracle_dstdgcn(tag):
     assert rel_err(y.numpy(), d["y64"]) < 1e-6
     # fp32 restatement lands within the reference's own fp32 error band
     y32 = O.dstdgcn(d["x"], sd, int(d["opt/num_layers"]), dtype=torch.float32)
-    assert rel_err(y32.numpy(), d["y64"]) < max(1e-4, 4 * float(d["ref32_err"]))
+    assert rel_err(y32.numpy(), d["y64"]) <= max(1e-4, 2 * float(d["ref32_err"]))
 
 
 def test_oracle_mpjpe():
