@@ -94,9 +94,10 @@ struct BlockFold {
   float* hl_rbias;  // [2T + V]: fused conv_rm biases (HLJob::bias_out) of rms0, rms1, rmt
 };
 
-// Which GC launches of a block run the split-f16 kernels.
+// Which GC launches of a block run the split-f16 kernels; tf: the temporal
+// one with its adjacency built in LDS (k_temporal_fused, no k_adj_hl<1>).
 struct BlockHL {
-  bool s, t;
+  bool s, t, tf;
 };
 
 struct BlockScratch {
@@ -257,7 +258,7 @@ struct BlockTail {
 // Split-f16 GC kernels (dstd_hilo.hip) where the shape has them, unless the
 // call asks for exact fp32 (DSTD_FWD_EXACT_FP32).
 BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V, bool exact) {
-  BlockHL r{false, false};
+  BlockHL r{false, false, false};
   if (exact) return r;
   r.s = spatial_hl_supported(T, V) &&
         ((p->cin == 64 && p->cout == 64) || (p->cin == 6 && p->cout == 64) || (p->cin == 64 && p->cout == 3));
@@ -265,6 +266,9 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V
         ((p->cout == 64 && (tail.epi == TEPI_ENC || tail.epi == TEPI_IN || tail.epi == TEPI_RAW) &&
           (!tail.next || tail.next->cin == 64)) ||
          (p->cout == 3 && (tail.epi == TEPI_OUT || tail.epi == TEPI_RAW) && !tail.next));
+#ifndef DSTD_NO_TFUSED
+  r.tf = r.t && temporal_fused_supported(T, V);
+#endif
   return r;
 }
 
@@ -482,28 +486,28 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ta.ldo = adj_ld_temporal(T);
     ta.out_sN = (long)V * ta.ldo;
   }
-  pf.begin(DSTD_KIND_ADJ_T, s);
+  AdjHLArgs aht{};
   if (hl.t) {
-    AdjHLArgs ah{};
-    ah.pq = ta.pq;
-    ah.pql = ta.pql;
-    ah.B = B;
-    ah.ngroups = 1;
-    ah.p_ch[0] = ta.p_ch[0];
-    ah.wimg[0] = f.hl_rmt;
-    ah.wscale[0] = hls(f, 7);
-    ah.bias[0] = f.hl_rbias + 2 * T;
-    ah.astat[0] = ta.astat[0];
-    ah.alpha = ta.alpha;
-    ah.out = reinterpret_cast<uint16_t*>(ta.out);
-    ah.out_sN = 2 * ta.out_sN;
-    ah.out_sG = 0;
-    e = launch_adj_hl(ah, 1, T, V, s);
-  } else {
-    e = launch_adj(ta, s);
+    aht.pq = ta.pq;
+    aht.pql = ta.pql;
+    aht.B = B;
+    aht.ngroups = 1;
+    aht.p_ch[0] = ta.p_ch[0];
+    aht.wimg[0] = f.hl_rmt;
+    aht.wscale[0] = hls(f, 7);
+    aht.bias[0] = f.hl_rbias + 2 * T;
+    aht.astat[0] = ta.astat[0];
+    aht.alpha = ta.alpha;
+    aht.out = reinterpret_cast<uint16_t*>(ta.out);
+    aht.out_sN = 2 * ta.out_sN;
+    aht.out_sG = 0;
   }
-  pf.end(s);
-  if (e != hipSuccess) return e;
+  if (!hl.tf) {  // the fused temporal kernel builds its adjacency itself
+    pf.begin(DSTD_KIND_ADJ_T, s);
+    e = hl.t ? launch_adj_hl(aht, 1, T, V, s) : launch_adj(ta, s);
+    pf.end(s);
+    if (e != hipSuccess) return e;
+  }
 
   // (4) temporal GC + tail epilogue (+ next block's spatial P/Q)
   if (hl.t) {
@@ -535,7 +539,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
       ht.pq = sc.pq_s;
     }
     pf.begin(DSTD_KIND_TEMPORAL, s);
-    e = launch_temporal_hl(ht, s);
+    e = hl.tf ? launch_temporal_fused(ht, aht, s) : launch_temporal_hl(ht, s);
     pf.end(s);
     return e;
   }

@@ -283,5 +283,10 @@ hipError_t launch_spatial_hl(const SpatialHLArgs& a, hipStream_t s);
 hipError_t launch_temporal_hl(const TemporalHLArgs& a, hipStream_t s);
 bool spatial_hl_supported(int T, int V);
 bool temporal_hl_supported(int T, int V);
+// the temporal GC with its adjacency built in LDS (k_temporal_fused): g as for
+// launch_temporal_hl (g.adj unused), j the adjacency's inputs as for
+// launch_adj_hl mode 1 (j.out unused); hipErrorNotSupported off its shapes
+hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, hipStream_t s);
+bool temporal_fused_supported(int T, int V);
 
 }  // namespace dstd

@@ -736,58 +736,89 @@ __device__ __forceinline__ void load_row8_at(__amdgpu_buffer_rsrc_t r, uint32_t 
   }
 }
 
-template <int T, int EPI, int C>
-__global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_per_eu(temporal_hl_wpe<T, C>(), temporal_hl_wpe<T, C>()))) void k_temporal_hl(
-    TemporalHLArgs a) {
-  using SM = SlotMap<T, false>;
-  constexpr int SL = SM::SL, MT = SM::MT, NS = SM::NS, NUT = cdiv(T, 16);
-  constexpr int KSI = cdiv(C, 32), NCT = cdiv(C, 16), KSO = cdiv(NCT, 2);
-  constexpr int WIMG = NCT * KSI * 2 * 64, PIMG = KSO * 2 * 64;
-  constexpr int VMAX = 32;
-  constexpr bool use_bn = EPI == TEPI_ENC || EPI == TEPI_IN;
-  constexpr bool use_res = EPI == TEPI_ENC || EPI == TEPI_OUT;
-  static_assert(C == 64 || (C == 3 && (EPI == TEPI_OUT || EPI == TEPI_RAW)), "shapes of the forward");
-  __shared__ uint4 wl[WIMG];
-  __shared__ uint4 pql[PIMG];
-  __shared__ float4 bnl[2][use_bn ? 4 * NCT * VMAX : 1];
-  __shared__ float bfl[16 * NCT];
-  __shared__ float bql[8];
-  __shared__ float scl[2];
-  __shared__ int rng[3];
+// LDS images of one temporal GC launch: conv_f fragments, the next block's
+// P/Q conv fragments, folded BN [c/4][v] for VB joints, biases and scalars
+template <int T, int EPI, int C, int VB>
+struct TemporalStage {
+  static constexpr int KSI = cdiv(C, 32), NCT = cdiv(C, 16), KSO = cdiv(NCT, 2);
+  static constexpr int WIMG = NCT * KSI * 2 * 64, PIMG = KSO * 2 * 64;
+  static constexpr bool use_bn = EPI == TEPI_ENC || EPI == TEPI_IN;
+  uint4 wl[WIMG];
+  uint4 pql[PIMG];
+  float4 bnl[2][use_bn ? 4 * NCT * VB : 1];
+  float bfl[16 * NCT];
+  float bql[8];
+  float scl[2];
+  int rng[3];
+};
 
-  const int tid = threadIdx.x, lane = tid & 63;
+template <int T, int EPI, int C, int VB>
+__device__ __forceinline__ void stage_temporal(const TemporalHLArgs& a, TemporalStage<T, EPI, C, VB>& st, int tid, int nt) {
+  using S = TemporalStage<T, EPI, C, VB>;
+  const bool has_pq = a.pq != nullptr;
+  for (int i = tid; i < S::WIMG; i += nt) st.wl[i] = a.wimg[i];
+  if (has_pq)
+    for (int i = tid; i < S::PIMG; i += nt) st.pql[i] = a.pqimg[i];
+  if constexpr (S::use_bn) {
+    // folded BN vectors [V][C] -> [c/4][v]
+    for (int i = tid; i < a.V * 4 * S::NCT; i += nt) {
+      const int v = i / (4 * S::NCT), c4 = i % (4 * S::NCT);
+      float e[2][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        e[0][q] = 4 * c4 + q < C ? a.bn_s[v * C + 4 * c4 + q] : 0.f;
+        e[1][q] = 4 * c4 + q < C ? a.bn_h[v * C + 4 * c4 + q] : 0.f;
+      }
+      st.bnl[0][c4 * a.V + v] = make_float4(e[0][0], e[0][1], e[0][2], e[0][3]);
+      st.bnl[1][c4 * a.V + v] = make_float4(e[1][0], e[1][1], e[1][2], e[1][3]);
+    }
+  }
+  if (tid < 16 * S::NCT) st.bfl[tid] = tid < C ? a.bf[tid] : 0.f;
+  if (tid < 8) st.bql[tid] = has_pq ? a.pqb[tid >> 1][tid & 1] : 0.f;
+  if (tid == 0) {
+    st.scl[0] = *a.wscale;
+    st.scl[1] = has_pq ? *a.pqscale : 0.f;
+    // range: |W_f|_inf, max|b_f| and the planes' shift
+    st.rng[0] = fexp_bits(__float_as_uint(fmaxf(1.f, a.wscale[HLS_BOUND])));
+    st.rng[1] = fexp_bits(__float_as_uint(a.wscale[HLS_BMAX]));
+    st.rng[2] = hl_range_shift(fexp_bits(__float_as_uint(a.adjb[HLS_BOUND])));
+  }
+}
+
+// The unit loop of the temporal GC over units u, u + ustep, ... < uend
+// (unit = (sample, joint) = n * V + v).  The unit's adjacency B fragments
+// [K-step][u tile] (hi, lo planes) come from load_adj: LAZY = false,
+// load_adj(u, bh[NS][NUT], bo[NS][NUT]) at the top of the unit (the planes in
+// HBM, k_temporal_hl: the loads fly during the conv); LAZY = true,
+// load_adj(u, s, bh[NUT], bo[NUT]) per aggregation K-step (the planes in LDS,
+// k_temporal_fused: 24 fewer live VGPRs).
+#ifndef DSTD_TF_LATE_RES
+#define DSTD_TF_LATE_RES 1
+#endif
+template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad>
+__device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const TemporalStage<T, EPI, C, VB>& st, int u,
+                                               int uend, int ustep, AdjLoad load_adj) {
+  using SM = SlotMap<T, false>;
+  using S = TemporalStage<T, EPI, C, VB>;
+  constexpr int MT = SM::MT, NS = SM::NS, NUT = cdiv(T, 16);
+  constexpr int KSI = S::KSI, NCT = S::NCT, KSO = S::KSO;
+  constexpr bool use_bn = S::use_bn;
+  constexpr bool use_res = EPI == TEPI_ENC || EPI == TEPI_OUT;
+  const uint4* wl = st.wl;
+  const uint4* pql = st.pql;
+  const float* bfl = st.bfl;
+  const float* bql = st.bql;
+  const float* scl = st.scl;
+  const int lane = threadIdx.x & 63;
   const int kl = lane >> 4, cl = lane & 15;
   const int V = a.V;
   const bool has_pq = a.pq != nullptr;
-  constexpr int NT = temporal_nt<T, C>();
-  for (int i = tid; i < WIMG; i += NT) wl[i] = a.wimg[i];
-  if (has_pq)
-    for (int i = tid; i < PIMG; i += NT) pql[i] = a.pqimg[i];
-  if constexpr (use_bn) {
-    stage_bnC<C, NCT>(bnl[0], a.bn_s, V, tid);
-    stage_bnC<C, NCT>(bnl[1], a.bn_h, V, tid);
-  }
-  if (tid < 16 * NCT) bfl[tid] = tid < C ? a.bf[tid] : 0.f;
-  if (tid < 8) bql[tid] = has_pq ? a.pqb[tid >> 1][tid & 1] : 0.f;
-  if (tid == 0) {
-    scl[0] = *a.wscale;
-    scl[1] = has_pq ? *a.pqscale : 0.f;
-    // range: |W_f|_inf, max|b_f| and the planes' shift
-    rng[0] = fexp_bits(__float_as_uint(fmaxf(1.f, a.wscale[HLS_BOUND])));
-    rng[1] = fexp_bits(__float_as_uint(a.wscale[HLS_BMAX]));
-    rng[2] = hl_range_shift(fexp_bits(__float_as_uint(a.adjb[HLS_BOUND])));
-  }
-  __syncthreads();
-  const int efb = __builtin_amdgcn_readfirstlane(rng[0]), eb = __builtin_amdgcn_readfirstlane(rng[1]);
-  const int sa = __builtin_amdgcn_readfirstlane(rng[2]);
-
-  int uend;
-  int u = unit_range(a.B * V, uend);
+  const int efb = __builtin_amdgcn_readfirstlane(st.rng[0]), eb = __builtin_amdgcn_readfirstlane(st.rng[1]);
+  const int sa = __builtin_amdgcn_readfirstlane(st.rng[2]);
   const float pw = use_bn ? *a.prelu : 0.f;
   // a unit's rows: frame t of joint v at t * V * C floats from the unit base
   const uint32_t col_bytes = (uint32_t)((T - 1) * V + 1) * C * 4;
   const uint32_t frame_bytes = (uint32_t)V * C * 4;
-  constexpr uint32_t adj_bytes = 2 * T * SL * 2;  // one (n, v): 2 planes of T x SL halves
   uint32_t xoff[MT];  // conv rows: frame 16m + cl (OOB past T)
 #pragma unroll
   for (int m = 0; m < MT; ++m) xoff[m] = 16 * m + cl < T ? (uint32_t)(16 * m + cl) * frame_bytes : OOB;
@@ -813,26 +844,14 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
   if (u < uend) load_x(u);
   while (u < uend) {
     const int n = u / V, v = u - n * V;
-    const int un = u + 1;
+    const int un = u + ustep;
     const int lz = lane + opaque_zero();
     const size_t cbase = ((size_t)n * T * V + v) * C;
     // Issue order matters: vmcnt retires in order, so every load this unit
     // waits for (adjacency, residual) is issued before the next unit's h-row
     // prefetch, which lands behind them.
-    uint4 bh[NS][NUT], bo[NS][NUT];  // adjacency B fragments [K-step][u tile]
-    {
-      const auto rh = rsrc(a.adj + (size_t)u * (adj_bytes / 2), adj_bytes / 2);  // hi plane
-      const auto rl = rsrc(a.adj + (size_t)u * (adj_bytes / 2) + T * SL, adj_bytes / 2);
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) {
-          const int uo = 16 * ut + cl;
-          const uint32_t off = uo < T && kl < SM::ng(s) ? (uint32_t)(uo * SL + 8 * (SM::goff(s) + kl)) * 2 : OOB;
-          bh[s][ut] = bldu4(rh, off);
-          bo[s][ut] = bldu4(rl, off);
-        }
-    }
+    uint4 bh[LAZY ? 1 : NS][NUT], bo[LAZY ? 1 : NS][NUT];  // adjacency B fragments [K-step][u tile]
+    if constexpr (!LAZY) load_adj(u, bh, bo);
     __builtin_amdgcn_sched_barrier(0);
     // range shift of the unit's rows (0 unless a half could overflow)
     float xm = 0.f;
@@ -889,15 +908,22 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
       }
     }
     // residual of the epilogue: the encoder input (ENC) or the model input's
-    // last observed frame (OUT)
+    // last observed frame (OUT); LAZY (LDS adjacency, no HBM loads to wait
+    // for in the aggregation) defers the ENC residual past the aggregation
+    // so its 48 registers are not live across it
     float4 R[use_res ? NCT : 1][use_res ? NUT : 1];
-    __builtin_amdgcn_sched_barrier(0);
-    if constexpr (EPI == TEPI_ENC) {
+    auto load_res_enc = [&]() {
       const auto rr = rsrc(a.xres + cbase, col_bytes);
 #pragma unroll
       for (int ut = 0; ut < NUT; ++ut)
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) R[ct][ut] = bld4(rr, uoff[ut] + 64 * ct);
+    };
+    constexpr bool late_res = LAZY && DSTD_TF_LATE_RES;
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (EPI == TEPI_ENC && !late_res) {
+      load_res_enc();
+    } else if constexpr (EPI == TEPI_ENC) {
     } else if constexpr (EPI == TEPI_OUT) {
       // x_model [B][T][V][C]: frame T-1 of joint v, 3 channels on lanes kl == 0
       const auto rr = rsrc(a.xres + (((size_t)n * T + T - 1) * V + v) * C, C * 4);
@@ -917,26 +943,29 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
       for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = zero4();
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
+      const int sb = LAZY ? 0 : s;
+      if constexpr (LAZY) load_adj(u, s, bh[0], bo[0]);
       f16x8 dh[NCT], dl[NCT];
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) split_acc(D[2 * s][ct], 2 * s + 1 < MT ? D[2 * s + 1][ct] : zero4(), dh[ct], dl[ct]);
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dl[ct], as_h8(bh[s][ut]), O[ct][ut]);
+        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dl[ct], as_h8(bh[sb][ut]), O[ct][ut]);
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bo[s][ut]), O[ct][ut]);
+        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bo[sb][ut]), O[ct][ut]);
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bh[s][ut]), O[ct][ut]);
+        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bh[sb][ut]), O[ct][ut]);
     }
     // next unit's h rows (unconditional -- the last unit reloads itself -- so
     // that no branch hides the loads from hipcc's vmcnt bookkeeping)
     __builtin_amdgcn_sched_barrier(0);
-    load_x(min(un, uend - 1));
+    if constexpr (EPI == TEPI_ENC && late_res) load_res_enc();
+    load_x(un < uend ? un : u);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- epilogue ----
@@ -961,7 +990,7 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
           o[3] += R[ct][ut].w;
         }
         if constexpr (use_bn) {
-          const float4 sc = bnl[0][(4 * ct + kl) * V + v], sh = bnl[1][(4 * ct + kl) * V + v];
+          const float4 sc = st.bnl[0][(4 * ct + kl) * V + v], sh = st.bnl[1][(4 * ct + kl) * V + v];
           o[0] = prelu_f(fmaf(o[0], sc.x, sh.x), pw);
           o[1] = prelu_f(fmaf(o[1], sc.y, sh.y), pw);
           o[2] = prelu_f(fmaf(o[2], sc.z, sh.z), pw);
@@ -1026,6 +1055,37 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
   }
 }
 
+
+template <int T, int EPI, int C>
+__global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_per_eu(temporal_hl_wpe<T, C>(), temporal_hl_wpe<T, C>()))) void k_temporal_hl(
+    TemporalHLArgs a) {
+  static_assert(C == 64 || (C == 3 && (EPI == TEPI_OUT || EPI == TEPI_RAW)), "shapes of the forward");
+  using SM = SlotMap<T, false>;
+  constexpr int SL = SM::SL, NS = SM::NS, NUT = cdiv(T, 16);
+  __shared__ TemporalStage<T, EPI, C, 32> st;
+  stage_temporal<T, EPI, C, 32>(a, st, threadIdx.x, temporal_nt<T, C>());
+  __syncthreads();
+  int uend;
+  const int u0 = unit_range(a.B * a.V, uend);
+  const int cl = threadIdx.x & 15, kl = (threadIdx.x & 63) >> 4;
+  constexpr uint32_t adj_bytes = 2 * T * SL * 2;  // one (n, v): 2 planes of T x SL halves
+  // the unit's planes in HBM ([B][V][2 planes][T][SL], k_adj_hl), one 16-byte load per fragment
+  auto load_adj = [&](int u, uint4 (&bh)[NS][NUT], uint4 (&bo)[NS][NUT]) {
+    const auto rh = rsrc(a.adj + (size_t)u * (adj_bytes / 2), adj_bytes / 2);  // hi plane
+    const auto rl = rsrc(a.adj + (size_t)u * (adj_bytes / 2) + T * SL, adj_bytes / 2);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int ut = 0; ut < NUT; ++ut) {
+        const int uo = 16 * ut + cl;
+        const uint32_t off = uo < T && kl < SM::ng(s) ? (uint32_t)(uo * SL + 8 * (SM::goff(s) + kl)) * 2 : OOB;
+        bh[s][ut] = bldu4(rh, off);
+        bo[s][ut] = bldu4(rl, off);
+      }
+  };
+  temporal_units<T, EPI, C, 32, false>(a, st, u0, uend, 1, load_adj);
+}
+
 // ===========================================================================
 // Dynamic adjacency in split-f16 planes (DSTDGC.forward model/dstdgcn.py:
 // 83-87 spatial, 88-93 temporal: tanh(P - Q), conv_rm, * alpha + A):
@@ -1040,6 +1100,97 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
 // fragments (HLJ_RM image in LDS) in three 16x16x32 f16 MFMAs.
 // Workgroup = (sample, graph, column chunk), 8 waves over 16-column tiles.
 // ===========================================================================
+
+// ---- pieces of the tanh GEMM shared by k_adj_hl and k_temporal_fused ----
+// N (8 or 4) consecutive tanh(P[k][p] - Q[k][q]) from the E / F rows: SEP:
+// E = 2^(cP), F = 2^(-cQ) and tanh = 1 - 2 / (E F + 1); else P, Q themselves
+template <bool SEP, int N>
+__device__ __forceinline__ void tanh_run(const float* ep, const float* fq, float (&tv)[8]) {
+  float ev[8], fv[8];
+#pragma unroll
+  for (int h = 0; h < N; h += 4) {
+    const float4 e = ld4(ep + h), f = ld4(fq + h);
+    ev[h] = e.x, ev[h + 1] = e.y, ev[h + 2] = e.z, ev[h + 3] = e.w;
+    fv[h] = f.x, fv[h + 1] = f.y, fv[h + 2] = f.z, fv[h + 3] = f.w;
+  }
+  if constexpr (SEP) {
+#pragma unroll
+    for (int e2 = 0; e2 < N; e2 += 2) {  // E F + 1 and 1 - 2 r as packed fp32 (v_pk_fma_f32)
+      const f32x2_t d = __builtin_elementwise_fma(f32x2_t{ev[e2], ev[e2 + 1]}, f32x2_t{fv[e2], fv[e2 + 1]}, f32x2_t{1.f, 1.f});
+      const f32x2_t t = __builtin_elementwise_fma(f32x2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)},
+                                                  f32x2_t{-2.f, -2.f}, f32x2_t{1.f, 1.f});
+      tv[e2] = t.x;
+      tv[e2 + 1] = t.y;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < N; ++e) tv[e] = fast_tanh(ev[e] - fv[e]);
+  }
+#pragma unroll
+  for (int e = N; e < 8; ++e) tv[e] = 0.f;
+}
+
+// B fragments of one 16-column tile: tanh(P[k][p] - Q[k][q]) for
+// k = 32s + 8kg + e (NS full 16x16x32 K-steps) and, with TAIL, k = 32 NS + 4kg
+// + e (one 16x16x16 step), split into hi / lo.  El / Fl: the [p][k] rows of
+// tanh_run; pr / qr: this lane's rows.
+template <bool SEP, int NS, int TAIL, int SE>
+__device__ __forceinline__ void tanh_frags(const float* El, const float* Fl, int pr, int qr, int kg, f16x8 (&bh)[NS],
+                                           f16x8 (&bo)[NS], f16x4& th, f16x4& to) {
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    float tv[8];
+    tanh_run<SEP, 8>(El + pr * SE + 32 * s + 8 * kg, Fl + qr * SE + 32 * s + 8 * kg, tv);
+    split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
+  }
+  if constexpr (TAIL) {
+    float tv[8];
+    tanh_run<SEP, 4>(El + pr * SE + 32 * NS + 4 * kg, Fl + qr * SE + 32 * NS + 4 * kg, tv);
+    uint4 hi, lo;
+    split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+    th = __builtin_bit_cast(f16x4, make_uint2(hi.x, hi.y));
+    to = __builtin_bit_cast(f16x4, make_uint2(lo.x, lo.y));
+  }
+}
+
+// conv_rm on one column tile: acc[rt][row][col] = sum_k W'[16 rt + row][k] B[k][col]
+// (W' = 2^s W, the HLJ_RM image of RT row tiles in LDS)
+template <int RT, int NS, int TAIL>
+__device__ __forceinline__ void rm_mfma(const uint4* wl, int lane, const f16x8 (&bh)[NS], const f16x8 (&bo)[NS],
+                                        const f16x4& th, const f16x4& to, f32x4 (&acc)[RT]) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) acc[rt] = zero4();
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    f16x8 ah[RT], ao[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      ah[rt] = as_h8(wl[((rt * NS + s) * 2 + 0) * 64 + lane]);
+      ao[rt] = as_h8(wl[((rt * NS + s) * 2 + 1) * 64 + lane]);
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ao[rt], bh[s], acc[rt]);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bo[s], acc[rt]);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bh[s], acc[rt]);
+  }
+  if constexpr (TAIL) {
+    const uint2* w16 = reinterpret_cast<const uint2*>(wl + RT * NS * 2 * 64);
+    f16x4 ah[RT], ao[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      ah[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
+      ao[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ao[rt], th, acc[rt], 0, 0, 0);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], to, acc[rt], 0, 0, 0);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], th, acc[rt], 0, 0, 0);
+  }
+}
 
 template <int MODE, int NROW, int K, int NA>
 struct AdjHLGeom {
@@ -1221,89 +1372,11 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       const int q = col / SL, pi = SM::slot_idx(col - q * SL);
       const bool valid = col < NCOL && pi < NA;
       const int pr = valid ? pi : NA, qr = col < NCOL ? q : NA;
-      // ---- B fragments: tanh(P[k][p] - Q[k][q]) for k = 32s + 8kg + e ----
       f16x8 bh[NS], bo[NS];
-  #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const float* ep = El + pr * SE + 32 * s + 8 * kg;
-        const float* fq = Fl + qr * SE + 32 * s + 8 * kg;
-        const float4 e0 = ld4(ep), e1 = ld4(ep + 4), f0 = ld4(fq), f1 = ld4(fq + 4);
-        float tv[8];
-        const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-        const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-        if constexpr (SEP) {
-  #pragma unroll
-          for (int e2 = 0; e2 < 8; e2 += 2) {  // E F + 1 and 1 - 2 r as packed fp32 (v_pk_fma_f32)
-            const f32x2_t d = __builtin_elementwise_fma(f32x2_t{ev[e2], ev[e2 + 1]}, f32x2_t{fv[e2], fv[e2 + 1]}, f32x2_t{1.f, 1.f});
-            const f32x2_t t = __builtin_elementwise_fma(
-                f32x2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}, f32x2_t{-2.f, -2.f}, f32x2_t{1.f, 1.f});
-            tv[e2] = t.x;
-            tv[e2 + 1] = t.y;
-          }
-        } else {
-  #pragma unroll
-          for (int e8 = 0; e8 < 8; ++e8) tv[e8] = fast_tanh(ev[e8] - fv[e8]);
-        }
-        split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
-      }
-      // tail K-step (16x16x16): k = 32 NS + 4kg + e, e < 4
       f16x4 th, to;
-      if constexpr (TAIL) {
-        const float4 e0 = ld4(El + pr * SE + 32 * NS + 4 * kg), f0 = ld4(Fl + qr * SE + 32 * NS + 4 * kg);
-        const float ev[4] = {e0.x, e0.y, e0.z, e0.w}, fv[4] = {f0.x, f0.y, f0.z, f0.w};
-        float tv[4];
-        if constexpr (SEP) {
-  #pragma unroll
-          for (int e2 = 0; e2 < 4; e2 += 2) {
-            const f32x2_t d = __builtin_elementwise_fma(f32x2_t{ev[e2], ev[e2 + 1]}, f32x2_t{fv[e2], fv[e2 + 1]}, f32x2_t{1.f, 1.f});
-            const f32x2_t t = __builtin_elementwise_fma(
-                f32x2_t{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}, f32x2_t{-2.f, -2.f}, f32x2_t{1.f, 1.f});
-            tv[e2] = t.x;
-            tv[e2 + 1] = t.y;
-          }
-        } else {
-  #pragma unroll
-          for (int e4 = 0; e4 < 4; ++e4) tv[e4] = fast_tanh(ev[e4] - fv[e4]);
-        }
-        uint4 hi, lo;
-        split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
-        th = __builtin_bit_cast(f16x4, make_uint2(hi.x, hi.y));
-        to = __builtin_bit_cast(f16x4, make_uint2(lo.x, lo.y));
-      }
-      // ---- conv_rm: acc[row][col] = sum_k W'[row][k] B[k][col] ----
+      tanh_frags<SEP, NS, TAIL, SE>(El, Fl, pr, qr, kg, bh, bo, th, to);
       f32x4 acc[RT];
-  #pragma unroll
-      for (int rt = 0; rt < RT; ++rt) acc[rt] = zero4();
-  #pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        f16x8 ah[RT], ao[RT];
-  #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          ah[rt] = as_h8(wl[((rt * NS + s) * 2 + 0) * 64 + lane]);
-          ao[rt] = as_h8(wl[((rt * NS + s) * 2 + 1) * 64 + lane]);
-        }
-  #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ao[rt], bh[s], acc[rt]);
-  #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bo[s], acc[rt]);
-  #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) acc[rt] = mfma32(ah[rt], bh[s], acc[rt]);
-      }
-      if constexpr (TAIL) {
-        const uint2* w16 = reinterpret_cast<const uint2*>(wl + RT * NS * 2 * 64);
-        f16x4 ah[RT], ao[RT];
-  #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) {
-          ah[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
-          ao[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
-        }
-  #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ao[rt], th, acc[rt], 0, 0, 0);
-  #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], to, acc[rt], 0, 0, 0);
-  #pragma unroll
-        for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], th, acc[rt], 0, 0, 0);
-      }
+      rm_mfma<RT, NS, TAIL>(wl, lane, bh, bo, th, to, acc);
       // ---- epilogue: alpha * (acc + b) + Astat, 0 on padding slots; staged
       // through this wave's LDS slot so a lane stores 8 consecutive slots ----
       // padding slots: alpha -> 0 and Astat[NA*NA] = 0, so the value is 0 without a select
@@ -1350,6 +1423,239 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
     g_tl_hl[MODE][blockIdx.x][3] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
                                    (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
 #endif
+}
+
+// ===========================================================================
+// Temporal DSTDGC with its dynamic adjacency built in LDS (DSTDGC.forward
+// temporal, model/dstdgcn.py:88-93, and the DSTDGCB tail epilogues of
+// k_temporal_hl).  One workgroup per sample, persistent over samples; per
+// chunk of RC joints:
+//  phase 1: Adj[v][t][u] = alpha (sum_k W_rm[v][k] tanh(P[k][t] - Q[k][u]) +
+//           b[v]) + Astat[t][u] for the chunk's joints -- the tanh GEMM of
+//           k_adj_hl (rows = joints, K = 2V, columns (u, slot)) -- written as
+//           split-f16 planes [v][2][T][SL] into LDS;
+//  phase 2: the temporal GC units (sample, joint) of the chunk, their B
+//           fragments read from those planes (temporal_units).
+// The planes never reach HBM (k_adj_hl<1> + k_temporal_hl wrote and re-read
+// 2 V T SL halves x 2 bytes per sample: 123 KB each way at H36M).  Phase 1 is
+// VALU-bound (the tanh), phase 2 MFMA / memory; the one workgroup per CU the
+// LDS allows runs them back to back.  Grid = B (a persistent sample loop kept
+// its loop-carried state live through phase 2 and spilled).
+// ===========================================================================
+constexpr int kLdsBudget = 160 * 1024;
+
+template <int T, int V, int EPI, int C>
+struct TFusedGeom {
+  using SM = SlotMap<T, false>;
+  static constexpr int K = 2 * V, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL, SE = KP + 4;
+  static constexpr int SL = SM::SL, NCOL = T * SL, NCTC = cdiv(NCOL, 16);
+  // halves per joint in LDS: two planes + 8 (a joint 4 rows down lands on other banks)
+  static constexpr int PJ = 2 * T * SL + 8;
+  static constexpr int RTG = cdiv(V, 16);  // row tiles of the whole HLJ_RM image
+  static constexpr size_t stage_bytes = sizeof(TemporalStage<T, EPI, C, V>);
+  static constexpr size_t p1_bytes(int rtc) {
+    return 2 * (size_t)(T + 1) * SE * 4 + (size_t)rtc * (NS * 2 * 64 + TAIL * 64) * 16 + ((size_t)T * T + 1) * 4 +
+           (size_t)rtc * 16 * 4;
+  }
+  static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
+  static constexpr int jn(int rc) { return rc < V ? rc : V; }  // joints stored per chunk
+  static constexpr size_t total(int rc) {
+    return al16((size_t)jn(rc) * PJ * 2) + al16(p1_bytes(rc / 16) > stage_bytes ? p1_bytes(rc / 16) : stage_bytes);
+  }
+  // joints per chunk: all of them when the planes fit, else one row tile
+  static constexpr int RC = total(16 * RTG) <= kLdsBudget ? 16 * RTG : 16;
+  static constexpr int RTC = RC / 16, NCHUNK = cdiv(V, RC);
+  static constexpr int WIMG = RTC * (NS * 2 * 64 + TAIL * 64);  // uint4 of the chunk's HLJ_RM rows
+  static constexpr size_t PLANES = al16((size_t)jn(RC) * PJ * 2), LDS = total(RC);
+  static_assert(LDS <= kLdsBudget, "planes of one row tile must fit");
+};
+
+struct TemporalFusedArgs {
+  TemporalHLArgs g;  // the GC launch (adj unused)
+  AdjHLArgs j;       // P/Q (pq, pql), HLJ_RM image (wimg[0], wscale[0]), bias[0], alpha, astat[0]
+};
+
+template <int T, int V, int EPI, int C>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_temporal_fused(TemporalFusedArgs fa) {
+  using Gm = TFusedGeom<T, V, EPI, C>;
+  using SM = typename Gm::SM;
+  constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
+  constexpr int RC = Gm::RC, RTC = Gm::RTC, PJ = Gm::PJ, WIMG = Gm::WIMG, NW = 8, NT = 512;
+  constexpr int NSG = SM::NS, NUT = cdiv(T, 16);  // aggregation K-steps / u tiles of the GC
+  constexpr float C2 = 2.8853900817779268f;       // 2*log2(e)
+  const TemporalHLArgs& a = fa.g;
+  const AdjHLArgs& j = fa.j;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  _Float16* planes = reinterpret_cast<_Float16*>(dsm);
+  unsigned char* un = dsm + Gm::PLANES;  // phase-1 scratch / phase-2 stage (union)
+  float* El = reinterpret_cast<float*>(un);
+  float* Fl = El + (T + 1) * SE;
+  uint4* wl = reinterpret_cast<uint4*>(Fl + (T + 1) * SE);
+  float* asl = reinterpret_cast<float*>(wl + WIMG);
+  float* bsl = asl + T * T + 1;
+  auto& st = *reinterpret_cast<TemporalStage<T, EPI, C, V>*>(un);
+
+  // wave index through readfirstlane: wave-uniform to the compiler, so the
+  // unit indices derived from it live in SGPRs (as tid >> 6 they took ~24
+  // VGPRs more and spilled)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = lane >> 4, cl = lane & 15;
+  const int n = blockIdx.x;  // one sample per workgroup
+
+  {
+    for (int ch = 0; ch < Gm::NCHUNK; ++ch) {
+      const int v0 = ch * RC, nv = min(RC, V - v0), rt0 = ch * RTC;
+      if (ch) __syncthreads();  // the previous chunk's phase 2 is done with the planes and the stage
+      // ---- phase 1 prologue: P/Q -> E/F rows, the chunk's conv_rm rows, Astat, bias ----
+      const PQLayout L = j.pql;
+      const float* pqb = j.pq + (size_t)n * L.sn + j.p_ch[0];
+      for (int i = tid; i < (T + 1) * (KP - K); i += NT) {  // padding k and the row t = T: E = F = 1 (tanh 0)
+        const int r = i / (KP - K), k = K + i % (KP - K);
+        El[r * SE + k] = 1.f;
+        Fl[r * SE + k] = 1.f;
+      }
+      for (int i = tid; i < K; i += NT) {
+        El[T * SE + i] = 1.f;
+        Fl[T * SE + i] = 1.f;
+      }
+      int bad = 0;
+      for (int i = tid; i < T * V; i += NT) {
+        const int t = i / V, v = i % V;
+        const float4 q4 = ld4(pqb + t * L.st + v * L.sv);  // (P_0, P_1, Q_0, Q_1)
+        const float ep0 = C2 * q4.x, ep1 = C2 * q4.y, eq0 = -C2 * q4.z, eq1 = -C2 * q4.w;
+        bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
+        El[t * SE + v] = __builtin_amdgcn_exp2f(ep0);
+        El[t * SE + V + v] = __builtin_amdgcn_exp2f(ep1);
+        Fl[t * SE + v] = __builtin_amdgcn_exp2f(eq0);
+        Fl[t * SE + V + v] = __builtin_amdgcn_exp2f(eq1);
+      }
+      {
+        const uint4* wg = j.wimg[0];
+        constexpr int FULL = NS * 2 * 64;  // uint4 per row tile (full K-steps)
+        for (int i = tid; i < RTC * FULL; i += NT) wl[i] = wg[rt0 * FULL + i];
+        if constexpr (TAIL)
+          for (int i = tid; i < RTC * 64; i += NT) wl[RTC * FULL + i] = wg[Gm::RTG * FULL + rt0 * 64 + i];
+      }
+      for (int i = tid; i < T * T; i += NT) asl[i] = j.astat[0][i];
+      if (tid == 0) asl[T * T] = 0.f;
+      if (tid < 16 * RTC) bsl[tid] = 16 * rt0 + tid < V ? j.bias[0][16 * rt0 + tid] : 0.f;
+      const bool sep = __syncthreads_or(bad) == 0;
+      __syncthreads();  // (__syncthreads_or alone did not order the LDS writes above before the reads below)
+      if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0)
+        for (int i = tid; i < T * V; i += NT) {
+          const int t = i / V, v = i % V;
+          const float4 q4 = ld4(pqb + t * L.st + v * L.sv);
+          El[t * SE + v] = q4.x;
+          El[t * SE + V + v] = q4.y;
+          Fl[t * SE + v] = q4.z;
+          Fl[t * SE + V + v] = q4.w;
+        }
+        for (int i = tid; i < (T + 1) * (KP - K); i += NT) {
+          const int r = i / (KP - K), k = K + i % (KP - K);
+          El[r * SE + k] = 0.f;
+          Fl[r * SE + k] = 0.f;
+        }
+        for (int i = tid; i < K; i += NT) {
+          El[T * SE + i] = 0.f;
+          Fl[T * SE + i] = 0.f;
+        }
+        __syncthreads();
+      }
+      // ---- phase 1: the chunk's planes ----
+      // planes stored as 2^-sa Adj (dstd_hilo.h "range scaling")
+      const float dna = pow2f(-hl_range_shift(fexp_bits(__float_as_uint(j.wscale[0][HLS_BOUND]))));
+      const float alpha = *j.alpha * dna, inv = j.wscale[0][HLS_INV];
+      // The GEMM runs transposed -- the tanh fragments as the A operand,
+      // W_rm as B (the same register layouts) -- so a lane's accumulator holds
+      // 4 consecutive slots (columns 16 ct + 4 kg + r) of one joint (16 rt +
+      // cl): one 8-byte LDS write per plane instead of eight 2-byte ones.
+      // (W fragments held in registers across tiles, or several tiles per
+      // iteration, gave wrong results on this toolchain -- measured, not
+      // understood; one tile per iteration with its own W reads is
+      // bit-exact against k_adj_hl<1> + k_temporal_hl.)
+      auto tiles = [&](auto sep_c) {
+        constexpr bool SEP = decltype(sep_c)::value;
+        for (int ct = wave; ct < Gm::NCTC; ct += NW) {
+          // this lane's A-operand row = column ct * 16 + cl of the planes
+          const int col = ct * 16 + cl;
+          const int qa = col / SL, pa = SM::slot_idx(col - qa * SL);
+          const bool va = col < NCOL && pa < T;
+          f16x8 bh[NS], bo[NS];
+          f16x4 th, to;
+          tanh_frags<SEP, NS, TAIL, SE>(El, Fl, va ? pa : T, col < NCOL ? qa : T, kg, bh, bo, th, to);
+          // columns colb .. colb+3 (one frame q, slots slot0 ..): alpha (acc + b) + Astat,
+          // 0 on padding slots (alpha -> 0, Astat[T*T] = 0)
+          const int colb = ct * 16 + 4 * kg;
+          const int q = colb / SL, slot0 = colb - q * SL;
+          float as[4], al[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int pi = SM::slot_idx(slot0 + r);
+            const bool valid = colb + r < NCOL && pi < T;
+            as[r] = asl[valid ? pi * T + q : T * T] * dna;
+            al[r] = valid ? alpha : 0.f;
+          }
+#pragma unroll
+          for (int rt = 0; rt < RTC; ++rt) {
+            f32x4 acc = zero4();
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+              const f16x8 wh = as_h8(wl[((rt * NS + s) * 2 + 0) * 64 + lane]);
+              const f16x8 wo = as_h8(wl[((rt * NS + s) * 2 + 1) * 64 + lane]);
+              acc = mfma32(bh[s], wo, acc);
+              acc = mfma32(bo[s], wh, acc);
+              acc = mfma32(bh[s], wh, acc);
+            }
+            if constexpr (TAIL) {
+              const uint2* w16 = reinterpret_cast<const uint2*>(wl + RTC * NS * 2 * 64);
+              const f16x4 wth = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
+              const f16x4 wto = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
+              acc = __builtin_amdgcn_mfma_f32_16x16x16f16(th, wto, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_16x16x16f16(to, wth, acc, 0, 0, 0);
+              acc = __builtin_amdgcn_mfma_f32_16x16x16f16(th, wth, acc, 0, 0, 0);
+            }
+            const float b = bsl[16 * rt + cl];
+            float vv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) vv[r] = fmaf(al[r], fmaf(acc[r], inv, b), as[r]);
+            uint4 hi, lo;
+            split8(make_float4(vv[0], vv[1], vv[2], vv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+            const int jv = 16 * rt + cl;
+            if (jv < nv && colb < NCOL) {
+              _Float16* dst = planes + jv * PJ + q * SL + slot0;
+              *reinterpret_cast<uint2*>(dst) = make_uint2(hi.x, hi.y);
+              *reinterpret_cast<uint2*>(dst + T * SL) = make_uint2(lo.x, lo.y);
+            }
+          }
+        }
+      };
+#ifndef DSTD_TF_SKIP_P1  // (timing experiments: phase 2 alone)
+      if (sep) tiles(std::true_type{});
+      else tiles(std::false_type{});
+#endif
+      __syncthreads();  // planes complete; the phase-1 scratch is free
+      // ---- phase 2: the stage, then the chunk's GC units ----
+      stage_temporal<T, EPI, C, V>(a, st, tid, NT);
+      __syncthreads();
+      const int ub = n * V + v0;
+      auto load_adj = [&](int u, int s, uint4 (&bh)[NUT], uint4 (&bo)[NUT]) {
+        const _Float16* base = planes + (u - ub) * PJ;
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) {
+          const int uo = 16 * ut + cl;
+          const bool ok = uo < T && kg < SM::ng(s);
+          const int off = ok ? uo * SL + 8 * (SM::goff(s) + kg) : 0;
+          const uint4 h = *reinterpret_cast<const uint4*>(base + off);
+          const uint4 l = *reinterpret_cast<const uint4*>(base + T * SL + off);
+          bh[ut] = ok ? h : make_uint4(0u, 0u, 0u, 0u);
+          bo[ut] = ok ? l : make_uint4(0u, 0u, 0u, 0u);
+        }
+      };
+#ifndef DSTD_TF_SKIP_P2  // (timing experiments: phase 1 alone)
+      temporal_units<T, EPI, C, V, true>(a, st, ub + wave, ub + nv, NW, load_adj);
+#endif
+    }
+  }
 }
 
 // ===========================================================================
@@ -1465,6 +1771,48 @@ hipError_t launch_spatial_hl(const SpatialHLArgs& a, hipStream_t s) {
   }
 }
 
+template <int T, int V, int EPI, int C>
+hipError_t tfused_run(const TemporalFusedArgs& a, hipStream_t s) {
+  using Gm = TFusedGeom<T, V, EPI, C>;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)k_temporal_fused<T, V, EPI, C>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::LDS);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_temporal_fused<T, V, EPI, C>), dim3(a.g.B), dim3(512), Gm::LDS, s, a);
+  return hipGetLastError();
+}
+
+template <int T, int V>
+hipError_t tfused_tv(const TemporalFusedArgs& a, hipStream_t s) {
+  if (a.g.C == 3) {
+    if (a.g.pq) return hipErrorNotSupported;
+    switch (a.g.epi) {
+      case TEPI_OUT: return tfused_run<T, V, TEPI_OUT, 3>(a, s);
+      case TEPI_RAW: return tfused_run<T, V, TEPI_RAW, 3>(a, s);
+      default: return hipErrorNotSupported;
+    }
+  }
+  if (a.g.C != 64) return hipErrorNotSupported;
+  switch (a.g.epi) {
+    case TEPI_ENC: return tfused_run<T, V, TEPI_ENC, 64>(a, s);
+    case TEPI_IN: return tfused_run<T, V, TEPI_IN, 64>(a, s);
+    case TEPI_RAW: return tfused_run<T, V, TEPI_RAW, 64>(a, s);
+    default: return hipErrorNotSupported;
+  }
+}
+
+bool temporal_fused_supported(int T, int V) { return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23); }
+
+hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, hipStream_t s) {
+  if (!temporal_fused_supported(g.T, g.V) || g.V != (int)(j.pql.st / 4) || j.pql.sch != 1 || j.pql.sv != 4 ||
+      ((uintptr_t)j.pq & 15))
+    return hipErrorNotSupported;
+  const TemporalFusedArgs a{g, j};
+  if (g.T == 35 && g.V == 22) return tfused_tv<35, 22>(a, s);
+  if (g.T == 35 && g.V == 25) return tfused_tv<35, 25>(a, s);
+  if (g.T == 40 && g.V == 23) return tfused_tv<40, 23>(a, s);
+  return hipErrorNotSupported;
+}
+
 hipError_t launch_temporal_hl(const TemporalHLArgs& a, hipStream_t s) {
   if (!temporal_hl_supported(a.T, a.V)) return hipErrorNotSupported;
   switch (a.T) {
@@ -1484,3 +1832,4 @@ extern "C" int dstd_debug_timeline_hl(int mode, unsigned long long* host, int n)
                                   mode * 2048 * 4 * sizeof(unsigned long long));
 }
 #endif
+
