@@ -117,15 +117,20 @@ def hl_sl_temporal(T):
     return 8 * g
 
 
+FUSED_TEMPORAL = {(35, 22), (35, 25), (40, 23)}  # dstd_hilo.hip temporal_fused_supported
+
+
 def block_bytes(cin, cout, T, V, tail, split):
-    """Algorithmic HBM bytes per sample of each kernel family of one DSTDGCB:
-    inputs read once, outputs written once, in the stored layouts (NTVC fp32
-    activations, channel-innermost P/Q, adjacencies as fp32 rows or split-f16
-    planes).  split: (spatial, temporal) launches run the
-    split-f16 kernels."""
+    """Layout bytes per sample of each kernel family of one DSTDGCB: what the
+    launches move by design -- inputs read once, outputs written once, in the
+    stored layouts (NTVC fp32 activations, channel-innermost P/Q, adjacencies
+    as fp32 rows or split-f16 planes).  split: (spatial,
+    temporal) launches run the split-f16 kernels; the split temporal launch of
+    a FUSED_TEMPORAL shape builds its adjacency in LDS (no adjacency bytes)."""
     TV = T * V
+    fused = split[1] and (T, V) in FUSED_TEMPORAL
     adj_s = 2 * T * (2 * V * hl_sl_spatial(V) * 2 if split[0] else 4 * ((V * V + 3) // 4 * 4))
-    adj_t = V * (2 * T * hl_sl_temporal(T) * 2 if split[1] else 4 * ((T * T + 3) // 4 * 4))
+    adj_t = 0 if fused else V * (2 * T * hl_sl_temporal(T) * 2 if split[1] else 4 * ((T * T + 3) // 4 * 4))
     pq_s, pq_t = TV * 8 * 4, TV * 4 * 4
     spatial = TV * cin * 4 + adj_s + TV * cout * 4 + pq_t
     temporal = TV * cout * 4 + adj_t + (TV * cout * 4 if tail == "enc" else 0) + TV * (cout if tail != "out" else 3) * 4
@@ -133,6 +138,9 @@ def block_bytes(cin, cout, T, V, tail, split):
         temporal += V * 3 * 4  # last observed frame of the model input
     else:
         temporal += pq_s
+    if fused:  # the temporal launch reads the temporal P/Q itself
+        return {native.KIND_ADJ_S: pq_s + adj_s, native.KIND_SPATIAL: spatial, native.KIND_ADJ_T: 0,
+                native.KIND_TEMPORAL: temporal + pq_t}
     return {native.KIND_ADJ_S: pq_s + adj_s, native.KIND_SPATIAL: spatial, native.KIND_ADJ_T: pq_t + adj_t,
             native.KIND_TEMPORAL: temporal}
 
@@ -222,7 +230,8 @@ def load_traffic(kernel, instance=None):
 
 def split_instance(kind, T, V):
     """Kernel instantiation of DSTDGCB 1 (an encoder) for kind."""
-    return {native.KIND_SPATIAL: f"k_spatial_hl<{V}, 64, 64>", native.KIND_TEMPORAL: f"k_temporal_hl<{T}, 1, 64>",
+    temporal = f"k_temporal_fused<{T}, {V}, 1, 64>" if (T, V) in FUSED_TEMPORAL else f"k_temporal_hl<{T}, 1, 64>"
+    return {native.KIND_SPATIAL: f"k_spatial_hl<{V}, 64, 64>", native.KIND_TEMPORAL: temporal,
             native.KIND_ADJ_S: f"k_adj_hl<0, {T}, {2 * T}, {V}>", native.KIND_ADJ_T: f"k_adj_hl<1, {V}, {2 * V}, {T}>"}.get(kind)
 
 

@@ -289,8 +289,8 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
 #endif
 // threads per workgroup: one workgroup of 4 x (waves per SIMD) waves per CU,
 // so a CU stages one copy of the weight images (A/B against two 4-wave
-// workgroups: forward -2.3%); at most 8 waves
-constexpr int spatial_nt() { return 64 * (4 * DSTD_HL_WPE < 8 ? 4 * DSTD_HL_WPE : 8); }
+// workgroups: forward -2.3%)
+constexpr int spatial_nt() { return 64 * 4 * DSTD_HL_WPE; }
 
 // 8 consecutive channels k0 .. k0+7 of row `row` of a unit (C channels per
 // row, zero past C; C % 8 == 0 or C == 6 / 3)

@@ -22,7 +22,7 @@ def family(name):
     # 64->64 launches whose bytes bench.py's roofline divides
     if "k_spatial_hl" in name:
         return "spatial_gc_split"
-    if "k_temporal_hl" in name:
+    if "k_temporal_hl" in name or "k_temporal_fused" in name:
         return "temporal_gc_split"
     if "k_adj_hl<0" in name:
         return "adj_spatial_split"
