@@ -57,6 +57,7 @@ from model import get_model  # noqa: E402
 METRIC = "pose-sequences/sec forward (H36M 22J×50T, B=256) at 1/2/4/8 GPUs; % HBM roofline"
 PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 MFMA / vector peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+PEAK_F16_DENSE_TFLOPS = 2500.0  # MI355X dense f16 MFMA (MI355X_MICROARCH.md); split-f16 runs 3 products per MAC
 
 CONFIGS = {
     "h36m": ("model_h36m.npz", "H36M-shape synthetic, T=10+25=35, V=22"),
@@ -414,6 +415,11 @@ def main():
     split_blk = split_on and opts["num_layers"] > 0
     traffic = load_traffic(kname + "_split" if split_blk else kname, split_instance(dominant, T, V) if split_blk else None)
     total_flop_per_seq = sum(sum(b.values()) for b in fl)
+    # algorithmic FLOPs of the probed launch (the fused temporal launch also
+    # builds its adjacency: the adjacency family's FLOPs count to it)
+    fused_t = split_on and (T, V) in FUSED_TEMPORAL
+    launch_flop = fl[1][dominant] + (fl[1][native.KIND_ADJ_T] if fused_t and dominant == native.KIND_TEMPORAL else 0)
+    flops = launch_flop * B / avg_launch_s / 1e12 if kernel_ms > 0 else 0.0
     whole_bytes = model_compulsory_bytes(opts) * G * args.steps / elapsed / 1e9
 
     if rank == 0:
@@ -446,6 +452,11 @@ def main():
                          "layout_bytes_per_launch": int(bb[1][dominant] * B) if launches else None,
                          "launches": len(launches), "probe_every": every,
                          "avg_launch_us": round(avg_launch_s * 1e6, 2),
+                         "compute": {"flop_per_launch": launch_flop * B, "achieved_tflops": round(flops, 2),
+                                     "frac_fp32_peak": round(flops / PEAK_FP32_TFLOPS, 4),
+                                     "frac_split_f16_ceiling": round(flops / (PEAK_F16_DENSE_TFLOPS / 3), 4),
+                                     "note": "fp32 FLOPs of the launch over the fp32 peak (157 TF, SURVEY §8(d)) and "
+                                             "over the split-f16 ceiling (dense f16 MFMA / 3 products)"},
                          "whole_forward": {"compulsory_bytes_per_seq": model_compulsory_bytes(opts),
                                            "achieved_gbs": round(whole_bytes, 1),
                                            "frac_hbm": round(whole_bytes / PEAK_HBM_GBS, 4),
