@@ -29,6 +29,8 @@ gradient is impossible.
 """
 import itertools
 import math
+import weakref
+from typing import List
 
 import numpy as np
 import torch
@@ -75,10 +77,23 @@ class _ForwardOnly(torch.autograd.Function):
                                   "built; call .train() for the native training path")
 
 
-# Native modules that cache folded constants in the workspace between
-# forwards (DSTDGCN) carry an instance token that is never reused (unlike id())
-# and a generation counter, both part of the reuse tag.
+# Native modules carry an instance token that is never reused (unlike id()):
+# part of the constant-reuse tag of DSTDGCN, and the key under which the
+# torch.library ops below find the module that lays out their C parameter
+# struct.  Copies (deepcopy / unpickling) get a token of their own.
 _UIDS = itertools.count(1)
+_INSTANCES = weakref.WeakValueDictionary()
+
+
+def _register(mod):
+    mod._dstd_uid = next(_UIDS)
+    _INSTANCES[mod._dstd_uid] = mod
+
+
+class _NativeModule(nn.Module):
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        _register(self)
 
 
 def invalidate_native_cache(module):
@@ -342,7 +357,7 @@ class BatchNorm(nn.Module):
         return y.reshape(n, c, v, t).transpose(2, 3).contiguous()
 
 
-class DSTDGC(nn.Module):
+class DSTDGC(_NativeModule):
     """Dynamic graph convolution (reference :53-94); ``mode`` spatial or temporal."""
 
     def __init__(self, in_channels, out_channels, ref_channels, kpt_channels, red_channels=2, mode="spatial"):
@@ -363,6 +378,7 @@ class DSTDGC(nn.Module):
         self.tanh = nn.Tanh()
         self.conv_f = nn.Conv2d(in_channels, out_channels, 1)
         self.init_parameter()
+        _register(self)
 
     def init_parameter(self):
         for m in self.modules():
@@ -387,6 +403,14 @@ class DSTDGC(nn.Module):
         params = list(self.parameters())
         if _needs_grad(x, A, alpha, *params):
             return _OpTrain.apply(self, mode, x, A, alpha, *params)
+        return torch.ops.dstd.dstdgc_forward(x, A, alpha, params, self._dstd_uid)
+
+    def _eval_native(self, x, A, alpha):
+        """dstd_dstdgc_fwd on prepared operands (torch.ops.dstd.dstdgc_forward)."""
+        L = native.lib()
+        B, cin, T, V = x.shape
+        dev = x.device
+        mode = native.MODE_SPATIAL if self.mode == "spatial" else native.MODE_TEMPORAL
         y = torch.empty(B, self.out_channels, T, V, dtype=torch.float32, device=dev)
         nbytes = L.dstd_dstdgc_workspace_bytes(mode, B, cin, self.out_channels, T, V)
         ws = native.workspace(dev, nbytes)
@@ -398,7 +422,7 @@ class DSTDGC(nn.Module):
         return y
 
 
-class DSTDGCB(nn.Module):
+class DSTDGCB(_NativeModule):
     """DSTD-GC block: two spatial DSTDGCs on the skeleton priors, BN + residual
     + PReLU, one temporal DSTDGC (reference :97-163)."""
 
@@ -433,6 +457,7 @@ class DSTDGCB(nn.Module):
         # arithmetic of the eval forward's graph convolutions, per call
         # (include/dstd_gcn.h DSTD_FWD_EXACT_FP32): "split" or "fp32"
         self.gc_arithmetic = "split"
+        _register(self)
 
     def init_parameter(self):
         stdt = 1.0 / math.sqrt(self.R_t.size(1))
@@ -449,15 +474,24 @@ class DSTDGCB(nn.Module):
             return _mark(x.new_empty(0, self.out_channels, T, V), x, *self.parameters())
         if self.training:
             return _BlockTrain.apply(self, x, *self.parameters())
+        tensors = list(self.parameters()) + list(self.buffers())
+        y = torch.ops.dstd.dstdgcb_forward(x, tensors, self._dstd_uid, self.out_channels,
+                                           native.arith_flags(self.gc_arithmetic))
+        return _mark(y, x, *self.parameters())
+
+    def _eval_native(self, x, flags):
+        """dstd_block_fwd_ex (torch.ops.dstd.dstdgcb_forward)."""
+        L = native.lib()
+        B, cin, T, V = x.shape
         dev = x.device
         y = torch.empty(B, self.out_channels, T, V, dtype=torch.float32, device=dev)
         nbytes = L.dstd_block_workspace_bytes(B, cin, self.out_channels, T, V)
         ws = native.workspace(dev, nbytes)
         p = native.block_struct(self)
         code = L.dstd_block_fwd_ex(p, native.ptr(x, "x"), B, T, V, native.ptr(y, "y"), ws.data_ptr(), ws.numel(),
-                                   native.stream_handle(dev), native.arith_flags(self.gc_arithmetic))
+                                   native.stream_handle(dev), flags)
         native.check(code, "dstd_block_fwd_ex")
-        return _mark(y, x, *self.parameters())
+        return y
 
 
 def _ptr_or_none(t):
@@ -614,7 +648,7 @@ class ST_GCNN_layer(nn.Module):
         return y
 
 
-class DSTDGCN(nn.Module):
+class DSTDGCN(_NativeModule):
     """The whole network (reference :252-317)."""
 
     def __init__(self, input_channels, input_time_frame, output_time_frame, st_gcnn_dropout, joints_to_consider,
@@ -644,8 +678,8 @@ class DSTDGCN(nn.Module):
         self._native = None
         self._tree = _TensorTree()
         self.gc_arithmetic = "split"  # see DSTDGCB; set_gc_arithmetic() sets the whole tree
-        self._dstd_uid = next(_UIDS)
         self._dstd_gen = 0
+        _register(self)
         self.register_load_state_dict_post_hook(lambda mod, incompatible: invalidate_native_cache(mod))
 
     def set_gc_arithmetic(self, mode):
@@ -709,11 +743,12 @@ class DSTDGCN(nn.Module):
             return _mark(torch.empty_like(x), x, *self._tree.get(self)[0])
         if self.training:
             return _ModelTrain.apply(self, x, *self._tree.get(self)[0])
-        y = torch.empty_like(x)
-        self._forward_native(x, y)
-        return _mark(y, x, *self._tree.get(self)[0]) if torch.is_grad_enabled() else y
+        params, buffers = self._tree.get(self)
+        y = torch.ops.dstd.dstdgcn_forward(x, params + buffers, self._dstd_uid,
+                                           native.arith_flags(self.gc_arithmetic))
+        return _mark(y, x, *params) if torch.is_grad_enabled() else y
 
-    def _forward_native(self, x, y, prof=None):
+    def _forward_native(self, x, y, prof=None, arith=None):
         """One eval forward through dstd_model_fwd_ex.  The folded constants
         and split-f16 weight images a forward leaves in the workspace are
         reused when nothing changed since: same model instance (a token never
@@ -725,7 +760,7 @@ class DSTDGCN(nn.Module):
         n, t, v, _ = x.shape
         dev = x.device
         p = self._native_params()
-        flags = native.arith_flags(self.gc_arithmetic)
+        flags = native.arith_flags(self.gc_arithmetic) if arith is None else arith
         try:
             versions = tuple(tt._version for tt in self._native_tensors)
             tag = (self._dstd_uid, self._dstd_gen, tuple(self._native[0]), n, flags, versions)
@@ -738,3 +773,56 @@ class DSTDGCN(nn.Module):
         code = L.dstd_model_fwd_ex(p, native.ptr(x, "x"), n, native.ptr(y, "y"), ws.data_ptr(), ws.numel(),
                                    native.stream_handle(dev), flags, prof)
         native.check(code, "dstd_model_fwd_ex")
+
+
+# ---------------------------------------------------------------------------
+# torch.library ops: the eval forwards as custom operators with
+# fake (meta) kernels, so torch.compile / FakeTensor tracing see them as single
+# ops with known output shapes.  Each op receives every tensor of its module
+# (the data dependencies) plus the module's instance token, under which the
+# implementation finds the module that lays out the C parameter struct
+# (include/dstd_gcn.h); underneath is the same C ABI call as before.
+# ---------------------------------------------------------------------------
+def _instance(uid):
+    mod = _INSTANCES.get(uid)
+    if mod is None:
+        raise RuntimeError(f"dstd op: no live DSTD module with instance token {uid}")
+    return mod
+
+
+@torch.library.custom_op("dstd::dstdgc_forward", mutates_args=())
+def _op_dstdgc_forward(x: torch.Tensor, A: torch.Tensor, alpha: torch.Tensor, weights: List[torch.Tensor],
+                       uid: int) -> torch.Tensor:
+    """DSTDGC.forward eval (reference :80-94) -> dstd_dstdgc_fwd."""
+    return _instance(uid)._eval_native(x, A, alpha)
+
+
+@_op_dstdgc_forward.register_fake
+def _(x, A, alpha, weights, uid):
+    # weights in DSTDGC.parameters() order: conv_m1, conv_m2, conv_rm, conv_f (weight, bias)
+    return x.new_empty(x.shape[0], weights[6].shape[0], x.shape[2], x.shape[3])
+
+
+@torch.library.custom_op("dstd::dstdgcb_forward", mutates_args=())
+def _op_dstdgcb_forward(x: torch.Tensor, tensors: List[torch.Tensor], uid: int, cout: int,
+                        flags: int) -> torch.Tensor:
+    """DSTDGCB.forward eval (reference :141-163) -> dstd_block_fwd_ex."""
+    return _instance(uid)._eval_native(x, flags)
+
+
+@_op_dstdgcb_forward.register_fake
+def _(x, tensors, uid, cout, flags):
+    return x.new_empty(x.shape[0], cout, x.shape[2], x.shape[3])
+
+
+@torch.library.custom_op("dstd::dstdgcn_forward", mutates_args=())
+def _op_dstdgcn_forward(x: torch.Tensor, tensors: List[torch.Tensor], uid: int, flags: int) -> torch.Tensor:
+    """DSTDGCN.forward eval (reference :293-317) -> dstd_model_fwd_ex."""
+    y = torch.empty_like(x)
+    _instance(uid)._forward_native(x, y, arith=flags)
+    return y
+
+
+@_op_dstdgcn_forward.register_fake
+def _(x, tensors, uid, flags):
+    return torch.empty_like(x)

@@ -175,3 +175,31 @@ def test_plain_st_gcnn_layer_schema_matches_reference():
             assert tuple(sd[k].shape) == ref[k].shape, k
         assert np.array_equal(sd["stgcn.0.A_fixed"].numpy(), ref["stgcn.0.A_fixed"])
         layer.load_state_dict({k: torch.from_numpy(v) for k, v in ref.items()})
+
+
+def test_torch_library_ops_and_fake_kernels():
+    """The eval forwards are torch.library custom ops whose fake
+    kernels give the output shapes without a GPU (meta tensors)."""
+    for name in ("dstdgc_forward", "dstdgcb_forward", "dstdgcn_forward"):
+        assert hasattr(torch.ops.dstd, name), name
+    m = get_model("dstdgcn", dstdgcn=H36M)
+    meta = [t.to("meta") for t in list(m.parameters()) + list(m.buffers())]
+    y = torch.ops.dstd.dstdgcn_forward(torch.empty(3, 35, 22, 3, device="meta"), meta, m._dstd_uid, 0)
+    assert y.shape == (3, 35, 22, 3) and y.device.type == "meta"
+    blk = m.encoders[0][0].stgcn[0][0]
+    out = m.conv_st_out.stgcn[0][0]
+    tb = [t.to("meta") for t in list(out.parameters()) + list(out.buffers())]
+    assert torch.ops.dstd.dstdgcb_forward(torch.empty(2, 64, 35, 22, device="meta"), tb, out._dstd_uid, 3,
+                                          0).shape == (2, 3, 35, 22)
+    op = blk.conv_s[0]
+    w = [t.to("meta") for t in op.parameters()]
+    assert torch.ops.dstd.dstdgc_forward(torch.empty(2, 64, 35, 22, device="meta"), torch.empty(22, 22, device="meta"),
+                                         torch.empty(1, device="meta"), w, op._dstd_uid).shape == (2, 64, 35, 22)
+
+
+def test_copies_get_their_own_instance_token():
+    import copy
+    m = get_model("dstdgcn", dstdgcn=H36M)
+    c = copy.deepcopy(m)
+    assert c._dstd_uid != m._dstd_uid
+    assert c.encoders[0][0].stgcn[0][0]._dstd_uid != m.encoders[0][0].stgcn[0][0]._dstd_uid

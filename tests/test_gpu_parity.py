@@ -438,3 +438,22 @@ def test_block_large_adjacency_and_activations(cin, cout, precision):
         y = blk(x.to(DEV)).cpu().numpy()
     assert np.isfinite(y).all()
     assert rel_err(y, y64) <= 1e-4
+
+
+def test_torch_library_ops_opcheck_and_compile():
+    """The custom ops pass torch.library.opcheck (schema, fake kernel vs the
+    real one) and a torch.compile'd model (aot_eager: no codegen) equals eager."""
+    m, d, sd, opts = load_model("h36m")
+    x = t(d["x"])
+    tensors = list(m.parameters()) + list(m.buffers())
+    with torch.no_grad():
+        torch.library.opcheck(torch.ops.dstd.dstdgcn_forward.default, (x, tensors, m._dstd_uid, 0),
+                              test_utils=("test_schema", "test_faketensor"))
+        blk = m.encoders[0][0].stgcn[0][0]
+        xb = torch.randn(2, 64, 35, 22, device=DEV)
+        tb = list(blk.parameters()) + list(blk.buffers())
+        torch.library.opcheck(torch.ops.dstd.dstdgcb_forward.default, (xb, tb, blk._dstd_uid, 64, 0),
+                              test_utils=("test_schema", "test_faketensor"))
+        y_eager = m(x)
+        mc = torch.compile(m, backend="aot_eager")
+        assert torch.equal(mc(x), y_eager)
