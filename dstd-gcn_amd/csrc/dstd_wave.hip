@@ -736,15 +736,14 @@ int wave_occupancy(K k) {
   return nb;
 }
 
+// (compile-time only: a -DDSTD_NO_WAVE build routes the exact-fp32 block
+// launches to the dstd_fast.hip kernels; no process-wide switch)
 bool wave_disabled() {
 #ifdef DSTD_NO_WAVE
   return true;
+#else
+  return false;
 #endif
-  static const bool off = [] {
-    const char* e = getenv("DSTD_WAVE_KERNELS");
-    return e && e[0] == '0';
-  }();
-  return off;
 }
 
 template <int V, int CIN, int COUT, bool RES>
