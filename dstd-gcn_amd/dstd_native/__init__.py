@@ -81,14 +81,41 @@ KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temp
 _lib = None
 
 
+def source_hash():
+    """sha256 (16 hex digits) of the sources the library is built from, in the
+    order dstd-gcn_amd/Makefile hashes them (HASHED); None when the sources
+    are not next to the package."""
+    import glob
+    import hashlib
+    pkg = os.path.dirname(_HERE)
+    rel = [os.path.relpath(p, pkg) for pat in ("csrc/*.hip", "csrc/*.h", "../include/*.h")
+           for p in glob.glob(os.path.join(pkg, pat))]
+    files = sorted(rel) + ["Makefile"]
+    h = hashlib.sha256()
+    for f in files:
+        path = os.path.join(pkg, f)
+        if not os.path.exists(path):
+            return None
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def lib():
-    """Load libdstd_gcn.so once; raise loudly if it is not built."""
+    """Load libdstd_gcn.so once; raise loudly if it is not built, or if it was
+    built from other sources than the tree it is loaded from (its embedded
+    dstd_source_hash() against source_hash())."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"DSTD native library not built: {LIB_PATH} (run `make -C dstd-gcn_amd`)")
         L = ctypes.CDLL(LIB_PATH)
         vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        L.dstd_source_hash.restype = ctypes.c_char_p
+        built, tree = L.dstd_source_hash().decode(), source_hash()
+        if tree is not None and built != tree:
+            raise RuntimeError(f"{LIB_PATH} was built from other sources (hash {built}, this tree {tree}): "
+                               "rebuild with `make -C dstd-gcn_amd`")
         L.dstd_version.restype = ctypes.c_char_p
         L.dstd_error_string.restype = ctypes.c_char_p
         L.dstd_error_string.argtypes = [ci]
@@ -166,7 +193,7 @@ def lib():
     return _lib
 
 
-EXPORTS = ("dstd_version", "dstd_error_string", "dstd_dstdgc_workspace_bytes", "dstd_block_workspace_bytes",
+EXPORTS = ("dstd_version", "dstd_source_hash", "dstd_error_string", "dstd_dstdgc_workspace_bytes", "dstd_block_workspace_bytes",
            "dstd_model_workspace_bytes", "dstd_dstdgc_fwd", "dstd_block_fwd", "dstd_model_fwd",
            "dstd_model_fwd_profiled", "dstd_events_create", "dstd_events_destroy", "dstd_event_elapsed_ms",
            "dstd_block_fwd_ex", "dstd_model_fwd_ex")

@@ -102,6 +102,9 @@ typedef struct dstd_model_params {
 } dstd_model_params;
 
 const char* dstd_version(void);
+/* sha256 (first 16 hex digits) of the sources this library was built from
+ * (dstd-gcn_amd/Makefile HASHED): ties a shipped binary to its tree. */
+const char* dstd_source_hash(void);
 const char* dstd_error_string(int code);
 
 size_t dstd_dstdgc_workspace_bytes(int mode, int B, int cin, int cout, int T, int V);

@@ -22,7 +22,7 @@ def header_symbols(name="dstd_gcn.h"):
 def test_library_exports_every_header_symbol():
     L = native.lib()
     syms = header_symbols()
-    assert len(syms) == 14, syms
+    assert len(syms) == 15, syms
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(native.EXPORTS)
@@ -79,6 +79,8 @@ def test_train_sizes_and_argument_checks_without_gpu():
 def test_version_and_errors():
     L = native.lib()
     assert b"gfx950" in L.dstd_version()
+    # provenance: the loaded binary was built from exactly this tree's sources
+    assert L.dstd_source_hash().decode() == native.source_hash()
     assert L.dstd_error_string(-2) == b"workspace too small"
     assert b"envelope" in L.dstd_error_string(-3)
 
