@@ -164,6 +164,105 @@ def dstdgc_forward(x, sd, A, alpha, mode, dtype=torch.float64):
     return dstdgc(_t(x, dtype), sd, _t(A, dtype), _t(alpha, dtype).reshape(()), mode)
 
 
+# ---------------------------------------------------------------------------
+# model/dstdgcn_fast.py: the channels-last variant.  Activations are NTVC,
+# conv_f and the block residual are nn.Linear, the spatial adjacency is the
+# trainable A_s itself, BN channels are ordered (v, c), and the graph product
+# contracts the adjacency's second index (matmul(xm, xf)).
+# ---------------------------------------------------------------------------
+def fast_dstdgc(x, p, A, alpha, mode):
+    """dstdgcn_fast.DSTDGC.forward (model/dstdgcn_fast.py:108-155).
+
+    x: [N, T, V, Cin] -> [N, T, V, Cout]; A: [1, V, V] / [1, T, T]."""
+    wf, bf = p["conv_f.weight"], p["conv_f.bias"]                     # nn.Linear :95
+    wrm = p["conv_rm.weight"].reshape(p["conv_rm.weight"].shape[0], -1)
+    brm = p["conv_rm.bias"]
+    if mode == "spatial":                                             # :111-125
+        xf = x @ wf.t() + bf                                          # [n, t, v, co]
+        xp = x.permute(0, 3, 1, 2)                                    # [n, c, t, v]
+        p1 = conv1x1(xp, p["conv_m1.weight"], p["conv_m1.bias"])
+        q1 = conv1x1(xp, p["conv_m2.weight"], p["conv_m2.bias"])
+        n, r, t, v = p1.shape
+        m = torch.tanh(p1.reshape(n, r * t, v)[:, :, :, None] - q1.reshape(n, r * t, v)[:, :, None, :])
+        adj = (torch.einsum("tk,nkvw->ntvw", wrm, m) + brm.view(1, -1, 1, 1)) * alpha + A
+        return torch.einsum("ntvw,ntwc->ntvc", adj, xf)               # matmul(xm, xf) :125
+    if mode == "temporal":                                            # :133-146
+        xp = x.permute(0, 3, 2, 1)                                    # [n, c, v, t]
+        xf = x.permute(0, 2, 1, 3) @ wf.t() + bf                      # [n, v, t, co]
+        p1 = conv1x1(xp, p["conv_m1.weight"], p["conv_m1.bias"])      # [n, 2, v, t]
+        q1 = conv1x1(xp, p["conv_m2.weight"], p["conv_m2.bias"])
+        n, r, v, t = p1.shape
+        m = torch.tanh(p1.reshape(n, r * v, t)[:, :, :, None] - q1.reshape(n, r * v, t)[:, :, None, :])
+        adj = (torch.einsum("vk,nktu->nvtu", wrm, m) + brm.view(1, -1, 1, 1)) * alpha + A
+        return torch.einsum("nvtu,nvuc->nvtc", adj, xf).permute(0, 2, 1, 3)   # :145-146
+    raise ValueError(mode)
+
+
+def fast_batchnorm(x, p, training=False, eps=BN_EPS):
+    """dstdgcn_fast.BatchNorm (model/dstdgcn_fast.py:41-56): BN1d over channel
+    v*C + c of an NTVC tensor, statistics over (n, t)."""
+    n, t, v, c = x.shape
+    xc = x.permute(0, 2, 3, 1).reshape(n, v * c, t)
+    if training:
+        mean = xc.mean(dim=(0, 2))
+        var = xc.var(dim=(0, 2), unbiased=False)
+        if BN_RECORD is not None:
+            BN_RECORD.append((mean.detach().clone(), xc.var(dim=(0, 2), unbiased=True).detach().clone()))
+    else:
+        mean, var = p["running_mean"], p["running_var"]
+    y = (xc - mean.view(1, -1, 1)) / torch.sqrt(var.view(1, -1, 1) + eps)
+    y = y * p["weight"].view(1, -1, 1) + p["bias"].view(1, -1, 1)
+    return y.reshape(n, v, c, t).permute(0, 3, 1, 2)
+
+
+def fast_dstdgcb(x, p, training=False):
+    """dstdgcn_fast.DSTDGCB.forward (model/dstdgcn_fast.py:248-275)."""
+    cin = x.shape[-1]
+    cout = p["conv_s.0.conv_f.weight"].shape[0]
+    if cin != cout:                                                   # :183-188 Linear + BN
+        r = x @ p["residual.0.weight"].t() + p["residual.0.bias"]
+        r = fast_batchnorm(r, sub(p, "residual.1.bn."), training)
+    else:
+        r = x
+    y = None
+    for i in range(p["A_s"].shape[0]):                                # :255-258 (A_s itself)
+        z = fast_dstdgc(x, sub(p, f"conv_s.{i}."), p["A_s"][i:i + 1], p["alpha_sm"], "spatial")
+        y = z if y is None else y + z
+    h = prelu(fast_batchnorm(y, sub(p, "bn.bn."), training) + r, p["prelu.weight"])   # :259-262
+    a_t = p["A_t"][0:1] + p["R_t"][0:1]                               # :266-271
+    return fast_dstdgc(h, sub(p, "conv_t.0."), a_t, p["alpha_tm"], "temporal")
+
+
+def fast_dstdgcn_fn(x, sd, num_layers, training=False):
+    """dstdgcn_fast.DSTDGCN.forward (model/dstdgcn_fast.py:548-614) on
+    tensors used as given; dropout treated as eval."""
+    residual = x[:, -1:]                                              # :555
+    h = torch.cat((x, x - residual), dim=-1)                          # :558-559 (stays NTVC)
+    h = fast_dstdgcb(h, sub(sd, "conv_st_in.stgcn.0.0."), training)   # :563
+    h = prelu(fast_batchnorm(h, sub(sd, "bn_in.bn."), training), sd["prelu.weight"])   # :570-572
+    for i in range(num_layers):                                       # :583-584
+        e = f"encoders.{i}."
+        y = fast_dstdgcb(h, sub(sd, e + "0.stgcn.0.0."), training) + h
+        h = prelu(fast_batchnorm(y, sub(sd, e + "1.bn."), training), sd[e + "2.weight"])
+    y = fast_dstdgcb(h, sub(sd, "conv_st_out.stgcn.0.0."), training)  # :601
+    return y + residual                                               # :610
+
+
+def fast_dstdgcn(x, sd, num_layers, dtype=torch.float64, training=False):
+    sd = {k: _t(v, dtype) for k, v in sd.items() if not k.endswith("num_batches_tracked")}
+    return fast_dstdgcn_fn(_t(x, dtype), sd, num_layers, training)
+
+
+def fast_dstdgcb_forward(x, sd, dtype=torch.float64):
+    sd = {k: _t(v, dtype) for k, v in sd.items() if not k.endswith("num_batches_tracked")}
+    return fast_dstdgcb(_t(x, dtype), sd)
+
+
+def fast_dstdgc_forward(x, sd, A, alpha, mode, dtype=torch.float64):
+    sd = {k: _t(v, dtype) for k, v in sd.items()}
+    return fast_dstdgc(_t(x, dtype), sd, _t(A, dtype), _t(alpha, dtype).reshape(()), mode)
+
+
 def mpjpe_error_3d(outputs, targets):
     """engine/utils/loss.py:52-65 with joint_weights=None (all-ones weights:
     the broadcast makes it a plain mean of per-joint L2)."""

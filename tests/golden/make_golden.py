@@ -20,9 +20,11 @@ Fixture list (all committed):
   engine.npz          mpjpe_error_3d + PredictionEngine.test metric + 3DPW loss curve
   train_grads.npz     fp64 gradients / loss curve of the engine.npz training run
   plain_layers.npz    ST_GCNN_layer(refine=False): ConvTemporalGraphical + KxK conv
+  dstdgcn_fast.npz    model/dstdgcn_fast.py (channels-last variant): ops, blocks,
+                      whole models (h36m, 3dpw) and fp64 gradients of one step
 
-``python tests/golden/make_golden.py train`` / ``plain`` regenerates
-train_grads.npz / plain_layers.npz only.
+``python tests/golden/make_golden.py train`` / ``plain`` / ``fast`` regenerates
+train_grads.npz / plain_layers.npz / dstdgcn_fast.npz only.
 """
 import copy
 import os
@@ -393,6 +395,133 @@ def gen_plain_layers(gen):
     np.savez_compressed(os.path.join(HERE, "plain_layers.npz"), **out)
 
 
+def gen_fast(gen):
+    """model/dstdgcn_fast.py: the channels-last variant (NTVC activations,
+    conv_f / residual as nn.Linear, a trainable A_s without W_s / R_s, BN
+    channels ordered (v, c), and the graph product contracted on the other
+    adjacency index: matmul(xm, xf), :125 / :145)."""
+    from model import dstdgcn_fast as F  # reference
+    from engine.utils.loss import mpjpe_error_3d  # reference
+
+    out = {}
+
+    def randomise_fast(block):
+        with torch.no_grad():
+            block.alpha_sm.copy_(torch.empty(1).uniform_(0.3, 1.0, generator=gen) *
+                                 (1 if torch.rand(1, generator=gen) > 0.3 else -1))
+            block.alpha_tm.copy_(torch.empty(1).uniform_(0.3, 1.0, generator=gen))
+            block.A_s.add_(0.1 * torch.randn(block.A_s.shape, generator=gen))
+            T = block.R_t.shape[-1]
+            block.R_t.copy_(torch.empty(block.R_t.shape).uniform_(-1 / T**0.5, 1 / T**0.5, generator=gen))
+            block.prelu.weight.copy_(torch.empty(1).uniform_(0.1, 0.4, generator=gen))
+
+    def bias_noise(module):
+        with torch.no_grad():
+            for m in module.modules():
+                if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear)) and m.bias is not None:
+                    m.bias.copy_(0.1 * torch.randn(m.bias.shape, generator=gen))
+
+    # single ops: x [B][T][V][C] -> y [B][T][V][Cout]
+    for name, mode, cin, cout, T, V in (("op_s_64_64", "spatial", 64, 64, 35, 22),
+                                        ("op_s_6_64", "spatial", 6, 64, 35, 22),
+                                        ("op_t_64_64", "temporal", 64, 64, 35, 22),
+                                        ("op_t_64_64_3dpw", "temporal", 64, 64, 40, 23)):
+        ref, kpt = (T, V) if mode == "spatial" else (V, T)
+        op = F.DSTDGC(cin, cout, ref, kpt, mode=mode).eval()
+        bias_noise(op)
+        Ad = V if mode == "spatial" else T
+        A = torch.randn(1, Ad, Ad, generator=gen) * 0.3
+        alpha = torch.empty(1).uniform_(0.5, 1.5, generator=gen)
+        x = torch.randn(1, T, V, cin, generator=gen)
+        with torch.no_grad():
+            y32 = op(x, A, alpha).numpy()
+        y64 = run64(op, x, A, alpha)
+        out.update({f"{name}/x": x.numpy(), f"{name}/A": A.numpy(), f"{name}/alpha": alpha.numpy()})
+        put_outputs(out, f"{name}/", y32, y64)
+        out.update({f"{name}/sd/{k}": v for k, v in sd_numpy(op).items()})
+
+    # blocks (eval, calibrated BN)
+    for name, cin, cout, layout, T, V in (("blk_64_64", 64, 64, "h36m", 35, 22), ("blk_6_64", 6, 64, "h36m", 35, 22),
+                                          ("blk_64_3", 64, 3, "h36m", 35, 22), ("blk_64_64_cmu", 64, 64, "cmu", 35, 25)):
+        blk = F.DSTDGCB(cin, cout, T, V, layout)
+        randomise_fast(blk)
+        perturb_bn(blk, gen)
+        bias_noise(blk)
+        calibrate(blk, lambda: torch.randn(8, T, V, cin, generator=gen))
+        x = torch.randn(1, T, V, cin, generator=gen)
+        with torch.no_grad():
+            y32 = blk(x).numpy()
+        y64 = run64(blk, x)
+        out[f"{name}/x"] = x.numpy()
+        put_outputs(out, f"{name}/", y32, y64)
+        out.update({f"{name}/sd/{k}": v for k, v in sd_numpy(blk).items()})
+
+    def build(cfg, dropout):
+        opts = dict(input_channels=6, input_time_frame=cfg["Tin"], output_time_frame=cfg["Tout"],
+                    st_gcnn_dropout=dropout, joints_to_consider=cfg["V"], num_feature=64, num_layers=5,
+                    layout=cfg["layout"])
+        m = F.DSTDGCN(**opts)
+        for b in m.modules():
+            if isinstance(b, F.DSTDGCB):
+                randomise_fast(b)
+        perturb_bn(m, gen)
+        return m, opts
+
+    # whole models (eval, calibrated BN)
+    for tag in ("h36m", "3dpw"):
+        cfg = CONFIGS[tag]
+        T = cfg["Tin"] + cfg["Tout"]
+        m, opts = build(cfg, 0.1)
+        calibrate(m, lambda: synth_input(gen, 16, T, cfg["V"], cfg["Tin"]))
+        x = synth_input(gen, 4, T, cfg["V"], cfg["Tin"])
+        with torch.no_grad():
+            y32 = m(x).numpy()
+        y64 = run64(m, x)
+        out[f"model_{tag}/x"] = x.numpy()
+        put_outputs(out, f"model_{tag}/", y32, y64)
+        out.update({f"model_{tag}/opt/{k}": np.array(v) for k, v in opts.items()})
+        out.update({f"model_{tag}/sd/{k}": v for k, v in sd_numpy(m).items()})
+
+    # one training step (forward + inverse pass, engine/prediction.py:258-290)
+    # in fp64 and fp32: gradients and the updated BN running statistics
+    cfg = CONFIGS["3dpw"]
+    T = cfg["Tin"] + cfg["Tout"]
+    m, opts = build(cfg, 0.0)
+    sd0 = {k: v.clone() for k, v in m.state_dict().items()}
+    seq = torch.randn(4, T, cfg["V"] * 3, generator=gen)
+    inp = seq.clone()
+    inp[:, cfg["Tin"]:] = inp[:, cfg["Tin"] - 1:cfg["Tin"]]
+    inv = seq.flip(1).clone()
+    inv[:, cfg["Tin"]:] = inv[:, cfg["Tin"] - 1:cfg["Tin"]]
+
+    def step(dtype):
+        mm = F.DSTDGCN(**opts)
+        mm.load_state_dict(sd0)
+        mm = mm.to(dtype).train()
+        i, iv, s = (t.to(dtype) for t in (inp, inv, seq))
+        B, T_, VC = i.shape
+        loss = mpjpe_error_3d(mm(i.view(B, T_, VC // 3, 3)).reshape(B, T_, VC), s)
+        loss_i = mpjpe_error_3d(mm(iv.view(B, T_, VC // 3, 3)).reshape(B, T_, VC), s.flip(1))
+        all_loss = (loss + loss_i) / 2
+        all_loss.backward()
+        g = {k: p.grad.detach().clone() for k, p in mm.named_parameters() if p.grad is not None}
+        return float(all_loss.detach()), g, {k: v.detach().clone() for k, v in mm.state_dict().items()}
+
+    l64, g64, sd64 = step(torch.float64)
+    l32, g32, _ = step(torch.float32)
+    out.update({"train/inp": inp.numpy(), "train/inv": inv.numpy(), "train/seq": seq.numpy(),
+                "train/loss64": np.array(l64), "train/loss32": np.array(l32)})
+    out.update({f"train/opt/{k}": np.array(v) for k, v in opts.items()})
+    out.update({f"train/sd0/{k}": v.numpy() for k, v in sd0.items()})
+    for k in g64:
+        out[f"train/g64/{k}"] = g64[k].float().numpy()  # fp64 values rounded to fp32
+        out[f"train/g32err/{k}"] = np.array(float((g32[k].double() - g64[k]).abs().max()))
+    for k, v in sd64.items():
+        if "running_" in k:
+            out[f"train/sd1/{k}"] = v.float().numpy()
+    np.savez_compressed(os.path.join(HERE, "dstdgcn_fast.npz"), **out)
+
+
 def main():
     torch.set_num_threads(8)
     gen = torch.Generator().manual_seed(20250725)
@@ -403,6 +532,9 @@ def main():
     if sys.argv[1:] == ["plain"]:
         gen_plain_layers(gen)
         return
+    if sys.argv[1:] == ["fast"]:
+        gen_fast(gen)
+        return
     gen_graphs()
     gen_ops(gen)
     gen_blocks(gen)
@@ -410,6 +542,7 @@ def main():
     gen_engine(gen)
     gen_train_grads(gen)
     gen_plain_layers(gen)
+    gen_fast(gen)
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(HERE, f)))

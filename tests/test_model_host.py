@@ -34,3 +34,35 @@ def test_tensor_tree_matches_torch_walk_and_invalidates():
     m2 = copy.deepcopy(m)
     assert same(m2)
     assert not any(x is y for x, y in zip(m2._tree.get(m2)[0], m.parameters()))
+
+
+def test_fast_variant_schema_and_derivation_cpu():
+    """model.dstdgcn_fast (reference model/dstdgcn_fast.py): the reference's
+    state_dict keys in order, and the dstdgcn.py-schema shadow derived from
+    it (m1/m2 swapped, -W_rm, A^T, Linear -> 1x1 conv, BN (v,c) -> (c,v))
+    reproduces the reference's fp64 output through the dstdgcn.py oracle;
+    building the shadow leaves the caller's RNG alone."""
+    import numpy as np
+
+    from conftest import group, load_npz
+    from model import dstdgcn_fast as F
+    from oracle import dstdgcn_oracle as O
+
+    d = load_npz("dstdgcn_fast.npz")
+    for tag in ("h36m", "3dpw"):
+        p = f"model_{tag}/"
+        sd = group(d, p + "sd/")
+        opts = {k[len(p + "opt/"):]: d[k].item() for k in d.files if k.startswith(p + "opt/")}
+        m = F.DSTDGCN(**opts)
+        assert list(m.state_dict()) == list(sd)
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        state = torch.random.get_rng_state()
+        sh = m._shadow_for(torch.device("cpu"))
+        assert torch.equal(state, torch.random.get_rng_state())
+        m._sync(sh)
+        y = O.dstdgcn(d[p + "x"], {k: v.detach() for k, v in sh.state_dict().items()}, opts["num_layers"])
+        ref = d[p + "y64"]
+        assert np.abs(y.numpy() - ref).max() / np.abs(ref).max() < 1e-6
+        assert not any(k.startswith("_shadow") for k in m.state_dict())
+        c = copy.deepcopy(m)
+        assert c.__dict__["_shadow"] is None

@@ -111,3 +111,59 @@ def test_oracle_plain_st_gcnn_layer(name):
     ks, stride = PLAIN[name]
     y = O.st_gcnn_layer_plain(torch.from_numpy(d[f"{name}/x"]).double(), p, ks, stride)
     assert rel_err(y.numpy(), d[f"{name}/y64"]) < 1e-6
+
+
+# ---- model/dstdgcn_fast.py (the channels-last variant, dstdgcn_fast.npz) ----
+FAST_OPS = ["op_s_64_64", "op_s_6_64", "op_t_64_64", "op_t_64_64_3dpw"]
+FAST_BLOCKS = ["blk_64_64", "blk_6_64", "blk_64_3", "blk_64_64_cmu"]
+
+
+@pytest.mark.parametrize("name", FAST_OPS)
+def test_oracle_fast_dstdgc_op(name):
+    d = load_npz("dstdgcn_fast.npz")
+    mode = "spatial" if name.startswith("op_s") else "temporal"
+    y = O.fast_dstdgc_forward(d[f"{name}/x"], group(d, f"{name}/sd/"), d[f"{name}/A"], d[f"{name}/alpha"], mode)
+    assert rel_err(y.numpy(), d[f"{name}/y64"]) < 1e-6
+
+
+@pytest.mark.parametrize("name", FAST_BLOCKS)
+def test_oracle_fast_dstdgcb(name):
+    d = load_npz("dstdgcn_fast.npz")
+    y = O.fast_dstdgcb_forward(d[f"{name}/x"], group(d, f"{name}/sd/"))
+    assert rel_err(y.numpy(), d[f"{name}/y64"]) < 1e-6
+
+
+@pytest.mark.parametrize("tag", ["h36m", "3dpw"])
+def test_oracle_fast_dstdgcn(tag):
+    d = load_npz("dstdgcn_fast.npz")
+    p = f"model_{tag}/"
+    y = O.fast_dstdgcn(d[p + "x"], group(d, p + "sd/"), int(d[p + "opt/num_layers"]))
+    assert rel_err(y.numpy(), d[p + "y64"]) < 1e-6
+
+
+def test_oracle_fast_train_step_fp64():
+    """One training step of the fast variant (forward + inverse pass) in fp64:
+    loss, every gradient and the BN running-stat updates of the reference."""
+    d = load_npz("dstdgcn_fast.npz")
+    sd0 = group(d, "train/sd0/")
+    P = {k: torch.tensor(v, dtype=torch.float64, requires_grad=not k.endswith(("A_t", "running_mean", "running_var")))
+         for k, v in sd0.items() if not k.endswith("num_batches_tracked")}
+    seq = torch.from_numpy(d["train/seq"]).double()
+    B, T, VC = seq.shape
+    O.BN_RECORD = []
+    try:
+        outs = [O.fast_dstdgcn_fn(torch.from_numpy(d[f"train/{n}"]).double().view(B, T, VC // 3, 3), P, 5,
+                                  training=True).reshape(B, T, VC) for n in ("inp", "inv")]
+        rec = O.BN_RECORD
+    finally:
+        O.BN_RECORD = None
+    loss = (O.mpjpe_error_3d(outs[0], seq) + O.mpjpe_error_3d(outs[1], seq.flip(1))) / 2
+    assert abs(float(loss.detach()) - float(d["train/loss64"])) < 1e-9 * float(d["train/loss64"])
+    loss.backward()
+    for k, p in P.items():
+        if p.requires_grad and f"train/g64/{k}" in d:
+            g = d[f"train/g64/{k}"]
+            assert np.abs(p.grad.numpy() - g).max() <= 1e-6 * max(np.abs(g).max(), 1e-3), k
+    # running statistics: momentum 0.1, two train forwards (batch, inverse)
+    keys = [k for k in sd0 if k.endswith("running_mean")]
+    assert len(rec) == 2 * len(keys)
