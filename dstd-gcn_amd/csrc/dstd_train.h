@@ -119,6 +119,7 @@ struct BnFwd {
   float* zsave = nullptr;
   float* mean;
   float* rstd;
+  int use_running = 0;  // eval-mode BN: mean / rstd from the running stats, no update
 };
 hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s);
 
@@ -139,6 +140,7 @@ struct BnBwd {
   float* dz_out = nullptr;
   float* dgamma;
   float* dbeta;
+  int use_running = 0;  // mean / rstd are constants (eval-mode BN): du = gamma * rstd * dz
 };
 // scratch (both directions) >= bn_scratch_floats(B, C, T, V)
 size_t bn_scratch_floats(int B, int C, int T, int V);
@@ -151,6 +153,11 @@ hipError_t sum_into(const float* partial, int n, float* out, hipStream_t s);
 hipError_t prep_nctv(const float* x, int B, int T, int V, int C, float* X0, hipStream_t s);
 // y[n][t][v][c] = O[n][c][t][v] + x[n][T-1][v][c]
 hipError_t out_ntvc(const float* O, const float* x, int B, int T, int V, int C, float* y, hipStream_t s);
+// Input gradient of the model boundary (prep_nctv and the output residual
+// y += x[:, T-1], model/dstdgcn.py:298-303, 315): dX0 [B][2C][T][V], dy
+// [B][T][V][C] -> dx [B][T][V][C] (=):  dx[t] = dX0[c][t] + dX0[C+c][t], and
+// dx[T-1] += sum_t (dy[t] - dX0[C+c][t]).
+hipError_t prep_nctv_bwd(const float* dX0, const float* dy, int B, int T, int V, int C, float* dx, hipStream_t s);
 // dO[n][c][t][v] = dy[n][t][v][c]
 hipError_t out_ntvc_bwd(const float* dy, int B, int T, int V, int C, float* dO, hipStream_t s);
 

@@ -505,6 +505,14 @@ __global__ void k_bn_stats_merge(BnFwd a, int B, int C, int T, int V, int splits
   }
 }
 
+// eval-mode BN: the saved mean / rstd are the running statistics
+__global__ void k_bn_eval_stats(BnFwd a, int CV) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= CV) return;
+  a.mean[ch] = a.running_mean[ch];
+  a.rstd[ch] = 1.f / sqrtf(a.running_var[ch] + a.eps);
+}
+
 __global__ void k_bn_apply(BnFwd a, size_t n, int CV, int TV, int V) {
   const float w = a.prelu ? *a.prelu : 0.f;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -587,7 +595,8 @@ __global__ void k_bn_bwd_apply(BnBwd a, size_t n, int CV, int TV, int V, int row
     const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
     const float mean = a.mean[ch], rstd = a.rstd[ch];
     const float xh = (u - mean) * rstd;
-    a.du[i] = a.gamma[ch] * rstd * (dz - sums[2 * ch] * inv - xh * sums[2 * ch + 1] * inv);
+    a.du[i] = a.use_running ? a.gamma[ch] * rstd * dz
+                            : a.gamma[ch] * rstd * (dz - sums[2 * ch] * inv - xh * sums[2 * ch + 1] * inv);
     if (a.dz_out) a.dz_out[i] = dz;
   }
 }
@@ -620,6 +629,23 @@ __global__ void k_out_ntvc(const float* O, const float* x, int B, int T, int V, 
     const int n = r / T;
     y[e] = O[(((size_t)n * C + c) * T + t) * V + v] + x[(((size_t)n * T + T - 1) * V + v) * C + c];
   }
+}
+
+// one thread per (n, v, c): the T-long column, then the x[T-1] terms
+__global__ void k_prep_nctv_bwd(const float* dX0, const float* dy, int B, int T, int V, int C, float* dx) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= B * V * C) return;
+  const int c = e % C, v = (e / C) % V, n = e / (C * V);
+  const size_t TV = (size_t)T * V;
+  const float* d0 = dX0 + ((size_t)n * 2 * C + c) * TV + v;
+  const float* d1 = d0 + (size_t)C * TV;
+  float last = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const size_t o = (((size_t)n * T + t) * V + v) * C + c;
+    dx[o] = d0[t * V] + d1[t * V];
+    last += dy[o] - d1[t * V];
+  }
+  dx[(((size_t)n * T + T - 1) * V + v) * C + c] += last;
 }
 
 __global__ void k_out_ntvc_bwd(const float* dy, int B, int T, int V, int C, float* dO) {
@@ -850,8 +876,13 @@ size_t bn_scratch_floats(int B, int C, int T, int V) {
 
 hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s) {
   const int splits = bn_splits(B, T);
-  k_bn_stats_part<<<dim3(C, splits), kRedThreads, 0, s>>>(a, B, C, T, V, splits, scratch);
-  k_bn_stats_merge<<<cdiv(C * V, 256), 256, 0, s>>>(a, B, C, T, V, splits, scratch);
+  if (a.use_running) {
+    if (!a.running_mean || !a.running_var) return hipErrorInvalidValue;
+    k_bn_eval_stats<<<cdiv(C * V, 256), 256, 0, s>>>(a, C * V);
+  } else {
+    k_bn_stats_part<<<dim3(C, splits), kRedThreads, 0, s>>>(a, B, C, T, V, splits, scratch);
+    k_bn_stats_merge<<<cdiv(C * V, 256), 256, 0, s>>>(a, B, C, T, V, splits, scratch);
+  }
   const size_t n = (size_t)B * C * T * V;
   k_bn_apply<<<grid_for(n), 256, 0, s>>>(a, n, C * V, T * V, V);
   return hipGetLastError();
@@ -877,6 +908,11 @@ hipError_t prep_nctv(const float* x, int B, int T, int V, int C, float* X0, hipS
 
 hipError_t out_ntvc(const float* O, const float* x, int B, int T, int V, int C, float* y, hipStream_t s) {
   k_out_ntvc<<<grid_for((size_t)B * C * T * V), 256, 0, s>>>(O, x, B, T, V, C, y);
+  return hipGetLastError();
+}
+
+hipError_t prep_nctv_bwd(const float* dX0, const float* dy, int B, int T, int V, int C, float* dx, hipStream_t s) {
+  k_prep_nctv_bwd<<<cdiv(B * V * C, 256), 256, 0, s>>>(dX0, dy, B, T, V, C, dx);
   return hipGetLastError();
 }
 

@@ -327,7 +327,7 @@ void carve_block_ws(Carver& cv, BlockWs& w, int B, int T, int V, std::initialize
 }
 
 hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum, float* y,
-                     const BlockSaved& S, hipStream_t s) {
+                     const BlockSaved& S, hipStream_t s, int run = 0) {
   const int cin = p->cin, cout = p->cout, TV = T * V;
   const bool res = cin != cout;
   // A_s*W_s + R_s, A_t + R_t (model/dstdgcn.py:146-149, 157-160)
@@ -356,6 +356,7 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.out = S.r;
     rb.mean = S.rmean;
     rb.rstd = S.rrstd;
+    rb.use_running = run;
     DSTD_TRYH(bn_train_fwd(rb, B, cout, T, V, S.red, s));
     r = S.r;
   }
@@ -373,12 +374,14 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.zsave = S.z;
   bb.mean = S.mean;
   bb.rstd = S.rstd;
+  bb.use_running = run;
   DSTD_TRYH(bn_train_fwd(bb, B, cout, T, V, S.red, s));
   return op_fwd(gt, S.h, &p->conv_t, S.at, p->alpha_tm, y, 0.f, S.op[2], s);  // :156-162
 }
 
 hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, int V, const BlockSaved& S,
-                     const float* dy, float* dx, const dstd_block_grads* g, const BlockWs& W, hipStream_t s) {
+                     const float* dy, float* dx, const dstd_block_grads* g, const BlockWs& W, hipStream_t s,
+                     int run = 0) {
   const int cin = p->cin, cout = p->cout, TV = T * V;
   const bool res = cin != cout;
   const size_t act = (size_t)B * cout * TV;
@@ -398,6 +401,7 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.dz_out = W.dr;
   bb.dgamma = g->bn.weight;
   bb.dbeta = g->bn.bias;
+  bb.use_running = run;
   DSTD_TRYH(bn_train_bwd(bb, B, cout, T, V, W.op.red, g->prelu, s));
   if (res) {
     BnBwd rb;
@@ -409,6 +413,7 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.du = W.drc;
     rb.dgamma = g->res_bn.weight;
     rb.dbeta = g->res_bn.bias;
+    rb.use_running = run;
     DSTD_TRYH(bn_train_bwd(rb, B, cout, T, V, W.op.red, nullptr, s));
     DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, W.op.red, s));
   } else if (dx) {
@@ -457,7 +462,7 @@ void carve_model_saved(Carver& cv, ModelSaved& s, int B, int T, int V, int C, in
 
 struct ModelWs {
   BlockWs blk;
-  float *dO, *dha, *dhb, *du, *pp;
+  float *dO, *dha, *dhb, *du, *pp, *dX0;
 };
 void carve_model_ws(Carver& cv, ModelWs& w, int B, int T, int V, int C) {
   carve_block_ws(cv, w.blk, B, T, V, {{6, C}, {C, C}, {C, 3}});
@@ -467,6 +472,7 @@ void carve_model_ws(Carver& cv, ModelWs& w, int B, int T, int V, int C) {
   w.dhb = cv.take(act);
   w.du = cv.take(act);
   w.pp = cv.take(C);
+  w.dX0 = cv.take((size_t)B * 6 * T * V);
 }
 
 }  // namespace
@@ -541,23 +547,29 @@ size_t dstd_block_train_workspace_bytes(int B, int cin, int cout, int T, int V) 
   return cv.off + 256;
 }
 
-int dstd_block_train_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum, float* y,
-                         void* saved, size_t saved_bytes, void* stream) {
-  if (!block_ok(p) || !x || !y || !saved) return DSTD_EINVAL;
+int dstd_block_train_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum,
+                            float* y, void* saved, size_t saved_bytes, void* stream, unsigned flags) {
+  if (!block_ok(p) || !x || !y || !saved || (flags & ~DSTD_TRAIN_RUNNING_STATS)) return DSTD_EINVAL;
   if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
   if (!shape_ok(B, T, V)) return DSTD_ELIMIT;
   if (saved_bytes < dstd_block_train_saved_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
   Carver cv{(char*)saved};
   BlockSaved S;
   carve_block_saved(cv, S, B, p->cin, p->cout, T, V);
-  DSTD_TRY(block_fwd(p, x, B, T, V, momentum, y, S, (hipStream_t)stream));
+  DSTD_TRY(block_fwd(p, x, B, T, V, momentum, y, S, (hipStream_t)stream, (flags & DSTD_TRAIN_RUNNING_STATS) != 0));
   return DSTD_OK;
 }
 
-int dstd_block_train_bwd(const dstd_block_params* p, const float* x, int B, int T, int V, const void* saved,
-                         size_t saved_bytes, const float* dy, float* dx, const dstd_block_grads* g,
-                         void* workspace, size_t workspace_bytes, void* stream) {
+int dstd_block_train_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum, float* y,
+                         void* saved, size_t saved_bytes, void* stream) {
+  return dstd_block_train_fwd_ex(p, x, B, T, V, momentum, y, saved, saved_bytes, stream, 0u);
+}
+
+int dstd_block_train_bwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, const void* saved,
+                            size_t saved_bytes, const float* dy, float* dx, const dstd_block_grads* g,
+                            void* workspace, size_t workspace_bytes, void* stream, unsigned flags) {
   if (!block_ok(p) || !block_grads_ok(p, g) || !x || !dy || !saved || !workspace) return DSTD_EINVAL;
+  if (flags & ~DSTD_TRAIN_RUNNING_STATS) return DSTD_EINVAL;
   if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
   if (!shape_ok(B, T, V)) return DSTD_ELIMIT;
   if (saved_bytes < dstd_block_train_saved_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
@@ -568,8 +580,15 @@ int dstd_block_train_bwd(const dstd_block_params* p, const float* x, int B, int 
   Carver cw{(char*)workspace};
   BlockWs W;
   carve_block_ws(cw, W, B, T, V, {{p->cin, p->cout}});
-  DSTD_TRY(block_bwd(p, x, B, T, V, S, dy, dx, g, W, (hipStream_t)stream));
+  DSTD_TRY(block_bwd(p, x, B, T, V, S, dy, dx, g, W, (hipStream_t)stream, (flags & DSTD_TRAIN_RUNNING_STATS) != 0));
   return DSTD_OK;
+}
+
+int dstd_block_train_bwd(const dstd_block_params* p, const float* x, int B, int T, int V, const void* saved,
+                         size_t saved_bytes, const float* dy, float* dx, const dstd_block_grads* g,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+  return dstd_block_train_bwd_ex(p, x, B, T, V, saved, saved_bytes, dy, dx, g, workspace, workspace_bytes, stream,
+                                 0u);
 }
 
 size_t dstd_model_train_saved_bytes(int B, int T, int V, int num_feature, int num_layers) {
@@ -587,9 +606,12 @@ size_t dstd_model_train_workspace_bytes(int B, int T, int V, int num_feature, in
   return cv.off + 256;
 }
 
-int dstd_model_train_fwd(const dstd_model_params* p, const float* x, int B, float momentum, float dropout_p,
-                         unsigned long long seed, float* y, void* saved, size_t saved_bytes, void* stream) {
+int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, float momentum, float dropout_p,
+                            unsigned long long seed, float* y, void* saved, size_t saved_bytes, void* stream,
+                            unsigned flags) {
   if (!model_ok(p) || !x || !y || !saved || !(dropout_p >= 0.f && dropout_p < 1.f)) return DSTD_EINVAL;
+  if (flags & ~DSTD_TRAIN_RUNNING_STATS) return DSTD_EINVAL;
+  const int run = (flags & DSTD_TRAIN_RUNNING_STATS) != 0;
   const int T = p->T, V = p->V, C = p->num_feature, L = p->num_layers;
   if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
   if (!shape_ok(B, T, V) || !ch_ok(C)) return DSTD_ELIMIT;
@@ -601,7 +623,7 @@ int dstd_model_train_fwd(const dstd_model_params* p, const float* x, int B, floa
   carve_model_saved(cv, S, B, T, V, C, L);
   const size_t act = (size_t)B * C * T * V;
   DSTD_TRY(prep_nctv(x, B, T, V, 3, S.X0, s));                                   // :298-303
-  DSTD_TRY(block_fwd(&p->st_in, S.X0, B, T, V, momentum, S.y0, S.st_in, s));      // :305
+  DSTD_TRY(block_fwd(&p->st_in, S.X0, B, T, V, momentum, S.y0, S.st_in, s, run));  // :305
   BnFwd b0;                                                                      // :306-308
   b0.x = S.y0;
   b0.gamma = p->bn_in.weight;
@@ -615,10 +637,11 @@ int dstd_model_train_fwd(const dstd_model_params* p, const float* x, int B, floa
   b0.zsave = S.z0;
   b0.mean = S.m0;
   b0.rstd = S.r0;
+  b0.use_running = run;
   DSTD_TRY(bn_train_fwd(b0, B, C, T, V, S.red, s));
   if (dropout_p > 0.f) DSTD_TRY(dropout(S.hp0, S.h[0], act, dropout_p, seed, s));  // do_in
   for (int i = 0; i < L; ++i) {                                                  // :310-311
-    DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s));
+    DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s, run));
     BnFwd be;  // BN(block(h) + h) -> PReLU  (:278-285, Identity residual :247-248)
     be.x = S.yb[i];
     be.x2 = S.h[i];
@@ -633,18 +656,27 @@ int dstd_model_train_fwd(const dstd_model_params* p, const float* x, int B, floa
     be.zsave = S.ze[i];
     be.mean = S.me[i];
     be.rstd = S.re[i];
+    be.use_running = run;
     DSTD_TRY(bn_train_fwd(be, B, C, T, V, S.red, s));
   }
-  DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s));  // :313
-  DSTD_TRY(out_ntvc(S.o, x, B, T, V, 3, y, s));                                  // :314-315
+  DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s, run));  // :313
+  DSTD_TRY(out_ntvc(S.o, x, B, T, V, 3, y, s));                                       // :314-315
   return DSTD_OK;
 }
 
-int dstd_model_train_bwd(const dstd_model_params* p, const float* x, int B, float dropout_p,
-                         unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
-                         const dstd_model_grads* g, void* workspace, size_t workspace_bytes, void* stream) {
+int dstd_model_train_fwd(const dstd_model_params* p, const float* x, int B, float momentum, float dropout_p,
+                         unsigned long long seed, float* y, void* saved, size_t saved_bytes, void* stream) {
+  return dstd_model_train_fwd_ex(p, x, B, momentum, dropout_p, seed, y, saved, saved_bytes, stream, 0u);
+}
+
+int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, float dropout_p,
+                            unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
+                            const dstd_model_grads* g, float* dx, void* workspace, size_t workspace_bytes,
+                            void* stream, unsigned flags) {
   if (!model_ok(p) || !g || !x || !dy || !saved || !workspace || !(dropout_p >= 0.f && dropout_p < 1.f))
     return DSTD_EINVAL;
+  if (flags & ~DSTD_TRAIN_RUNNING_STATS) return DSTD_EINVAL;
+  const int run = (flags & DSTD_TRAIN_RUNNING_STATS) != 0;
   const int T = p->T, V = p->V, C = p->num_feature, L = p->num_layers;
   if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
   if (!shape_ok(B, T, V) || !ch_ok(C)) return DSTD_ELIMIT;
@@ -667,7 +699,7 @@ int dstd_model_train_bwd(const dstd_model_params* p, const float* x, int B, floa
   float* dha = W.dha;
   float* dhb = W.dhb;
   DSTD_TRY(hipMemsetAsync(dha, 0, act * sizeof(float), s));
-  DSTD_TRY(block_bwd(&p->st_out, S.h[L], B, T, V, S.st_out, W.dO, dha, &g->st_out, W.blk, s));
+  DSTD_TRY(block_bwd(&p->st_out, S.h[L], B, T, V, S.st_out, W.dO, dha, &g->st_out, W.blk, s, run));
   for (int i = L - 1; i >= 0; --i) {
     BnBwd be;
     be.x = S.yb[i];
@@ -681,10 +713,11 @@ int dstd_model_train_bwd(const dstd_model_params* p, const float* x, int B, floa
     be.du = W.du;
     be.dgamma = g->enc_bn[i].weight;
     be.dbeta = g->enc_bn[i].bias;
+    be.use_running = run;
     DSTD_TRY(bn_train_bwd(be, B, C, T, V, W.blk.op.red, g->enc_prelu[i], s));
     // u = block(h) + h: dh = du (identity path) + block backward
     DSTD_TRY(hipMemcpyAsync(dhb, W.du, act * sizeof(float), hipMemcpyDeviceToDevice, s));
-    DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s));
+    DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s, run));
     std::swap(dha, dhb);
   }
   if (dropout_p > 0.f) DSTD_TRY(dropout(dha, dha, act, dropout_p, seed, s));
@@ -699,9 +732,19 @@ int dstd_model_train_bwd(const dstd_model_params* p, const float* x, int B, floa
   b0.du = W.du;
   b0.dgamma = g->bn_in.weight;
   b0.dbeta = g->bn_in.bias;
+  b0.use_running = run;
   DSTD_TRY(bn_train_bwd(b0, B, C, T, V, W.blk.op.red, g->prelu, s));
-  DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, nullptr, &g->st_in, W.blk, s));
+  if (dx) DSTD_TRY(hipMemsetAsync(W.dX0, 0, (size_t)B * 6 * T * V * sizeof(float), s));
+  DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, dx ? W.dX0 : nullptr, &g->st_in, W.blk, s, run));
+  if (dx) DSTD_TRY(prep_nctv_bwd(W.dX0, dy, B, T, V, 3, dx, s));  // :298-303, 315
   return DSTD_OK;
+}
+
+int dstd_model_train_bwd(const dstd_model_params* p, const float* x, int B, float dropout_p,
+                         unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
+                         const dstd_model_grads* g, void* workspace, size_t workspace_bytes, void* stream) {
+  return dstd_model_train_bwd_ex(p, x, B, dropout_p, seed, saved, saved_bytes, dy, g, nullptr, workspace,
+                                 workspace_bytes, stream, 0u);
 }
 
 size_t dstd_loss_workspace_bytes(void) { return (size_t)mpjpe_partials() * sizeof(float) + 256; }

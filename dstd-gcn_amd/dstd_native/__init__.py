@@ -73,6 +73,7 @@ class ModelGrads(ctypes.Structure):
                 ("enc_prelu", ctypes.c_void_p * MAX_LAYERS), ("st_out", BlockGrads)]
 
 
+TRAIN_RUNNING_STATS = 1  # include/dstd_gcn_train.h DSTD_TRAIN_RUNNING_STATS
 FWD_REUSE_CONSTANTS = 1  # include/dstd_gcn.h DSTD_FWD_REUSE_CONSTANTS
 FWD_EXACT_FP32 = 2  # include/dstd_gcn.h DSTD_FWD_EXACT_FP32
 KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL = range(6)
@@ -168,6 +169,16 @@ def lib():
         L.dstd_model_train_bwd.restype = ci
         L.dstd_model_train_bwd.argtypes = [ctypes.POINTER(ModelParams), vp, ci, f32, u64, vp, sz, vp,
                                            ctypes.POINTER(ModelGrads), vp, sz, vp]
+        uf = ctypes.c_uint
+        L.dstd_block_train_fwd_ex.restype = ci
+        L.dstd_block_train_fwd_ex.argtypes = L.dstd_block_train_fwd.argtypes + [uf]
+        L.dstd_block_train_bwd_ex.restype = ci
+        L.dstd_block_train_bwd_ex.argtypes = L.dstd_block_train_bwd.argtypes + [uf]
+        L.dstd_model_train_fwd_ex.restype = ci
+        L.dstd_model_train_fwd_ex.argtypes = L.dstd_model_train_fwd.argtypes + [uf]
+        L.dstd_model_train_bwd_ex.restype = ci
+        L.dstd_model_train_bwd_ex.argtypes = [ctypes.POINTER(ModelParams), vp, ci, f32, u64, vp, sz, vp,
+                                              ctypes.POINTER(ModelGrads), vp, vp, sz, vp, uf]
         L.dstd_loss_workspace_bytes.restype = sz
         L.dstd_loss_workspace_bytes.argtypes = []
         L.dstd_mpjpe_fwd.restype = ci
@@ -201,7 +212,9 @@ TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_b
                  "dstd_dstdgc_train_bwd", "dstd_block_train_saved_bytes", "dstd_block_train_workspace_bytes",
                  "dstd_block_train_fwd", "dstd_block_train_bwd", "dstd_model_train_saved_bytes",
                  "dstd_model_train_workspace_bytes", "dstd_model_train_fwd", "dstd_model_train_bwd",
-                 "dstd_loss_workspace_bytes", "dstd_mpjpe_fwd", "dstd_mpjpe_bwd", "dstd_frame_mpjpe")
+                 "dstd_loss_workspace_bytes", "dstd_mpjpe_fwd", "dstd_mpjpe_bwd", "dstd_frame_mpjpe",
+                 "dstd_block_train_fwd_ex", "dstd_block_train_bwd_ex", "dstd_model_train_fwd_ex",
+                 "dstd_model_train_bwd_ex")
 AUX_EXPORTS = ("dstd_ctg_workspace_bytes", "dstd_ctg_fwd", "dstd_ctg_bwd", "dstd_conv2d_workspace_bytes",
                "dstd_conv2d_fwd", "dstd_conv2d_bwd")
 

@@ -22,10 +22,12 @@ backward, with the reference's gradient semantics (A_s / A_t constant, R_s
 aliasing A_s's storage, alpha_sm shared by both spatial convs).
 
 There is no CPU / eager fallback: a tensor off the GPU or a missing library
-raises.  An eval-mode DSTDGCB / DSTDGCN output that needs a gradient carries a
-grad_fn whose backward raises (the reference would back-propagate through
-running-statistics BN there; no shipped recipe does), so a silent wrong
-gradient is impossible.
+raises.  An eval-mode DSTDGCB / DSTDGCN forward that autograd will
+differentiate (grad enabled and an input or parameter requiring grad) runs
+the native training path with BatchNorm on its running statistics
+(include/dstd_gcn_train.h DSTD_TRAIN_RUNNING_STATS), as the reference
+back-propagates through its eval-mode modules; under torch.no_grad() (or
+with frozen parameters and input) eval runs the fused inference kernels.
 """
 import itertools
 import math
@@ -64,17 +66,17 @@ def weights_init(m):
 
 
 class _ForwardOnly(torch.autograd.Function):
-    """Marks eval-mode block / model outputs: forward is identity, backward
-    refuses loudly (train-mode modules carry the native backward instead)."""
+    """Empty-batch outputs: forward is identity, backward gives the zero
+    gradients torch's own ops would (nothing flows through an empty batch)."""
 
     @staticmethod
     def forward(ctx, y, *deps):
+        ctx.shapes = [(d.shape, d.dtype, d.device) for d in deps]
         return y
 
     @staticmethod
-    def backward(ctx, *grads):
-        raise NotImplementedError("backward through an eval-mode DSTDGCB / DSTDGCN (running-statistics BN) is not "
-                                  "built; call .train() for the native training path")
+    def backward(ctx, dy, *rest):
+        return (dy, *[torch.zeros(sh, dtype=dt, device=dev) for sh, dt, dev in ctx.shapes])
 
 
 # Native modules carry an instance token that is never reused (unlike id()):
@@ -240,8 +242,15 @@ class _OpTrain(torch.autograd.Function):
         return (None, None, dx, dA, dalpha, *arena.views())
 
 
+def _bn_flags(module):
+    """Batch statistics in train mode; the running statistics, not updated,
+    under .eval() (an eval-mode forward that autograd differentiates)."""
+    return 0 if module.training else native.TRAIN_RUNNING_STATS
+
+
 class _BlockTrain(torch.autograd.Function):
-    """Train-mode DSTDGCB forward + native backward (reference :141-163)."""
+    """DSTDGCB forward + native backward (reference :141-163): train-mode BN,
+    or running-statistics BN for an eval-mode block under autograd."""
 
     @staticmethod
     def forward(ctx, blk, x, *params):
@@ -252,11 +261,13 @@ class _BlockTrain(torch.autograd.Function):
         nbytes = L.dstd_block_train_saved_bytes(B, cin, blk.out_channels, T, V)
         saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         p = native.block_struct(blk)
-        code = L.dstd_block_train_fwd(p, native.ptr(x, "x"), B, T, V, _bn_momentum(blk), native.ptr(y, "y"),
-                                      saved.data_ptr(), nbytes, native.stream_handle(dev))
-        native.check(code, "dstd_block_train_fwd")
-        _count_batch(blk)
-        ctx.blk, ctx.saved_buf = blk, saved
+        flags = _bn_flags(blk)
+        code = L.dstd_block_train_fwd_ex(p, native.ptr(x, "x"), B, T, V, _bn_momentum(blk), native.ptr(y, "y"),
+                                         saved.data_ptr(), nbytes, native.stream_handle(dev), flags)
+        native.check(code, "dstd_block_train_fwd_ex")
+        if not flags:
+            _count_batch(blk)
+        ctx.blk, ctx.saved_buf, ctx.flags = blk, saved, flags
         ctx.save_for_backward(x)
         return y
 
@@ -272,17 +283,18 @@ class _BlockTrain(torch.autograd.Function):
         dx = torch.zeros_like(x) if ctx.needs_input_grad[1] else None
         nbytes = L.dstd_block_train_workspace_bytes(B, cin, blk.out_channels, T, V)
         ws = native.workspace(dev, nbytes)
-        code = L.dstd_block_train_bwd(native.block_struct(blk), native.ptr(x, "x"), B, T, V,
-                                      ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(), native.ptr(dy, "dy"),
-                                      dx.data_ptr() if dx is not None else None, native.block_grads(blk, arena),
-                                      ws.data_ptr(), ws.numel(), native.stream_handle(dev))
-        native.check(code, "dstd_block_train_bwd")
+        code = L.dstd_block_train_bwd_ex(native.block_struct(blk), native.ptr(x, "x"), B, T, V,
+                                         ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(), native.ptr(dy, "dy"),
+                                         dx.data_ptr() if dx is not None else None, native.block_grads(blk, arena),
+                                         ws.data_ptr(), ws.numel(), native.stream_handle(dev), ctx.flags)
+        native.check(code, "dstd_block_train_bwd_ex")
         ctx.saved_buf = None
         return (None, dx, *arena.views())
 
 
 class _ModelTrain(torch.autograd.Function):
-    """Train-mode DSTDGCN forward + native backward (reference :293-317)."""
+    """DSTDGCN forward + native backward (reference :293-317): train mode, or
+    an eval-mode model under autograd (running-statistics BN, no dropout)."""
 
     @staticmethod
     def forward(ctx, model, x, *params):
@@ -293,13 +305,16 @@ class _ModelTrain(torch.autograd.Function):
         y = torch.empty_like(x)
         nbytes = L.dstd_model_train_saved_bytes(n, t, v, model.num_feature, model.num_layers)
         saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        drop = float(model.do_in.p)
+        flags = _bn_flags(model)
+        drop = float(model.do_in.p) if model.do_in.training else 0.0
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop > 0 else 0
-        code = L.dstd_model_train_fwd(p, native.ptr(x, "x"), n, _bn_momentum(model), drop, seed,
-                                      native.ptr(y, "y"), saved.data_ptr(), nbytes, native.stream_handle(dev))
-        native.check(code, "dstd_model_train_fwd")
-        _count_batch(model)
-        ctx.model, ctx.saved_buf, ctx.drop, ctx.seed = model, saved, drop, seed
+        code = L.dstd_model_train_fwd_ex(p, native.ptr(x, "x"), n, _bn_momentum(model), drop, seed,
+                                         native.ptr(y, "y"), saved.data_ptr(), nbytes, native.stream_handle(dev),
+                                         flags)
+        native.check(code, "dstd_model_train_fwd_ex")
+        if not flags:
+            _count_batch(model)
+        ctx.model, ctx.saved_buf, ctx.drop, ctx.seed, ctx.flags = model, saved, drop, seed, flags
         ctx.params = list(params)  # the backward reuses them (a module walk costs ~0.7 ms)
         ctx.save_for_backward(x)
         return y
@@ -329,14 +344,16 @@ class _ModelTrain(torch.autograd.Function):
                 arena.model_grads = g
         nbytes = L.dstd_model_train_workspace_bytes(n, t, v, model.num_feature, model.num_layers)
         ws = native.workspace(dev, nbytes)
-        code = L.dstd_model_train_bwd(model._native_params(), native.ptr(x, "x"), n, ctx.drop, ctx.seed,
-                                      ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(), native.ptr(dy, "dy"), g,
-                                      ws.data_ptr(), ws.numel(), native.stream_handle(dev))
-        native.check(code, "dstd_model_train_bwd")
+        dx = torch.empty_like(x) if ctx.needs_input_grad[1] else None
+        code = L.dstd_model_train_bwd_ex(model._native_params(), native.ptr(x, "x"), n, ctx.drop, ctx.seed,
+                                         ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(), native.ptr(dy, "dy"), g,
+                                         dx.data_ptr() if dx is not None else None, ws.data_ptr(), ws.numel(),
+                                         native.stream_handle(dev), ctx.flags)
+        native.check(code, "dstd_model_train_bwd_ex")
         ctx.saved_buf = None
         if direct:
-            return (None, None, *([None] * len(arena.params)))
-        return (None, None, *arena.views())
+            return (None, dx, *([None] * len(arena.params)))
+        return (None, dx, *arena.views())
 
 
 class BatchNorm(nn.Module):
@@ -472,12 +489,14 @@ class DSTDGCB(_NativeModule):
         native.require_device(x, "x")
         if B == 0 and not self.training:  # empty batch: empty output (reference torch semantics)
             return _mark(x.new_empty(0, self.out_channels, T, V), x, *self.parameters())
-        if self.training:
-            return _BlockTrain.apply(self, x, *self.parameters())
-        tensors = list(self.parameters()) + list(self.buffers())
-        y = torch.ops.dstd.dstdgcb_forward(x, tensors, self._dstd_uid, self.out_channels,
-                                           native.arith_flags(self.gc_arithmetic))
-        return _mark(y, x, *self.parameters())
+        params = list(self.parameters())
+        if self.training or _needs_grad(x, *params):
+            # train mode, or an eval-mode output autograd differentiates: the
+            # native training path (running-statistics BN in eval mode)
+            return _BlockTrain.apply(self, x, *params)
+        tensors = params + list(self.buffers())
+        return torch.ops.dstd.dstdgcb_forward(x, tensors, self._dstd_uid, self.out_channels,
+                                              native.arith_flags(self.gc_arithmetic))
 
     def _eval_native(self, x, flags):
         """dstd_block_fwd_ex (torch.ops.dstd.dstdgcb_forward)."""
@@ -741,12 +760,13 @@ class DSTDGCN(_NativeModule):
         native.require_device(x, "x")
         if n == 0 and not self.training:  # empty batch: empty output (reference torch semantics)
             return _mark(torch.empty_like(x), x, *self._tree.get(self)[0])
-        if self.training:
-            return _ModelTrain.apply(self, x, *self._tree.get(self)[0])
         params, buffers = self._tree.get(self)
-        y = torch.ops.dstd.dstdgcn_forward(x, params + buffers, self._dstd_uid,
-                                           native.arith_flags(self.gc_arithmetic))
-        return _mark(y, x, *params) if torch.is_grad_enabled() else y
+        if self.training or _needs_grad(x, *params):
+            # train mode, or an eval-mode forward autograd differentiates (the
+            # reference back-propagates through running-statistics BN there)
+            return _ModelTrain.apply(self, x, *params)
+        return torch.ops.dstd.dstdgcn_forward(x, params + buffers, self._dstd_uid,
+                                              native.arith_flags(self.gc_arithmetic))
 
     def _forward_native(self, x, y, prof=None, arith=None):
         """One eval forward through dstd_model_fwd_ex.  The folded constants

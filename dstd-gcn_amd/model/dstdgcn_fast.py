@@ -29,7 +29,7 @@ module of the dstdgcn.py schema whose tensors are derived from this module's
 Eval forwards re-derive the shadow only when a tensor changed (torch version
 counters, storage, the cache generation -- ``invalidate_native_cache``), then
 run the shadow's single C call (``dstd_model_fwd_ex`` for the model).  The
-training path runs the shadow's native autograd Functions with the derived
+training path (and an eval forward under autograd) runs the shadow's native autograd Functions with the derived
 tensors as their inputs, so autograd carries the native gradients back
 through the (linear) derivation onto this module's parameters, and the
 shadow's updated BN running statistics are written back after each
@@ -335,10 +335,12 @@ class DSTDGCB(_Shadowed):
         native.require_device(x, "x")
         sh = self._shadow_for(x.device)
         xs = x.permute(0, 3, 1, 2).contiguous()
-        if self.training:
+        if self.training or base._needs_grad(x, *self.parameters()):
+            # train mode, or eval under autograd (running-statistics BN)
             self._sync(sh, params=False)
             y = _BlockTrainM.apply(sh, xs, *self._derived_params(sh))
-            self._write_back_running_stats(sh)
+            if self.training:
+                self._write_back_running_stats(sh)
         else:
             self._sync(sh)
             y = sh(xs)
@@ -436,10 +438,11 @@ class DSTDGCN(_Shadowed):
         native.require_device(x, "x")
         sh = self._shadow_for(x.device)
         sh.do_in.p = self.do_in.p
-        if self.training:
+        if self.training or base._needs_grad(x, *self.parameters()):
             self._sync(sh, params=False)
             y = _ModelTrainM.apply(sh, x.contiguous(), *self._derived_params(sh))
-            self._write_back_running_stats(sh)
+            if self.training:
+                self._write_back_running_stats(sh)
             return y
         self._sync(sh)
         return sh(x)

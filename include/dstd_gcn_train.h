@@ -8,6 +8,7 @@
  *   dstd_dstdgc_train_fwd/bwd  <- DSTDGC.forward + autograd   model/dstdgcn.py:80-94
  *   dstd_block_train_fwd/bwd   <- DSTDGCB.forward (train BN)  model/dstdgcn.py:141-163
  *   dstd_model_train_fwd/bwd   <- DSTDGCN.forward (train)     model/dstdgcn.py:293-317
+ *   *_train_*_ex(RUNNING_STATS) <- the same under .eval() with autograd (BN on running stats)
  *   dstd_mpjpe_fwd/bwd         <- mpjpe_error_3d              engine/utils/loss.py:52-65
  *   dstd_frame_mpjpe           <- PredictionEngine.test       engine/prediction.py:366-404
  *
@@ -99,6 +100,18 @@ int dstd_block_train_bwd(const dstd_block_params* p, const float* x, int B, int 
                          size_t saved_bytes, const float* dy, float* dx, const dstd_block_grads* g,
                          void* workspace, size_t workspace_bytes, void* stream);
 
+/* _ex variants: flags DSTD_TRAIN_RUNNING_STATS runs every BatchNorm on its
+ * running statistics without updating them (eval-mode BN: the forward of an
+ * eval-mode DSTDGCB / DSTDGCN whose output needs a gradient, and its
+ * backward -- pass the same flags to both).  flags = 0 is the plain entry
+ * point (batch statistics, running stats updated with momentum). */
+#define DSTD_TRAIN_RUNNING_STATS 1u
+int dstd_block_train_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum,
+                            float* y, void* saved, size_t saved_bytes, void* stream, unsigned flags);
+int dstd_block_train_bwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, const void* saved,
+                            size_t saved_bytes, const float* dy, float* dx, const dstd_block_grads* g,
+                            void* workspace, size_t workspace_bytes, void* stream, unsigned flags);
+
 /* ---- whole DSTDGCN ------------------------------------------------------- */
 /* x, y [B][T][V][in_channels/2].  dropout_p is the model's do_in rate
  * (st_gcnn_dropout); the mask is a counter-based hash of (seed, element) so
@@ -110,6 +123,15 @@ int dstd_model_train_fwd(const dstd_model_params* p, const float* x, int B, floa
 int dstd_model_train_bwd(const dstd_model_params* p, const float* x, int B, float dropout_p,
                          unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
                          const dstd_model_grads* g, void* workspace, size_t workspace_bytes, void* stream);
+
+int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, float momentum, float dropout_p,
+                            unsigned long long seed, float* y, void* saved, size_t saved_bytes, void* stream,
+                            unsigned flags);
+/* dx (may be NULL): the input gradient [B][T][V][in_channels/2] (=). */
+int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, float dropout_p,
+                            unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
+                            const dstd_model_grads* g, float* dx, void* workspace, size_t workspace_bytes,
+                            void* stream, unsigned flags);
 
 /* ---- engine: loss and test metric --------------------------------------- */
 size_t dstd_loss_workspace_bytes(void);

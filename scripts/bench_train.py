@@ -35,6 +35,7 @@ def main():
     for B in a.batch:
         torch.manual_seed(0)
         m = get_model("dstdgcn", dstdgcn=opts).to(dev).train()
+        m._dstd_inplace_grads = True  # what engine.PredictionEngine.train opts into (prediction.py:161)
         opt = torch.optim.Adam(m.parameters(), lr=3e-3)
         g = torch.Generator().manual_seed(1234)
         seq = torch.randn(B, 40, 69, generator=g)

@@ -47,7 +47,7 @@ def test_arithmetic_is_a_per_call_flag():
 def test_library_exports_every_training_header_symbol():
     L = native.lib()
     syms = header_symbols("dstd_gcn_train.h")
-    assert len(syms) == 16, syms
+    assert len(syms) == 20, syms
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(native.TRAIN_EXPORTS)
@@ -72,6 +72,9 @@ def test_train_sizes_and_argument_checks_without_gpu():
     assert L.dstd_block_train_fwd(None, None, 4, 35, 22, 0.1, None, None, 0, None) == -1
     assert L.dstd_model_train_fwd(None, None, 4, 0.1, 0.0, 0, None, None, 0, None) == -1
     assert L.dstd_model_train_bwd(None, None, 4, 0.0, 0, None, 0, None, None, None, 0, None) == -1
+    # _ex entry points: unknown flag bits are rejected
+    assert L.dstd_block_train_fwd_ex(None, None, 4, 35, 22, 0.1, None, None, 0, None, 1) == -1
+    assert L.dstd_model_train_fwd_ex(None, None, 4, 0.1, 0.0, 0, None, None, 0, None, 4) == -1
     assert L.dstd_mpjpe_fwd(None, None, 10, None, None, 0, None) == -1
     assert L.dstd_frame_mpjpe(None, None, 1, 35, 96, 0, None, 66, None, None, 6, None, None) == -1
 

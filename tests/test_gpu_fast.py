@@ -217,3 +217,42 @@ def test_fast_op_and_block_gradients_vs_oracle():
         if p.requires_grad:
             assert rel_err(named[k].grad.cpu().numpy(), p.grad.numpy()) <= 2e-4, k
     assert rel_err(x.grad.cpu().numpy(), x64.grad.numpy()) <= 2e-4
+
+
+def test_fast_eval_mode_backward():
+    """An eval-mode fast model under autograd: gradients reach the fast
+    parameters (through the derivation) and equal the fast oracle's fp64
+    autograd within the fp32 noise band; running statistics untouched."""
+    d = load_npz("dstdgcn_fast.npz")
+    m, opts = _model("h36m", d)
+    before = {k: v.clone() for k, v in m.state_dict().items() if "running_" in k or "num_batches" in k}
+    x = t(d["model_h36m/x"]).requires_grad_()
+    y = m(x)
+    gy = torch.randn(y.shape, generator=torch.Generator().manual_seed(13))
+    (y * gy.to(DEV)).sum().backward()
+    assert all(torch.equal(m.state_dict()[k], v) for k, v in before.items())
+    sd = group(d, "model_h36m/sd/")
+
+    def oracle(dtype, device="cpu"):
+        P = {k: torch.tensor(v, dtype=dtype, device=device) for k, v in sd.items()
+             if not k.endswith("num_batches_tracked")}
+        for k, v in P.items():
+            if not k.endswith(("A_t", "running_mean", "running_var")):
+                v.requires_grad_(True)
+        xo = torch.tensor(d["model_h36m/x"], dtype=dtype, device=device)
+        (O.fast_dstdgcn_fn(xo, P, 5) * gy.to(device, dtype)).sum().backward()
+        return P
+
+    # fp32 noise of two other implementations: the oracle on the CPU and on the GPU (torch-ROCm ops)
+    P, P32s = oracle(torch.float64), (oracle(torch.float32), oracle(torch.float32, DEV))
+    named = dict(m.named_parameters())
+    r = []
+    for k, p in P.items():
+        if p.requires_grad:
+            ref = p.grad.numpy()
+            noise = max(max(float(np.abs(Q[k].grad.double().cpu().numpy() - ref).max()) for Q in P32s),
+                        1e-4 * float(np.abs(ref).max()))
+            r.append((float(np.abs(named[k].grad.double().cpu().numpy() - ref).max()) / noise, k))
+    r.sort(reverse=True)
+    v = np.array([a for a, _ in r])
+    assert np.median(v) <= 1.5 and np.quantile(v, 0.9) <= 3.0 and v.max() <= 12.0, r[:8]
