@@ -120,6 +120,7 @@ struct BnFwd {
   float* mean;
   float* rstd;
   int use_running = 0;  // eval-mode BN: mean / rstd from the running stats, no update
+  int cv = 0;           // (set by bn_train_fwd: C * V)
 };
 hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s);
 

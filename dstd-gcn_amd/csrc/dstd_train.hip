@@ -478,49 +478,67 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_stats_part(BnFwd a, int B, i
   }
 }
 
-__global__ void k_bn_stats_merge(BnFwd a, int B, int C, int T, int V, int splits, const float* part) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= C * V) return;
-  const int rows = B * T, per = (rows + splits - 1) / splits;
-  float mean = 0.f;
-  for (int sp = 0; sp < splits; ++sp) {
-    const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
-    mean += cnt * part[((size_t)sp * C * V + ch) * 2];
+// Merge + apply in one launch: workgroup (c, n) first merges the V channels
+// (c, v) from the split partials (Chan merge in split order -- every
+// workgroup of channel c computes the same values; the n == 0 one stores
+// mean / rstd and updates the running statistics), then normalises the
+// sample's contiguous [T][V] plane of channel c.
+constexpr int kBnMaxV = 64;
+__device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows, int splits, const float* part,
+                                               float& mean, float& rstd, bool store) {
+  if (a.use_running) {
+    mean = a.running_mean[ch];
+    rstd = 1.f / sqrtf(a.running_var[ch] + a.eps);
+  } else {
+    const int per = (rows + splits - 1) / splits;
+    float m = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+      m += cnt * part[((size_t)sp * a.cv + ch) * 2];
+    }
+    m /= rows;
+    float m2 = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+      const float* p = part + ((size_t)sp * a.cv + ch) * 2;
+      const float d = p[0] - m;
+      m2 += p[1] + cnt * d * d;
+    }
+    const float var = m2 / rows;
+    mean = m;
+    rstd = 1.f / sqrtf(var + a.eps);
+    if (store && a.running_mean) {
+      const float unb = rows > 1 ? m2 / (rows - 1) : var;
+      a.running_mean[ch] = (1.f - a.momentum) * a.running_mean[ch] + a.momentum * m;
+      a.running_var[ch] = (1.f - a.momentum) * a.running_var[ch] + a.momentum * unb;
+    }
   }
-  mean /= rows;
-  float m2 = 0.f;
-  for (int sp = 0; sp < splits; ++sp) {
-    const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
-    const float* p = part + ((size_t)sp * C * V + ch) * 2;
-    const float d = p[0] - mean;
-    m2 += p[1] + cnt * d * d;
-  }
-  const float var = m2 / rows;
-  a.mean[ch] = mean;
-  a.rstd[ch] = 1.f / sqrtf(var + a.eps);
-  if (a.running_mean) {
-    const float unb = rows > 1 ? m2 / (rows - 1) : var;
-    a.running_mean[ch] = (1.f - a.momentum) * a.running_mean[ch] + a.momentum * mean;
-    a.running_var[ch] = (1.f - a.momentum) * a.running_var[ch] + a.momentum * unb;
+  if (store) {
+    a.mean[ch] = mean;
+    a.rstd[ch] = rstd;
   }
 }
 
-// eval-mode BN: the saved mean / rstd are the running statistics
-__global__ void k_bn_eval_stats(BnFwd a, int CV) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= CV) return;
-  a.mean[ch] = a.running_mean[ch];
-  a.rstd[ch] = 1.f / sqrtf(a.running_var[ch] + a.eps);
-}
-
-__global__ void k_bn_apply(BnFwd a, size_t n, int CV, int TV, int V) {
+__global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, int T, int V, int splits,
+                                                         const float* part) {
+  __shared__ float scl[kBnMaxV], shl[kBnMaxV];
+  const int c = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  if (tid < V) {
+    const int ch = c * V + tid;
+    float mean, rstd;
+    bn_merge_stats(a, ch, B * T, splits, part, mean, rstd, n == 0);
+    const float sc = rstd * a.gamma[ch];
+    scl[tid] = sc;
+    shl[tid] = a.beta[ch] - mean * sc;
+  }
+  __syncthreads();
   const float w = a.prelu ? *a.prelu : 0.f;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)((i / TV) % (CV / V)), v = (int)(i % V);
-    const int ch = c * V + v;
-    const float sc = a.rstd[ch] * a.gamma[ch], sh = a.beta[ch] - a.mean[ch] * sc;
+  const size_t base = ((size_t)n * C + c) * T * V;
+  for (int e = tid; e < T * V; e += blockDim.x) {
+    const size_t i = base + e;
+    const int v = e % V;
     const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
-    float z = fmaf(u, sc, sh);
+    float z = fmaf(u, scl[v], shl[v]);
     if (a.res) z += a.res[i];
     if (a.prelu) {
       a.zsave[i] = z;
@@ -568,35 +586,50 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_bwd_part(BnBwd a, int B, int
   }
 }
 
-// sums[ch] = (sum dz, sum dz*xhat) for the apply pass; dgamma / dbeta accumulate
-__global__ void k_bn_bwd_merge(BnBwd a, int CV, int splits, const float* part, float* sums) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= CV) return;
-  float sd = 0.f, sdx = 0.f;
-  for (int sp = 0; sp < splits; ++sp) {
-    const float* p = part + ((size_t)sp * CV + ch) * 2;
-    sd += p[0];
-    sdx += p[1];
+// Merge + apply of the backward in one launch: workgroup (c, n) sums the
+// split partials of its V channels (split order), the n == 0 one accumulates
+// dgamma / dbeta (and workgroup (0, 0) the PReLU slope: the partials in the
+// order of the former sum_into pass), then writes du over the sample's plane.
+__global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int C, int T, int V, int splits,
+                                                             const float* part, const float* wpart, float* dprelu) {
+  __shared__ float sdl[kBnMaxV], sxl[kBnMaxV], red[kRedThreads / 64];
+  const int c = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
+  const int CV = C * V;
+  if (tid < V) {
+    const int ch = c * V + tid;
+    float sd = 0.f, sdx = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float* p = part + ((size_t)sp * CV + ch) * 2;
+      sd += p[0];
+      sdx += p[1];
+    }
+    sdl[tid] = sd;
+    sxl[tid] = sdx;
+    if (n == 0) {
+      a.dbeta[ch] += sd;
+      a.dgamma[ch] += sdx;
+    }
   }
-  sums[2 * ch] = sd;
-  sums[2 * ch + 1] = sdx;
-  a.dbeta[ch] += sd;
-  a.dgamma[ch] += sdx;
-}
-
-__global__ void k_bn_bwd_apply(BnBwd a, size_t n, int CV, int TV, int V, int rows, const float* sums) {
+  if (a.prelu && c == 0 && n == 0) {  // uniform per workgroup: block_sum's barriers are safe
+    float t = 0.f;
+    for (int e = tid; e < splits * C; e += blockDim.x) t += wpart[e];
+    t = block_sum(t, red);
+    if (tid == 0) dprelu[0] += t;
+  }
+  __syncthreads();
   const float w = a.prelu ? *a.prelu : 0.f;
-  const float inv = 1.f / rows;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)((i / TV) % (CV / V)), v = (int)(i % V);
-    const int ch = c * V + v;
+  const float inv = 1.f / (B * T);
+  const size_t base = ((size_t)n * C + c) * T * V;
+  for (int e = tid; e < T * V; e += blockDim.x) {
+    const size_t i = base + e;
+    const int v = e % V, ch = c * V + v;
     const float d = a.dout[i];
     const float dz = (a.prelu && !(a.zsave[i] > 0.f)) ? w * d : d;
     const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
     const float mean = a.mean[ch], rstd = a.rstd[ch];
     const float xh = (u - mean) * rstd;
     a.du[i] = a.use_running ? a.gamma[ch] * rstd * dz
-                            : a.gamma[ch] * rstd * (dz - sums[2 * ch] * inv - xh * sums[2 * ch + 1] * inv);
+                            : a.gamma[ch] * rstd * (dz - sdl[v] * inv - xh * sxl[v] * inv);
     if (a.dz_out) a.dz_out[i] = dz;
   }
 }
@@ -875,29 +908,23 @@ size_t bn_scratch_floats(int B, int C, int T, int V) {
 }
 
 hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s) {
+  if (V > kBnMaxV) return hipErrorInvalidValue;
+  if (a.use_running && (!a.running_mean || !a.running_var)) return hipErrorInvalidValue;
   const int splits = bn_splits(B, T);
-  if (a.use_running) {
-    if (!a.running_mean || !a.running_var) return hipErrorInvalidValue;
-    k_bn_eval_stats<<<cdiv(C * V, 256), 256, 0, s>>>(a, C * V);
-  } else {
-    k_bn_stats_part<<<dim3(C, splits), kRedThreads, 0, s>>>(a, B, C, T, V, splits, scratch);
-    k_bn_stats_merge<<<cdiv(C * V, 256), 256, 0, s>>>(a, B, C, T, V, splits, scratch);
-  }
-  const size_t n = (size_t)B * C * T * V;
-  k_bn_apply<<<grid_for(n), 256, 0, s>>>(a, n, C * V, T * V, V);
+  BnFwd b = a;
+  b.cv = C * V;
+  if (!a.use_running) k_bn_stats_part<<<dim3(C, splits), kRedThreads, 0, s>>>(b, B, C, T, V, splits, scratch);
+  k_bn_apply_merged<<<dim3(C, B), 256, 0, s>>>(b, B, C, T, V, splits, scratch);
   return hipGetLastError();
 }
 
 hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scratch, float* dprelu, hipStream_t s) {
+  if (V > kBnMaxV) return hipErrorInvalidValue;
   const int splits = bn_splits(B, T);
   float* part = scratch;
   float* wpart = part + (size_t)splits * C * V * 2;
-  float* sums = wpart + (size_t)splits * C;
   k_bn_bwd_part<<<dim3(C, splits), kRedThreads, 0, s>>>(a, B, C, T, V, splits, part, wpart);
-  k_bn_bwd_merge<<<cdiv(C * V, 256), 256, 0, s>>>(a, C * V, splits, part, sums);
-  if (a.prelu) k_sum_into<<<1, kRedThreads, 0, s>>>(wpart, splits * C, dprelu);
-  const size_t n = (size_t)B * C * T * V;
-  k_bn_bwd_apply<<<grid_for(n), 256, 0, s>>>(a, n, C * V, T * V, V, B * T, sums);
+  k_bn_bwd_apply_merged<<<dim3(C, B), 256, 0, s>>>(a, B, C, T, V, splits, part, wpart, dprelu);
   return hipGetLastError();
 }
 
