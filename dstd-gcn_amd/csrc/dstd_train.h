@@ -31,6 +31,25 @@ struct Gemm {
   const float* bias_m = nullptr;
   int reduce = 0;
   int b_ones_last = 0;  // B(k, N-1) = 1: the last output column is sum_k A(m, k) (bias gradients)
+  // nseg > 0: C is not written; output row m of segment i (row0 <= m <
+  // row0 + rows) ACCUMULATES into seg[i].w[(m - row0) * (N - 1) + n] for
+  // n < N - 1 and into seg[i].b[m - row0] for n = N - 1 (the [W | b]
+  // gradient of packed convs lands in the parameters' own gradients)
+  struct Seg {
+    int row0, rows;
+    float* w;
+    float* b;
+  };
+  int nseg = 0;
+  Seg seg[3];
+  // d_out: also D = (*d_alpha) * C + (d_A[n] (* d_W[n]) + d_R[n]), same
+  // layout as C (the DSTDGC adjacency alpha * conv_rm(M) + A_comb with the
+  // block's A_s * W_s + R_s / A_t + R_t formed on the fly; d_W, d_R may be null)
+  float* d_out = nullptr;
+  const float* d_alpha = nullptr;
+  const float* d_A = nullptr;
+  const float* d_W = nullptr;
+  const float* d_R = nullptr;
 };
 
 // Scratch (floats) a reduce-GEMM may need for its split-over-batches partials.
@@ -49,15 +68,13 @@ hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int A
 hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int A, int NN, float* dP, float* dQ,
                           hipStream_t s);
 
-// D[n][a][ij] = alpha * E[n][a][ij] + Acomb[ij]   (alpha: device scalar)
-hipError_t adj_combine(const float* E, const float* Acomb, const float* alpha, int B, int A, int NN2, float* D,
-                       hipStream_t s);
 // Backward of adj_combine + the conv_rm bias, fused: dD -> dE = alpha * dD in
 // place, and dalpha += <dD, E>, dA[ij] += sum_{n,a} dD, dbrm[a] += sum_{n,ij} dE.
 // scratch >= adj_bwd_scratch_floats(B, A, NN2).
 size_t adj_bwd_scratch_floats(int B, int A, int NN2);
+// assign_dA: dA (=) instead of (+=)
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
-                   float* dalpha, float* scratch, hipStream_t s);
+                   float* dalpha, float* scratch, hipStream_t s, int assign_dA = 0);
 
 // Batched strided 2-D copies in one launch: dst[r*dst_ld + c] (+)= src[r*src_ld + c].
 struct CopyJob {
@@ -92,10 +109,9 @@ hipError_t reduce_rows(const float* X, int M, int nb, int nj, long long sb, long
 int dot_partials();
 hipError_t dot(const float* x, const float* y, size_t n, float* out, float* partials, hipStream_t s);
 
-// out = a * b + c (b may be null: out = a + c), element-wise over n.
-hipError_t fma3(const float* a, const float* b, const float* c, float* out, size_t n, hipStream_t s);
-// out += a (* b when b != null)
-hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStream_t s);
+// out (+)= a (* b when b != null) (+ c when c != null); assign: '=' instead of '+='
+hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStream_t s, const float* c = nullptr,
+                   int assign = 0);
 
 // Train-mode BatchNorm over an NCTV tensor, channel (c, v), statistics over
 // (n, t) (reference model/dstdgcn.py:35-50, nn.BatchNorm1d semantics):

@@ -35,6 +35,31 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 // whose fastest index is the operand's unit stride, so row- and column-major
 // operands both load in contiguous runs.
 // ---------------------------------------------------------------------------
+// final value of output (gm, gn): into C (with beta), or accumulated into
+// its segment's destination (Gemm::nseg)
+__device__ __forceinline__ void gemm_store(const Gemm& g, float* Cb, float* Db, int gm, int gn, float v) {
+  if (Db) {
+    float ac = g.d_A[gn];
+    if (g.d_W) ac *= g.d_W[gn];
+    if (g.d_R) ac += g.d_R[gn];
+    Db[gm * g.c_m + gn * g.c_n] = fmaf(*g.d_alpha, v, ac);
+  }
+  if (g.nseg) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i < g.nseg && gm >= g.seg[i].row0 && gm < g.seg[i].row0 + g.seg[i].rows) {
+        const int r = gm - g.seg[i].row0;
+        float* d = gn < g.N - 1 ? g.seg[i].w + (size_t)r * (g.N - 1) + gn : g.seg[i].b + r;
+        *d += v;
+      }
+    }
+    return;
+  }
+  float* c = Cb + gm * g.c_m + gn * g.c_n;
+  if (g.beta != 0.f) v += g.beta * *c;
+  *c = v;
+}
+
 template <int TM, int TN>
 __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int kc_len, float* partial) {
   constexpr int KT = 16;
@@ -150,6 +175,7 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
   }
   const int b1 = g.reduce ? 0 : blockIdx.z / g.nb2, b2 = g.reduce ? 0 : blockIdx.z - b1 * g.nb2;
   float* Cb = g.C + b1 * g.c_b1 + b2 * g.c_b2;
+  float* Db = g.d_out ? g.d_out + b1 * g.c_b1 + b2 * g.c_b2 : nullptr;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -160,9 +186,7 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
         if (gm < g.M && gn < g.N) {
           float v = g.alpha * acc[i][j][r];
           if (g.bias_m) v += g.bias_m[gm];
-          float* c = Cb + gm * g.c_m + gn * g.c_n;
-          if (g.beta != 0.f) v += g.beta * *c;
-          *c = v;
+          gemm_store(g, Cb, Db, gm, gn, v);
         }
       }
 }
@@ -186,9 +210,7 @@ __global__ __launch_bounds__(256) void k_gemm_finish(Gemm g, int nsplit, const f
   const int m = idx / g.N, n = idx - m * g.N;
   float v = g.alpha * t;
   if (g.bias_m) v += g.bias_m[m];
-  float* c = g.C + m * g.c_m + n * g.c_n;
-  if (g.beta != 0.f) v += g.beta * *c;
-  *c = v;
+  gemm_store(g, g.C, g.d_out, m, n, v);
 }
 
 constexpr int kMaxSplit = 128;
@@ -235,11 +257,6 @@ __global__ void k_tanh_outer_bwd(const float* M, const float* dM, PQView v, int 
   }
 }
 
-__global__ void k_adj_combine(const float* E, const float* Acomb, const float* alpha, size_t n, int NN2, float* D) {
-  const float al = *alpha;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
-    D[e] = fmaf(al, E[e], Acomb[e % NN2]);
-}
 
 // Fused adjacency backward, stage 1: workgroup (row a, sample chunk); each
 // thread owns entries ij and walks the chunk's samples (no atomics).
@@ -273,7 +290,8 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* dD, const float* E,
 // stage 2: blocks [0, cdiv(NN2,16)) finish dA (16 outputs x 16 slices over the
 // A*nch partial rows); the last block finishes dbrm and dalpha.
 __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* pdA, const float* pbr, const float* pal, int A,
-                                                        int NN2, int nch, float* dA, float* dbrm, float* dalpha) {
+                                                        int NN2, int nch, float* dA, float* dbrm, float* dalpha,
+                                                        int assign_dA) {
   __shared__ float lds[16][17];
   __shared__ float red[4];
   const int nblk = (NN2 + 15) / 16;
@@ -288,7 +306,7 @@ __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* pdA, const 
     if (sl == 0 && ij < NN2) {
       float t = 0.f;
       for (int k = 0; k < 16; ++k) t += lds[k][el];
-      dA[ij] += t;
+      dA[ij] = assign_dA ? t : dA[ij] + t;
     }
     return;
   }
@@ -400,14 +418,13 @@ __global__ void k_sum_into(const float* partials, int n, float* out) {
   if (threadIdx.x == 0) out[0] += s;
 }
 
-__global__ void k_fma3(const float* a, const float* b, const float* c, float* out, size_t n) {
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
-    out[e] = b ? fmaf(a[e], b[e], c[e]) : a[e] + c[e];
-}
 
-__global__ void k_acc_mul(const float* a, const float* b, float* out, size_t n) {
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x)
-    out[e] += b ? a[e] * b[e] : a[e];
+__global__ void k_acc_mul(const float* a, const float* b, const float* c, float* out, size_t n, int assign) {
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+    float v = b ? a[e] * b[e] : a[e];
+    if (c) v += c[e];
+    out[e] = assign ? v : out[e] + v;
+  }
 }
 
 
@@ -778,6 +795,7 @@ size_t gemm_scratch_floats(int M, int N) { return (size_t)kMaxSplit * M * N; }
 
 hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
+  if (g.d_out && (g.reduce || !g.d_A || !g.d_alpha)) return hipErrorInvalidValue;
   const int TM = g.M <= 32 ? 32 : 64, TN = g.N <= 32 ? 32 : 64;
   const int tiles = cdiv(g.M, TM) * cdiv(g.N, TN);
   const int nbat = g.nb1 * g.nb2;
@@ -816,12 +834,6 @@ hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int 
   return hipGetLastError();
 }
 
-hipError_t adj_combine(const float* E, const float* Acomb, const float* alpha, int B, int A, int NN2, float* D,
-                       hipStream_t s) {
-  const size_t n = (size_t)B * A * NN2;
-  k_adj_combine<<<grid_for(n), 256, 0, s>>>(E, Acomb, alpha, n, NN2, D);
-  return hipGetLastError();
-}
 
 int adj_bwd_chunks(int B, int A) { return std::max(1, std::min(std::min(B, 16), cdiv(512, A))); }
 
@@ -831,13 +843,13 @@ size_t adj_bwd_scratch_floats(int B, int A, int NN2) {
 }
 
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
-                   float* dalpha, float* scratch, hipStream_t s) {
+                   float* dalpha, float* scratch, hipStream_t s, int assign_dA) {
   const int nch = adj_bwd_chunks(B, A);
   float* pdA = scratch;
   float* pbr = pdA + (size_t)nch * A * NN2;
   float* pal = pbr + (size_t)nch * A;
   k_adj_bwd_part<<<dim3(A, nch), 256, 0, s>>>(dD, E, alpha, B, A, NN2, nch, pdA, pbr, pal);
-  k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(pdA, pbr, pal, A, NN2, nch, dA, dbrm, dalpha);
+  k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(pdA, pbr, pal, A, NN2, nch, dA, dbrm, dalpha, assign_dA);
   return hipGetLastError();
 }
 
@@ -891,13 +903,10 @@ hipError_t sum_into(const float* partial, int n, float* out, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t fma3(const float* a, const float* b, const float* c, float* out, size_t n, hipStream_t s) {
-  k_fma3<<<grid_for(n), 256, 0, s>>>(a, b, c, out, n);
-  return hipGetLastError();
-}
 
-hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStream_t s) {
-  k_acc_mul<<<grid_for(n), 256, 0, s>>>(a, b, out, n);
+hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStream_t s, const float* c,
+                   int assign) {
+  k_acc_mul<<<grid_for(n), 256, 0, s>>>(a, b, c, out, n, assign);
   return hipGetLastError();
 }
 

@@ -184,16 +184,21 @@ Gemm conv_dw(const float* dY, const float* X, float* dW, int B, int cin, int cou
   return g;
 }
 hipError_t conv_bwd(const float* W, const float* X, const float* dY, float* dX, float* dW, float* db, int B, int cin,
-                    int cout, int TV, float* gs, float* red, hipStream_t s) {
-  if (dX) DSTD_TRYH(gemm(conv_dx(W, dY, dX, B, cin, cout, TV), gs, s));
+                    int cout, int TV, float* gs, float* red, hipStream_t s, float dx_beta = 1.f) {
+  if (dX) {
+    Gemm gx = conv_dx(W, dY, dX, B, cin, cout, TV);
+    gx.beta = dx_beta;
+    DSTD_TRYH(gemm(gx, gs, s));
+  }
   DSTD_TRYH(gemm(conv_dw(dY, X, dW, B, cin, cout, TV), gs, s));
   return reduce_rows(dY, cout, B, TV, (long long)cout * TV, TV, 1, db, 1.f, red, s);
 }
 
 // y (beta_y: 0 '=' / 1 '+=') = DSTDGC(x, Acomb, alpha); fills sv.  The packed
 // weights sv.Wp / sv.bp must already hold the op's conv weights (pack_jobs).
-hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* Acomb, const float* alpha,
-                  float* y, float beta_y, const OpSaved& sv, hipStream_t s) {
+// Acomb = A0 (* W0) (+ R0), formed by the conv_rm GEMM's epilogue (W0, R0 may be null).
+hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* A0, const float* W0,
+                  const float* R0, const float* alpha, float* y, float beta_y, const OpSaved& sv, hipStream_t s) {
   // conv_f, conv_m1, conv_m2 in one GEMM                         :81-82
   DSTD_TRYH(gemm(conv_fwd(sv.Wp, sv.bp, x, sv.G, g.B, g.cin, g.CG(), g.TV), nullptr, s));
   const float* P = sv.G + (size_t)g.cout * g.TV;
@@ -205,8 +210,12 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   e.B = sv.M, e.b_b1 = 2LL * g.A * g.NN2, e.b_k = g.NN2, e.b_n = 1;
   e.C = sv.E, e.c_b1 = (long long)g.A * g.NN2, e.c_m = g.NN2, e.c_n = 1;
   e.bias_m = w->brm;
+  e.d_out = sv.D;  // D = alpha * E + Acomb                          :86 / :92
+  e.d_alpha = alpha;
+  e.d_A = A0;
+  e.d_W = W0;
+  e.d_R = R0;
   DSTD_TRYH(gemm(e, nullptr, s));
-  DSTD_TRYH(adj_combine(sv.E, Acomb, alpha, g.B, g.A, g.NN2, sv.D, s));                    // :86 / :92
   Gemm a;  // y[c][j] = sum_i F[c][i] D[i][j] per (n, a)               :87 / :93
   a.M = g.cout, a.N = g.NN, a.K = g.NN, a.nb1 = g.B, a.nb2 = g.A;
   a.A = sv.G, a.a_b1 = (long long)g.CG() * g.TV, a.a_b2 = g.ps_a, a.a_m = g.TV, a.a_k = g.ps_i;
@@ -216,9 +225,11 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   return gemm(a, nullptr, s);
 }
 
+// dx_beta 0: dx (=) instead of (+=); assign_dA: dA likewise (block-internal
+// buffers; the op entry point accumulates both)
 hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* alpha, const OpSaved& sv,
                   const float* dy, float* dx, const dstd_gc_grads* gr, float* dA, float* dalpha, const OpWs& ws,
-                  hipStream_t s) {
+                  hipStream_t s, float dx_beta = 1.f, int assign_dA = 0) {
   const long long ldG = (long long)g.CG() * g.TV;
   Gemm f;  // dF[c][i] = sum_j dy[c][j] D[i][j]  -> rows [0, cout) of dG
   f.M = g.cout, f.N = g.NN, f.K = g.NN, f.nb1 = g.B, f.nb2 = g.A;
@@ -233,7 +244,7 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   d.C = ws.dD, d.c_b1 = (long long)g.A * g.NN2, d.c_b2 = g.NN2, d.c_m = g.NN, d.c_n = 1;
   DSTD_TRYH(gemm(d, nullptr, s));
   // Adj = alpha * (conv_rm(M)) + A:  dalpha, dA, d b_rm, and dE = alpha dD in place
-  DSTD_TRYH(adj_bwd(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, dA, gr->brm, dalpha, ws.red, s));
+  DSTD_TRYH(adj_bwd(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, dA, gr->brm, dalpha, ws.red, s, assign_dA));
   const float* dE = ws.dD;
   Gemm wr;  // dWrm[a][k] = sum_{n,ij} dE[n][a][ij] M[n][k][ij]
   wr.M = g.A, wr.N = 2 * g.A, wr.K = g.NN2, wr.nb1 = g.B, wr.reduce = 1;
@@ -252,28 +263,27 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   float* dP = ws.dG + (size_t)g.cout * g.TV;
   DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.A, g.NN, dP, dP + 2 * (size_t)g.TV, s));
   // the three 1x1 convs at once: dx += Wp^T dG;  [dWp | dbp] = sum dG [x; 1]^T
-  if (dx) DSTD_TRYH(gemm(conv_dx(sv.Wp, ws.dG, dx, g.B, g.cin, g.CG(), g.TV), ws.gs, s));
+  if (dx) {
+    Gemm gx = conv_dx(sv.Wp, ws.dG, dx, g.B, g.cin, g.CG(), g.TV);
+    gx.beta = dx_beta;
+    DSTD_TRYH(gemm(gx, ws.gs, s));
+  }
+  // rows [0, cout) / [cout, cout+2) / [cout+2, cout+4) of [dWp | dbp]
+  // accumulate straight into the conv_f / conv_m1 / conv_m2 gradients
   Gemm gw = conv_dw(ws.dG, x, ws.gW, g.B, g.cin + 1, g.CG(), g.TV);
   gw.b_ones_last = 1;
-  gw.beta = 0.f;
   gw.b_b1 = (long long)g.cin * g.TV;
-  DSTD_TRYH(gemm(gw, ws.gs, s));
-  const int ld = g.cin + 1;
-  CopyJobs js;
-  js.add(ws.gW, gr->wf, g.cout, g.cin, ld, g.cin, 1);
-  js.add(ws.gW + (size_t)g.cout * ld, gr->wm1, 2, g.cin, ld, g.cin, 1);
-  js.add(ws.gW + (size_t)(g.cout + 2) * ld, gr->wm2, 2, g.cin, ld, g.cin, 1);
-  js.add(ws.gW + g.cin, gr->bf, g.cout, 1, ld, 1, 1);
-  js.add(ws.gW + (size_t)g.cout * ld + g.cin, gr->bm1, 2, 1, ld, 1, 1);
-  js.add(ws.gW + (size_t)(g.cout + 2) * ld + g.cin, gr->bm2, 2, 1, ld, 1, 1);
-  return copy_jobs(js, s);
+  gw.nseg = 3;
+  gw.seg[0] = Gemm::Seg{0, g.cout, gr->wf, gr->bf};
+  gw.seg[1] = Gemm::Seg{g.cout, 2, gr->wm1, gr->bm1};
+  gw.seg[2] = Gemm::Seg{g.cout + 2, 2, gr->wm2, gr->bm2};
+  return gemm(gw, ws.gs, s);
 }
 
 // ---------------------------------------------------------------------------
 // one DSTDGCB
 // ---------------------------------------------------------------------------
 struct BlockSaved {
-  float *as, *at;
   OpSaved op[3];
   float *ysp, *z, *h, *mean, *rstd;
   float *rc, *r, *rmean, *rrstd;
@@ -281,8 +291,6 @@ struct BlockSaved {
 };
 void carve_block_saved(Carver& cv, BlockSaved& s, int B, int cin, int cout, int T, int V) {
   const size_t act = (size_t)B * cout * T * V;
-  s.as = cv.take(2 * V * V);
-  s.at = cv.take(T * T);
   for (int i = 0; i < 2; ++i) carve_op_saved(cv, s.op[i], OpGeom(DSTD_MODE_SPATIAL, B, cin, cout, T, V));
   carve_op_saved(cv, s.op[2], OpGeom(DSTD_MODE_TEMPORAL, B, cout, cout, T, V));
   s.ysp = cv.take(act);
@@ -330,9 +338,6 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
                      const BlockSaved& S, hipStream_t s, int run = 0) {
   const int cin = p->cin, cout = p->cout, TV = T * V;
   const bool res = cin != cout;
-  // A_s*W_s + R_s, A_t + R_t (model/dstdgcn.py:146-149, 157-160)
-  DSTD_TRYH(fma3(p->A_s, p->W_s, p->R_s, S.as, (size_t)2 * V * V, s));
-  DSTD_TRYH(fma3(p->A_t, nullptr, p->R_t, S.at, (size_t)T * T, s));
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
   const OpGeom gt(DSTD_MODE_TEMPORAL, B, cout, cout, T, V);
   CopyJobs js;  // conv weights of the block's three ops -> packed [W_f; W_m1; W_m2]
@@ -340,8 +345,9 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
   pack_jobs(js, &p->conv_s[1], S.op[1], gs);
   pack_jobs(js, &p->conv_t, S.op[2], gt);
   DSTD_TRYH(copy_jobs(js, s));
-  for (int i = 0; i < 2; ++i)  // :145-150
-    DSTD_TRYH(op_fwd(gs, x, &p->conv_s[i], S.as + i * V * V, p->alpha_sm, S.ysp, i ? 1.f : 0.f, S.op[i], s));
+  for (int i = 0; i < 2; ++i)  // :145-150, A_s*W_s + R_s (:146-149)
+    DSTD_TRYH(op_fwd(gs, x, &p->conv_s[i], p->A_s + i * V * V, p->W_s + i * V * V, p->R_s + i * V * V, p->alpha_sm,
+                     S.ysp, i ? 1.f : 0.f, S.op[i], s));
   const float* r = x;
   if (res) {  // residual Conv1x1 + BatchNorm (:117-121)
     DSTD_TRYH(gemm(conv_fwd(p->res_w, p->res_b, x, S.rc, B, cin, cout, TV), nullptr, s));
@@ -376,19 +382,22 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.rstd = S.rstd;
   bb.use_running = run;
   DSTD_TRYH(bn_train_fwd(bb, B, cout, T, V, S.red, s));
-  return op_fwd(gt, S.h, &p->conv_t, S.at, p->alpha_tm, y, 0.f, S.op[2], s);  // :156-162
+  return op_fwd(gt, S.h, &p->conv_t, p->A_t, nullptr, p->R_t, p->alpha_tm, y, 0.f, S.op[2], s);  // :156-162
 }
 
+// dx_init: dx holds nothing yet -- the first contribution assigns (no
+// memset); dx_extra (no residual conv only): also added to dx (the
+// encoders' identity path of the model backward).
 hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, int V, const BlockSaved& S,
                      const float* dy, float* dx, const dstd_block_grads* g, const BlockWs& W, hipStream_t s,
-                     int run = 0) {
+                     int run = 0, bool dx_init = false, const float* dx_extra = nullptr) {
   const int cin = p->cin, cout = p->cout, TV = T * V;
   const bool res = cin != cout;
   const size_t act = (size_t)B * cout * TV;
-  DSTD_TRYH(hipMemsetAsync(W.dh, 0, act * sizeof(float), s));
   const OpGeom gt(DSTD_MODE_TEMPORAL, B, cout, cout, T, V);
-  // A_t + R_t: dR_t = dA
-  DSTD_TRYH(op_bwd(gt, S.h, &p->conv_t, p->alpha_tm, S.op[2], dy, W.dh, &g->conv_t, g->R_t, g->alpha_tm, W.op, s));
+  // A_t + R_t: dR_t = dA; dh (=) the temporal op's input gradient
+  DSTD_TRYH(op_bwd(gt, S.h, &p->conv_t, p->alpha_tm, S.op[2], dy, W.dh, &g->conv_t, g->R_t, g->alpha_tm, W.op, s,
+                   0.f));
   BnBwd bb;
   bb.x = S.ysp;
   bb.zsave = S.z;
@@ -415,15 +424,16 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.dbeta = g->res_bn.bias;
     rb.use_running = run;
     DSTD_TRYH(bn_train_bwd(rb, B, cout, T, V, W.op.red, nullptr, s));
-    DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, W.op.red, s));
+    if (dx_extra) return hipErrorInvalidValue;
+    DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, W.op.red, s,
+                       dx_init ? 0.f : 1.f));
   } else if (dx) {
-    DSTD_TRYH(acc_mul(W.dr, nullptr, dx, act, s));
+    DSTD_TRYH(acc_mul(W.dr, nullptr, dx, act, s, dx_extra, dx_init ? 1 : 0));
   }
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
-  DSTD_TRYH(hipMemsetAsync(W.dAs, 0, (size_t)2 * V * V * sizeof(float), s));
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i)  // each graph's dA (=) into its own half of dAs
     DSTD_TRYH(op_bwd(gs, x, &p->conv_s[i], p->alpha_sm, S.op[i], W.dysp, dx, &g->conv_s[i], W.dAs + i * V * V,
-                     g->alpha_sm, W.op, s));
+                     g->alpha_sm, W.op, s, 1.f, 1));
   // A_s*W_s + R_s with A_s constant: dR_s = dA, dW_s = dA * A_s (both graphs)
   return adj_param_grads(W.dAs, p->A_s, g->R_s, g->W_s, (size_t)2 * V * V, s);
 }
@@ -508,7 +518,7 @@ int dstd_dstdgc_train_fwd(int mode, const float* x, int B, int cin, int cout, in
   CopyJobs js;
   pack_jobs(js, w, sv, g);
   DSTD_TRY(copy_jobs(js, (hipStream_t)stream));
-  DSTD_TRY(op_fwd(g, x, w, A, alpha, y, 0.f, sv, (hipStream_t)stream));
+  DSTD_TRY(op_fwd(g, x, w, A, nullptr, nullptr, alpha, y, 0.f, sv, (hipStream_t)stream));
   return DSTD_OK;
 }
 
@@ -698,8 +708,7 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
   DSTD_TRY(out_ntvc_bwd(dy, B, T, V, 3, W.dO, s));
   float* dha = W.dha;
   float* dhb = W.dhb;
-  DSTD_TRY(hipMemsetAsync(dha, 0, act * sizeof(float), s));
-  DSTD_TRY(block_bwd(&p->st_out, S.h[L], B, T, V, S.st_out, W.dO, dha, &g->st_out, W.blk, s, run));
+  DSTD_TRY(block_bwd(&p->st_out, S.h[L], B, T, V, S.st_out, W.dO, dha, &g->st_out, W.blk, s, run, true));
   for (int i = L - 1; i >= 0; --i) {
     BnBwd be;
     be.x = S.yb[i];
@@ -716,8 +725,7 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
     be.use_running = run;
     DSTD_TRY(bn_train_bwd(be, B, C, T, V, W.blk.op.red, g->enc_prelu[i], s));
     // u = block(h) + h: dh = du (identity path) + block backward
-    DSTD_TRY(hipMemcpyAsync(dhb, W.du, act * sizeof(float), hipMemcpyDeviceToDevice, s));
-    DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s, run));
+    DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s, run, true, W.du));
     std::swap(dha, dhb);
   }
   if (dropout_p > 0.f) DSTD_TRY(dropout(dha, dha, act, dropout_p, seed, s));
@@ -734,8 +742,7 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
   b0.dbeta = g->bn_in.bias;
   b0.use_running = run;
   DSTD_TRY(bn_train_bwd(b0, B, C, T, V, W.blk.op.red, g->prelu, s));
-  if (dx) DSTD_TRY(hipMemsetAsync(W.dX0, 0, (size_t)B * 6 * T * V * sizeof(float), s));
-  DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, dx ? W.dX0 : nullptr, &g->st_in, W.blk, s, run));
+  DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, dx ? W.dX0 : nullptr, &g->st_in, W.blk, s, run, true));
   if (dx) DSTD_TRY(prep_nctv_bwd(W.dX0, dy, B, T, V, 3, dx, s));  // :298-303, 315
   return DSTD_OK;
 }
