@@ -256,3 +256,33 @@ def test_fast_eval_mode_backward():
     r.sort(reverse=True)
     v = np.array([a for a, _ in r])
     assert np.median(v) <= 1.5 and np.quantile(v, 0.9) <= 3.0 and v.max() <= 12.0, r[:8]
+
+
+def test_fast_model_in_the_engine():
+    """engine.PredictionEngine trains the fast variant unchanged: the first
+    epoch's loss equals the fp64 fast oracle's (train-mode BN), the loss falls
+    over three one-batch epochs, Adam moves the fast parameters (through the
+    derivation) and the batch counters advance once per forward."""
+    from engine import PredictionEngine
+
+    class _Log:
+        def info(self, *a, **k):
+            pass
+
+    d = load_npz("dstdgcn_fast.npz")
+    opts = {k[len("train/opt/"):]: d[k].item() for k in d.files if k.startswith("train/opt/")}
+    sd0 = group(d, "train/sd0/")
+    m = _load(F.DSTDGCN(**opts), sd0).to(DEV)
+    cfg = dict(learn=dict(opt="adam", lr=3e-3, weight_decay=0, gamma=0.9, step_size=5),
+               loss=dict(joint=["jl2", 1]), n_out=1, transform="tsc", use_weight=False, inverse=True)
+    eng = PredictionEngine(cfg, m, _Log())
+    inp, inv, seq = (torch.from_numpy(d[f"train/{n}"]) for n in ("inp", "inv", "seq"))
+    B, T, VC = inp.shape
+    w0 = m.encoders[0][0].stgcn[0][0].conv_s[0].conv_f.weight.detach().clone()
+    losses = [eng.train([(inp, inv, seq, seq)], s, max_iter=1) for s in range(3)]
+    y64 = O.fast_dstdgcn(inp.view(B, T, VC // 3, 3), sd0, opts["num_layers"], training=True).reshape(B, T, VC)
+    l64 = float(O.mpjpe_error_3d(y64, seq.double()))
+    assert abs(losses[0] - l64) / l64 < 1e-5, (losses[0], l64)
+    assert np.isfinite(losses).all() and losses[-1] < losses[0]
+    assert not torch.equal(w0, m.encoders[0][0].stgcn[0][0].conv_s[0].conv_f.weight.detach())
+    assert int(m.bn_in.bn.num_batches_tracked) == int(sd0["bn_in.bn.num_batches_tracked"]) + 6
