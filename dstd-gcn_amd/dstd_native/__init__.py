@@ -324,7 +324,7 @@ class GradArena:
     the order given, None for parameters that do not require grad (A_s, A_t
     and anything frozen)."""
 
-    def __init__(self, params, device):
+    def __init__(self, params, device, buf=None):
         self.params = list(params)
         self.offsets = {}
         n = 0
@@ -332,7 +332,12 @@ class GradArena:
             if id(p) not in self.offsets:
                 self.offsets[id(p)] = n
                 n += (p.numel() + 63) // 64 * 64
-        self.buf = torch.zeros(max(n, 1), dtype=torch.float32, device=device)
+        if buf is not None:  # an arena a backward op returned (same params, same layout)
+            if buf.numel() != max(n, 1):
+                raise ValueError(f"gradient arena of {buf.numel()} floats for a layout of {max(n, 1)}")
+            self.buf = buf
+        else:
+            self.buf = torch.zeros(max(n, 1), dtype=torch.float32, device=device)
 
     def ptr(self, p):
         return self.buf.data_ptr() + 4 * self.offsets[id(p)]
@@ -343,6 +348,17 @@ class GradArena:
             off = self.offsets[id(p)]
             out.append(self.buf[off:off + p.numel()].view(p.shape) if p.requires_grad else None)
         return out
+
+
+def arena_numel(params):
+    """Floats of a GradArena over ``params`` (64-float aligned slices, shared
+    tensors once)."""
+    seen, n = set(), 0
+    for p in params:
+        if id(p) not in seen:
+            seen.add(id(p))
+            n += (p.numel() + 63) // 64 * 64
+    return max(n, 1)
 
 
 def grad_sink(owner, params, device):

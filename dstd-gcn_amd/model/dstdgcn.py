@@ -32,7 +32,7 @@ with frozen parameters and input) eval runs the fused inference kernels.
 import itertools
 import math
 import weakref
-from typing import List
+from typing import List, Tuple
 
 import numpy as np
 import torch
@@ -194,52 +194,43 @@ def _count_batch(module):
         torch._foreach_add_(t, 1)
 
 
+def _op_train_fwd_native(mod, mode, x, A, alpha):
+    L = native.lib()
+    B, cin, T, V = x.shape
+    dev = x.device
+    cout = mod.out_channels
+    y = torch.empty(B, cout, T, V, dtype=torch.float32, device=dev)
+    nbytes = L.dstd_dstdgc_train_saved_bytes(mode, B, cin, cout, T, V)
+    saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    code = L.dstd_dstdgc_train_fwd(mode, native.ptr(x, "x"), B, cin, cout, T, V, native.gc_weights(mod),
+                                   native.ptr(A, "A"), native.ptr(alpha, "alpha_m"), native.ptr(y, "y"),
+                                   saved.data_ptr(), nbytes, native.stream_handle(dev))
+    native.check(code, "dstd_dstdgc_train_fwd")
+    return y, saved
+
+
 class _OpTrain(torch.autograd.Function):
-    """DSTDGC forward + native backward (reference :80-94 under autograd)."""
+    """DSTDGC forward + native backward (reference :80-94 under autograd);
+    both directions are torch.library ops (dstd::dstdgc_train_forward /
+    dstdgc_train_backward, below)."""
 
     @staticmethod
     def forward(ctx, mod, mode, x, A, alpha, *params):
-        L = native.lib()
-        B, cin, T, V = x.shape
-        dev = x.device
-        cout = mod.out_channels
-        y = torch.empty(B, cout, T, V, dtype=torch.float32, device=dev)
-        nbytes = L.dstd_dstdgc_train_saved_bytes(mode, B, cin, cout, T, V)
-        saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        w = native.gc_weights(mod)
-        code = L.dstd_dstdgc_train_fwd(mode, native.ptr(x, "x"), B, cin, cout, T, V, w, native.ptr(A, "A"),
-                                       native.ptr(alpha, "alpha_m"), native.ptr(y, "y"), saved.data_ptr(), nbytes,
-                                       native.stream_handle(dev))
-        native.check(code, "dstd_dstdgc_train_fwd")
-        ctx.mod, ctx.mode, ctx.saved_buf = mod, mode, saved
+        y, saved = torch.ops.dstd.dstdgc_train_forward(x, A, alpha, list(params), mod._dstd_uid)
+        ctx.mod, ctx.saved_buf = mod, saved
+        ctx.params = list(params)
         ctx.save_for_backward(x, A, alpha)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        L = native.lib()
         x, A, alpha = ctx.saved_tensors
-        mod, mode = ctx.mod, ctx.mode
-        B, cin, T, V = x.shape
-        dev = x.device
-        cout = mod.out_channels
-        dy = dy.contiguous()
-        params = list(mod.parameters())
-        arena = native.GradArena(params, dev)
-        dx = torch.zeros_like(x) if ctx.needs_input_grad[2] else None
-        dA = torch.zeros_like(A)
-        dalpha = torch.zeros_like(alpha)
-        nbytes = L.dstd_dstdgc_train_workspace_bytes(mode, B, cin, cout, T, V)
-        ws = native.workspace(dev, nbytes)
-        code = L.dstd_dstdgc_train_bwd(mode, native.ptr(x, "x"), B, cin, cout, T, V, native.gc_weights(mod),
-                                       native.ptr(alpha, "alpha_m"), ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(),
-                                       native.ptr(dy, "dy"), dx.data_ptr() if dx is not None else None,
-                                       native.gc_grads(mod, arena), native.ptr(dA, "dA"),
-                                       native.ptr(dalpha, "dalpha"), ws.data_ptr(), ws.numel(),
-                                       native.stream_handle(dev))
-        native.check(code, "dstd_dstdgc_train_bwd")
+        need_dx = bool(ctx.needs_input_grad[2])
+        dx, dA, dalpha, flat = torch.ops.dstd.dstdgc_train_backward(x, A, alpha, ctx.saved_buf, dy.contiguous(),
+                                                                    ctx.params, ctx.mod._dstd_uid, need_dx)
         ctx.saved_buf = None
-        return (None, None, dx, dA, dalpha, *arena.views())
+        arena = native.GradArena(ctx.params, x.device, buf=flat)
+        return (None, None, dx if need_dx else None, dA, dalpha, *arena.views())
 
 
 def _bn_flags(module):
@@ -248,70 +239,103 @@ def _bn_flags(module):
     return 0 if module.training else native.TRAIN_RUNNING_STATS
 
 
+def _block_train_fwd_native(blk, x, flags, momentum):
+    L = native.lib()
+    B, cin, T, V = x.shape
+    dev = x.device
+    y = torch.empty(B, blk.out_channels, T, V, dtype=torch.float32, device=dev)
+    nbytes = L.dstd_block_train_saved_bytes(B, cin, blk.out_channels, T, V)
+    saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    code = L.dstd_block_train_fwd_ex(native.block_struct(blk), native.ptr(x, "x"), B, T, V, momentum,
+                                     native.ptr(y, "y"), saved.data_ptr(), nbytes, native.stream_handle(dev), flags)
+    native.check(code, "dstd_block_train_fwd_ex")
+    return y, saved
+
+
+def _block_train_bwd_native(blk, x, saved, dy, flags, arena, need_dx):
+    L = native.lib()
+    B, cin, T, V = x.shape
+    dev = x.device
+    dx = torch.zeros_like(x) if need_dx else None
+    ws = native.workspace(dev, L.dstd_block_train_workspace_bytes(B, cin, blk.out_channels, T, V))
+    code = L.dstd_block_train_bwd_ex(native.block_struct(blk), native.ptr(x, "x"), B, T, V, saved.data_ptr(),
+                                     saved.numel(), native.ptr(dy, "dy"), dx.data_ptr() if dx is not None else None,
+                                     native.block_grads(blk, arena), ws.data_ptr(), ws.numel(),
+                                     native.stream_handle(dev), flags)
+    native.check(code, "dstd_block_train_bwd_ex")
+    return dx
+
+
+def _model_train_fwd_native(model, x, flags, momentum, drop, seed):
+    L = native.lib()
+    n, t, v, c = x.shape
+    dev = x.device
+    y = torch.empty_like(x)
+    nbytes = L.dstd_model_train_saved_bytes(n, t, v, model.num_feature, model.num_layers)
+    saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    code = L.dstd_model_train_fwd_ex(model._native_params(), native.ptr(x, "x"), n, momentum, drop, seed,
+                                     native.ptr(y, "y"), saved.data_ptr(), nbytes, native.stream_handle(dev), flags)
+    native.check(code, "dstd_model_train_fwd_ex")
+    return y, saved
+
+
+def _model_train_bwd_native(model, x, saved, dy, flags, drop, seed, g, need_dx):
+    L = native.lib()
+    n, t, v, c = x.shape
+    dev = x.device
+    ws = native.workspace(dev, L.dstd_model_train_workspace_bytes(n, t, v, model.num_feature, model.num_layers))
+    dx = torch.empty_like(x) if need_dx else None
+    code = L.dstd_model_train_bwd_ex(model._native_params(), native.ptr(x, "x"), n, drop, seed, saved.data_ptr(),
+                                     saved.numel(), native.ptr(dy, "dy"), g, dx.data_ptr() if dx is not None else None,
+                                     ws.data_ptr(), ws.numel(), native.stream_handle(dev), flags)
+    native.check(code, "dstd_model_train_bwd_ex")
+    return dx
+
+
 class _BlockTrain(torch.autograd.Function):
     """DSTDGCB forward + native backward (reference :141-163): train-mode BN,
-    or running-statistics BN for an eval-mode block under autograd."""
+    or running-statistics BN for an eval-mode block under autograd.  Both
+    directions are torch.library ops (dstd::dstdgcb_train_forward /
+    dstdgcb_train_backward, below) over the C ABI."""
 
     @staticmethod
     def forward(ctx, blk, x, *params):
-        L = native.lib()
-        B, cin, T, V = x.shape
-        dev = x.device
-        y = torch.empty(B, blk.out_channels, T, V, dtype=torch.float32, device=dev)
-        nbytes = L.dstd_block_train_saved_bytes(B, cin, blk.out_channels, T, V)
-        saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        p = native.block_struct(blk)
         flags = _bn_flags(blk)
-        code = L.dstd_block_train_fwd_ex(p, native.ptr(x, "x"), B, T, V, _bn_momentum(blk), native.ptr(y, "y"),
-                                         saved.data_ptr(), nbytes, native.stream_handle(dev), flags)
-        native.check(code, "dstd_block_train_fwd_ex")
+        y, saved = torch.ops.dstd.dstdgcb_train_forward(x, list(params), list(blk.buffers()), blk._dstd_uid, flags,
+                                                        _bn_momentum(blk))
         if not flags:
             _count_batch(blk)
         ctx.blk, ctx.saved_buf, ctx.flags = blk, saved, flags
+        ctx.params = list(params)
         ctx.save_for_backward(x)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        L = native.lib()
         (x,) = ctx.saved_tensors
-        blk = ctx.blk
-        B, cin, T, V = x.shape
-        dev = x.device
-        dy = dy.contiguous()
-        arena = native.GradArena(list(blk.parameters()), dev)
-        dx = torch.zeros_like(x) if ctx.needs_input_grad[1] else None
-        nbytes = L.dstd_block_train_workspace_bytes(B, cin, blk.out_channels, T, V)
-        ws = native.workspace(dev, nbytes)
-        code = L.dstd_block_train_bwd_ex(native.block_struct(blk), native.ptr(x, "x"), B, T, V,
-                                         ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(), native.ptr(dy, "dy"),
-                                         dx.data_ptr() if dx is not None else None, native.block_grads(blk, arena),
-                                         ws.data_ptr(), ws.numel(), native.stream_handle(dev), ctx.flags)
-        native.check(code, "dstd_block_train_bwd_ex")
+        need_dx = bool(ctx.needs_input_grad[1])
+        dx, flat = torch.ops.dstd.dstdgcb_train_backward(x, ctx.saved_buf, dy.contiguous(), ctx.params,
+                                                         ctx.blk._dstd_uid, ctx.flags, need_dx)
         ctx.saved_buf = None
-        return (None, dx, *arena.views())
+        arena = native.GradArena(ctx.params, x.device, buf=flat)
+        return (None, dx if need_dx else None, *arena.views())
 
 
 class _ModelTrain(torch.autograd.Function):
     """DSTDGCN forward + native backward (reference :293-317): train mode, or
-    an eval-mode model under autograd (running-statistics BN, no dropout)."""
+    an eval-mode model under autograd (running-statistics BN, no dropout).
+    Both directions are torch.library ops (dstd::dstdgcn_train_forward /
+    dstdgcn_train_backward, below) over the C ABI; the opt-in in-place
+    gradient arena calls the C ABI directly (it writes .grad as a side
+    effect, which an op cannot)."""
 
     @staticmethod
     def forward(ctx, model, x, *params):
-        L = native.lib()
-        n, t, v, c = x.shape
-        dev = x.device
-        p = model._native_params()
-        y = torch.empty_like(x)
-        nbytes = L.dstd_model_train_saved_bytes(n, t, v, model.num_feature, model.num_layers)
-        saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         flags = _bn_flags(model)
         drop = float(model.do_in.p) if model.do_in.training else 0.0
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop > 0 else 0
-        code = L.dstd_model_train_fwd_ex(p, native.ptr(x, "x"), n, _bn_momentum(model), drop, seed,
-                                         native.ptr(y, "y"), saved.data_ptr(), nbytes, native.stream_handle(dev),
-                                         flags)
-        native.check(code, "dstd_model_train_fwd_ex")
+        y, saved = torch.ops.dstd.dstdgcn_train_forward(x, list(params), model._tree.get(model)[1], model._dstd_uid,
+                                                        flags, _bn_momentum(model), drop, seed)
         if not flags:
             _count_batch(model)
         ctx.model, ctx.saved_buf, ctx.drop, ctx.seed, ctx.flags = model, saved, drop, seed, flags
@@ -321,39 +345,31 @@ class _ModelTrain(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        L = native.lib()
         (x,) = ctx.saved_tensors
         model = ctx.model
-        n, t, v, c = x.shape
         dev = x.device
         dy = dy.contiguous()
+        need_dx = bool(ctx.needs_input_grad[1])
         # gradients accumulate straight into the parameters' .grad (one arena,
         # native +=) when the caller opted in (engine.PredictionEngine.train
         # sets model._dstd_inplace_grads) and no parameter carries hooks; else
-        # into a fresh arena whose views autograd accumulates (hooks, DDP and
-        # torch.autograd.grad see ordinary gradients)
+        # the backward op fills a fresh arena whose views autograd accumulates
+        # (hooks, DDP and torch.autograd.grad see ordinary gradients)
         if getattr(model, "_dstd_inplace_grads", False) and not any(
                 p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None) for p in ctx.params):
             arena, direct = native.grad_sink(model, ctx.params, dev)
-        else:
-            arena, direct = native.GradArena(ctx.params, dev), False
-        g = getattr(arena, "model_grads", None) if direct else None
-        if g is None:
-            g = model._native_grads(arena)
-            if direct:  # the persistent arena: its pointer table is reused
-                arena.model_grads = g
-        nbytes = L.dstd_model_train_workspace_bytes(n, t, v, model.num_feature, model.num_layers)
-        ws = native.workspace(dev, nbytes)
-        dx = torch.empty_like(x) if ctx.needs_input_grad[1] else None
-        code = L.dstd_model_train_bwd_ex(model._native_params(), native.ptr(x, "x"), n, ctx.drop, ctx.seed,
-                                         ctx.saved_buf.data_ptr(), ctx.saved_buf.numel(), native.ptr(dy, "dy"), g,
-                                         dx.data_ptr() if dx is not None else None, ws.data_ptr(), ws.numel(),
-                                         native.stream_handle(dev), ctx.flags)
-        native.check(code, "dstd_model_train_bwd_ex")
+            if direct:
+                g = getattr(arena, "model_grads", None)
+                if g is None:  # the persistent arena: its pointer table is reused
+                    g = arena.model_grads = model._native_grads(arena)
+                dx = _model_train_bwd_native(model, x, ctx.saved_buf, dy, ctx.flags, ctx.drop, ctx.seed, g, need_dx)
+                ctx.saved_buf = None
+                return (None, dx, *([None] * len(arena.params)))
+        dx, flat = torch.ops.dstd.dstdgcn_train_backward(x, ctx.saved_buf, dy, ctx.params, model._dstd_uid, ctx.flags,
+                                                         ctx.drop, ctx.seed, need_dx)
         ctx.saved_buf = None
-        if direct:
-            return (None, dx, *([None] * len(arena.params)))
-        return (None, dx, *arena.views())
+        arena = native.GradArena(ctx.params, dev, buf=flat)
+        return (None, dx if need_dx else None, *arena.views())
 
 
 class BatchNorm(nn.Module):
@@ -846,3 +862,122 @@ def _op_dstdgcn_forward(x: torch.Tensor, tensors: List[torch.Tensor], uid: int, 
 @_op_dstdgcn_forward.register_fake
 def _(x, tensors, uid, flags):
     return torch.empty_like(x)
+
+
+# Training directions: forward ops return the
+# output and the saved-state buffer the backward op consumes; backward ops
+# return the input gradient (empty when not needed) and every parameter
+# gradient in one flat arena (dstd_native.GradArena layout, in params order).
+# The forward ops update the BN running statistics among `buffers` in train
+# mode (declared mutated).
+@torch.library.custom_op("dstd::dstdgcb_train_forward", mutates_args=("buffers",))
+def _op_dstdgcb_train_forward(x: torch.Tensor, params: List[torch.Tensor], buffers: List[torch.Tensor], uid: int,
+                              flags: int, momentum: float) -> Tuple[torch.Tensor, torch.Tensor]:
+    """DSTDGCB forward with train-mode (or running-stats) BN -> dstd_block_train_fwd_ex."""
+    return _block_train_fwd_native(_instance(uid), x, flags, momentum)
+
+
+@_op_dstdgcb_train_forward.register_fake
+def _(x, params, buffers, uid, flags, momentum):
+    blk = _instance(uid)
+    B, cin, T, V = x.shape
+    nbytes = native.lib().dstd_block_train_saved_bytes(B, cin, blk.out_channels, T, V)
+    return x.new_empty(B, blk.out_channels, T, V), x.new_empty(nbytes, dtype=torch.uint8)
+
+
+@torch.library.custom_op("dstd::dstdgcb_train_backward", mutates_args=())
+def _op_dstdgcb_train_backward(x: torch.Tensor, saved: torch.Tensor, dy: torch.Tensor, params: List[torch.Tensor],
+                               uid: int, flags: int, need_dx: bool) -> Tuple[torch.Tensor, torch.Tensor]:
+    """DSTDGCB backward -> dstd_block_train_bwd_ex."""
+    blk = _instance(uid)
+    # the arena is laid out over the module's own parameters (the native
+    # pointer table resolves them by identity); `params` -- the same tensors
+    # in normal use, copies under opcheck -- match them slot for slot
+    arena = native.GradArena(list(blk.parameters()), x.device)
+    dx = _block_train_bwd_native(blk, x, saved, dy, flags, arena, need_dx)
+    return (dx if dx is not None else x.new_empty(0)), arena.buf
+
+
+@_op_dstdgcb_train_backward.register_fake
+def _(x, saved, dy, params, uid, flags, need_dx):
+    return (torch.empty_like(x) if need_dx else x.new_empty(0)), x.new_empty(native.arena_numel(params))
+
+
+@torch.library.custom_op("dstd::dstdgcn_train_forward", mutates_args=("buffers",))
+def _op_dstdgcn_train_forward(x: torch.Tensor, params: List[torch.Tensor], buffers: List[torch.Tensor], uid: int,
+                              flags: int, momentum: float, drop: float, seed: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """DSTDGCN forward with train-mode (or running-stats) BN -> dstd_model_train_fwd_ex."""
+    return _model_train_fwd_native(_instance(uid), x, flags, momentum, drop, seed)
+
+
+@_op_dstdgcn_train_forward.register_fake
+def _(x, params, buffers, uid, flags, momentum, drop, seed):
+    m = _instance(uid)
+    n, t, v, c = x.shape
+    nbytes = native.lib().dstd_model_train_saved_bytes(n, t, v, m.num_feature, m.num_layers)
+    return torch.empty_like(x), x.new_empty(nbytes, dtype=torch.uint8)
+
+
+@torch.library.custom_op("dstd::dstdgcn_train_backward", mutates_args=())
+def _op_dstdgcn_train_backward(x: torch.Tensor, saved: torch.Tensor, dy: torch.Tensor, params: List[torch.Tensor],
+                               uid: int, flags: int, drop: float, seed: int,
+                               need_dx: bool) -> Tuple[torch.Tensor, torch.Tensor]:
+    """DSTDGCN backward -> dstd_model_train_bwd_ex."""
+    m = _instance(uid)
+    arena = native.GradArena(m._tree.get(m)[0], x.device)  # (see dstdgcb_train_backward)
+    dx = _model_train_bwd_native(m, x, saved, dy, flags, drop, seed, m._native_grads(arena), need_dx)
+    return (dx if dx is not None else x.new_empty(0)), arena.buf
+
+
+@_op_dstdgcn_train_backward.register_fake
+def _(x, saved, dy, params, uid, flags, drop, seed, need_dx):
+    return (torch.empty_like(x) if need_dx else x.new_empty(0)), x.new_empty(native.arena_numel(params))
+
+
+@torch.library.custom_op("dstd::dstdgc_train_forward", mutates_args=())
+def _op_dstdgc_train_forward(x: torch.Tensor, A: torch.Tensor, alpha: torch.Tensor, weights: List[torch.Tensor],
+                             uid: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """DSTDGC forward keeping the backward's state -> dstd_dstdgc_train_fwd."""
+    mod = _instance(uid)
+    mode = native.MODE_SPATIAL if mod.mode == "spatial" else native.MODE_TEMPORAL
+    return _op_train_fwd_native(mod, mode, x, A, alpha)
+
+
+@_op_dstdgc_train_forward.register_fake
+def _(x, A, alpha, weights, uid):
+    mod = _instance(uid)
+    mode = native.MODE_SPATIAL if mod.mode == "spatial" else native.MODE_TEMPORAL
+    B, cin, T, V = x.shape
+    nbytes = native.lib().dstd_dstdgc_train_saved_bytes(mode, B, cin, mod.out_channels, T, V)
+    return x.new_empty(B, mod.out_channels, T, V), x.new_empty(nbytes, dtype=torch.uint8)
+
+
+@torch.library.custom_op("dstd::dstdgc_train_backward", mutates_args=())
+def _op_dstdgc_train_backward(x: torch.Tensor, A: torch.Tensor, alpha: torch.Tensor, saved: torch.Tensor,
+                              dy: torch.Tensor, weights: List[torch.Tensor], uid: int,
+                              need_dx: bool) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor]:
+    """DSTDGC backward -> dstd_dstdgc_train_bwd: (dx, dA, dalpha, weight-gradient arena)."""
+    L = native.lib()
+    mod = _instance(uid)
+    mode = native.MODE_SPATIAL if mod.mode == "spatial" else native.MODE_TEMPORAL
+    B, cin, T, V = x.shape
+    dev = x.device
+    cout = mod.out_channels
+    arena = native.GradArena(list(mod.parameters()), dev)  # (see dstdgcb_train_backward)
+    dx = torch.zeros_like(x) if need_dx else x.new_empty(0)
+    dA = torch.zeros_like(A)
+    dalpha = torch.zeros_like(alpha)
+    ws = native.workspace(dev, L.dstd_dstdgc_train_workspace_bytes(mode, B, cin, cout, T, V))
+    code = L.dstd_dstdgc_train_bwd(mode, native.ptr(x, "x"), B, cin, cout, T, V, native.gc_weights(mod),
+                                   native.ptr(alpha, "alpha_m"), saved.data_ptr(), saved.numel(), native.ptr(dy, "dy"),
+                                   dx.data_ptr() if need_dx else None, native.gc_grads(mod, arena),
+                                   native.ptr(dA, "dA"), native.ptr(dalpha, "dalpha"), ws.data_ptr(), ws.numel(),
+                                   native.stream_handle(dev))
+    native.check(code, "dstd_dstdgc_train_bwd")
+    return dx, dA, dalpha, arena.buf
+
+
+@_op_dstdgc_train_backward.register_fake
+def _(x, A, alpha, saved, dy, weights, uid, need_dx):
+    return ((torch.empty_like(x) if need_dx else x.new_empty(0)), torch.empty_like(A), torch.empty_like(alpha),
+            x.new_empty(native.arena_numel(weights)))

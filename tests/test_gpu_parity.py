@@ -560,8 +560,10 @@ def test_block_large_adjacency_and_activations(cin, cout, precision):
 
 
 def test_torch_library_ops_opcheck_and_compile():
-    """The custom ops pass torch.library.opcheck (schema, fake kernel vs the
-    real one) and a torch.compile'd model (aot_eager: no codegen) equals eager."""
+    """The custom ops -- eval forwards and both training directions of op,
+    block and model -- pass torch.library.opcheck (schema incl. the declared
+    BN-buffer mutation, fake kernel vs the real one), and a torch.compile'd
+    model (aot_eager: no codegen) equals eager."""
     m, d, sd, opts = load_model("h36m")
     x = t(d["x"])
     tensors = list(m.parameters()) + list(m.buffers())
@@ -576,3 +578,29 @@ def test_torch_library_ops_opcheck_and_compile():
         y_eager = m(x)
         mc = torch.compile(m, backend="aot_eager")
         assert torch.equal(mc(x), y_eager)
+    # the training directions (forward + saved state, backward + gradient arena)
+    ut = ("test_schema", "test_faketensor")
+    params, buffers = list(m.parameters()), list(m.buffers())
+    m.train()
+    args = (x, params, buffers, m._dstd_uid, 0, 0.1, 0.0, 0)
+    torch.library.opcheck(torch.ops.dstd.dstdgcn_train_forward.default, args, test_utils=ut)
+    y, saved = torch.ops.dstd.dstdgcn_train_forward(*args)
+    torch.library.opcheck(torch.ops.dstd.dstdgcn_train_backward.default,
+                          (x, saved, torch.randn_like(y), params, m._dstd_uid, 0, 0.0, 0, True), test_utils=ut)
+    blk = m.encoders[0][0].stgcn[0][0]
+    bp, bb = list(blk.parameters()), list(blk.buffers())
+    xb = torch.randn(2, 64, 35, 22, device=DEV)
+    torch.library.opcheck(torch.ops.dstd.dstdgcb_train_forward.default, (xb, bp, bb, blk._dstd_uid, 0, 0.1),
+                          test_utils=ut)
+    yb, sb = torch.ops.dstd.dstdgcb_train_forward(xb, bp, bb, blk._dstd_uid, 0, 0.1)
+    torch.library.opcheck(torch.ops.dstd.dstdgcb_train_backward.default,
+                          (xb, sb, torch.randn_like(yb), bp, blk._dstd_uid, 0, True), test_utils=ut)
+    op = blk.conv_s[0]
+    A = torch.randn(22, 22, device=DEV)
+    al = torch.full((1,), 0.7, device=DEV)
+    op_p = list(op.parameters())
+    torch.library.opcheck(torch.ops.dstd.dstdgc_train_forward.default, (xb, A, al, op_p, op._dstd_uid),
+                          test_utils=ut)
+    yo, so = torch.ops.dstd.dstdgc_train_forward(xb, A, al, op_p, op._dstd_uid)
+    torch.library.opcheck(torch.ops.dstd.dstdgc_train_backward.default,
+                          (xb, A, al, so, torch.randn_like(yo), op_p, op._dstd_uid, True), test_utils=ut)
