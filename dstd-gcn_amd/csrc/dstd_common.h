@@ -15,6 +15,24 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #define DSTD_THREADS 256
 #define DSTD_WAVES (DSTD_THREADS / DSTD_WAVE)
 
+// The C entry points launch on the device of the caller's stream: a module
+// on cuda:1 called while cuda:0 is current switches for the call and back.
+struct StreamDeviceGuard {
+  int prev = -1;
+  explicit StreamDeviceGuard(void* stream) {
+    if (!stream) return;
+    int cur = 0;
+    hipDevice_t sd = 0;
+    if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice((hipStream_t)stream, &sd) != hipSuccess) return;
+    if (sd != cur && hipSetDevice(sd) == hipSuccess) prev = cur;
+  }
+  ~StreamDeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  StreamDeviceGuard(const StreamDeviceGuard&) = delete;
+  StreamDeviceGuard& operator=(const StreamDeviceGuard&) = delete;
+};
+
 __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
