@@ -16,7 +16,7 @@ using namespace dstd;
 
 namespace {
 
-constexpr int kMaxT = 112;  // the generic spatial adjacency kernel's LDS (K = 2T) fits up to here
+constexpr int kMaxT = 128;  // the generic kernels cover T <= 128 (adjacency row groups past 112)
 constexpr int kMaxV = 32;
 constexpr int kMaxC = 64;
 
@@ -672,7 +672,7 @@ const char* dstd_error_string(int code) {
     case DSTD_OK: return "ok";
     case DSTD_EINVAL: return "invalid argument (null pointer or bad shape)";
     case DSTD_EWORKSPACE: return "workspace too small";
-    case DSTD_ELIMIT: return "shape outside the supported envelope (T<=112, V<=32, C<=64)";
+    case DSTD_ELIMIT: return "shape outside the supported envelope (T<=128, V<=32, C<=64)";
     default: return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
   }
 }

@@ -90,6 +90,7 @@ struct AdjArgs {
                        //    ldo counts halves (2 * ncol), out_sN / out_sG still count floats,
                        //    ncol = NA * SL
   int ctiles_per_wg, nchunks;
+  int rgroups;         // generic writer: row groups of RT 16-row tiles per (n, g) (set by launch_adj)
 };
 
 // ---- spatial GC (both graphs) + DSTDGCB mid epilogue ----------------------

@@ -102,16 +102,18 @@ __global__ __launch_bounds__(256) void k_adj(AdjArgs a) {
   extern __shared__ float lds[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int chunk = blockIdx.x % a.nchunks;
-  const int g = (blockIdx.x / a.nchunks) % a.ngroups;
-  const int n = blockIdx.x / (a.nchunks * a.ngroups);
-  const int K = a.K, NA = a.NA, ncol = a.ncol, nrow = a.nrow;
+  const int rg = (blockIdx.x / a.nchunks) % a.rgroups;
+  const int g = (blockIdx.x / (a.nchunks * a.rgroups)) % a.ngroups;
+  const int n = blockIdx.x / (a.nchunks * a.rgroups * a.ngroups);
+  const int K = a.K, NA = a.NA, ncol = a.ncol;
+  const int row0 = rg * RT * 16, nrow = min(a.nrow - row0, RT * 16);  // this group's rows
   const int Kp = rup(K, 4);
   const int SR = stride_mod32(RT * 16, 16);
   float* Wl = lds;              // [Kp][SR]   Wl[k][row] = W[row][k]
   float* Pl = Wl + Kp * SR;     // [Kp][NA]
   float* Ql = Pl + Kp * NA;     // [Kp][NA]
 
-  const float* W = a.W[g];
+  const float* W = a.W[g] + (size_t)row0 * K;
   for (int i = tid; i < Kp * SR; i += 256) {
     const int k = i / SR, r = i % SR;
     Wl[i] = (k < K && r < nrow) ? W[r * K + k] : 0.f;
@@ -137,9 +139,9 @@ __global__ __launch_bounds__(256) void k_adj(AdjArgs a) {
   __syncthreads();
 
   const float alpha = *a.alpha;
-  const float* bias = a.bias[g];
+  const float* bias = a.bias[g] + row0;
   const float* astat = a.astat[g];
-  float* out = a.out + (size_t)n * a.out_sN + (size_t)g * a.out_sG;
+  float* out = a.out + (size_t)n * a.out_sN + (size_t)g * a.out_sG + (size_t)row0 * a.ldo;
   const int nct = cdiv(ncol, 16);
   const int ct0 = chunk * a.ctiles_per_wg;
   const int ct1 = min(nct, ct0 + a.ctiles_per_wg);
@@ -190,9 +192,17 @@ static hipError_t launch_adj_rt(const AdjArgs& a, hipStream_t s, int nblocks, si
 }
 
 hipError_t launch_adj(AdjArgs a, hipStream_t s) {
-  const int RT = cdiv(a.nrow, 16);
-  if (RT < 1 || RT > 8 || a.ngroups < 1 || a.ngroups > 2 || adj_lds_bytes(RT, a.K, a.NA) > 160 * 1024)
-    return hipErrorInvalidValue;
+  // rows split into the fewest groups whose W tile (Kp x RT*16) and P/Q planes fit in LDS;
+  // each group re-evaluates the tanh operand (only T > 112 spatial needs more than one)
+  const int RT_all = cdiv(a.nrow, 16);
+  if (RT_all < 1 || a.ngroups < 1 || a.ngroups > 2) return hipErrorInvalidValue;
+  a.rgroups = 1;
+  while (a.rgroups <= RT_all &&
+         (cdiv(RT_all, a.rgroups) > 8 || adj_lds_bytes(cdiv(RT_all, a.rgroups), a.K, a.NA) > 160 * 1024))
+    ++a.rgroups;
+  if (a.rgroups > RT_all) return hipErrorInvalidValue;
+  const int RT = cdiv(RT_all, a.rgroups);
+  a.rgroups = cdiv(RT_all, RT);
   const int nct = cdiv(a.ncol, 16);
   // enough workgroups to fill the chip (>= ~1024), each a multiple of 4 tiles
   int chunks = cdiv(1024, a.B * a.ngroups);
@@ -201,11 +211,11 @@ hipError_t launch_adj(AdjArgs a, hipStream_t s) {
   chunks = chunks > max_chunks ? max_chunks : chunks;
   a.ctiles_per_wg = rup(cdiv(nct, chunks), DSTD_WAVES);
   a.nchunks = cdiv(nct, a.ctiles_per_wg);
-  const int nblocks = a.B * a.ngroups * a.nchunks;
   {
-    const hipError_t fe = launch_adj_fast(a, s, nblocks);
+    const hipError_t fe = launch_adj_fast(a, s, a.B * a.ngroups * a.nchunks);
     if (fe != hipErrorNotSupported || a.hl) return fe;  // the split-f16 layout has no generic writer
   }
+  const int nblocks = a.B * a.ngroups * a.rgroups * a.nchunks;
   const size_t lds = adj_lds_bytes(RT, a.K, a.NA);
   switch (RT) {
     case 1: return launch_adj_rt<1>(a, s, nblocks, lds);

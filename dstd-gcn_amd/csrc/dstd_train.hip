@@ -829,7 +829,9 @@ hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int A
 
 hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int A, int NN, float* dP, float* dQ,
                           hipStream_t s) {
-  const size_t lds = (size_t)NN * (NN + 1) * sizeof(float);
+  const size_t lds = (size_t)NN * (NN + 1) * sizeof(float);  // 66 KB at the T = 128 envelope top
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_tanh_outer_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   k_tanh_outer_bwd<<<B * 2 * A, 256, lds, s>>>(M, dM, v, A, NN, dP, dQ);
   return hipGetLastError();
 }

@@ -23,7 +23,7 @@ using namespace dstd::train;
 
 namespace {
 
-constexpr int kMaxT = 112;  // the generic spatial adjacency kernel's LDS (K = 2T) fits up to here
+constexpr int kMaxT = 128;  // same envelope as the forward (dstd_capi.hip)
 constexpr int kMaxV = 32;
 constexpr int kMaxC = 64;
 

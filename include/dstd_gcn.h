@@ -25,7 +25,7 @@
  *   - Every call is enqueued on `stream` (hipStream_t passed as void*).
  *   - Return 0 on success, a positive hipError_t from a failed launch, or a
  *     negative DSTD_E* code for bad arguments.  dstd_error_string() names it.
- *   - Limits: T <= 112, V <= 32, channels <= 64, red_channels == 2.
+ *   - Limits: T <= 128, V <= 32, channels <= 64, red_channels == 2.
  */
 #ifndef DSTD_GCN_H
 #define DSTD_GCN_H

@@ -401,12 +401,14 @@ def test_dstdgcn_generic_T30():
 
 
 @pytest.mark.parametrize("precision", ["split", "fp32"])
-def test_dstdgcn_generic_T100(precision):
-    """H36M "50 in / 50 out" (T=100, near the top of the T <= 112 envelope):
-    no split-f16 kernels for this T, the generic exact-fp32 ones run in both
+@pytest.mark.parametrize("t_in,t_out", [(50, 50), (64, 64)])
+def test_dstdgcn_generic_long(precision, t_in, t_out):
+    """H36M "50 in / 50 out" (T=100) and "64 in / 64 out" (T=128, the top of
+    the envelope, where the spatial adjacency runs in two row groups): no
+    split-f16 kernels for these T, the generic exact-fp32 ones run in both
     arithmetics; against the fp64 oracle at the fp32 oracle's own error."""
     torch.manual_seed(5)
-    opts = dict(input_channels=6, input_time_frame=50, output_time_frame=50, st_gcnn_dropout=0.1,
+    opts = dict(input_channels=6, input_time_frame=t_in, output_time_frame=t_out, st_gcnn_dropout=0.1,
                 joints_to_consider=22, num_feature=64, num_layers=2, layout="h36m")
     m = get_model("dstdgcn", dstdgcn=opts)
     with torch.no_grad():
@@ -418,7 +420,7 @@ def test_dstdgcn_generic_T100(precision):
         for mod in m.modules():
             if isinstance(mod, torch.nn.BatchNorm1d):
                 mod.running_var.fill_(4.0)
-    x = synth(2, 100, 22, 50, 12)
+    x = synth(2, t_in + t_out, 22, t_in, 12)
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     y64 = O.dstdgcn(x, sd, 2).numpy()
     ref32 = rel_err(O.dstdgcn(x, sd, 2, dtype=torch.float32).numpy(), y64)
@@ -427,7 +429,7 @@ def test_dstdgcn_generic_T100(precision):
         y = m(x.to(DEV)).cpu().numpy()
     assert rel_err(y, y64) <= model_tol(ref32), ref32
     # past the envelope: a clear error, not a wrong answer
-    opts["output_time_frame"] = 80
+    opts["input_time_frame"], opts["output_time_frame"] = 50, 80
     big = get_model("dstdgcn", dstdgcn=opts).to(DEV).eval()
     with pytest.raises(RuntimeError, match="envelope"):
         with torch.no_grad():

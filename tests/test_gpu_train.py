@@ -92,7 +92,8 @@ def test_dstdgc_op_backward(mode, cin, cout, T, V):
 
 # ---- DSTDGCB in train mode ---------------------------------------------------
 BLOCKS = [(6, 64, "h36m", 35, 22), (64, 64, "3dpw", 40, 23), (64, 3, "cmu", 35, 25),
-          (64, 64, "h36m", 100, 22)]  # T=100 ("50 in / 50 out"): generic kernels at the envelope's top
+          (64, 64, "h36m", 100, 22),  # T=100 ("50 in / 50 out"): generic kernels
+          (64, 64, "h36m", 128, 22)]  # T=128: the envelope's top
 
 
 @pytest.mark.parametrize("cin,cout,layout,T,V", BLOCKS)
