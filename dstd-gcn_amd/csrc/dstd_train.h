@@ -61,12 +61,12 @@ struct PQView {
   long long sn, sr, sa, si;
 };
 
-// M[n][r*A + a][i][j] = tanh(P(n,r,a,i) - Q(n,r,a,j)), r < 2.
-hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int A, int NN, float* M,
+// M[n][r*A + a][i][j] = tanh(P(n,r,a,i) - Q(n,r,a,j)), r < R (red_channels).
+hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int R, int A, int NN, float* M,
                           hipStream_t s);
 // dZ = dM * (1 - M^2);  dP(n,r,a,i) = sum_j dZ;  dQ(n,r,a,j) = -sum_i dZ.
-hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int A, int NN, float* dP, float* dQ,
-                          hipStream_t s);
+hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int R, int A, int NN, float* dP,
+                          float* dQ, hipStream_t s);
 
 // Backward of adj_combine + the conv_rm bias, fused: dD -> dE = alpha * dD in
 // place, and dalpha += <dD, E>, dA[ij] += sum_{n,a} dD, dbrm[a] += sum_{n,ij} dE.

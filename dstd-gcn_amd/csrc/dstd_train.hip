@@ -218,10 +218,10 @@ constexpr int kMaxSplit = 128;
 // ---------------------------------------------------------------------------
 // tanh outer difference
 // ---------------------------------------------------------------------------
-__global__ void k_tanh_outer_fwd(const float* P, const float* Q, PQView v, int A, int NN, float* M) {
+__global__ void k_tanh_outer_fwd(const float* P, const float* Q, PQView v, int R, int A, int NN, float* M) {
   // one workgroup per (n, r, a); M block [NN][NN]
   const int blk = blockIdx.x;
-  const int n = blk / (2 * A), ra = blk - n * 2 * A, r = ra / A, a = ra - r * A;
+  const int n = blk / (R * A), ra = blk - n * R * A, r = ra / A, a = ra - r * A;
   const float* p = P + n * v.sn + r * v.sr + a * v.sa;
   const float* q = Q + n * v.sn + r * v.sr + a * v.sa;
   float* m = M + (size_t)blk * NN * NN;
@@ -231,10 +231,11 @@ __global__ void k_tanh_outer_fwd(const float* P, const float* Q, PQView v, int A
   }
 }
 
-__global__ void k_tanh_outer_bwd(const float* M, const float* dM, PQView v, int A, int NN, float* dP, float* dQ) {
+__global__ void k_tanh_outer_bwd(const float* M, const float* dM, PQView v, int R, int A, int NN, float* dP,
+                                 float* dQ) {
   extern __shared__ float dz[];  // [NN][NN+1]
   const int blk = blockIdx.x;
-  const int n = blk / (2 * A), ra = blk - n * 2 * A, r = ra / A, a = ra - r * A;
+  const int n = blk / (R * A), ra = blk - n * R * A, r = ra / A, a = ra - r * A;
   const float* m = M + (size_t)blk * NN * NN;
   const float* dm = dM + (size_t)blk * NN * NN;
   for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
@@ -822,17 +823,18 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int A, int NN, float* M, hipStream_t s) {
-  k_tanh_outer_fwd<<<B * 2 * A, 256, 0, s>>>(P, Q, v, A, NN, M);
+hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int R, int A, int NN, float* M,
+                          hipStream_t s) {
+  k_tanh_outer_fwd<<<B * R * A, 256, 0, s>>>(P, Q, v, R, A, NN, M);
   return hipGetLastError();
 }
 
-hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int A, int NN, float* dP, float* dQ,
-                          hipStream_t s) {
+hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int R, int A, int NN, float* dP,
+                          float* dQ, hipStream_t s) {
   const size_t lds = (size_t)NN * (NN + 1) * sizeof(float);  // 66 KB at the T = 128 envelope top
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_tanh_outer_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  k_tanh_outer_bwd<<<B * 2 * A, 256, lds, s>>>(M, dM, v, A, NN, dP, dQ);
+  k_tanh_outer_bwd<<<B * R * A, 256, lds, s>>>(M, dM, v, R, A, NN, dP, dQ);
   return hipGetLastError();
 }
 

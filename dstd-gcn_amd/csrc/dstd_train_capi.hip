@@ -26,6 +26,7 @@ namespace {
 constexpr int kMaxT = 128;  // same envelope as the forward (dstd_capi.hip)
 constexpr int kMaxV = 32;
 constexpr int kMaxC = 64;
+constexpr int kMaxRed = 8;  // red_channels of one DSTDGC (P / Q channels each)
 
 struct Carver {
   char* base;
@@ -87,10 +88,11 @@ bool model_ok(const dstd_model_params* p) {
 // ---------------------------------------------------------------------------
 struct OpGeom {
   int B, cin, cout, T, V, TV;
+  int R;  // red_channels: P / Q channels per op (2 in every block of the reference)
   int A, NN, NN2;
   long long ps_a, ps_i;
-  OpGeom(int mode, int B_, int cin_, int cout_, int T_, int V_)
-      : B(B_), cin(cin_), cout(cout_), T(T_), V(V_), TV(T_ * V_) {
+  OpGeom(int mode, int B_, int cin_, int cout_, int T_, int V_, int R_ = 2)
+      : B(B_), cin(cin_), cout(cout_), T(T_), V(V_), TV(T_ * V_), R(R_) {
     const bool sp = mode == DSTD_MODE_SPATIAL;
     A = sp ? T : V;
     NN = sp ? V : T;
@@ -98,7 +100,7 @@ struct OpGeom {
     ps_a = sp ? V : 1;
     ps_i = sp ? 1 : V;
   }
-  int CG() const { return cout + 4; }  // rows of the packed conv output G = [F; P; Q]
+  int CG() const { return cout + 2 * R; }  // rows of the packed conv output G = [F; P; Q]
   // P (Q) rows of G: element (n, r, a, i) at n*CG*TV + r*TV + a*ps_a + i*ps_i
   PQView pq() const { return PQView{(long long)CG() * TV, (long long)TV, ps_a, ps_i}; }
 };
@@ -113,17 +115,18 @@ void carve_op_saved(Carver& cv, OpSaved& s, const OpGeom& g) {
   s.Wp = cv.take((size_t)g.CG() * g.cin);
   s.bp = cv.take(g.CG());
   s.G = cv.take((size_t)g.B * g.CG() * g.TV);
-  s.M = cv.take((size_t)g.B * 2 * g.A * g.NN2);
+  s.M = cv.take((size_t)g.B * g.R * g.A * g.NN2);
   s.E = cv.take((size_t)g.B * g.A * g.NN2);
   s.D = cv.take((size_t)g.B * g.A * g.NN2);
 }
 // Copy jobs packing one op's conv weights into Wp / bp.
 bool pack_jobs(CopyJobs& js, const dstd_gc_weights* w, const OpSaved& sv, const OpGeom& g) {
+  const int R = g.R;
   return js.add(w->wf, sv.Wp, g.cout, g.cin, g.cin, g.cin, 0) &&
-         js.add(w->wm1, sv.Wp + (size_t)g.cout * g.cin, 2, g.cin, g.cin, g.cin, 0) &&
-         js.add(w->wm2, sv.Wp + (size_t)(g.cout + 2) * g.cin, 2, g.cin, g.cin, g.cin, 0) &&
-         js.add(w->bf, sv.bp, 1, g.cout, g.cout, g.cout, 0) && js.add(w->bm1, sv.bp + g.cout, 1, 2, 2, 2, 0) &&
-         js.add(w->bm2, sv.bp + g.cout + 2, 1, 2, 2, 2, 0);
+         js.add(w->wm1, sv.Wp + (size_t)g.cout * g.cin, R, g.cin, g.cin, g.cin, 0) &&
+         js.add(w->wm2, sv.Wp + (size_t)(g.cout + R) * g.cin, R, g.cin, g.cin, g.cin, 0) &&
+         js.add(w->bf, sv.bp, 1, g.cout, g.cout, g.cout, 0) && js.add(w->bm1, sv.bp + g.cout, 1, R, R, R, 0) &&
+         js.add(w->bm2, sv.bp + g.cout + R, 1, R, R, R, 0);
 }
 
 struct OpWs {
@@ -138,17 +141,18 @@ size_t red_floats(const OpGeom& g) {
 // Sized for the largest of the given op geometries (one workspace serves every
 // op of a block / model in turn).
 void carve_op_ws(Carver& cv, OpWs& w, const std::vector<OpGeom>& gl) {
-  size_t nG = 0, nD = 0, nW = 0, nmn = 0, nred = 0;
+  size_t nG = 0, nD = 0, nM = 0, nW = 0, nmn = 0, nred = 0;
   for (const OpGeom& g : gl) {
     nG = std::max(nG, (size_t)g.B * g.CG() * g.TV);
     nD = std::max(nD, (size_t)g.B * g.A * g.NN2);
+    nM = std::max(nM, (size_t)g.B * g.R * g.A * g.NN2);
     nW = std::max(nW, (size_t)g.CG() * (g.cin + 1));
-    nmn = std::max(nmn, (size_t)std::max(std::max(g.CG() * (g.cin + 1), 2 * g.A * g.A), g.cout * g.cin));
+    nmn = std::max(nmn, (size_t)std::max(std::max(g.CG() * (g.cin + 1), g.R * g.A * g.A), g.cout * g.cin));
     nred = std::max(nred, red_floats(g));
   }
   w.dG = cv.take(nG);
   w.dD = cv.take(nD);
-  w.dM = cv.take(2 * nD);
+  w.dM = cv.take(nM);
   w.gW = cv.take(nW);
   w.gs = cv.take(gemm_scratch_floats((int)nmn, 1));
   w.part = cv.take(std::max(dot_partials(), mpjpe_partials()));
@@ -202,12 +206,12 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   // conv_f, conv_m1, conv_m2 in one GEMM                         :81-82
   DSTD_TRYH(gemm(conv_fwd(sv.Wp, sv.bp, x, sv.G, g.B, g.cin, g.CG(), g.TV), nullptr, s));
   const float* P = sv.G + (size_t)g.cout * g.TV;
-  const float* Q = P + 2 * (size_t)g.TV;
-  DSTD_TRYH(tanh_outer_fwd(P, Q, g.pq(), g.B, g.A, g.NN, sv.M, s));                        // :84 / :90
-  Gemm e;  // E = conv_rm(M): [A x 2A] . [2A x NN^2] + b_rm           :85 / :91
-  e.M = g.A, e.N = g.NN2, e.K = 2 * g.A, e.nb1 = g.B;
-  e.A = w->wrm, e.a_m = 2 * g.A, e.a_k = 1;
-  e.B = sv.M, e.b_b1 = 2LL * g.A * g.NN2, e.b_k = g.NN2, e.b_n = 1;
+  const float* Q = P + (size_t)g.R * g.TV;
+  DSTD_TRYH(tanh_outer_fwd(P, Q, g.pq(), g.B, g.R, g.A, g.NN, sv.M, s));                   // :84 / :90
+  Gemm e;  // E = conv_rm(M): [A x RA] . [RA x NN^2] + b_rm           :85 / :91
+  e.M = g.A, e.N = g.NN2, e.K = g.R * g.A, e.nb1 = g.B;
+  e.A = w->wrm, e.a_m = g.R * g.A, e.a_k = 1;
+  e.B = sv.M, e.b_b1 = (long long)g.R * g.A * g.NN2, e.b_k = g.NN2, e.b_n = 1;
   e.C = sv.E, e.c_b1 = (long long)g.A * g.NN2, e.c_m = g.NN2, e.c_n = 1;
   e.bias_m = w->brm;
   e.d_out = sv.D;  // D = alpha * E + Acomb                          :86 / :92
@@ -247,36 +251,36 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   DSTD_TRYH(adj_bwd(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, dA, gr->brm, dalpha, ws.red, s, assign_dA));
   const float* dE = ws.dD;
   Gemm wr;  // dWrm[a][k] = sum_{n,ij} dE[n][a][ij] M[n][k][ij]
-  wr.M = g.A, wr.N = 2 * g.A, wr.K = g.NN2, wr.nb1 = g.B, wr.reduce = 1;
+  wr.M = g.A, wr.N = g.R * g.A, wr.K = g.NN2, wr.nb1 = g.B, wr.reduce = 1;
   wr.A = dE, wr.a_b1 = (long long)g.A * g.NN2, wr.a_m = g.NN2, wr.a_k = 1;
-  wr.B = sv.M, wr.b_b1 = 2LL * g.A * g.NN2, wr.b_k = 1, wr.b_n = g.NN2;
-  wr.C = gr->wrm, wr.c_m = 2 * g.A, wr.c_n = 1;
+  wr.B = sv.M, wr.b_b1 = (long long)g.R * g.A * g.NN2, wr.b_k = 1, wr.b_n = g.NN2;
+  wr.C = gr->wrm, wr.c_m = g.R * g.A, wr.c_n = 1;
   wr.beta = 1.f;
   DSTD_TRYH(gemm(wr, ws.gs, s));
   Gemm dm;  // dM[n][k][ij] = sum_a Wrm[a][k] dE[n][a][ij]
-  dm.M = 2 * g.A, dm.N = g.NN2, dm.K = g.A, dm.nb1 = g.B;
-  dm.A = w->wrm, dm.a_m = 1, dm.a_k = 2 * g.A;
+  dm.M = g.R * g.A, dm.N = g.NN2, dm.K = g.A, dm.nb1 = g.B;
+  dm.A = w->wrm, dm.a_m = 1, dm.a_k = g.R * g.A;
   dm.B = dE, dm.b_b1 = (long long)g.A * g.NN2, dm.b_k = g.NN2, dm.b_n = 1;
-  dm.C = ws.dM, dm.c_b1 = 2LL * g.A * g.NN2, dm.c_m = g.NN2, dm.c_n = 1;
+  dm.C = ws.dM, dm.c_b1 = (long long)g.R * g.A * g.NN2, dm.c_m = g.NN2, dm.c_n = 1;
   DSTD_TRYH(gemm(dm, nullptr, s));
-  // dP, dQ -> rows [cout, cout+4) of dG
+  // dP, dQ -> rows [cout, cout + 2R) of dG
   float* dP = ws.dG + (size_t)g.cout * g.TV;
-  DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.A, g.NN, dP, dP + 2 * (size_t)g.TV, s));
+  DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.R, g.A, g.NN, dP, dP + (size_t)g.R * g.TV, s));
   // the three 1x1 convs at once: dx += Wp^T dG;  [dWp | dbp] = sum dG [x; 1]^T
   if (dx) {
     Gemm gx = conv_dx(sv.Wp, ws.dG, dx, g.B, g.cin, g.CG(), g.TV);
     gx.beta = dx_beta;
     DSTD_TRYH(gemm(gx, ws.gs, s));
   }
-  // rows [0, cout) / [cout, cout+2) / [cout+2, cout+4) of [dWp | dbp]
+  // rows [0, cout) / [cout, cout+R) / [cout+R, cout+2R) of [dWp | dbp]
   // accumulate straight into the conv_f / conv_m1 / conv_m2 gradients
   Gemm gw = conv_dw(ws.dG, x, ws.gW, g.B, g.cin + 1, g.CG(), g.TV);
   gw.b_ones_last = 1;
   gw.b_b1 = (long long)g.cin * g.TV;
   gw.nseg = 3;
   gw.seg[0] = Gemm::Seg{0, g.cout, gr->wf, gr->bf};
-  gw.seg[1] = Gemm::Seg{g.cout, 2, gr->wm1, gr->bm1};
-  gw.seg[2] = Gemm::Seg{g.cout + 2, 2, gr->wm2, gr->bm2};
+  gw.seg[1] = Gemm::Seg{g.cout, g.R, gr->wm1, gr->bm1};
+  gw.seg[2] = Gemm::Seg{g.cout + g.R, g.R, gr->wm2, gr->bm2};
   return gemm(gw, ws.gs, s);
 }
 
@@ -489,30 +493,30 @@ void carve_model_ws(Carver& cv, ModelWs& w, int B, int T, int V, int C) {
 
 extern "C" {
 
-size_t dstd_dstdgc_train_saved_bytes(int mode, int B, int cin, int cout, int T, int V) {
+size_t dstd_dstdgc_train_saved_bytes_r(int mode, int B, int cin, int cout, int T, int V, int red) {
   Carver cv{nullptr};
   OpSaved s;
-  carve_op_saved(cv, s, OpGeom(mode, B, cin, cout, T, V));
+  carve_op_saved(cv, s, OpGeom(mode, B, cin, cout, T, V, red));
   return cv.off + 256;
 }
 
-size_t dstd_dstdgc_train_workspace_bytes(int mode, int B, int cin, int cout, int T, int V) {
+size_t dstd_dstdgc_train_workspace_bytes_r(int mode, int B, int cin, int cout, int T, int V, int red) {
   Carver cv{nullptr};
   OpWs w;
-  carve_op_ws(cv, w, {OpGeom(mode, B, cin, cout, T, V)});
+  carve_op_ws(cv, w, {OpGeom(mode, B, cin, cout, T, V, red)});
   return cv.off + 256;
 }
 
-int dstd_dstdgc_train_fwd(int mode, const float* x, int B, int cin, int cout, int T, int V,
-                          const dstd_gc_weights* w, const float* A, const float* alpha, float* y, void* saved,
-                          size_t saved_bytes, void* stream) {
+int dstd_dstdgc_train_fwd_r(int mode, const float* x, int B, int cin, int cout, int T, int V, int red,
+                            const dstd_gc_weights* w, const float* A, const float* alpha, float* y, void* saved,
+                            size_t saved_bytes, void* stream) {
   StreamDeviceGuard dev_guard_(stream);
   if (!x || !y || !A || !alpha || !gc_ok(w) || !saved) return DSTD_EINVAL;
   if (mode != DSTD_MODE_SPATIAL && mode != DSTD_MODE_TEMPORAL) return DSTD_EINVAL;
-  if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
-  if (!shape_ok(B, T, V) || !ch_ok(cin) || !ch_ok(cout)) return DSTD_ELIMIT;
-  if (saved_bytes < dstd_dstdgc_train_saved_bytes(mode, B, cin, cout, T, V)) return DSTD_EWORKSPACE;
-  const OpGeom g(mode, B, cin, cout, T, V);
+  if (B <= 0 || T <= 1 || V <= 0 || red <= 0) return DSTD_EINVAL;
+  if (!shape_ok(B, T, V) || !ch_ok(cin) || !ch_ok(cout) || red > kMaxRed) return DSTD_ELIMIT;
+  if (saved_bytes < dstd_dstdgc_train_saved_bytes_r(mode, B, cin, cout, T, V, red)) return DSTD_EWORKSPACE;
+  const OpGeom g(mode, B, cin, cout, T, V, red);
   Carver cv{(char*)saved};
   OpSaved sv;
   carve_op_saved(cv, sv, g);
@@ -523,18 +527,19 @@ int dstd_dstdgc_train_fwd(int mode, const float* x, int B, int cin, int cout, in
   return DSTD_OK;
 }
 
-int dstd_dstdgc_train_bwd(int mode, const float* x, int B, int cin, int cout, int T, int V,
-                          const dstd_gc_weights* w, const float* alpha, const void* saved, size_t saved_bytes,
-                          const float* dy, float* dx, const dstd_gc_grads* g, float* dA, float* dalpha,
-                          void* workspace, size_t workspace_bytes, void* stream) {
+int dstd_dstdgc_train_bwd_r(int mode, const float* x, int B, int cin, int cout, int T, int V, int red,
+                            const dstd_gc_weights* w, const float* alpha, const void* saved, size_t saved_bytes,
+                            const float* dy, float* dx, const dstd_gc_grads* g, float* dA, float* dalpha,
+                            void* workspace, size_t workspace_bytes, void* stream) {
   StreamDeviceGuard dev_guard_(stream);
   if (!x || !dy || !alpha || !gc_ok(w) || !gg_ok(g) || !dA || !dalpha || !saved || !workspace) return DSTD_EINVAL;
   if (mode != DSTD_MODE_SPATIAL && mode != DSTD_MODE_TEMPORAL) return DSTD_EINVAL;
-  if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
-  if (!shape_ok(B, T, V) || !ch_ok(cin) || !ch_ok(cout)) return DSTD_ELIMIT;
-  if (saved_bytes < dstd_dstdgc_train_saved_bytes(mode, B, cin, cout, T, V)) return DSTD_EWORKSPACE;
-  if (workspace_bytes < dstd_dstdgc_train_workspace_bytes(mode, B, cin, cout, T, V)) return DSTD_EWORKSPACE;
-  const OpGeom geo(mode, B, cin, cout, T, V);
+  if (B <= 0 || T <= 1 || V <= 0 || red <= 0) return DSTD_EINVAL;
+  if (!shape_ok(B, T, V) || !ch_ok(cin) || !ch_ok(cout) || red > kMaxRed) return DSTD_ELIMIT;
+  if (saved_bytes < dstd_dstdgc_train_saved_bytes_r(mode, B, cin, cout, T, V, red)) return DSTD_EWORKSPACE;
+  if (workspace_bytes < dstd_dstdgc_train_workspace_bytes_r(mode, B, cin, cout, T, V, red))
+    return DSTD_EWORKSPACE;
+  const OpGeom geo(mode, B, cin, cout, T, V, red);
   Carver cs{(char*)const_cast<void*>(saved)};
   OpSaved sv;
   carve_op_saved(cs, sv, geo);
@@ -543,6 +548,28 @@ int dstd_dstdgc_train_bwd(int mode, const float* x, int B, int cin, int cout, in
   carve_op_ws(cw, ws, {geo});
   DSTD_TRY(op_bwd(geo, x, w, alpha, sv, dy, dx, g, dA, dalpha, ws, (hipStream_t)stream));
   return DSTD_OK;
+}
+
+size_t dstd_dstdgc_train_saved_bytes(int mode, int B, int cin, int cout, int T, int V) {
+  return dstd_dstdgc_train_saved_bytes_r(mode, B, cin, cout, T, V, 2);
+}
+
+size_t dstd_dstdgc_train_workspace_bytes(int mode, int B, int cin, int cout, int T, int V) {
+  return dstd_dstdgc_train_workspace_bytes_r(mode, B, cin, cout, T, V, 2);
+}
+
+int dstd_dstdgc_train_fwd(int mode, const float* x, int B, int cin, int cout, int T, int V,
+                          const dstd_gc_weights* w, const float* A, const float* alpha, float* y, void* saved,
+                          size_t saved_bytes, void* stream) {
+  return dstd_dstdgc_train_fwd_r(mode, x, B, cin, cout, T, V, 2, w, A, alpha, y, saved, saved_bytes, stream);
+}
+
+int dstd_dstdgc_train_bwd(int mode, const float* x, int B, int cin, int cout, int T, int V,
+                          const dstd_gc_weights* w, const float* alpha, const void* saved, size_t saved_bytes,
+                          const float* dy, float* dx, const dstd_gc_grads* g, float* dA, float* dalpha,
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  return dstd_dstdgc_train_bwd_r(mode, x, B, cin, cout, T, V, 2, w, alpha, saved, saved_bytes, dy, dx, g, dA, dalpha,
+                                 workspace, workspace_bytes, stream);
 }
 
 size_t dstd_block_train_saved_bytes(int B, int cin, int cout, int T, int V) {

@@ -150,7 +150,8 @@ def lib():
         u64, f32 = ctypes.c_ulonglong, ctypes.c_float
         for n, k in (("dstd_dstdgc_train_saved_bytes", 6), ("dstd_dstdgc_train_workspace_bytes", 6),
                      ("dstd_block_train_saved_bytes", 5), ("dstd_block_train_workspace_bytes", 5),
-                     ("dstd_model_train_saved_bytes", 5), ("dstd_model_train_workspace_bytes", 5)):
+                     ("dstd_model_train_saved_bytes", 5), ("dstd_model_train_workspace_bytes", 5),
+                     ("dstd_dstdgc_train_saved_bytes_r", 7), ("dstd_dstdgc_train_workspace_bytes_r", 7)):
             getattr(L, n).restype = sz
             getattr(L, n).argtypes = [ci] * k
         L.dstd_dstdgc_train_fwd.restype = ci
@@ -159,6 +160,12 @@ def lib():
         L.dstd_dstdgc_train_bwd.restype = ci
         L.dstd_dstdgc_train_bwd.argtypes = [ci, vp, ci, ci, ci, ci, ci, ctypes.POINTER(GCWeights), vp, vp, sz, vp, vp,
                                             ctypes.POINTER(GCGrads), vp, vp, vp, sz, vp]
+        L.dstd_dstdgc_train_fwd_r.restype = ci
+        L.dstd_dstdgc_train_fwd_r.argtypes = [ci, vp, ci, ci, ci, ci, ci, ci, ctypes.POINTER(GCWeights), vp, vp, vp,
+                                              vp, sz, vp]
+        L.dstd_dstdgc_train_bwd_r.restype = ci
+        L.dstd_dstdgc_train_bwd_r.argtypes = [ci, vp, ci, ci, ci, ci, ci, ci, ctypes.POINTER(GCWeights), vp, vp, sz,
+                                              vp, vp, ctypes.POINTER(GCGrads), vp, vp, vp, sz, vp]
         L.dstd_block_train_fwd.restype = ci
         L.dstd_block_train_fwd.argtypes = [ctypes.POINTER(BlockParams), vp, ci, ci, ci, f32, vp, vp, sz, vp]
         L.dstd_block_train_bwd.restype = ci
@@ -214,7 +221,8 @@ TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_b
                  "dstd_model_train_workspace_bytes", "dstd_model_train_fwd", "dstd_model_train_bwd",
                  "dstd_loss_workspace_bytes", "dstd_mpjpe_fwd", "dstd_mpjpe_bwd", "dstd_frame_mpjpe",
                  "dstd_block_train_fwd_ex", "dstd_block_train_bwd_ex", "dstd_model_train_fwd_ex",
-                 "dstd_model_train_bwd_ex")
+                 "dstd_model_train_bwd_ex", "dstd_dstdgc_train_saved_bytes_r",
+                 "dstd_dstdgc_train_workspace_bytes_r", "dstd_dstdgc_train_fwd_r", "dstd_dstdgc_train_bwd_r")
 AUX_EXPORTS = ("dstd_ctg_workspace_bytes", "dstd_ctg_fwd", "dstd_ctg_bwd", "dstd_conv2d_workspace_bytes",
                "dstd_conv2d_fwd", "dstd_conv2d_bwd")
 

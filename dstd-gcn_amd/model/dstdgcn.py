@@ -198,14 +198,14 @@ def _op_train_fwd_native(mod, mode, x, A, alpha):
     L = native.lib()
     B, cin, T, V = x.shape
     dev = x.device
-    cout = mod.out_channels
+    cout, red = mod.out_channels, mod.red_channels
     y = torch.empty(B, cout, T, V, dtype=torch.float32, device=dev)
-    nbytes = L.dstd_dstdgc_train_saved_bytes(mode, B, cin, cout, T, V)
+    nbytes = L.dstd_dstdgc_train_saved_bytes_r(mode, B, cin, cout, T, V, red)
     saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    code = L.dstd_dstdgc_train_fwd(mode, native.ptr(x, "x"), B, cin, cout, T, V, native.gc_weights(mod),
-                                   native.ptr(A, "A"), native.ptr(alpha, "alpha_m"), native.ptr(y, "y"),
-                                   saved.data_ptr(), nbytes, native.stream_handle(dev))
-    native.check(code, "dstd_dstdgc_train_fwd")
+    code = L.dstd_dstdgc_train_fwd_r(mode, native.ptr(x, "x"), B, cin, cout, T, V, red, native.gc_weights(mod),
+                                     native.ptr(A, "A"), native.ptr(alpha, "alpha_m"), native.ptr(y, "y"),
+                                     saved.data_ptr(), nbytes, native.stream_handle(dev))
+    native.check(code, "dstd_dstdgc_train_fwd_r")
     return y, saved
 
 
@@ -397,8 +397,8 @@ class DSTDGC(_NativeModule):
         super().__init__()
         if mode not in ("spatial", "temporal"):
             raise AssertionError(f"mode must be spatial or temporal, got {mode}")
-        if red_channels != 2:
-            raise NotImplementedError("the MI355X kernels are built for red_channels == 2 (every shipped config)")
+        if not 1 <= red_channels <= 8:
+            raise NotImplementedError(f"red_channels={red_channels}: this build covers 1..8 (every shipped config uses 2)")
         self.in_channels = in_channels
         self.out_channels = out_channels
         self.ref_channels = ref_channels
@@ -444,6 +444,11 @@ class DSTDGC(_NativeModule):
         B, cin, T, V = x.shape
         dev = x.device
         mode = native.MODE_SPATIAL if self.mode == "spatial" else native.MODE_TEMPORAL
+        if self.red_channels != 2:
+            # the inference kernels carry exactly two P / Q channels; any other
+            # red_channels runs the training forward (generic in it, exact fp32,
+            # and the same function: DSTDGC has no BN or dropout)
+            return _op_train_fwd_native(self, mode, x, A, alpha)[0]
         y = torch.empty(B, self.out_channels, T, V, dtype=torch.float32, device=dev)
         nbytes = L.dstd_dstdgc_workspace_bytes(mode, B, cin, self.out_channels, T, V)
         ws = native.workspace(dev, nbytes)
@@ -948,7 +953,7 @@ def _(x, A, alpha, weights, uid):
     mod = _instance(uid)
     mode = native.MODE_SPATIAL if mod.mode == "spatial" else native.MODE_TEMPORAL
     B, cin, T, V = x.shape
-    nbytes = native.lib().dstd_dstdgc_train_saved_bytes(mode, B, cin, mod.out_channels, T, V)
+    nbytes = native.lib().dstd_dstdgc_train_saved_bytes_r(mode, B, cin, mod.out_channels, T, V, mod.red_channels)
     return x.new_empty(B, mod.out_channels, T, V), x.new_empty(nbytes, dtype=torch.uint8)
 
 
@@ -967,13 +972,14 @@ def _op_dstdgc_train_backward(x: torch.Tensor, A: torch.Tensor, alpha: torch.Ten
     dx = torch.zeros_like(x) if need_dx else x.new_empty(0)
     dA = torch.zeros_like(A)
     dalpha = torch.zeros_like(alpha)
-    ws = native.workspace(dev, L.dstd_dstdgc_train_workspace_bytes(mode, B, cin, cout, T, V))
-    code = L.dstd_dstdgc_train_bwd(mode, native.ptr(x, "x"), B, cin, cout, T, V, native.gc_weights(mod),
-                                   native.ptr(alpha, "alpha_m"), saved.data_ptr(), saved.numel(), native.ptr(dy, "dy"),
-                                   dx.data_ptr() if need_dx else None, native.gc_grads(mod, arena),
-                                   native.ptr(dA, "dA"), native.ptr(dalpha, "dalpha"), ws.data_ptr(), ws.numel(),
-                                   native.stream_handle(dev))
-    native.check(code, "dstd_dstdgc_train_bwd")
+    red = mod.red_channels
+    ws = native.workspace(dev, L.dstd_dstdgc_train_workspace_bytes_r(mode, B, cin, cout, T, V, red))
+    code = L.dstd_dstdgc_train_bwd_r(mode, native.ptr(x, "x"), B, cin, cout, T, V, red, native.gc_weights(mod),
+                                     native.ptr(alpha, "alpha_m"), saved.data_ptr(), saved.numel(),
+                                     native.ptr(dy, "dy"), dx.data_ptr() if need_dx else None,
+                                     native.gc_grads(mod, arena), native.ptr(dA, "dA"), native.ptr(dalpha, "dalpha"),
+                                     ws.data_ptr(), ws.numel(), native.stream_handle(dev))
+    native.check(code, "dstd_dstdgc_train_bwd_r")
     return dx, dA, dalpha, arena.buf
 
 

@@ -239,8 +239,8 @@ class DSTDGC(_Shadowed):
     def __init__(self, in_channels, out_channels, ref_channels, kpt_channels, red_channels=2, mode="spatial"):
         super().__init__()
         assert mode in {"spatial", "temporal"}
-        if red_channels != 2:
-            raise NotImplementedError("the MI355X kernels are built for red_channels == 2 (every shipped config)")
+        if not 1 <= red_channels <= 8:
+            raise NotImplementedError(f"red_channels={red_channels}: this build covers 1..8 (every shipped config uses 2)")
         self.in_channels = in_channels
         self.out_channels = out_channels
         self.ref_channels = ref_channels

@@ -25,7 +25,8 @@
  *   - Every call is enqueued on `stream` (hipStream_t passed as void*).
  *   - Return 0 on success, a positive hipError_t from a failed launch, or a
  *     negative DSTD_E* code for bad arguments.  dstd_error_string() names it.
- *   - Limits: T <= 128, V <= 32, channels <= 64, red_channels == 2.
+ *   - Limits: T <= 128, V <= 32, channels <= 64, red_channels == 2 (any other
+ *     red_channels: dstd_dstdgc_train_fwd_r in dstd_gcn_train.h).
  */
 #ifndef DSTD_GCN_H
 #define DSTD_GCN_H

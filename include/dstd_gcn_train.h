@@ -91,6 +91,20 @@ int dstd_dstdgc_train_bwd(int mode, const float* x, int B, int cin, int cout, in
                           const float* dy, float* dx, const dstd_gc_grads* g, float* dA, float* dalpha,
                           void* workspace, size_t workspace_bytes, void* stream);
 
+/* The same for any red_channels (the reference's DSTDGC(..., red_channels=R),
+ * model/dstdgcn.py:55-68: conv_m1 / conv_m2 have R output channels and conv_rm
+ * R*ref input channels; w->wm1/bm1/wm2/bm2/wrm sized accordingly).  The four
+ * entries above are these with red = 2.  Limits: 1 <= red <= 8. */
+size_t dstd_dstdgc_train_saved_bytes_r(int mode, int B, int cin, int cout, int T, int V, int red);
+size_t dstd_dstdgc_train_workspace_bytes_r(int mode, int B, int cin, int cout, int T, int V, int red);
+int dstd_dstdgc_train_fwd_r(int mode, const float* x, int B, int cin, int cout, int T, int V, int red,
+                            const dstd_gc_weights* w, const float* A, const float* alpha, float* y, void* saved,
+                            size_t saved_bytes, void* stream);
+int dstd_dstdgc_train_bwd_r(int mode, const float* x, int B, int cin, int cout, int T, int V, int red,
+                            const dstd_gc_weights* w, const float* alpha, const void* saved, size_t saved_bytes,
+                            const float* dy, float* dx, const dstd_gc_grads* g, float* dA, float* dalpha,
+                            void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- one DSTDGCB --------------------------------------------------------- */
 size_t dstd_block_train_saved_bytes(int B, int cin, int cout, int T, int V);
 size_t dstd_block_train_workspace_bytes(int B, int cin, int cout, int T, int V);

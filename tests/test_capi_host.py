@@ -47,7 +47,7 @@ def test_arithmetic_is_a_per_call_flag():
 def test_library_exports_every_training_header_symbol():
     L = native.lib()
     syms = header_symbols("dstd_gcn_train.h")
-    assert len(syms) == 20, syms
+    assert len(syms) == 24, syms
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(native.TRAIN_EXPORTS)
@@ -62,6 +62,14 @@ def test_train_sizes_and_argument_checks_without_gpu():
     assert L.dstd_model_train_workspace_bytes(8, 40, 23, 64, 5) > 0
     assert L.dstd_block_train_saved_bytes(4, 6, 64, 35, 22) > L.dstd_block_train_saved_bytes(4, 64, 64, 35, 22) // 2
     assert L.dstd_dstdgc_train_saved_bytes(1, 4, 64, 64, 35, 22) > 0
+    # red_channels: the red = 2 entry points are the _r ones at 2; more P / Q
+    # channels, more saved state (the tanh planes grow with red)
+    assert L.dstd_dstdgc_train_saved_bytes_r(1, 4, 64, 64, 35, 22, 2) == L.dstd_dstdgc_train_saved_bytes(
+        1, 4, 64, 64, 35, 22)
+    assert L.dstd_dstdgc_train_workspace_bytes_r(0, 4, 64, 64, 35, 22, 2) == L.dstd_dstdgc_train_workspace_bytes(
+        0, 4, 64, 64, 35, 22)
+    assert (L.dstd_dstdgc_train_saved_bytes_r(0, 4, 64, 64, 35, 22, 1) < L.dstd_dstdgc_train_saved_bytes_r(
+        0, 4, 64, 64, 35, 22, 2) < L.dstd_dstdgc_train_saved_bytes_r(0, 4, 64, 64, 35, 22, 5))
     assert L.dstd_loss_workspace_bytes() > 0
     # null pointers / bad shapes are rejected before any device work
     w = native.GCWeights()
@@ -69,6 +77,9 @@ def test_train_sizes_and_argument_checks_without_gpu():
     assert L.dstd_dstdgc_train_fwd(0, None, 4, 64, 64, 35, 22, w, None, None, None, None, 0, None) == -1
     assert L.dstd_dstdgc_train_bwd(0, None, 4, 64, 64, 35, 22, w, None, None, 0, None, None, g, None, None, None, 0,
                                    None) == -1
+    assert L.dstd_dstdgc_train_fwd_r(0, None, 4, 64, 64, 35, 22, 3, w, None, None, None, None, 0, None) == -1
+    assert L.dstd_dstdgc_train_bwd_r(0, None, 4, 64, 64, 35, 22, 3, w, None, None, 0, None, None, g, None, None,
+                                     None, 0, None) == -1
     assert L.dstd_block_train_fwd(None, None, 4, 35, 22, 0.1, None, None, 0, None) == -1
     assert L.dstd_model_train_fwd(None, None, 4, 0.1, 0.0, 0, None, None, 0, None) == -1
     assert L.dstd_model_train_bwd(None, None, 4, 0.0, 0, None, 0, None, None, None, 0, None) == -1

@@ -90,6 +90,64 @@ def test_dstdgc_op_backward(mode, cin, cout, T, V):
         assert rel(p.grad, sd64[name].grad) < 1e-4, name
 
 
+@pytest.mark.parametrize("mode", ["spatial", "temporal"])
+@pytest.mark.parametrize("red", [1, 3, 8])
+def test_dstdgc_op_red_channels(mode, red):
+    """DSTDGC(..., red_channels=R) (reference model/dstdgcn.py:55-68, any R):
+    R P / Q channels, conv_rm over R*ref.  No-grad forward and backward both
+    run the generic training kernels (the inference ones carry R = 2)."""
+    torch.manual_seed(red)
+    cin, cout, T, V = 32, 48, 35, 22
+    ref_c, kpt = (T, V) if mode == "spatial" else (V, T)
+    op = DSTDGC(cin, cout, ref_c, kpt, red_channels=red, mode=mode)
+    assert op.conv_m1.weight.shape[0] == red and op.conv_rm.weight.shape[1] == red * ref_c
+    randomise(op, 11 * red)
+    NN = V if mode == "spatial" else T
+    B = 3
+    x = torch.randn(B, cin, T, V)
+    A = 0.3 * torch.randn(1, NN, NN)
+    alpha = torch.tensor([0.6])
+    w = torch.randn(B, cout, T, V)
+    sd64 = {k: v.detach().double().requires_grad_(True) for k, v in op.state_dict().items()}
+    x64, A64, a64 = (t.double().requires_grad_(True) for t in (x, A, alpha))
+    y64 = O.dstdgc(x64, sd64, A64, a64.reshape(()), mode)
+    (y64 * w.double()).sum().backward()
+    op = op.to(DEV)
+    with torch.no_grad():
+        y0 = op(x.to(DEV), A.to(DEV), alpha.to(DEV))
+    assert rel(y0, y64) < 1e-4
+    xg, Ag, ag = (t.to(DEV).requires_grad_(True) for t in (x, A, alpha))
+    y = op(xg, Ag, ag)
+    (y * w.to(DEV)).sum().backward()
+    assert rel(y, y64) < 1e-4
+    assert rel(xg.grad, x64.grad) < 1e-4
+    assert rel(Ag.grad, A64.grad) < 1e-4
+    assert rel(ag.grad, a64.grad) < 1e-4
+    for name, p in op.named_parameters():
+        assert rel(p.grad, sd64[name].grad) < 1e-4, name
+
+
+@pytest.mark.parametrize("mode", ["spatial", "temporal"])
+def test_fast_dstdgc_op_red_channels(mode):
+    """The channels-last op (reference dstdgcn_fast.py:59-155) at R = 3."""
+    from model.dstdgcn_fast import DSTDGC as FastDSTDGC
+    torch.manual_seed(3)
+    cin, cout, T, V = 16, 24, 40, 23
+    ref_c, kpt = (T, V) if mode == "spatial" else (V, T)
+    op = FastDSTDGC(cin, cout, ref_c, kpt, red_channels=3, mode=mode)
+    randomise(op, 33)
+    NN = V if mode == "spatial" else T
+    x = torch.randn(2, T, V, cin)
+    A = 0.3 * torch.randn(1, NN, NN)
+    alpha = torch.tensor([0.6])
+    sd = {k: v.detach().double() for k, v in op.state_dict().items()}
+    y64 = O.fast_dstdgc(x.double(), sd, A.double(), alpha.double().reshape(()), mode)
+    op = op.to(DEV)
+    with torch.no_grad():
+        y = op(x.to(DEV), A.to(DEV), alpha.to(DEV))
+    assert rel(y, y64) < 1e-4
+
+
 # ---- DSTDGCB in train mode ---------------------------------------------------
 BLOCKS = [(6, 64, "h36m", 35, 22), (64, 64, "3dpw", 40, 23), (64, 3, "cmu", 35, 25),
           (64, 64, "h36m", 100, 22),  # T=100 ("50 in / 50 out"): generic kernels
