@@ -463,10 +463,27 @@ __device__ __forceinline__ float slice_sum(float v, float* lds, int V, int S) {
   return t;
 }
 
-__device__ __forceinline__ size_t bn_at(int row, int c, int v, int C, int T, int V) {
-  const int n = row / T, t = row - n * T;
-  return ((size_t)n * C + c) * T * V + (size_t)t * V + v;
-}
+// Rows are visited RB at a time with all RB loads issued before the first
+// use (a row-at-a-time loop pays one memory latency per row, ~8 per chunk at
+// the config-5 batch); the accumulation order is unchanged.
+constexpr int kBnRB = 8;
+struct BnRows {  // the rows row0, row0 + S, ... of one batch as (n, t)
+  int n[kBnRB], t[kBnRB];
+  bool ok[kBnRB];
+  __device__ BnRows(int row0, int r1, int S, int T) {
+    int nn = row0 / T, tt = row0 - nn * T;
+#pragma unroll
+    for (int j = 0; j < kBnRB; ++j) {
+      ok[j] = row0 + j * S < r1;
+      n[j] = nn, t[j] = tt;
+      tt += S;
+      while (tt >= T) tt -= T, ++nn;
+    }
+  }
+  __device__ size_t at(int j, int c, int v, int C, int T, int V) const {
+    return ((size_t)n[j] * C + c) * T * V + (size_t)t[j] * V + v;
+  }
+};
 
 // part: [splits][C*V][2] = (chunk mean, chunk M2)
 __global__ __launch_bounds__(kRedThreads) void k_bn_stats_part(BnFwd a, int B, int C, int T, int V, int splits,
@@ -478,15 +495,34 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_stats_part(BnFwd a, int B, i
   const int v = tid % V, s0 = tid / V;
   const int cnt = max(G.r1 - G.r0, 0);
   auto u_of = [&](size_t i) { return a.x2 ? a.x[i] + a.x2[i] : a.x[i]; };
+  // one batch covers the thread's rows when the chunk has <= RB * S rows:
+  // its values stay in registers for the second pass
+  const bool one = cnt <= kBnRB * G.S;
+  float keep[kBnRB];
   float s = 0.f;
   if (act)
-    for (int row = G.r0 + s0; row < G.r1; row += G.S) s += u_of(bn_at(row, c, v, C, T, V));
+    for (int row0 = G.r0 + s0; row0 < G.r1; row0 += kBnRB * G.S) {
+      const BnRows R(row0, G.r1, G.S, T);
+#pragma unroll
+      for (int j = 0; j < kBnRB; ++j) keep[j] = R.ok[j] ? u_of(R.at(j, c, v, C, T, V)) : 0.f;
+#pragma unroll
+      for (int j = 0; j < kBnRB; ++j)
+        if (R.ok[j]) s += keep[j];
+    }
   const float mean = cnt ? slice_sum(s, lds, V, G.S) / cnt : slice_sum(0.f, lds, V, G.S);
   float q = 0.f;
   if (act)
-    for (int row = G.r0 + s0; row < G.r1; row += G.S) {
-      const float d = u_of(bn_at(row, c, v, C, T, V)) - mean;
-      q = fmaf(d, d, q);
+    for (int row0 = G.r0 + s0; row0 < G.r1; row0 += kBnRB * G.S) {
+      const BnRows R(row0, G.r1, G.S, T);
+      float u[kBnRB];
+#pragma unroll
+      for (int j = 0; j < kBnRB; ++j) u[j] = one ? keep[j] : (R.ok[j] ? u_of(R.at(j, c, v, C, T, V)) : 0.f);
+#pragma unroll
+      for (int j = 0; j < kBnRB; ++j)
+        if (R.ok[j]) {
+          const float d = u[j] - mean;
+          q = fmaf(d, d, q);
+        }
     }
   const float m2 = slice_sum(q, lds, V, G.S);
   if (tid < V) {
@@ -552,17 +588,30 @@ __global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, 
   __syncthreads();
   const float w = a.prelu ? *a.prelu : 0.f;
   const size_t base = ((size_t)n * C + c) * T * V;
-  for (int e = tid; e < T * V; e += blockDim.x) {
-    const size_t i = base + e;
-    const int v = e % V;
-    const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
-    float z = fmaf(u, scl[v], shl[v]);
-    if (a.res) z += a.res[i];
-    if (a.prelu) {
-      a.zsave[i] = z;
-      a.out[i] = prelu_f(z, w);
-    } else {
-      a.out[i] = z;
+  constexpr int EB = 4;  // elements per thread per batch, loads issued first
+  for (int e0 = tid; e0 < T * V; e0 += EB * 256) {
+    float u[EB], r[EB];
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      const int e = e0 + j * 256;
+      const size_t i = base + e;
+      u[j] = e < T * V ? (a.x2 ? a.x[i] + a.x2[i] : a.x[i]) : 0.f;
+      r[j] = (e < T * V && a.res) ? a.res[i] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      const int e = e0 + j * 256;
+      if (e >= T * V) break;
+      const size_t i = base + e;
+      const int v = e % V;
+      float z = fmaf(u[j], scl[v], shl[v]);
+      if (a.res) z += r[j];
+      if (a.prelu) {
+        a.zsave[i] = z;
+        a.out[i] = prelu_f(z, w);
+      } else {
+        a.out[i] = z;
+      }
     }
   }
 }
@@ -580,15 +629,26 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_bwd_part(BnBwd a, int B, int
   const float mean = act ? a.mean[ch] : 0.f, rstd = act ? a.rstd[ch] : 0.f;
   float sd = 0.f, sdx = 0.f, sw = 0.f;
   if (act)
-    for (int row = G.r0 + s0; row < G.r1; row += G.S) {
-      const size_t i = bn_at(row, c, v, C, T, V);
-      const float d = a.dout[i];
-      // PReLU' (torch convention: the slope for z <= 0)
-      const float dz = (a.prelu && !(a.zsave[i] > 0.f)) ? w * d : d;
-      const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
-      sd += dz;
-      sdx = fmaf(dz, (u - mean) * rstd, sdx);
-      if (a.prelu) sw = fmaf(d, fminf(a.zsave[i], 0.f), sw);
+    for (int row0 = G.r0 + s0; row0 < G.r1; row0 += kBnRB * G.S) {
+      const BnRows R(row0, G.r1, G.S, T);
+      float dv[kBnRB], zv[kBnRB], uv[kBnRB];
+#pragma unroll
+      for (int j = 0; j < kBnRB; ++j) {
+        const size_t i = R.at(j, c, v, C, T, V);
+        dv[j] = R.ok[j] ? a.dout[i] : 0.f;
+        zv[j] = (R.ok[j] && a.prelu) ? a.zsave[i] : 0.f;
+        uv[j] = R.ok[j] ? (a.x2 ? a.x[i] + a.x2[i] : a.x[i]) : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < kBnRB; ++j) {
+        if (!R.ok[j]) continue;
+        const float d = dv[j];
+        // PReLU' (torch convention: the slope for z <= 0)
+        const float dz = (a.prelu && !(zv[j] > 0.f)) ? w * d : d;
+        sd += dz;
+        sdx = fmaf(dz, (uv[j] - mean) * rstd, sdx);
+        if (a.prelu) sw = fmaf(d, fminf(zv[j], 0.f), sw);
+      }
     }
   const float t0 = slice_sum(sd, lds, V, G.S);
   const float t1 = slice_sum(sdx, lds, V, G.S);
@@ -638,17 +698,32 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int
   const float w = a.prelu ? *a.prelu : 0.f;
   const float inv = 1.f / (B * T);
   const size_t base = ((size_t)n * C + c) * T * V;
-  for (int e = tid; e < T * V; e += blockDim.x) {
-    const size_t i = base + e;
-    const int v = e % V, ch = c * V + v;
-    const float d = a.dout[i];
-    const float dz = (a.prelu && !(a.zsave[i] > 0.f)) ? w * d : d;
-    const float u = a.x2 ? a.x[i] + a.x2[i] : a.x[i];
-    const float mean = a.mean[ch], rstd = a.rstd[ch];
-    const float xh = (u - mean) * rstd;
-    a.du[i] = a.use_running ? a.gamma[ch] * rstd * dz
-                            : a.gamma[ch] * rstd * (dz - sdl[v] * inv - xh * sxl[v] * inv);
-    if (a.dz_out) a.dz_out[i] = dz;
+  constexpr int EB = 4;  // elements per thread per batch, loads issued first
+  for (int e0 = tid; e0 < T * V; e0 += EB * 256) {
+    float dv[EB], zv[EB], uv[EB];
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      const int e = e0 + j * 256;
+      const size_t i = base + e;
+      const bool in = e < T * V;
+      dv[j] = in ? a.dout[i] : 0.f;
+      zv[j] = (in && a.prelu) ? a.zsave[i] : 0.f;
+      uv[j] = in ? (a.x2 ? a.x[i] + a.x2[i] : a.x[i]) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      const int e = e0 + j * 256;
+      if (e >= T * V) break;
+      const size_t i = base + e;
+      const int v = e % V, ch = c * V + v;
+      const float d = dv[j];
+      const float dz = (a.prelu && !(zv[j] > 0.f)) ? w * d : d;
+      const float mean = a.mean[ch], rstd = a.rstd[ch];
+      const float xh = (uv[j] - mean) * rstd;
+      a.du[i] = a.use_running ? a.gamma[ch] * rstd * dz
+                              : a.gamma[ch] * rstd * (dz - sdl[v] * inv - xh * sxl[v] * inv);
+      if (a.dz_out) a.dz_out[i] = dz;
+    }
   }
 }
 
