@@ -218,26 +218,29 @@ constexpr int kMaxSplit = 128;
 // ---------------------------------------------------------------------------
 // tanh outer difference
 // ---------------------------------------------------------------------------
-__global__ void k_tanh_outer_fwd(const float* P, const float* Q, PQView v, int R, int A, int NN, float* M) {
+__global__ void k_tanh_outer_fwd(const float* __restrict__ P, const float* __restrict__ Q, PQView v, int R, int A,
+                                 int NN, float* __restrict__ M) {
   // one workgroup per (n, r, a); M block [NN][NN]
   const int blk = blockIdx.x;
   const int n = blk / (R * A), ra = blk - n * R * A, r = ra / A, a = ra - r * A;
   const float* p = P + n * v.sn + r * v.sr + a * v.sa;
   const float* q = Q + n * v.sn + r * v.sr + a * v.sa;
   float* m = M + (size_t)blk * NN * NN;
+#pragma unroll 4
   for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
     const int i = e / NN, j = e - i * NN;
     m[e] = tanhf(p[i * v.si] - q[j * v.si]);
   }
 }
 
-__global__ void k_tanh_outer_bwd(const float* M, const float* dM, PQView v, int R, int A, int NN, float* dP,
-                                 float* dQ) {
+__global__ void k_tanh_outer_bwd(const float* __restrict__ M, const float* __restrict__ dM, PQView v, int R, int A,
+                                 int NN, float* __restrict__ dP, float* __restrict__ dQ) {
   extern __shared__ float dz[];  // [NN][NN+1]
   const int blk = blockIdx.x;
   const int n = blk / (R * A), ra = blk - n * R * A, r = ra / A, a = ra - r * A;
   const float* m = M + (size_t)blk * NN * NN;
   const float* dm = dM + (size_t)blk * NN * NN;
+#pragma unroll 4
   for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
     const int i = e / NN, j = e - i * NN;
     const float t = m[e];
@@ -261,8 +264,10 @@ __global__ void k_tanh_outer_bwd(const float* M, const float* dM, PQView v, int 
 
 // Fused adjacency backward, stage 1: workgroup (row a, sample chunk); each
 // thread owns entries ij and walks the chunk's samples (no atomics).
-__global__ __launch_bounds__(256) void k_adj_bwd_part(float* dD, const float* E, const float* alpha, int B, int A,
-                                                      int NN2, int nch, float* pdA, float* pbr, float* pal) {
+__global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, const float* __restrict__ E,
+                                                      const float* __restrict__ alpha, int B, int A, int NN2, int nch,
+                                                      float* __restrict__ pdA, float* __restrict__ pbr,
+                                                      float* __restrict__ pal) {
   __shared__ float red[4];
   const int a = blockIdx.x, ch = blockIdx.y;
   const int per = (B + nch - 1) / nch, n0 = ch * per, n1 = min(B, n0 + per);
@@ -270,12 +275,21 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* dD, const float* E,
   float sbr = 0.f, sal = 0.f;
   for (int ij = threadIdx.x; ij < NN2; ij += blockDim.x) {
     float sa = 0.f;
-    for (int n = n0; n < n1; ++n) {
-      const size_t i = ((size_t)n * A + a) * NN2 + ij;
-      const float d = dD[i];
-      sa += d;
-      sal = fmaf(d, E[i], sal);
-      dD[i] = al * d;
+    for (int nb = n0; nb < n1; nb += 4) {  // 4 samples' loads in flight, then use in order
+      float dv[4], ev[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const size_t i = ((size_t)(nb + u) * A + a) * NN2 + ij;
+        dv[u] = nb + u < n1 ? dD[i] : 0.f;
+        ev[u] = nb + u < n1 ? E[i] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (nb + u >= n1) break;
+        sa += dv[u];
+        sal = fmaf(dv[u], ev[u], sal);
+        dD[((size_t)(nb + u) * A + a) * NN2 + ij] = al * dv[u];
+      }
     }
     pdA[((size_t)ch * A + a) * NN2 + ij] = sa;
     sbr += sa;
@@ -290,9 +304,10 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* dD, const float* E,
 
 // stage 2: blocks [0, cdiv(NN2,16)) finish dA (16 outputs x 16 slices over the
 // A*nch partial rows); the last block finishes dbrm and dalpha.
-__global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* pdA, const float* pbr, const float* pal, int A,
-                                                        int NN2, int nch, float* dA, float* dbrm, float* dalpha,
-                                                        int assign_dA) {
+__global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict__ pdA, const float* __restrict__ pbr,
+                                                        const float* __restrict__ pal, int A, int NN2, int nch,
+                                                        float* __restrict__ dA, float* __restrict__ dbrm,
+                                                        float* __restrict__ dalpha, int assign_dA) {
   __shared__ float lds[16][17];
   __shared__ float red[4];
   const int nblk = (NN2 + 15) / 16;
@@ -301,6 +316,7 @@ __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* pdA, const 
     const int ij = blockIdx.x * 16 + el;
     float s = 0.f;
     if (ij < NN2)
+#pragma unroll 8
       for (int r = sl; r < A * nch; r += 16) s += pdA[(size_t)r * NN2 + ij];
     lds[sl][el] = s;
     __syncthreads();
