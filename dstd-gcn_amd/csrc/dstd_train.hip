@@ -201,6 +201,7 @@ __global__ __launch_bounds__(256) void k_gemm_finish(Gemm g, int nsplit, const f
   const int MN = g.M * g.N;
   float s = 0.f;
   if (idx < MN)
+#pragma unroll 8
     for (int z = sl; z < nsplit; z += 16) s += partial[(size_t)z * MN + idx];
   red[sl][el] = s;
   __syncthreads();
@@ -378,8 +379,11 @@ __global__ void k_red_part_j(const float* X, int M, int nb, int nj, long long sb
   const long long tot = (long long)nb * nj, per = (tot + splits - 1) / splits;
   const long long lo = sp * per, hi = min(tot, lo + per);
   float s = 0.f;
-  for (long long e = lo + threadIdx.x; e < hi; e += blockDim.x) {
-    const long long b = e / nj, j = e - b * nj;
+  // int index math (tot < 2^31 here): a 64-bit divide per element costs more
+  // than the load it addresses
+#pragma unroll 4
+  for (int e = (int)lo + threadIdx.x; e < (int)hi; e += blockDim.x) {
+    const int b = e / nj, j = e - b * nj;
     s += X[b * sb + m * sm + j * sj];
   }
   s = block_sum(s, red);
@@ -393,9 +397,11 @@ __global__ void k_red_part_m(const float* X, int M, int nb, int nj, long long sb
   const long long tot = (long long)nb * nj, per = (tot + splits - 1) / splits;
   const long long lo = sp * per, hi = min(tot, lo + per);
   float s = 0.f;
+  int b = (int)(lo / nj), j = (int)(lo - (long long)b * nj);  // (b, j) advance by carry
+#pragma unroll 4
   for (long long e = lo; e < hi; ++e) {
-    const long long b = e / nj, j = e - b * nj;
     s += X[b * sb + m + j * sj];
+    if (++j == nj) j = 0, ++b;
   }
   part[(size_t)sp * M + m] = s;
 }
@@ -407,6 +413,7 @@ __global__ __launch_bounds__(256) void k_red_finish(const float* part, int M, in
   const int m = blockIdx.x * 16 + el;
   float s = 0.f;
   if (m < M)
+#pragma unroll 4
     for (int sp = sl; sp < splits; sp += 16) s += part[(size_t)sp * M + m];
   red[sl][el] = s;
   __syncthreads();
@@ -971,6 +978,7 @@ size_t reduce_scratch_floats(int M) { return (size_t)kRedSplit * M; }
 hipError_t reduce_rows(const float* X, int M, int nb, int nj, long long sb, long long sm, long long sj, float* out,
                        float scale, float* scratch, hipStream_t s) {
   const long long tot = (long long)nb * nj;
+  if (tot >= (1LL << 31)) return hipErrorInvalidValue;  // k_red_part_j indexes in int
   const bool by_m = sm == 1 && M > 1;
   // ~1024 workgroups, each with a useful amount of work
   const long long want = by_m ? std::min(kRedSplit, 1024 / cdiv(M, kRedThreads)) : std::min(kRedSplit, std::max(1, 1024 / M));
