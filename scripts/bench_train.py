@@ -6,6 +6,14 @@ train-mode forward of the batch and of its time reversal, two mpjpe losses,
 native backward, Adam.  Prints one JSON line per batch size.
 
   python scripts/bench_train.py [--batch 32 256] [--steps 20] [--warmup 5]
+
+Data parallel (32 sequences per GPU on 8 GPUs), one
+process per GPU over RCCL, the engine's step (dstd_dist: weights broadcast
+once, one flat all-reduce of the gradient arena per step before Adam);
+the time is the max over ranks, the value the sequences of all ranks:
+
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+      scripts/bench_train.py --batch 32
 """
 import argparse
 import json
@@ -19,6 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "dstd-gcn_amd")):
     sys.path.insert(0, p)
 
+import dstd_dist  # noqa: E402
 from engine import mpjpe_error_3d  # noqa: E402
 from model import get_model  # noqa: E402
 
@@ -29,7 +38,15 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     a = ap.parse_args()
-    dev = torch.device("cuda:0")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1 or "LOCAL_RANK" in os.environ:
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", torch.cuda.current_device())
+    distributed = torch.distributed.is_available() and torch.distributed.is_initialized()
     opts = dict(input_channels=6, input_time_frame=10, output_time_frame=30, st_gcnn_dropout=0.0,
                  joints_to_consider=23, num_feature=64, num_layers=5, layout="3dpw")
     for B in a.batch:
@@ -37,7 +54,9 @@ def main():
         m = get_model("dstdgcn", dstdgcn=opts).to(dev).train()
         m._dstd_inplace_grads = True  # what engine.PredictionEngine.train opts into (prediction.py:161)
         opt = torch.optim.Adam(m.parameters(), lr=3e-3)
-        g = torch.Generator().manual_seed(1234)
+        if distributed:
+            dstd_dist.broadcast_module(m)
+        g = torch.Generator().manual_seed(1234 + rank)  # each rank its own shard of sequences
         seq = torch.randn(B, 40, 69, generator=g)
         inp = seq.clone()
         inp[:, 10:] = inp[:, 9:10]
@@ -52,12 +71,16 @@ def main():
             loss = (mpjpe_error_3d(out, seq) + mpjpe_error_3d(out_i, seq_inv)) / 2
             opt.zero_grad()
             loss.backward()
+            if distributed:
+                dstd_dist.allreduce_grads(m.parameters())
             opt.step()
             return loss
 
         for _ in range(a.warmup):
             step()
         torch.cuda.synchronize()
+        if distributed:
+            torch.distributed.barrier()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         e0.record()
@@ -67,11 +90,20 @@ def main():
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / a.steps * 1e3
         ms = e0.elapsed_time(e1) / a.steps
-        print(json.dumps({"metric": "train_sequences_per_sec", "value": round(B / ms * 1e3, 1),
-                          "unit": "sequences/s", "ms_per_step": round(ms, 3), "host_ms_per_step": round(wall, 3),
-                          "batch": B, "steps": a.steps, "dtype": "f32", "loss": round(float(loss), 4),
-                          "config": {"workload": "3dpw T=40 V=23, 2 fwd + 1 bwd + Adam", "inverse": True}}),
-              flush=True)
+        if distributed:  # the slowest rank sets the step
+            t = torch.tensor([ms, wall], device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            ms, wall = float(t[0]), float(t[1])
+        if rank == 0:
+            print(json.dumps({"metric": "train_sequences_per_sec", "value": round(world * B / ms * 1e3, 1),
+                              "unit": "sequences/s", "ms_per_step": round(ms, 3), "host_ms_per_step": round(wall, 3),
+                              "batch": B, "n_gpus": world, "steps": a.steps, "dtype": "f32",
+                              "loss": round(float(loss.detach()), 4), "scaling": "weak",
+                              "config": {"workload": "3dpw T=40 V=23, 2 fwd + 1 bwd + Adam", "inverse": True,
+                                         "parallelism": f"dp{world}"}}),
+                  flush=True)
+    if distributed:
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":
