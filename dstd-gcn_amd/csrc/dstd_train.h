@@ -137,6 +137,11 @@ struct BnFwd {
   float* rstd;
   int use_running = 0;  // eval-mode BN: mean / rstd from the running stats, no update
   int cv = 0;           // (set by bn_train_fwd: C * V)
+  // groups > 1: the batch is `groups` independent BN batches of B / groups
+  // samples (statistics per group; the running statistics take the groups'
+  // updates in order; mean / rstd hold groups x C*V) -- the engine's forward
+  // of a batch and of its time reversal as ONE launch sequence
+  int groups = 1;
 };
 hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s);
 
@@ -158,8 +163,9 @@ struct BnBwd {
   float* dgamma;
   float* dbeta;
   int use_running = 0;  // mean / rstd are constants (eval-mode BN): du = gamma * rstd * dz
+  int groups = 1;       // as BnFwd::groups (the forward's grouping)
 };
-// scratch (both directions) >= bn_scratch_floats(B, C, T, V)
+// scratch (both directions) >= bn_scratch_floats(B, C, T, V) (any groups)
 size_t bn_scratch_floats(int B, int C, int T, int V);
 hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scratch, float* dprelu, hipStream_t s);
 

@@ -464,13 +464,14 @@ __global__ void k_acc_mul(const float* a, const float* b, const float* c, float*
 // s + S, ... so a wave reads runs of V consecutive floats; slice sums are
 // combined in LDS in a fixed order (deterministic).
 // ---------------------------------------------------------------------------
-struct BnChunk {
+struct BnChunk {  // blockIdx.y = group * splits + split; rows of the chunk [r0, r1) (absolute)
   int V, S, rows, r0, r1;
-  __device__ BnChunk(int V_, int B, int T, int splits)
-      : V(V_), S(kRedThreads / V_), rows(B * T) {
+  __device__ BnChunk(int V_, int B, int T, int splits, int groups)
+      : V(V_), S(kRedThreads / V_), rows(B / groups * T) {
+    const int g = blockIdx.y / splits, sp = blockIdx.y - g * splits;
     const int per = (rows + splits - 1) / splits;
-    r0 = blockIdx.y * per;
-    r1 = min(rows, r0 + per);
+    r0 = g * rows + sp * per;
+    r1 = g * rows + min(rows, sp * per + per);
   }
 };
 
@@ -513,7 +514,7 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_stats_part(BnFwd a, int B, i
                                                                float* part) {
   __shared__ float lds[kRedThreads];
   const int c = blockIdx.x, tid = threadIdx.x;
-  const BnChunk G(V, B, T, splits);
+  const BnChunk G(V, B, T, splits, a.groups);
   const bool act = tid < G.S * V;
   const int v = tid % V, s0 = tid / V;
   const int cnt = max(G.r1 - G.r0, 0);
@@ -561,13 +562,15 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_stats_part(BnFwd a, int B, i
 // mean / rstd and updates the running statistics), then normalises the
 // sample's contiguous [T][V] plane of channel c.
 constexpr int kBnMaxV = 64;
-__device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows, int splits, const float* part,
+// rows: rows per group; g: the group whose split partials merge
+__device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows, int splits, const float* part, int g,
                                                float& mean, float& rstd, bool store) {
   if (a.use_running) {
     mean = a.running_mean[ch];
     rstd = 1.f / sqrtf(a.running_var[ch] + a.eps);
   } else {
     const int per = (rows + splits - 1) / splits;
+    part += (size_t)g * splits * a.cv * 2;
     float m = 0.f;
     for (int sp = 0; sp < splits; ++sp) {
       const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
@@ -591,8 +594,8 @@ __device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows,
     }
   }
   if (store) {
-    a.mean[ch] = mean;
-    a.rstd[ch] = rstd;
+    a.mean[g * a.cv + ch] = mean;
+    a.rstd[g * a.cv + ch] = rstd;
   }
 }
 
@@ -602,8 +605,17 @@ __global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, 
   const int c = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
   if (tid < V) {
     const int ch = c * V + tid;
+    const int Bg = B / a.groups, g = n / Bg;
     float mean, rstd;
-    bn_merge_stats(a, ch, B * T, splits, part, mean, rstd, n == 0);
+    // workgroup (c, 0) stores every group's mean / rstd and applies the
+    // groups' running-statistics updates in group order
+    if (n == 0)
+      for (int gg = 1; gg < a.groups; ++gg) {
+        float m_, r_;
+        bn_merge_stats(a, ch, Bg * T, splits, part, gg - 1, m_, r_, true);
+      }
+    bn_merge_stats(a, ch, Bg * T, splits, part, n == 0 ? a.groups - 1 : g, mean, rstd, n == 0);
+    if (n == 0 && a.groups > 1) bn_merge_stats(a, ch, Bg * T, splits, part, 0, mean, rstd, false);
     const float sc = rstd * a.gamma[ch];
     scl[tid] = sc;
     shl[tid] = a.beta[ch] - mean * sc;
@@ -644,12 +656,13 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_bwd_part(BnBwd a, int B, int
                                                              float* part, float* wpart) {
   __shared__ float lds[kRedThreads];
   const int c = blockIdx.x, tid = threadIdx.x;
-  const BnChunk G(V, B, T, splits);
+  const BnChunk G(V, B, T, splits, a.groups);
   const bool act = tid < G.S * V;
   const int v = tid % V, s0 = tid / V;
   const int ch = c * V + v;
   const float w = a.prelu ? *a.prelu : 0.f;
-  const float mean = act ? a.mean[ch] : 0.f, rstd = act ? a.rstd[ch] : 0.f;
+  const int grp = blockIdx.y / splits;
+  const float mean = act ? a.mean[grp * C * V + ch] : 0.f, rstd = act ? a.rstd[grp * C * V + ch] : 0.f;
   float sd = 0.f, sdx = 0.f, sw = 0.f;
   if (act)
     for (int row0 = G.r0 + s0; row0 < G.r1; row0 += kBnRB * G.S) {
@@ -696,30 +709,40 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int
   __shared__ float sdl[kBnMaxV], sxl[kBnMaxV], red[kRedThreads / 64];
   const int c = blockIdx.x, n = blockIdx.y, tid = threadIdx.x;
   const int CV = C * V;
+  const int Bg = B / a.groups, grp = n / Bg;
   if (tid < V) {
     const int ch = c * V + tid;
-    float sd = 0.f, sdx = 0.f;
-    for (int sp = 0; sp < splits; ++sp) {
-      const float* p = part + ((size_t)sp * CV + ch) * 2;
-      sd += p[0];
-      sdx += p[1];
+    // group sums; workgroup (c, 0) adds every group's into dgamma / dbeta
+    float tb = 0.f, tg = 0.f;
+    for (int gg = 0; gg < a.groups; ++gg) {
+      if (n != 0 && gg != grp) continue;
+      float sd = 0.f, sdx = 0.f;
+      for (int sp = 0; sp < splits; ++sp) {
+        const float* p = part + ((size_t)(gg * splits + sp) * CV + ch) * 2;
+        sd += p[0];
+        sdx += p[1];
+      }
+      if (gg == grp) {
+        sdl[tid] = sd;
+        sxl[tid] = sdx;
+      }
+      tb += sd;
+      tg += sdx;
     }
-    sdl[tid] = sd;
-    sxl[tid] = sdx;
     if (n == 0) {
-      a.dbeta[ch] += sd;
-      a.dgamma[ch] += sdx;
+      a.dbeta[ch] += tb;
+      a.dgamma[ch] += tg;
     }
   }
   if (a.prelu && c == 0 && n == 0) {  // uniform per workgroup: block_sum's barriers are safe
     float t = 0.f;
-    for (int e = tid; e < splits * C; e += blockDim.x) t += wpart[e];
+    for (int e = tid; e < splits * a.groups * C; e += blockDim.x) t += wpart[e];
     t = block_sum(t, red);
     if (tid == 0) dprelu[0] += t;
   }
   __syncthreads();
   const float w = a.prelu ? *a.prelu : 0.f;
-  const float inv = 1.f / (B * T);
+  const float inv = 1.f / (Bg * T);
   const size_t base = ((size_t)n * C + c) * T * V;
   constexpr int EB = 4;  // elements per thread per batch, loads issued first
   for (int e0 = tid; e0 < T * V; e0 += EB * 256) {
@@ -741,7 +764,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int
       const int v = e % V, ch = c * V + v;
       const float d = dv[j];
       const float dz = (a.prelu && !(zv[j] > 0.f)) ? w * d : d;
-      const float mean = a.mean[ch], rstd = a.rstd[ch];
+      const float mean = a.mean[grp * CV + ch], rstd = a.rstd[grp * CV + ch];
       const float xh = (uv[j] - mean) * rstd;
       a.du[i] = a.use_running ? a.gamma[ch] * rstd * dz
                               : a.gamma[ch] * rstd * (dz - sdl[v] * inv - xh * sxl[v] * inv);
@@ -1015,27 +1038,30 @@ hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStre
 
 int bn_splits(int B, int T) { return std::max(1, std::min(16, cdiv(B * T, 64))); }
 
-size_t bn_scratch_floats(int B, int C, int T, int V) {
-  return (size_t)bn_splits(B, T) * C * V * 2 + (size_t)bn_splits(B, T) * C + (size_t)2 * C * V;
+size_t bn_scratch_floats(int B, int C, int T, int V) {  // sized for up to 2 groups
+  return 2 * ((size_t)bn_splits(B, T) * C * V * 2 + (size_t)bn_splits(B, T) * C) + (size_t)2 * C * V;
 }
 
 hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s) {
   if (V > kBnMaxV) return hipErrorInvalidValue;
   if (a.use_running && (!a.running_mean || !a.running_var)) return hipErrorInvalidValue;
-  const int splits = bn_splits(B, T);
+  if (a.groups < 1 || a.groups > 2 || B % a.groups) return hipErrorInvalidValue;
+  const int splits = bn_splits(B / a.groups, T);
   BnFwd b = a;
   b.cv = C * V;
-  if (!a.use_running) k_bn_stats_part<<<dim3(C, splits), kRedThreads, 0, s>>>(b, B, C, T, V, splits, scratch);
+  if (!a.use_running)
+    k_bn_stats_part<<<dim3(C, splits * a.groups), kRedThreads, 0, s>>>(b, B, C, T, V, splits, scratch);
   k_bn_apply_merged<<<dim3(C, B), 256, 0, s>>>(b, B, C, T, V, splits, scratch);
   return hipGetLastError();
 }
 
 hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scratch, float* dprelu, hipStream_t s) {
   if (V > kBnMaxV) return hipErrorInvalidValue;
-  const int splits = bn_splits(B, T);
+  if (a.groups < 1 || a.groups > 2 || B % a.groups) return hipErrorInvalidValue;
+  const int splits = bn_splits(B / a.groups, T);
   float* part = scratch;
-  float* wpart = part + (size_t)splits * C * V * 2;
-  k_bn_bwd_part<<<dim3(C, splits), kRedThreads, 0, s>>>(a, B, C, T, V, splits, part, wpart);
+  float* wpart = part + (size_t)a.groups * splits * C * V * 2;
+  k_bn_bwd_part<<<dim3(C, splits * a.groups), kRedThreads, 0, s>>>(a, B, C, T, V, splits, part, wpart);
   k_bn_bwd_apply_merged<<<dim3(C, B), 256, 0, s>>>(a, B, C, T, V, splits, part, wpart, dprelu);
   return hipGetLastError();
 }

@@ -27,6 +27,7 @@ constexpr int kMaxT = 128;  // same envelope as the forward (dstd_capi.hip)
 constexpr int kMaxV = 32;
 constexpr int kMaxC = 64;
 constexpr int kMaxRed = 8;  // red_channels of one DSTDGC (P / Q channels each)
+constexpr unsigned kTrainFlags = DSTD_TRAIN_RUNNING_STATS | DSTD_TRAIN_PAIRED;
 
 struct Carver {
   char* base;
@@ -300,13 +301,13 @@ void carve_block_saved(Carver& cv, BlockSaved& s, int B, int cin, int cout, int 
   s.ysp = cv.take(act);
   s.z = cv.take(act);
   s.h = cv.take(act);
-  s.mean = cv.take(cout * V);
-  s.rstd = cv.take(cout * V);
+  s.mean = cv.take(2 * cout * V);  // per BN group (DSTD_TRAIN_PAIRED: 2)
+  s.rstd = cv.take(2 * cout * V);
   const bool res = cin != cout;
   s.rc = res ? cv.take(act) : nullptr;
   s.r = res ? cv.take(act) : nullptr;
-  s.rmean = res ? cv.take(cout * V) : nullptr;
-  s.rrstd = res ? cv.take(cout * V) : nullptr;
+  s.rmean = res ? cv.take(2 * cout * V) : nullptr;
+  s.rrstd = res ? cv.take(2 * cout * V) : nullptr;
   s.red = cv.take(bn_scratch_floats(B, cout, T, V));
 }
 
@@ -366,7 +367,8 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.out = S.r;
     rb.mean = S.rmean;
     rb.rstd = S.rrstd;
-    rb.use_running = run;
+    rb.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
+  rb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
     DSTD_TRYH(bn_train_fwd(rb, B, cout, T, V, S.red, s));
     r = S.r;
   }
@@ -384,7 +386,8 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.zsave = S.z;
   bb.mean = S.mean;
   bb.rstd = S.rstd;
-  bb.use_running = run;
+  bb.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
+  bb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
   DSTD_TRYH(bn_train_fwd(bb, B, cout, T, V, S.red, s));
   return op_fwd(gt, S.h, &p->conv_t, p->A_t, nullptr, p->R_t, p->alpha_tm, y, 0.f, S.op[2], s);  // :156-162
 }
@@ -414,7 +417,8 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.dz_out = W.dr;
   bb.dgamma = g->bn.weight;
   bb.dbeta = g->bn.bias;
-  bb.use_running = run;
+  bb.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
+  bb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
   DSTD_TRYH(bn_train_bwd(bb, B, cout, T, V, W.op.red, g->prelu, s));
   if (res) {
     BnBwd rb;
@@ -426,7 +430,8 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.du = W.drc;
     rb.dgamma = g->res_bn.weight;
     rb.dbeta = g->res_bn.bias;
-    rb.use_running = run;
+    rb.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
+  rb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
     DSTD_TRYH(bn_train_bwd(rb, B, cout, T, V, W.op.red, nullptr, s));
     if (dx_extra) return hipErrorInvalidValue;
     DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, W.op.red, s,
@@ -459,15 +464,15 @@ void carve_model_saved(Carver& cv, ModelSaved& s, int B, int T, int V, int C, in
   s.y0 = cv.take(act);
   s.z0 = cv.take(act);
   s.hp0 = cv.take(act);
-  s.m0 = cv.take(C * V);
-  s.r0 = cv.take(C * V);
+  s.m0 = cv.take(2 * C * V);  // per BN group (DSTD_TRAIN_PAIRED: 2)
+  s.r0 = cv.take(2 * C * V);
   for (int i = 0; i <= L; ++i) s.h[i] = cv.take(act);
   for (int i = 0; i < L; ++i) {
     carve_block_saved(cv, s.enc[i], B, C, C, T, V);
     s.yb[i] = cv.take(act);
     s.ze[i] = cv.take(act);
-    s.me[i] = cv.take(C * V);
-    s.re[i] = cv.take(C * V);
+    s.me[i] = cv.take(2 * C * V);
+    s.re[i] = cv.take(2 * C * V);
   }
   carve_block_saved(cv, s.st_out, B, C, 3, T, V);
   s.o = cv.take((size_t)B * 3 * T * V);
@@ -589,14 +594,15 @@ size_t dstd_block_train_workspace_bytes(int B, int cin, int cout, int T, int V) 
 int dstd_block_train_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum,
                             float* y, void* saved, size_t saved_bytes, void* stream, unsigned flags) {
   StreamDeviceGuard dev_guard_(stream);
-  if (!block_ok(p) || !x || !y || !saved || (flags & ~DSTD_TRAIN_RUNNING_STATS)) return DSTD_EINVAL;
+  if (!block_ok(p) || !x || !y || !saved || (flags & ~kTrainFlags)) return DSTD_EINVAL;
+  if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
   if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
   if (!shape_ok(B, T, V)) return DSTD_ELIMIT;
   if (saved_bytes < dstd_block_train_saved_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
   Carver cv{(char*)saved};
   BlockSaved S;
   carve_block_saved(cv, S, B, p->cin, p->cout, T, V);
-  DSTD_TRY(block_fwd(p, x, B, T, V, momentum, y, S, (hipStream_t)stream, (flags & DSTD_TRAIN_RUNNING_STATS) != 0));
+  DSTD_TRY(block_fwd(p, x, B, T, V, momentum, y, S, (hipStream_t)stream, (int)flags));
   return DSTD_OK;
 }
 
@@ -610,7 +616,8 @@ int dstd_block_train_bwd_ex(const dstd_block_params* p, const float* x, int B, i
                             void* workspace, size_t workspace_bytes, void* stream, unsigned flags) {
   StreamDeviceGuard dev_guard_(stream);
   if (!block_ok(p) || !block_grads_ok(p, g) || !x || !dy || !saved || !workspace) return DSTD_EINVAL;
-  if (flags & ~DSTD_TRAIN_RUNNING_STATS) return DSTD_EINVAL;
+  if (flags & ~kTrainFlags) return DSTD_EINVAL;
+  if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
   if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
   if (!shape_ok(B, T, V)) return DSTD_ELIMIT;
   if (saved_bytes < dstd_block_train_saved_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
@@ -621,7 +628,7 @@ int dstd_block_train_bwd_ex(const dstd_block_params* p, const float* x, int B, i
   Carver cw{(char*)workspace};
   BlockWs W;
   carve_block_ws(cw, W, B, T, V, {{p->cin, p->cout}});
-  DSTD_TRY(block_bwd(p, x, B, T, V, S, dy, dx, g, W, (hipStream_t)stream, (flags & DSTD_TRAIN_RUNNING_STATS) != 0));
+  DSTD_TRY(block_bwd(p, x, B, T, V, S, dy, dx, g, W, (hipStream_t)stream, (int)flags));
   return DSTD_OK;
 }
 
@@ -652,8 +659,9 @@ int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, f
                             unsigned flags) {
   StreamDeviceGuard dev_guard_(stream);
   if (!model_ok(p) || !x || !y || !saved || !(dropout_p >= 0.f && dropout_p < 1.f)) return DSTD_EINVAL;
-  if (flags & ~DSTD_TRAIN_RUNNING_STATS) return DSTD_EINVAL;
-  const int run = (flags & DSTD_TRAIN_RUNNING_STATS) != 0;
+  if (flags & ~kTrainFlags) return DSTD_EINVAL;
+  if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
+  const int run = (int)flags;
   const int T = p->T, V = p->V, C = p->num_feature, L = p->num_layers;
   if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
   if (!shape_ok(B, T, V) || !ch_ok(C)) return DSTD_ELIMIT;
@@ -679,7 +687,8 @@ int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, f
   b0.zsave = S.z0;
   b0.mean = S.m0;
   b0.rstd = S.r0;
-  b0.use_running = run;
+  b0.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
+  b0.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
   DSTD_TRY(bn_train_fwd(b0, B, C, T, V, S.red, s));
   if (dropout_p > 0.f) DSTD_TRY(dropout(S.hp0, S.h[0], act, dropout_p, seed, s));  // do_in
   for (int i = 0; i < L; ++i) {                                                  // :310-311
@@ -698,7 +707,8 @@ int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, f
     be.zsave = S.ze[i];
     be.mean = S.me[i];
     be.rstd = S.re[i];
-    be.use_running = run;
+    be.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
+  be.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
     DSTD_TRY(bn_train_fwd(be, B, C, T, V, S.red, s));
   }
   DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s, run));  // :313
@@ -718,8 +728,9 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
   StreamDeviceGuard dev_guard_(stream);
   if (!model_ok(p) || !g || !x || !dy || !saved || !workspace || !(dropout_p >= 0.f && dropout_p < 1.f))
     return DSTD_EINVAL;
-  if (flags & ~DSTD_TRAIN_RUNNING_STATS) return DSTD_EINVAL;
-  const int run = (flags & DSTD_TRAIN_RUNNING_STATS) != 0;
+  if (flags & ~kTrainFlags) return DSTD_EINVAL;
+  if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
+  const int run = (int)flags;
   const int T = p->T, V = p->V, C = p->num_feature, L = p->num_layers;
   if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
   if (!shape_ok(B, T, V) || !ch_ok(C)) return DSTD_ELIMIT;
@@ -755,7 +766,8 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
     be.du = W.du;
     be.dgamma = g->enc_bn[i].weight;
     be.dbeta = g->enc_bn[i].bias;
-    be.use_running = run;
+    be.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
+  be.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
     DSTD_TRY(bn_train_bwd(be, B, C, T, V, W.blk.op.red, g->enc_prelu[i], s));
     // u = block(h) + h: dh = du (identity path) + block backward
     DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s, run, true, W.du));
@@ -773,7 +785,8 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
   b0.du = W.du;
   b0.dgamma = g->bn_in.weight;
   b0.dbeta = g->bn_in.bias;
-  b0.use_running = run;
+  b0.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
+  b0.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
   DSTD_TRY(bn_train_bwd(b0, B, C, T, V, W.blk.op.red, g->prelu, s));
   DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, dx ? W.dX0 : nullptr, &g->st_in, W.blk, s, run, true));
   if (dx) DSTD_TRY(prep_nctv_bwd(W.dX0, dy, B, T, V, 3, dx, s));  // :298-303, 315

@@ -167,7 +167,18 @@ class PredictionEngine:
             if time_tsfm is not None:
                 inputs = time_tsfm.transform(inputs)
             inputs = self.transform(inputs)
-            outputs = self.inverse(self.model(inputs, False))
+            # the batch and its time reversal as one native forward pair
+            # (DSTDGCN.forward_pair: per-half BatchNorm statistics, so the same
+            # step as the two calls of the reference, with half the launches)
+            pair = self.config["inverse"] and hasattr(self.model.model, "forward_pair")
+            if pair:
+                if time_tsfm is not None:
+                    inputs_inv = time_tsfm.transform(inputs_inv)
+                inputs_inv = self.transform(inputs_inv)
+                out_pair = self.model.model.forward_pair(inputs, inputs_inv)
+                outputs = self.inverse(out_pair[0])
+            else:
+                outputs = self.inverse(self.model(inputs, False))
             if scale_tsfm is not None:
                 outputs = scale_tsfm.inverse(outputs)
             if time_tsfm is not None:
@@ -180,10 +191,13 @@ class PredictionEngine:
                 all_loss = all_loss + loss[ls]
                 t_l[ls].update(loss[ls] * N, N)
             if self.config["inverse"]:  # time-reversed augmentation pass (:267-287)
-                if time_tsfm is not None:
-                    inputs_inv = time_tsfm.transform(inputs_inv)
-                inputs_inv = self.transform(inputs_inv)
-                outputs_inv = self.inverse(self.model(inputs_inv, True))
+                if pair:
+                    outputs_inv = self.inverse(out_pair[1])
+                else:
+                    if time_tsfm is not None:
+                        inputs_inv = time_tsfm.transform(inputs_inv)
+                    inputs_inv = self.transform(inputs_inv)
+                    outputs_inv = self.inverse(self.model(inputs_inv, True))
                 targets_inv = targets.flip(1)
                 t = outputs_inv.shape[1]
                 targets_il = targets_inv[:, -t:] if t != targets_inv.shape[1] else targets_inv

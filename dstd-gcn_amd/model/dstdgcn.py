@@ -330,14 +330,17 @@ class _ModelTrain(torch.autograd.Function):
     effect, which an op cannot)."""
 
     @staticmethod
-    def forward(ctx, model, x, *params):
-        flags = _bn_flags(model)
+    def forward(ctx, model, paired, x, *params):
+        # paired: x is two train-mode batches of B/2 (DSTDGCN.forward_pair)
+        flags = _bn_flags(model) | (native.TRAIN_PAIRED if paired else 0)
         drop = float(model.do_in.p) if model.do_in.training else 0.0
         seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop > 0 else 0
         y, saved = torch.ops.dstd.dstdgcn_train_forward(x, list(params), model._tree.get(model)[1], model._dstd_uid,
                                                         flags, _bn_momentum(model), drop, seed)
-        if not flags:
+        if not flags & native.TRAIN_RUNNING_STATS:
             _count_batch(model)
+            if paired:
+                _count_batch(model)
         ctx.model, ctx.saved_buf, ctx.drop, ctx.seed, ctx.flags = model, saved, drop, seed, flags
         ctx.params = list(params)  # the backward reuses them (a module walk costs ~0.7 ms)
         ctx.save_for_backward(x)
@@ -349,7 +352,7 @@ class _ModelTrain(torch.autograd.Function):
         model = ctx.model
         dev = x.device
         dy = dy.contiguous()
-        need_dx = bool(ctx.needs_input_grad[1])
+        need_dx = bool(ctx.needs_input_grad[2])
         # gradients accumulate straight into the parameters' .grad (one arena,
         # native +=) when the caller opted in (engine.PredictionEngine.train
         # sets model._dstd_inplace_grads) and no parameter carries hooks; else
@@ -364,12 +367,12 @@ class _ModelTrain(torch.autograd.Function):
                     g = arena.model_grads = model._native_grads(arena)
                 dx = _model_train_bwd_native(model, x, ctx.saved_buf, dy, ctx.flags, ctx.drop, ctx.seed, g, need_dx)
                 ctx.saved_buf = None
-                return (None, dx, *([None] * len(arena.params)))
+                return (None, None, dx, *([None] * len(arena.params)))
         dx, flat = torch.ops.dstd.dstdgcn_train_backward(x, ctx.saved_buf, dy, ctx.params, model._dstd_uid, ctx.flags,
                                                          ctx.drop, ctx.seed, need_dx)
         ctx.saved_buf = None
         arena = native.GradArena(ctx.params, dev, buf=flat)
-        return (None, dx if need_dx else None, *arena.views())
+        return (None, None, dx if need_dx else None, *arena.views())
 
 
 class BatchNorm(nn.Module):
@@ -785,9 +788,31 @@ class DSTDGCN(_NativeModule):
         if self.training or _needs_grad(x, *params):
             # train mode, or an eval-mode forward autograd differentiates (the
             # reference back-propagates through running-statistics BN there)
-            return _ModelTrain.apply(self, x, *params)
+            return _ModelTrain.apply(self, False, x, *params)
         return torch.ops.dstd.dstdgcn_forward(x, params + buffers, self._dstd_uid,
                                               native.arith_flags(self.gc_arithmetic))
+
+    def forward_pair(self, x1, x2):
+        """``(self(x1), self(x2))`` -- PredictionEngine.train's forward of a
+        batch and of its time reversal (engine/prediction.py:231-287) -- as
+        ONE native launch sequence over the concatenated batch.  In train mode
+        every BatchNorm keeps each half's own batch statistics and the running
+        statistics take x1's update then x2's (DSTD_TRAIN_PAIRED), so outputs,
+        gradients and buffers are those of the two calls; elsewhere (eval, or
+        shapes that differ) it is the two calls."""
+        if not self.training or x1.shape != x2.shape or x1.shape[0] == 0 or x1.device != x2.device:
+            return self(x1), self(x2)
+        n, t, v, c = x1.shape
+        assert t == self.input_time_frame + self.output_time_frame
+        if c != self.input_channels // 2 or v != self.joints_to_consider:
+            raise ValueError(f"DSTDGCN: expected [N, {t}, {self.joints_to_consider}, {self.input_channels // 2}], "
+                             f"got {list(x1.shape)}")
+        native.lib()
+        x = torch.cat([x1, x2]).contiguous()
+        native.require_device(x, "x")
+        params = self._tree.get(self)[0]
+        y = _ModelTrain.apply(self, True, x, *params)
+        return y[:n], y[n:]
 
     def _forward_native(self, x, y, prof=None, arith=None):
         """One eval forward through dstd_model_fwd_ex.  The folded constants

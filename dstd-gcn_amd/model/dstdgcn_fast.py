@@ -440,7 +440,7 @@ class DSTDGCN(_Shadowed):
         sh.do_in.p = self.do_in.p
         if self.training or base._needs_grad(x, *self.parameters()):
             self._sync(sh, params=False)
-            y = _ModelTrainM.apply(sh, x.contiguous(), *self._derived_params(sh))
+            y = _ModelTrainM.apply(sh, False, x.contiguous(), *self._derived_params(sh))
             if self.training:
                 self._write_back_running_stats(sh)
             return y

@@ -120,6 +120,12 @@ int dstd_block_train_bwd(const dstd_block_params* p, const float* x, int B, int 
  * backward -- pass the same flags to both).  flags = 0 is the plain entry
  * point (batch statistics, running stats updated with momentum). */
 #define DSTD_TRAIN_RUNNING_STATS 1u
+/* DSTD_TRAIN_PAIRED: the batch is two independent BatchNorm batches of B/2
+ * samples each (B even): statistics per half, running statistics updated by
+ * the first half then the second -- exactly two train-mode forwards of B/2
+ * (the engine's batch and its time reversal, engine/prediction.py:231-287)
+ * in one launch sequence.  Pass the same flags to the backward. */
+#define DSTD_TRAIN_PAIRED 2u
 int dstd_block_train_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum,
                             float* y, void* saved, size_t saved_bytes, void* stream, unsigned flags);
 int dstd_block_train_bwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, const void* saved,

@@ -2,8 +2,10 @@
 T=40, V=23, 32 sequences per GPU per step; also a large-batch variant).
 
 One step = PredictionEngine.train's body (engine/prediction.py:231-294):
-train-mode forward of the batch and of its time reversal, two mpjpe losses,
-native backward, Adam.  Prints one JSON line per batch size.
+train-mode forward of the batch and of its time reversal (as the engine runs
+it: one DSTDGCN.forward_pair, per-half BatchNorm statistics; --two-calls for
+two separate forwards), two mpjpe losses, native backward, Adam.  Prints one
+JSON line per batch size.
 
   python scripts/bench_train.py [--batch 32 256] [--steps 20] [--warmup 5]
 
@@ -37,6 +39,7 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[32, 256])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--two-calls", action="store_true", help="two model calls instead of forward_pair")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -66,8 +69,11 @@ def main():
         seq_inv = seq.flip(1).contiguous()
 
         def step():
-            out = m(inp.view(B, 40, 23, 3)).view(B, 40, 69)
-            out_i = m(inv.view(B, 40, 23, 3)).view(B, 40, 69)
+            if a.two_calls:
+                out, out_i = m(inp.view(B, 40, 23, 3)), m(inv.view(B, 40, 23, 3))
+            else:
+                out, out_i = m.forward_pair(inp.view(B, 40, 23, 3), inv.view(B, 40, 23, 3))
+            out, out_i = out.reshape(B, 40, 69), out_i.reshape(B, 40, 69)
             loss = (mpjpe_error_3d(out, seq) + mpjpe_error_3d(out_i, seq_inv)) / 2
             opt.zero_grad()
             loss.backward()
@@ -100,6 +106,7 @@ def main():
                               "batch": B, "n_gpus": world, "steps": a.steps, "dtype": "f32",
                               "loss": round(float(loss.detach()), 4), "scaling": "weak",
                               "config": {"workload": "3dpw T=40 V=23, 2 fwd + 1 bwd + Adam", "inverse": True,
+                                         "forward": "two calls" if a.two_calls else "forward_pair",
                                          "parallelism": f"dp{world}"}}),
                   flush=True)
     if distributed:

@@ -273,6 +273,52 @@ def test_model_step_gradients_vs_reference_fp64():
     assert named["conv_st_in.stgcn.0.0.A_s"].grad is None
 
 
+@pytest.mark.parametrize("inplace", [True, False])
+def test_forward_pair_equals_two_calls(inplace):
+    """DSTDGCN.forward_pair (DSTD_TRAIN_PAIRED: one launch sequence over the
+    batch and its time reversal, BatchNorm statistics per half, running
+    statistics updated by the first half then the second) against the two
+    train-mode calls of engine/prediction.py:231-287: outputs, every gradient,
+    running statistics and num_batches_tracked.  The paths differ only in
+    GEMM summation order (split-K over 64 samples vs 32 + 32)."""
+    from engine import mpjpe_error_3d
+    m1, d = _model_3dpw()
+    m2, _ = _model_3dpw()
+    m1._dstd_inplace_grads = m2._dstd_inplace_grads = inplace
+    inp, inv, seq = (torch.from_numpy(d[f"train/{n}0"]).to(DEV) for n in ("inp", "inv", "seq"))
+    B, T, VC = inp.shape
+    x1, x2 = inp.view(B, T, 23, 3), inv.view(B, T, 23, 3)
+
+    def loss_of(o1, o2):
+        return (mpjpe_error_3d(o1.reshape(B, T, VC), seq) + mpjpe_error_3d(o2.reshape(B, T, VC), seq.flip(1))) / 2
+
+    y1, y2 = m1(x1), m1(x2)
+    loss_of(y1, y2).backward()
+    p1, p2 = m2.forward_pair(x1, x2)
+    loss_of(p1, p2).backward()
+    assert rel(p1, y1) < 1e-5 and rel(p2, y2) < 1e-5
+    for (name, a), b in zip(m1.named_parameters(), m2.parameters()):
+        if a.grad is None:
+            assert b.grad is None, name
+            continue
+        if name.endswith("residual.0.bias"):
+            # analytically zero (the train-mode BN right after it cancels a
+            # per-channel constant): both paths hold fp32 rounding noise
+            assert float(b.grad.abs().max()) < 1e-3, name
+            continue
+        assert float((a.grad - b.grad).abs().max()) <= 1e-4 * float(a.grad.abs().max()) + 1e-12, name
+    for (name, a), b in zip(m1.named_buffers(), m2.buffers()):
+        if name.endswith("num_batches_tracked"):
+            assert int(a) == int(b) == 2, name
+        else:
+            assert rel(b, a) < 1e-5, name
+    # eval mode: the two plain calls
+    m2.eval()
+    with torch.no_grad():
+        e1, e2 = m2.forward_pair(x1, x2)
+        assert torch.equal(e1, m2(x1)) and torch.equal(e2, m2(x2))
+
+
 def test_gradient_sink_paths_agree():
     """The model backward accumulates into the parameters' .grad in place
     (dstd_native.grad_sink) when they are its own arena views, and hands
