@@ -446,3 +446,19 @@ class DSTDGCN(_Shadowed):
             return y
         self._sync(sh)
         return sh(x)
+
+    def forward_pair(self, x1, x2):
+        """``(self(x1), self(x2))`` as one paired native train step
+        (dstdgcn.DSTDGCN.forward_pair: per-half BatchNorm statistics, running
+        statistics updated in call order); the two calls outside train mode."""
+        if not self.training or x1.shape != x2.shape or x1.shape[0] == 0 or x1.device != x2.device:
+            return self(x1), self(x2)
+        n, t, v, c = x1.shape
+        assert t == self.input_time_frame + self.output_time_frame
+        native.require_device(x1, "x")
+        sh = self._shadow_for(x1.device)
+        sh.do_in.p = self.do_in.p
+        self._sync(sh, params=False)
+        y = _ModelTrainM.apply(sh, True, torch.cat([x1, x2]).contiguous(), *self._derived_params(sh))
+        self._write_back_running_stats(sh)
+        return y[:n], y[n:]

@@ -124,10 +124,12 @@ def test_fast_schema_and_cache():
         assert torch.equal(m2(x), y2)
 
 
-def test_fast_train_step_vs_reference_fp64():
+@pytest.mark.parametrize("paired", [False, True])
+def test_fast_train_step_vs_reference_fp64(paired):
     """One training step (forward + inverse pass, two losses, backward) of the
-    fast model in train mode: loss, every gradient and the BN running-stat
-    updates against the reference's fp64 run (dstdgcn_fast.npz train/*)."""
+    fast model in train mode -- two calls, or one forward_pair -- loss, every
+    gradient and the BN running-stat updates against the reference's fp64 run
+    (dstdgcn_fast.npz train/*)."""
     from engine import mpjpe_error_3d
     d = load_npz("dstdgcn_fast.npz")
     opts = {k[len("train/opt/"):]: d[k].item() for k in d.files if k.startswith("train/opt/")}
@@ -136,8 +138,12 @@ def test_fast_train_step_vs_reference_fp64():
     inp, inv, seq = (t(d[f"train/{n}"]) for n in ("inp", "inv", "seq"))
     B, T, VC = inp.shape
     V = VC // 3
-    loss = mpjpe_error_3d(m(inp.view(B, T, V, 3)).reshape(B, T, VC), seq)
-    loss_i = mpjpe_error_3d(m(inv.view(B, T, V, 3)).reshape(B, T, VC), seq.flip(1))
+    if paired:
+        y, y_i = m.forward_pair(inp.view(B, T, V, 3), inv.view(B, T, V, 3))
+    else:
+        y, y_i = m(inp.view(B, T, V, 3)), m(inv.view(B, T, V, 3))
+    loss = mpjpe_error_3d(y.reshape(B, T, VC), seq)
+    loss_i = mpjpe_error_3d(y_i.reshape(B, T, VC), seq.flip(1))
     all_loss = (loss + loss_i) / 2
     all_loss.backward()
     assert abs(float(all_loss.detach()) - float(d["train/loss64"])) / float(d["train/loss64"]) < 1e-5
