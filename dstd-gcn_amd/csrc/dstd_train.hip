@@ -72,8 +72,8 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
   const int wm = (wave >> 1) * (TM / 2), wn = (wave & 1) * (TN / 2);
-  const bool a_kfast = g.a_k == 1 && g.a_m != 1;
-  const bool b_kfast = g.b_k == 1 && g.b_n != 1;
+  const bool a_kfast = g.a_k < g.a_m;  // the smaller stride runs across lanes (unit stride when there is one)
+  const bool b_kfast = g.b_k < g.b_n;
 
   f32x4 acc[FM][FN];
 #pragma unroll
