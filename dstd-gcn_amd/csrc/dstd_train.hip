@@ -562,6 +562,7 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_stats_part(BnFwd a, int B, i
 // mean / rstd and updates the running statistics), then normalises the
 // sample's contiguous [T][V] plane of channel c.
 constexpr int kBnMaxV = 64;
+constexpr int kBnMaxSplits = 16;  // bn_splits() never exceeds it
 // rows: rows per group; g: the group whose split partials merge
 __device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows, int splits, const float* part, int g,
                                                float& mean, float& rstd, bool store) {
@@ -571,19 +572,32 @@ __device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows,
   } else {
     const int per = (rows + splits - 1) / splits;
     part += (size_t)g * splits * a.cv * 2;
+    // every partial is loaded before the first use (a loop of dependent
+    // load-use pairs pays one memory latency per split); same summation order
+    float pm[kBnMaxSplits], pq[kBnMaxSplits];
+#pragma unroll
+    for (int sp = 0; sp < kBnMaxSplits; ++sp)
+      if (sp < splits) {
+        const float2 p = *reinterpret_cast<const float2*>(part + ((size_t)sp * a.cv + ch) * 2);
+        pm[sp] = p.x;
+        pq[sp] = p.y;
+      }
     float m = 0.f;
-    for (int sp = 0; sp < splits; ++sp) {
-      const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
-      m += cnt * part[((size_t)sp * a.cv + ch) * 2];
-    }
+#pragma unroll
+    for (int sp = 0; sp < kBnMaxSplits; ++sp)
+      if (sp < splits) {
+        const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+        m += cnt * pm[sp];
+      }
     m /= rows;
     float m2 = 0.f;
-    for (int sp = 0; sp < splits; ++sp) {
-      const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
-      const float* p = part + ((size_t)sp * a.cv + ch) * 2;
-      const float d = p[0] - m;
-      m2 += p[1] + cnt * d * d;
-    }
+#pragma unroll
+    for (int sp = 0; sp < kBnMaxSplits; ++sp)
+      if (sp < splits) {
+        const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+        const float d = pm[sp] - m;
+        m2 += pq[sp] + cnt * d * d;
+      }
     const float var = m2 / rows;
     mean = m;
     rstd = 1.f / sqrtf(var + a.eps);
@@ -710,21 +724,30 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int
                                                              const float* part, const float* wpart, float* dprelu,
                                                              int ns) {
   __shared__ float sdl[kBnMaxV], sxl[kBnMaxV], red[kRedThreads / 64];
+  __shared__ float mnl[kBnMaxV], rsl[kBnMaxV], gml[kBnMaxV];  // the group's mean / rstd and gamma per v
   const int c = blockIdx.x, n = blockIdx.y * ns, tid = threadIdx.x;
   const int CV = C * V;
   const int Bg = B / a.groups, grp = n / Bg;
   if (tid < V) {
     const int ch = c * V + tid;
+    mnl[tid] = a.mean[grp * CV + ch];
+    rsl[tid] = a.rstd[grp * CV + ch];
+    gml[tid] = a.gamma[ch];
     // group sums; workgroup (c, 0) adds every group's into dgamma / dbeta
     float tb = 0.f, tg = 0.f;
     for (int gg = 0; gg < a.groups; ++gg) {
       if (n != 0 && gg != grp) continue;
+      float2 pv[kBnMaxSplits];  // loads first, then the split-order sums
+#pragma unroll
+      for (int sp = 0; sp < kBnMaxSplits; ++sp)
+        if (sp < splits) pv[sp] = *reinterpret_cast<const float2*>(part + ((size_t)(gg * splits + sp) * CV + ch) * 2);
       float sd = 0.f, sdx = 0.f;
-      for (int sp = 0; sp < splits; ++sp) {
-        const float* p = part + ((size_t)(gg * splits + sp) * CV + ch) * 2;
-        sd += p[0];
-        sdx += p[1];
-      }
+#pragma unroll
+      for (int sp = 0; sp < kBnMaxSplits; ++sp)
+        if (sp < splits) {
+          sd += pv[sp].x;
+          sdx += pv[sp].y;
+        }
       if (gg == grp) {
         sdl[tid] = sd;
         sxl[tid] = sdx;
@@ -765,13 +788,12 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int
       const int e = e0 + j * 256;
       if (e >= T * V) break;
       const size_t i = base + e;
-      const int v = e % V, ch = c * V + v;
+      const int v = e % V;
       const float d = dv[j];
       const float dz = (a.prelu && !(zv[j] > 0.f)) ? w * d : d;
-      const float mean = a.mean[grp * CV + ch], rstd = a.rstd[grp * CV + ch];
+      const float mean = mnl[v], rstd = rsl[v];
       const float xh = (uv[j] - mean) * rstd;
-      a.du[i] = a.use_running ? a.gamma[ch] * rstd * dz
-                              : a.gamma[ch] * rstd * (dz - sdl[v] * inv - xh * sxl[v] * inv);
+      a.du[i] = a.use_running ? gml[v] * rstd * dz : gml[v] * rstd * (dz - sdl[v] * inv - xh * sxl[v] * inv);
       if (a.dz_out) a.dz_out[i] = dz;
     }
   }
@@ -1048,7 +1070,7 @@ int bn_apply_samples(int Bg, int B, int C) {
   return 1;
 }
 
-int bn_splits(int B, int T) { return std::max(1, std::min(16, cdiv(B * T, 64))); }
+int bn_splits(int B, int T) { return std::max(1, std::min(kBnMaxSplits, cdiv(B * T, 64))); }
 
 size_t bn_scratch_floats(int B, int C, int T, int V) {  // sized for up to 2 groups
   return 2 * ((size_t)bn_splits(B, T) * C * V * 2 + (size_t)bn_splits(B, T) * C) + (size_t)2 * C * V;
