@@ -219,6 +219,7 @@ constexpr int kMaxSplit = 128;
 // ---------------------------------------------------------------------------
 // tanh outer difference
 // ---------------------------------------------------------------------------
+constexpr int kTanhMaxNN = 128;  // the frame envelope (T <= 128; V <= 64)
 __global__ void k_tanh_outer_fwd(const float* __restrict__ P, const float* __restrict__ Q, PQView v, int R, int A,
                                  int NN, float* __restrict__ M) {
   // one workgroup per (n, r, a); M block [NN][NN]
@@ -227,10 +228,18 @@ __global__ void k_tanh_outer_fwd(const float* __restrict__ P, const float* __res
   const float* p = P + n * v.sn + r * v.sr + a * v.sa;
   const float* q = Q + n * v.sn + r * v.sr + a * v.sa;
   float* m = M + (size_t)blk * NN * NN;
+  // the block's P and Q rows (strided in the caller's layout) staged once in
+  // LDS instead of two strided loads per output element
+  __shared__ float ps[kTanhMaxNN], qs[kTanhMaxNN];
+  for (int i = threadIdx.x; i < NN; i += blockDim.x) {
+    ps[i] = p[i * v.si];
+    qs[i] = q[i * v.si];
+  }
+  __syncthreads();
 #pragma unroll 4
   for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
     const int i = e / NN, j = e - i * NN;
-    m[e] = tanhf(p[i * v.si] - q[j * v.si]);
+    m[e] = tanhf(ps[i] - qs[j]);
   }
 }
 
@@ -572,32 +581,19 @@ __device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows,
   } else {
     const int per = (rows + splits - 1) / splits;
     part += (size_t)g * splits * a.cv * 2;
-    // every partial is loaded before the first use (a loop of dependent
-    // load-use pairs pays one memory latency per split); same summation order
-    float pm[kBnMaxSplits], pq[kBnMaxSplits];
-#pragma unroll
-    for (int sp = 0; sp < kBnMaxSplits; ++sp)
-      if (sp < splits) {
-        const float2 p = *reinterpret_cast<const float2*>(part + ((size_t)sp * a.cv + ch) * 2);
-        pm[sp] = p.x;
-        pq[sp] = p.y;
-      }
     float m = 0.f;
-#pragma unroll
-    for (int sp = 0; sp < kBnMaxSplits; ++sp)
-      if (sp < splits) {
-        const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
-        m += cnt * pm[sp];
-      }
+    for (int sp = 0; sp < splits; ++sp) {
+      const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+      m += cnt * part[((size_t)sp * a.cv + ch) * 2];
+    }
     m /= rows;
     float m2 = 0.f;
-#pragma unroll
-    for (int sp = 0; sp < kBnMaxSplits; ++sp)
-      if (sp < splits) {
-        const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
-        const float d = pm[sp] - m;
-        m2 += pq[sp] + cnt * d * d;
-      }
+    for (int sp = 0; sp < splits; ++sp) {
+      const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+      const float* p = part + ((size_t)sp * a.cv + ch) * 2;
+      const float d = p[0] - m;
+      m2 += p[1] + cnt * d * d;
+    }
     const float var = m2 / rows;
     mean = m;
     rstd = 1.f / sqrtf(var + a.eps);
@@ -972,6 +968,7 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
 
 hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int R, int A, int NN, float* M,
                           hipStream_t s) {
+  if (NN > kTanhMaxNN) return hipErrorInvalidValue;
   k_tanh_outer_fwd<<<B * R * A, 256, 0, s>>>(P, Q, v, R, A, NN, M);
   return hipGetLastError();
 }
