@@ -309,6 +309,90 @@ def variant_throughput(config, B, device, steps, warmup):
             "value": round(B * steps / el, 2), "unit": "seq/s", "ms_per_step": round(el / steps * 1e3, 4)}
 
 
+def timed_calls(fn, steps, warmup):
+    """(ms per call on the device clock, host us per call): fn() `steps` times
+    between two synchronisations, after `warmup` untimed calls."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    host = 0.0
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        h0 = time.perf_counter()
+        fn()
+        host += time.perf_counter() - h0
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps * 1e3, host / steps * 1e6
+
+
+def arithmetic_leg(model, x, arith, steps, warmup):
+    """Side measurement (not `value`): the same B=256 drop-in forward with the
+    graph convolutions in another arithmetic (DSTDGCN.set_gc_arithmetic;
+    "fp32" = exact-fp32 MFMA v_mfma_f32_16x16x4_f32 everywhere)."""
+    prev = model.gc_arithmetic
+    model.set_gc_arithmetic(arith)
+    try:
+        with torch.no_grad():
+            ms, host = timed_calls(lambda: model(x), steps, warmup)
+    finally:
+        model.set_gc_arithmetic(prev)
+    B = x.shape[0]
+    return {"workload": f"same as the line, gc arithmetic {arith}", "value": round(B / ms * 1e3, 2), "unit": "seq/s",
+            "ms_per_step": round(ms, 4), "host_us_per_call": round(host, 2)}
+
+
+def small_batch_leg(model, x, B, steps, warmup):
+    """Side measurement: eval throughput at the reference's test batch
+    (dstdgcn_h36m.yaml:19 test_batch_size 32) through model(x), and the same
+    forward replayed from a captured HIP graph (DSTDGCN.graphed)."""
+    xb = x[:B].contiguous()
+    with torch.no_grad():
+        ms, host = timed_calls(lambda: model(xb), steps, warmup)
+        out = {"workload": f"H36M-shape synthetic, B={B} (test_batch_size), eval forward", "value": round(B / ms * 1e3, 2),
+               "unit": "seq/s", "ms_per_step": round(ms, 4), "host_us_per_call": round(host, 2)}
+        if hasattr(model, "graphed"):
+            g = model.graphed(xb)
+            gms, ghost = timed_calls(lambda: g(xb), steps, warmup)
+            out["graph_replay"] = {"value": round(B / gms * 1e3, 2), "ms_per_step": round(gms, 4),
+                                   "host_us_per_call": round(ghost, 2)}
+    return out
+
+
+def train_leg(device, B, steps, warmup):
+    """Side measurement, SURVEY §8(d) config 5 on one GPU: one training step of
+    the 3DPW model (T = 10 + 30, V = 23; dstdgcn_3dpw.yaml) = the engine's
+    step (engine/prediction.py:231-294): train-mode forward of the batch and
+    its time reversal (DSTDGCN.forward_pair), two mpjpe losses, native
+    backward, Adam.  Random-init weights, synthetic poses."""
+    from engine import mpjpe_error_3d
+    opts = dict(input_channels=6, input_time_frame=10, output_time_frame=30, st_gcnn_dropout=0.0,
+                joints_to_consider=23, num_feature=64, num_layers=5, layout="3dpw")
+    torch.manual_seed(0)
+    m = get_model("dstdgcn", dstdgcn=opts).to(device).train()
+    m._dstd_inplace_grads = True  # as engine.PredictionEngine.train opts in
+    opt = torch.optim.Adam(m.parameters(), lr=3e-3)
+    g = torch.Generator().manual_seed(1234)
+    seq = torch.randn(B, 40, 69, generator=g)
+    inp = seq.clone()
+    inp[:, 10:] = inp[:, 9:10]
+    inv = seq.flip(1).clone()
+    inv[:, 10:] = inv[:, 9:10]
+    seq, inp, inv = seq.to(device), inp.to(device), inv.to(device)
+    seq_inv = seq.flip(1).contiguous()
+
+    def step():
+        out, out_i = m.forward_pair(inp.view(B, 40, 23, 3), inv.view(B, 40, 23, 3))
+        loss = (mpjpe_error_3d(out.reshape(B, 40, 69), seq) + mpjpe_error_3d(out_i.reshape(B, 40, 69), seq_inv)) / 2
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    ms, host = timed_calls(step, steps, warmup)
+    return {"workload": f"3DPW-shape synthetic T=40 V=23, B={B}: forward pair + 2 mpjpe + backward + Adam (fp32)",
+            "value": round(B / ms * 1e3, 2), "unit": "train seq/s", "ms_per_step": round(ms, 4),
+            "host_us_per_step": round(host, 2)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -322,6 +406,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variant", action="store_true",
                     help="skip the side measurement of the '50 in / 25 out' (T=75) H36M variant at N=1")
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the N=1 side legs (exact fp32, B=32 eval, B=32 3DPW training step)")
     ap.add_argument("--probe-every", type=int, default=5,
                     help="bracket the dominant launch with HIP events in one of every P timed steps "
                          "(an event pair costs ~5%% of a step)")
@@ -380,14 +466,20 @@ def main():
         every = max(1, args.probe_every)
         prof = Profiler(L, (args.steps + every - 1) // every, 1 << dominant)
         prof.prof.only_block = 1
+        probe = ctypes.byref(prof.prof)
+        host_s = 0.0
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
+            # the drop-in call itself (DSTDGCN.forward -> torch.ops.dstd.dstdgcn_forward);
+            # a probed step carries the event brackets through the module
             if i % every == 0:
-                forward_profiled(model, x, y, prof)
-            else:
-                model._forward_native(x, y)
+                model._dstd_profile = probe
+            h0 = time.perf_counter()
+            y = model(x)
+            host_s += time.perf_counter() - h0
+            model._dstd_profile = None
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         barrier()
@@ -465,9 +557,15 @@ def main():
                                                                     3)}},
             "kernel_ms_per_step_event_bracketed": {native.KIND_NAMES[k]: round(v / args.steps, 4)
                                                    for k, v in sorted(per_kind.items())},
+            "host_us_per_call": round(host_s / args.steps * 1e6, 2),
+            "timed_call": "model(x): DSTDGCN.forward -> torch.ops.dstd.dstdgcn_forward (the drop-in path)",
         }
         if world == 1 and args.config == "h36m" and not args.no_variant:
             out["variant_t75"] = variant_throughput("h36m75", B, device, args.steps, args.warmup)
+        if world == 1 and not args.no_side:
+            out["exact_fp32"] = arithmetic_leg(model, x, "fp32", args.steps, args.warmup)
+            out["eval_b32"] = small_batch_leg(model, x, 32, max(args.steps, 100), args.warmup)
+            out["train_b32"] = train_leg(device, 32, 20, 5)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(opts, sd, x_cpu, args.cpu_seconds, 30.0)
         else:

@@ -701,7 +701,7 @@ size_t dstd_model_workspace_bytes(int B, int T, int V, int num_feature, int num_
 int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, int V, const dstd_gc_weights* w,
                     const float* A, const float* alpha, float* y, void* workspace, size_t workspace_bytes,
                     void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (!x || !y || !A || !alpha || !gc_ok(w) || !workspace || !shape_ok(B, T, V)) return DSTD_EINVAL;
   if (mode != DSTD_MODE_SPATIAL && mode != DSTD_MODE_TEMPORAL) return DSTD_EINVAL;
   if (!limits_ok(T, V, cin, cout)) return DSTD_ELIMIT;
@@ -802,7 +802,7 @@ int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int
 
 int dstd_block_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (flags & ~DSTD_FWD_EXACT_FP32) return DSTD_EINVAL;
   if (!x || !y || !workspace || !block_ok(p) || !shape_ok(B, T, V)) return DSTD_EINVAL;
   if (!limits_ok(T, V, p->cin, p->cout)) return DSTD_ELIMIT;
@@ -839,7 +839,7 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
 
 int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   const bool reuse = (flags & DSTD_FWD_REUSE_CONSTANTS) != 0;
   const bool exact = (flags & DSTD_FWD_EXACT_FP32) != 0;
   if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32)) return DSTD_EINVAL;

@@ -17,14 +17,35 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // The C entry points launch on the device of the caller's stream: a module
 // on cuda:1 called while cuda:0 is current switches for the call and back.
+// The null stream (torch's default stream) names no device -- it is the
+// CURRENT device's -- so there the device comes from the call's first
+// device pointer (hipPointerGetAttributes; skipped on a single-GPU process).
+inline int dstd_device_count() {
+  static const int n = [] {
+    int c = 0;
+    return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+  }();
+  return n;
+}
 struct StreamDeviceGuard {
   int prev = -1;
-  explicit StreamDeviceGuard(void* stream) {
-    if (!stream) return;
-    int cur = 0;
-    hipDevice_t sd = 0;
-    if (hipGetDevice(&cur) != hipSuccess || hipStreamGetDevice((hipStream_t)stream, &sd) != hipSuccess) return;
-    if (sd != cur && hipSetDevice(sd) == hipSuccess) prev = cur;
+  explicit StreamDeviceGuard(void* stream, const void* devptr = nullptr) {
+    int cur = 0, sd = -1;
+    if (hipGetDevice(&cur) != hipSuccess) return;
+    if (stream) {
+      hipDevice_t d = 0;
+      if (hipStreamGetDevice((hipStream_t)stream, &d) != hipSuccess) return;
+      sd = (int)d;
+    } else if (devptr && dstd_device_count() > 1) {
+      hipPointerAttribute_t at{};
+      if (hipPointerGetAttributes(&at, devptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+      }
+      if (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeManaged) return;
+      sd = at.device;
+    }
+    if (sd >= 0 && sd != cur && hipSetDevice(sd) == hipSuccess) prev = cur;
   }
   ~StreamDeviceGuard() {
     if (prev >= 0) (void)hipSetDevice(prev);

@@ -172,7 +172,7 @@ size_t dstd_ctg_workspace_bytes(int B, int C, int T, int V) {
 
 int dstd_ctg_fwd(const float* x, int B, int C, int T, int V, const float* Tm, const float* A, const float* A_fixed,
                  float* y, void* workspace, size_t workspace_bytes, void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (!x || !Tm || !A || !A_fixed || !y || !workspace || B <= 0 || C <= 0 || T <= 0 || V <= 0) return DSTD_EINVAL;
   if (workspace_bytes < dstd_ctg_workspace_bytes(B, C, T, V)) return DSTD_EWORKSPACE;
   hipStream_t s = (hipStream_t)stream;
@@ -188,7 +188,7 @@ int dstd_ctg_fwd(const float* x, int B, int C, int T, int V, const float* Tm, co
 int dstd_ctg_bwd(const float* x, int B, int C, int T, int V, const float* Tm, const float* A, const float* A_fixed,
                  const float* dy, float* dx, float* dTm, float* dA, void* workspace, size_t workspace_bytes,
                  void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (!x || !Tm || !A || !A_fixed || !dy || !dTm || !dA || !workspace || B <= 0 || C <= 0 || T <= 0 || V <= 0)
     return DSTD_EINVAL;
   if (workspace_bytes < dstd_ctg_workspace_bytes(B, C, T, V)) return DSTD_EWORKSPACE;
@@ -245,7 +245,7 @@ size_t dstd_conv2d_workspace_bytes(int B, int cin, int cout, int H, int W, int k
 int dstd_conv2d_fwd(const float* x, int B, int cin, int H, int W, const float* w, const float* bias, int cout,
                     int kh, int kw, int sh, int sw, int ph, int pw, float* y, void* workspace,
                     size_t workspace_bytes, void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   ConvGeom g;
   if (!x || !w || !y || !conv_geom(g, B, cin, H, W, cout, kh, kw, sh, sw, ph, pw)) return DSTD_EINVAL;
   (void)workspace, (void)workspace_bytes;
@@ -269,7 +269,7 @@ int dstd_conv2d_fwd(const float* x, int B, int cin, int H, int W, const float* w
 int dstd_conv2d_bwd(const float* x, int B, int cin, int H, int W, const float* w, int cout, int kh, int kw, int sh,
                     int sw, int ph, int pw, const float* dy, float* dx, float* dw, float* db, void* workspace,
                     size_t workspace_bytes, void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   ConvGeom g;
   if (!x || !w || !dy || !dw || !workspace || !conv_geom(g, B, cin, H, W, cout, kh, kw, sh, sw, ph, pw))
     return DSTD_EINVAL;

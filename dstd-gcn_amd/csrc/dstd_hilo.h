@@ -125,6 +125,23 @@ struct SlotMap {
   }
 };
 
+// ---- a gfx950 MFMA hazard hipcc (ROCm 7.2) does not pad -----------------
+// Mixed-shape MFMA chains: an MFMA that takes the previous MFMA's result whole as
+// its C operand (an accumulate chain) computes with a stale accumulator when
+// the two MFMAs have DIFFERENT shapes (v_mfma_f32_16x16x32_f16 followed by
+// v_mfma_f32_16x16x16_f16 or the reverse) and fewer than 5 wait states lie
+// between them; same-shape chains are exact back to back and at any gap.
+// Measured with scripts/micro/mfma_read_hazard.hip (64 K lanes, gaps 0..7:
+// ~90% of lanes wrong at gaps 0-3 for both mixed orders, 0 at gap >= 4 and
+// for every same-shape pair).  hipcc's hazard recognizer asks 0 wait states
+// for any XDL -> XDL "full SrcC" dependency, so mixed-shape chains are wrong
+// or right depending on how the scheduler interleaves them (round 2's
+// "wrong results, not understood": DESIGN.md §4).  Rule in this tree: a
+// chain never changes MFMA shape on one accumulator -- the 16x16x16 tail
+// steps of the conv_rm GEMMs accumulate from zero into an accumulator of
+// their own, added with four VALU adds; scripts/mfma_hazard_audit.py checks
+// the built library's ISA for the pattern (tests/test_capi_host.py).
+
 // Halves per adjacency row (one output column, one plane) on the host.
 inline int hl_sl_spatial(int V) { return 8 * cdiv(V, 8); }
 inline int hl_sl_temporal(int T) {

@@ -29,6 +29,18 @@
 // Workgroup timeline of the split adjacency kernel (debug builds,
 // -DDSTD_STAMPS; scripts/timeline.py --hl): s_memrealtime at entry, prologue
 // done, tiles done, exit.
+#ifdef DSTD_TF_DUMPP
+__device__ unsigned g_dbg_planes[64 * 1024];
+extern "C" int dstd_debug_planes(unsigned* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg_planes), sizeof(g_dbg_planes), 0);
+}
+#endif
+#ifdef DSTD_TF_DEBUGW
+__device__ unsigned g_dbg_w[2 * 512 * 24];
+extern "C" int dstd_debug_w(unsigned* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg_w), sizeof(g_dbg_w), 0);
+}
+#endif
 #ifdef DSTD_STAMPS
 __device__ unsigned long long g_tl_hl[2][2048][4];
 #define TLH(m, i) \
@@ -1183,12 +1195,16 @@ __device__ __forceinline__ void rm_mfma(const uint4* wl, int lane, const f16x8 (
       ah[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
       ao[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
     }
+    // the tail runs on an accumulator of its own (dstd_hilo.h: mixed-shape MFMA chains)
+    f32x4 tac[RT];
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ao[rt], th, acc[rt], 0, 0, 0);
+    for (int rt = 0; rt < RT; ++rt) tac[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ao[rt], th, zero4(), 0, 0, 0);
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], to, acc[rt], 0, 0, 0);
+    for (int rt = 0; rt < RT; ++rt) tac[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], to, tac[rt], 0, 0, 0);
 #pragma unroll
-    for (int rt = 0; rt < RT; ++rt) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], th, acc[rt], 0, 0, 0);
+    for (int rt = 0; rt < RT; ++rt) tac[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(ah[rt], th, tac[rt], 0, 0, 0);
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) acc[rt] += tac[rt];
   }
 }
 
@@ -1569,62 +1585,119 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // W_rm as B (the same register layouts) -- so a lane's accumulator holds
       // 4 consecutive slots (columns 16 ct + 4 kg + r) of one joint (16 rt +
       // cl): one 8-byte LDS write per plane instead of eight 2-byte ones.
-      // (W fragments held in registers across tiles, or several tiles per
-      // iteration, gave wrong results on this toolchain -- measured, not
-      // understood; one tile per iteration with its own W reads is
-      // bit-exact against k_adj_hl<1> + k_temporal_hl.)
+      // (Round 2 saw wrong planes with the W fragments held in registers
+      // across tiles.  Cause, found in round 3: hipcc had scheduled a
+      // 16x16x16 tail MFMA right behind a 16x16x32 one on the same
+      // accumulator -- dstd_hilo.h, mixed-shape MFMA chains.  With the tail on its
+      // own accumulator, TPI 1/2 and HOISTW 0/1 are all bit-exact.)
+#ifndef DSTD_TF_TPI
+#define DSTD_TF_TPI 1
+#endif
+#ifndef DSTD_TF_HOISTW
+#define DSTD_TF_HOISTW 0
+#endif
+      constexpr int TPI = DSTD_TF_TPI;  // column tiles per iteration (independent chains)
+      // W_rm fragments of the chunk's row tiles (HOISTW: read once, held across tiles)
+      f16x8 wfh[DSTD_TF_HOISTW ? RTC : 1][NS], wfo[DSTD_TF_HOISTW ? RTC : 1][NS];
+      f16x4 wth[DSTD_TF_HOISTW ? RTC : 1], wto[DSTD_TF_HOISTW ? RTC : 1];
+      auto load_w = [&](int rt, f16x8 (&h)[NS], f16x8 (&o)[NS], f16x4& th4, f16x4& to4) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          h[s] = as_h8(wl[((rt * NS + s) * 2 + 0) * 64 + lane]);
+          o[s] = as_h8(wl[((rt * NS + s) * 2 + 1) * 64 + lane]);
+        }
+        if constexpr (TAIL) {
+          const uint2* w16 = reinterpret_cast<const uint2*>(wl + RTC * NS * 2 * 64);
+          th4 = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
+          to4 = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
+        }
+      };
+      if constexpr (DSTD_TF_HOISTW) {
+#pragma unroll
+        for (int rt = 0; rt < RTC; ++rt) load_w(rt, wfh[rt], wfo[rt], wth[rt], wto[rt]);
+      }
       auto tiles = [&](auto sep_c) {
         constexpr bool SEP = decltype(sep_c)::value;
-        for (int ct = wave; ct < Gm::NCTC; ct += NW) {
-          // this lane's A-operand row = column ct * 16 + cl of the planes
-          const int col = ct * 16 + cl;
-          const int qa = col / SL, pa = SM::slot_idx(col - qa * SL);
-          const bool va = col < NCOL && pa < T;
-          f16x8 bh[NS], bo[NS];
-          f16x4 th, to;
-          tanh_frags<SEP, NS, TAIL, SE>(El, Fl, va ? pa : T, col < NCOL ? qa : T, kg, bh, bo, th, to);
-          // columns colb .. colb+3 (one frame q, slots slot0 ..): alpha (acc + b) + Astat,
-          // 0 on padding slots (alpha -> 0, Astat[T*T] = 0)
-          const int colb = ct * 16 + 4 * kg;
-          const int q = colb / SL, slot0 = colb - q * SL;
-          float as[4], al[4];
+        for (int ct0 = wave; ct0 < Gm::NCTC; ct0 += TPI * NW) {
+          // TPI column tiles ct0, ct0 + NW, ...; a tile past the planes
+          // computes padding (its stores are dropped)
+          f16x8 bh[TPI][NS], bo[TPI][NS];
+          f16x4 th[TPI], to[TPI];
+          float as[TPI][4], al[TPI][4];
+          int colb[TPI], q[TPI], slot0[TPI];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int pi = SM::slot_idx(slot0 + r);
-            const bool valid = colb + r < NCOL && pi < T;
-            as[r] = asl[valid ? pi * T + q : T * T] * dna;
-            al[r] = valid ? alpha : 0.f;
+          for (int i = 0; i < TPI; ++i) {
+            const int ct = ct0 + i * NW;
+            // this lane's A-operand row = column ct * 16 + cl of the planes
+            const int col = ct * 16 + cl;
+            const int qa = col / SL, pa = SM::slot_idx(col - qa * SL);
+            const bool va = col < NCOL && pa < T;
+            tanh_frags<SEP, NS, TAIL, SE>(El, Fl, va ? pa : T, col < NCOL ? qa : T, kg, bh[i], bo[i], th[i], to[i]);
+            // columns colb .. colb+3 (one frame q, slots slot0 ..): alpha (acc + b) + Astat,
+            // 0 on padding slots (alpha -> 0, Astat[T*T] = 0)
+            colb[i] = ct * 16 + 4 * kg;
+            q[i] = colb[i] / SL;
+            slot0[i] = colb[i] - q[i] * SL;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int pi = SM::slot_idx(slot0[i] + r);
+              const bool valid = colb[i] + r < NCOL && pi < T;
+              as[i][r] = asl[valid ? pi * T + q[i] : T * T] * dna;
+              al[i][r] = valid ? alpha : 0.f;
+            }
           }
 #pragma unroll
           for (int rt = 0; rt < RTC; ++rt) {
-            f32x4 acc = zero4();
+            f16x8 wh_[NS], wo_[NS];
+            f16x4 wth_, wto_;
+            if constexpr (DSTD_TF_HOISTW) {
+#pragma unroll
+              for (int s = 0; s < NS; ++s) {
+                wh_[s] = wfh[rt][s];
+                wo_[s] = wfo[rt][s];
+              }
+              wth_ = wth[rt];
+              wto_ = wto[rt];
+            } else {
+              load_w(rt, wh_, wo_, wth_, wto_);
+            }
+            f32x4 acc[TPI];
+#pragma unroll
+            for (int i = 0; i < TPI; ++i) acc[i] = zero4();
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
-              const f16x8 wh = as_h8(wl[((rt * NS + s) * 2 + 0) * 64 + lane]);
-              const f16x8 wo = as_h8(wl[((rt * NS + s) * 2 + 1) * 64 + lane]);
-              acc = mfma32(bh[s], wo, acc);
-              acc = mfma32(bo[s], wh, acc);
-              acc = mfma32(bh[s], wh, acc);
+#pragma unroll
+              for (int i = 0; i < TPI; ++i) acc[i] = mfma32(bh[i][s], wo_[s], acc[i]);
+#pragma unroll
+              for (int i = 0; i < TPI; ++i) acc[i] = mfma32(bo[i][s], wh_[s], acc[i]);
+#pragma unroll
+              for (int i = 0; i < TPI; ++i) acc[i] = mfma32(bh[i][s], wh_[s], acc[i]);
             }
-            if constexpr (TAIL) {
-              const uint2* w16 = reinterpret_cast<const uint2*>(wl + RTC * NS * 2 * 64);
-              const f16x4 wth = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
-              const f16x4 wto = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
-              acc = __builtin_amdgcn_mfma_f32_16x16x16f16(th, wto, acc, 0, 0, 0);
-              acc = __builtin_amdgcn_mfma_f32_16x16x16f16(to, wth, acc, 0, 0, 0);
-              acc = __builtin_amdgcn_mfma_f32_16x16x16f16(th, wth, acc, 0, 0, 0);
+            if constexpr (TAIL) {  // on an accumulator of its own (dstd_hilo.h: mixed-shape MFMA chains)
+              f32x4 tac[TPI];
+#pragma unroll
+              for (int i = 0; i < TPI; ++i) tac[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[i], wto_, zero4(), 0, 0, 0);
+#pragma unroll
+              for (int i = 0; i < TPI; ++i) tac[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(to[i], wth_, tac[i], 0, 0, 0);
+#pragma unroll
+              for (int i = 0; i < TPI; ++i) tac[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[i], wth_, tac[i], 0, 0, 0);
+#pragma unroll
+              for (int i = 0; i < TPI; ++i) acc[i] += tac[i];
             }
             const float b = bsl[16 * rt + cl];
-            float vv[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) vv[r] = fmaf(al[r], fmaf(acc[r], inv, b), as[r]);
-            uint4 hi, lo;
-            split8(make_float4(vv[0], vv[1], vv[2], vv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
             const int jv = 16 * rt + cl;
-            if (jv < nv && colb < NCOL) {
-              _Float16* dst = planes + jv * PJ + q * SL + slot0;
-              *reinterpret_cast<uint2*>(dst) = make_uint2(hi.x, hi.y);
-              *reinterpret_cast<uint2*>(dst + T * SL) = make_uint2(lo.x, lo.y);
+#pragma unroll
+            for (int i = 0; i < TPI; ++i) {
+              float vv[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) vv[r] = fmaf(al[i][r], fmaf(acc[i][r], inv, b), as[i][r]);
+              uint4 hi, lo;
+              split8(make_float4(vv[0], vv[1], vv[2], vv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+              if (jv < nv && colb[i] < NCOL) {
+                _Float16* dst = planes + jv * PJ + q[i] * SL + slot0[i];
+                *reinterpret_cast<uint2*>(dst) = make_uint2(hi.x, hi.y);
+                *reinterpret_cast<uint2*>(dst + T * SL) = make_uint2(lo.x, lo.y);
+              }
             }
           }
         }
@@ -1633,7 +1706,34 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if (sep) tiles(std::true_type{});
       else tiles(std::false_type{});
 #endif
+#if defined(DSTD_TF_DEBUGW) && DSTD_TF_HOISTW
+      // (bisection build: the hoisted W registers after the tile loop against
+      // a fresh read of the same LDS words, workgroup 0, every lane)
+      if (blockIdx.x == 0 && ch == 0) {
+#pragma unroll
+        for (int rt = 0; rt < RTC; ++rt) {
+          f16x8 h2[NS], o2[NS];
+          f16x4 th2, to2;
+          load_w(rt, h2, o2, th2, to2);
+          const uint4 a0 = __builtin_bit_cast(uint4, wfh[rt][0]), a1 = __builtin_bit_cast(uint4, wfo[rt][0]);
+          const uint4 b0 = __builtin_bit_cast(uint4, h2[0]), b1 = __builtin_bit_cast(uint4, o2[0]);
+          const uint2 a2 = __builtin_bit_cast(uint2, wth[rt]), a3 = __builtin_bit_cast(uint2, wto[rt]);
+          const uint2 b2 = __builtin_bit_cast(uint2, th2), b3 = __builtin_bit_cast(uint2, to2);
+          unsigned* d = g_dbg_w + ((rt * NT + tid) * 24);
+          const unsigned v[24] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w, a2.x, a2.y, a3.x, a3.y,
+                                  b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b3.x, b3.y};
+          for (int i = 0; i < 24; ++i) d[i] = v[i];
+        }
+      }
+#endif
       __syncthreads();  // planes complete; the phase-1 scratch is free
+#ifdef DSTD_TF_DUMPP
+      // (bisection build: workgroup 0's planes of chunk 0 to g_dbg_planes)
+      if (blockIdx.x == 0 && ch == 0) {
+        const unsigned* src = reinterpret_cast<const unsigned*>(planes);
+        for (int i = tid; i < (int)(Gm::PLANES / 4) && i < 64 * 1024; i += NT) g_dbg_planes[i] = src[i];
+      }
+#endif
       // ---- phase 2: the stage, then the chunk's GC units ----
       stage_temporal<T, EPI, C, V>(a, st, tid, NT);
       __syncthreads();

@@ -515,7 +515,7 @@ size_t dstd_dstdgc_train_workspace_bytes_r(int mode, int B, int cin, int cout, i
 int dstd_dstdgc_train_fwd_r(int mode, const float* x, int B, int cin, int cout, int T, int V, int red,
                             const dstd_gc_weights* w, const float* A, const float* alpha, float* y, void* saved,
                             size_t saved_bytes, void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (!x || !y || !A || !alpha || !gc_ok(w) || !saved) return DSTD_EINVAL;
   if (mode != DSTD_MODE_SPATIAL && mode != DSTD_MODE_TEMPORAL) return DSTD_EINVAL;
   if (B <= 0 || T <= 1 || V <= 0 || red <= 0) return DSTD_EINVAL;
@@ -536,7 +536,7 @@ int dstd_dstdgc_train_bwd_r(int mode, const float* x, int B, int cin, int cout, 
                             const dstd_gc_weights* w, const float* alpha, const void* saved, size_t saved_bytes,
                             const float* dy, float* dx, const dstd_gc_grads* g, float* dA, float* dalpha,
                             void* workspace, size_t workspace_bytes, void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (!x || !dy || !alpha || !gc_ok(w) || !gg_ok(g) || !dA || !dalpha || !saved || !workspace) return DSTD_EINVAL;
   if (mode != DSTD_MODE_SPATIAL && mode != DSTD_MODE_TEMPORAL) return DSTD_EINVAL;
   if (B <= 0 || T <= 1 || V <= 0 || red <= 0) return DSTD_EINVAL;
@@ -593,7 +593,7 @@ size_t dstd_block_train_workspace_bytes(int B, int cin, int cout, int T, int V) 
 
 int dstd_block_train_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum,
                             float* y, void* saved, size_t saved_bytes, void* stream, unsigned flags) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (!block_ok(p) || !x || !y || !saved || (flags & ~kTrainFlags)) return DSTD_EINVAL;
   if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
   if (B <= 0 || T <= 1 || V <= 0) return DSTD_EINVAL;
@@ -614,7 +614,7 @@ int dstd_block_train_fwd(const dstd_block_params* p, const float* x, int B, int 
 int dstd_block_train_bwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, const void* saved,
                             size_t saved_bytes, const float* dy, float* dx, const dstd_block_grads* g,
                             void* workspace, size_t workspace_bytes, void* stream, unsigned flags) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (!block_ok(p) || !block_grads_ok(p, g) || !x || !dy || !saved || !workspace) return DSTD_EINVAL;
   if (flags & ~kTrainFlags) return DSTD_EINVAL;
   if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
@@ -657,7 +657,7 @@ size_t dstd_model_train_workspace_bytes(int B, int T, int V, int num_feature, in
 int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, float momentum, float dropout_p,
                             unsigned long long seed, float* y, void* saved, size_t saved_bytes, void* stream,
                             unsigned flags) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (!model_ok(p) || !x || !y || !saved || !(dropout_p >= 0.f && dropout_p < 1.f)) return DSTD_EINVAL;
   if (flags & ~kTrainFlags) return DSTD_EINVAL;
   if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
@@ -725,7 +725,7 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
                             unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
                             const dstd_model_grads* g, float* dx, void* workspace, size_t workspace_bytes,
                             void* stream, unsigned flags) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, x);
   if (!model_ok(p) || !g || !x || !dy || !saved || !workspace || !(dropout_p >= 0.f && dropout_p < 1.f))
     return DSTD_EINVAL;
   if (flags & ~kTrainFlags) return DSTD_EINVAL;
@@ -804,7 +804,7 @@ size_t dstd_loss_workspace_bytes(void) { return (size_t)mpjpe_partials() * sizeo
 
 int dstd_mpjpe_fwd(const float* pred, const float* targ, size_t n_points, float* loss, void* workspace,
                    size_t workspace_bytes, void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, pred);
   if (!pred || !targ || !loss || !workspace || n_points == 0) return DSTD_EINVAL;
   if (workspace_bytes < dstd_loss_workspace_bytes()) return DSTD_EWORKSPACE;
   DSTD_TRY(mpjpe_fwd(pred, targ, n_points, loss, (float*)workspace, (hipStream_t)stream));
@@ -813,7 +813,7 @@ int dstd_mpjpe_fwd(const float* pred, const float* targ, size_t n_points, float*
 
 int dstd_mpjpe_bwd(const float* pred, const float* targ, size_t n_points, const float* grad_loss, float scale,
                    float* dpred, void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, pred);
   if (!pred || !targ || !dpred || n_points == 0) return DSTD_EINVAL;
   DSTD_TRY(mpjpe_bwd(pred, targ, n_points, grad_loss, scale, dpred, (hipStream_t)stream));
   return DSTD_OK;
@@ -822,7 +822,7 @@ int dstd_mpjpe_bwd(const float* pred, const float* targ, size_t n_points, const 
 int dstd_frame_mpjpe(const float* all_seqs, const float* outputs, int B, int T, int D, int t_out0,
                      const int* used_pos, int n_used, const int* joint_src, const int* frames, int n_frames,
                      float* sums, void* stream) {
-  StreamDeviceGuard dev_guard_(stream);
+  StreamDeviceGuard dev_guard_(stream, all_seqs);
   if (!all_seqs || !outputs || !used_pos || !joint_src || !frames || !sums) return DSTD_EINVAL;
   if (B <= 0 || T <= 0 || D <= 0 || D % 3 || n_used <= 0 || n_frames <= 0 || t_out0 < 0 || t_out0 >= T)
     return DSTD_EINVAL;

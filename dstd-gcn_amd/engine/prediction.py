@@ -157,8 +157,20 @@ class PredictionEngine:
         dev = self.device
         t_l = {key_loss: DeviceAccum(dev) for key_loss in self.config["loss"]}
         self.model.train()
-        # backward accumulates straight into .grad (dstd_native.grad_sink)
-        self.model.model._dstd_inplace_grads = True
+        # backward accumulates straight into .grad (dstd_native.grad_sink) for
+        # this epoch's steps only: the flag is restored on the way out, so a
+        # caller that later wraps the model (DDP reducer hooks, user hooks)
+        # gets ordinary autograd gradients
+        net = self.model.model
+        prev_inplace = getattr(net, "_dstd_inplace_grads", False)
+        net._dstd_inplace_grads = True
+        try:
+            return self._train_epoch(train_loader, epoch, time_tsfm, scale_tsfm, weights, max_iter, t_l)
+        finally:
+            net._dstd_inplace_grads = prev_inplace
+
+    def _train_epoch(self, train_loader, epoch, time_tsfm, scale_tsfm, weights, max_iter, t_l):
+        dev = self.device
         distributed = _world()[1] > 1
         num_iter = len(train_loader) if max_iter == -1 else min(len(train_loader), max_iter)
         for i, (inputs, inputs_inv, targets, all_seqs) in enumerate(train_loader):
@@ -244,7 +256,7 @@ class PredictionEngine:
         dev = self.device
         sums = torch.zeros(len(eval_frame), dtype=torch.float32, device=dev)
         N = 0
-        save_results = dict() if save_path is not None else None
+        save_results = [] if save_path is not None else None
         index_cache = {}
         rank, world = _world()
         presharded = isinstance(getattr(test_loader, "sampler", None), torch.utils.data.DistributedSampler)
@@ -277,9 +289,7 @@ class PredictionEngine:
                 if save_results is not None:
                     pred = self._fill_pred(all_seqs, outputs, used_pos, joint_src, t_out0)[:, input_n:]
                     targ = all_seqs.view(n, seq_len, -1, 3)[:, input_n:]
-                    for k, v in (("result", pred), ("target", targ)):
-                        a = v.cpu().numpy()
-                        save_results[k] = a if k not in save_results else np.concatenate((save_results[k], a), 0)
+                    save_results.append((i, rank, pred.cpu().numpy(), targ.cpu().numpy()))
             if action is None:
                 action = "NA"
             if world > 1:  # per-frame sums and sample counts of every rank
@@ -289,9 +299,27 @@ class PredictionEngine:
             t_metric = sums.double().cpu().numpy() / N  # the one synchronisation
             self.logger.info(f"action: {action}|test|loss:{t_metric.mean():.2f}")
             if save_results is not None:
-                np.savez(save_path + ".npz", target=save_results["target"], result=save_results["result"])
+                self._save_results(save_path, save_results, rank, world)
         # t_l.avg of the reference = sum over (batch, frame) of metric_k / (N * frames)
         return float(t_metric.mean()), t_metric
+
+    @staticmethod
+    def _save_results(save_path, parts, rank, world):
+        """np.savez of every batch's (result, target) (:405-409).  With several
+        ranks the per-rank parts are gathered to rank 0, put back in loader
+        order (batch index, then rank: round-robin sharding gives each batch
+        index to one rank) and written by rank 0 alone; a rank without batches
+        contributes nothing."""
+        if world > 1:
+            gathered = [None] * world
+            dist.all_gather_object(gathered, parts)
+            if rank != 0:
+                return
+            parts = sorted((p for g in gathered for p in g), key=lambda p: (p[0], p[1]))
+        if not parts:
+            return
+        np.savez(save_path + ".npz", target=np.concatenate([p[3] for p in parts], 0),
+                 result=np.concatenate([p[2] for p in parts], 0))
 
     def _frame_metric(self, all_seqs, outputs, t_out0, used_pos, joint_src, frames, sums):
         """sums[k] += sum over the batch of the MPJPE at frames[k] (:366-404),

@@ -814,6 +814,44 @@ class DSTDGCN(_NativeModule):
         y = _ModelTrain.apply(self, True, x, *params)
         return y[:n], y[n:]
 
+    def graphed(self, x):
+        """The eval forward for inputs shaped like ``x`` captured once into a
+        HIP graph (no per-call launch or Python cost at small
+        batch).  Returns ``run(x_new) -> y``: copies ``x_new`` into the graph's
+        static input (skipped when it is that tensor, ``run.input``), replays
+        the 21 launches plus the two that fold BatchNorm and prepare the split
+        weight images -- so in-place parameter updates are seen by the next
+        replay -- and returns the graph's static output ``run.output``
+        (overwritten by the next replay).  New parameter storage (e.g.
+        ``load_state_dict`` into fresh tensors, ``.to()``) needs a new capture."""
+        if self.training:
+            raise RuntimeError("DSTDGCN.graphed captures the eval forward: call .eval() first")
+        dev = x.device
+        native.require_device(x, "x")
+        x_static = x.detach().clone().contiguous()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.no_grad(), torch.cuda.stream(side):
+            for _ in range(2):  # library load, per-kernel attributes, workspace
+                self(x_static)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(device=dev)  # a stream of its own: its workspace is private to this graph
+        with torch.no_grad(), torch.cuda.graph(g, stream=cap):
+            y_static = self(x_static)
+        # the capture's workspace lives in the graph's memory pool: keep it
+        # with the graph and out of the eager cache
+        ws = native._ws_cache.pop((str(dev), cap.cuda_stream), (None, None))[0]
+
+        def run(x_new):
+            if x_new is not x_static:
+                x_static.copy_(x_new)
+            g.replay()
+            return y_static
+
+        run.graph, run.input, run.output, run._workspace = g, x_static, y_static, ws
+        return run
+
     def _forward_native(self, x, y, prof=None, arith=None):
         """One eval forward through dstd_model_fwd_ex.  The folded constants
         and split-f16 weight images a forward leaves in the workspace are
@@ -825,6 +863,8 @@ class DSTDGCN(_NativeModule):
         L = native.lib()
         n, t, v, _ = x.shape
         dev = x.device
+        if prof is None:  # event brackets requested through the module (bench.py probes model(x) itself)
+            prof = getattr(self, "_dstd_profile", None)
         p = self._native_params()
         flags = native.arith_flags(self.gc_arithmetic) if arith is None else arith
         try:

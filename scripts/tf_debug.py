@@ -9,7 +9,9 @@ from conftest import group, load_npz
 from model import DSTDGCB
 d = load_npz("dstdgcb.npz")
 name = sys.argv[1] if len(sys.argv) > 1 else "b_64_64_h36m"
-blk = DSTDGCB(64, 64, 35, 22, "h36m")
+layout = name.rsplit("_", 1)[1]
+V = {"h36m": 22, "cmu": 25, "3dpw": 23}[layout]
+blk = DSTDGCB(64, 64, 35, V, layout)
 blk.load_state_dict({k: torch.from_numpy(v) for k, v in group(d, f"{name}/sd/").items()})
 blk = blk.to("cuda:0").eval()
 x = torch.from_numpy(d[f"{name}/x"]).to("cuda:0")

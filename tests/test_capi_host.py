@@ -219,3 +219,17 @@ def test_copies_get_their_own_instance_token():
     c = copy.deepcopy(m)
     assert c._dstd_uid != m._dstd_uid
     assert c.encoders[0][0].stgcn[0][0]._dstd_uid != m.encoders[0][0].stgcn[0][0]._dstd_uid
+
+
+def test_no_mixed_shape_mfma_chains_in_the_library():
+    """The built library's gfx950 ISA holds no MFMA that accumulates onto the
+    previous MFMA's result with a different MFMA shape within 5 wait states
+    (dstd_hilo.h, "a gfx950 MFMA hazard hipcc does not pad"; reproducer
+    scripts/micro/mfma_read_hazard.hip).  hipcc pads nothing there, so this is
+    checked on the code object itself (scripts/mfma_hazard_audit.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import mfma_hazard_audit as A
+    findings, n_mfma, n_funcs = A.audit(native.LIB_PATH)
+    assert n_funcs > 100 and n_mfma > 10000  # every translation unit's code object was read
+    assert not findings, findings[:5]

@@ -200,7 +200,16 @@ def test_allreduce_grads_reduces_the_arena_in_place():
 
 
 # ---- sharded test metric of the engine (engine/prediction.py:391-404) -------
-def _engine_metric_body(rank, world):
+def _engine_save_body(rank, world):
+    """PredictionEngine.test(save_path=...) under torch.distributed: the ranks'
+    (result, target) parts are gathered to rank 0 in loader order and written
+    once (a rank without a batch contributes nothing)."""
+    out = _engine_metric_body(rank, world, save_path=os.environ["DSTD_TEST_SAVE"], n_batches=int(
+        os.environ.get("DSTD_TEST_BATCHES", "3")))
+    return out[2]
+
+
+def _engine_metric_body(rank, world, save_path=None, n_batches=3):
     """PredictionEngine.test under torch.distributed: each rank evaluates its
     round-robin share of the loader's batches and the per-frame sums / counts
     are all-reduced.  No GPU in this leg: the model is the fp64 oracle and the
@@ -241,9 +250,10 @@ def _engine_metric_body(rank, world):
     all_seqs = torch.from_numpy(d["test/all_seqs"])
     # three batches (2, 1, 1): rank 0 takes batches 0 and 2, rank 1 batch 1
     loader = [(inputs[:2], None, None, all_seqs[:2]), (inputs[2:3], None, None, all_seqs[2:3]),
-              (inputs[3:], None, None, all_seqs[3:])]
+              (inputs[3:], None, None, all_seqs[3:])][:n_batches]
     avg, metric = eng.test(loader, input_n=10, eval_frame=list(d["test/eval_frame"]), dim_used=d["test/dim_used"],
-                           joint_to_ignore=d["test/joint_to_ignore"], joint_equal=d["test/joint_equal"])
+                           joint_to_ignore=d["test/joint_to_ignore"], joint_equal=d["test/joint_equal"],
+                           save_path=save_path)
     return avg, metric, list(CPUEngine.seen)
 
 
@@ -256,3 +266,23 @@ def test_engine_test_metric_sharded_equals_reference():
         avg, metric, _ = res[r]
         assert float((torch.as_tensor(metric) - torch.from_numpy(ref)).abs().max()) <= 2e-4 * float(abs(ref).max())
         assert abs(avg - ref_avg) <= 2e-4 * ref_avg
+
+
+@pytest.mark.parametrize("n_batches", [3, 1])
+def test_engine_test_save_path_sharded(tmp_path, n_batches):
+    """save_path with two ranks: one file, written by rank 0, holding every
+    batch in loader order (n_batches = 1: rank 1 evaluates nothing)."""
+    import numpy as np
+    d = load_npz("engine.npz")
+    prefix = str(tmp_path / "res")
+    os.environ["DSTD_TEST_SAVE"], os.environ["DSTD_TEST_BATCHES"] = prefix, str(n_batches)
+    try:
+        seen = run_world("_engine_save_body")
+    finally:
+        del os.environ["DSTD_TEST_SAVE"], os.environ["DSTD_TEST_BATCHES"]
+    assert seen[0] == ([2, 1] if n_batches == 3 else [2]) and seen[1] == ([1] if n_batches == 3 else [])
+    f = np.load(prefix + ".npz")
+    n = 4 if n_batches == 3 else 2
+    all_seqs = d["test/all_seqs"][:n]
+    assert f["target"].shape[0] == n and f["result"].shape == f["target"].shape
+    np.testing.assert_array_equal(f["target"], all_seqs.reshape(n, all_seqs.shape[1], -1, 3)[:, 10:])

@@ -238,6 +238,32 @@ def test_constant_reuse_tracks_parameter_updates():
         assert torch.equal(m5(xi), y0) and torch.equal(m5(xi), y0)
 
 
+@pytest.mark.parametrize("B", [4, 32])
+def test_graphed_forward_matches_eager(B):
+    """DSTDGCN.graphed (a HIP graph of the eval forward):
+    replays equal the eager drop-in bit for bit, for a new input copied into
+    the static one, and after an in-place parameter update (the graph refolds
+    BatchNorm and the weight images on every replay)."""
+    m, d, sd, opts = load_model("h36m")
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    x1 = synth(B, T, 22, opts["input_time_frame"], 11).to(DEV)
+    x2 = synth(B, T, 22, opts["input_time_frame"], 12).to(DEV)
+    with torch.no_grad():
+        run = m.graphed(x1)
+        y1 = run(x1).clone()
+        assert torch.equal(y1, m(x1))
+        y2 = run(x2).clone()
+        assert torch.equal(y2, m(x2))
+        assert torch.equal(run.output, y2)
+        # in-place update of an encoder's BatchNorm and a conv weight
+        m.encoders[1][1].bn.running_mean.add_(0.01)
+        m.conv_st_in.stgcn[0][0].conv_s[0].conv_f.weight.mul_(1.01)
+        y3 = run(x2).clone()
+        invalidate_native_cache(m)
+        assert torch.equal(y3, m(x2))
+        assert not torch.equal(y3, y2)
+
+
 def test_deterministic_repeat():
     m, d, _, _ = load_model("cmu")
     x = t(d["x"])
