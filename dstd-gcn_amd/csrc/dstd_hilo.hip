@@ -1594,7 +1594,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #define DSTD_TF_TPI 1
 #endif
 #ifndef DSTD_TF_HOISTW
-#define DSTD_TF_HOISTW 0
+#define DSTD_TF_HOISTW 1  // (A/B r03a: -1..2% per launch at H36M / 3DPW, tie at CMU)
 #endif
       constexpr int TPI = DSTD_TF_TPI;  // column tiles per iteration (independent chains)
       // W_rm fragments of the chunk's row tiles (HOISTW: read once, held across tiles)

@@ -30,6 +30,7 @@ back-propagates through its eval-mode modules; under torch.no_grad() (or
 with frozen parameters and input) eval runs the fused inference kernels.
 """
 import itertools
+import operator
 import math
 import weakref
 from typing import List, Tuple
@@ -97,6 +98,11 @@ class _NativeModule(nn.Module):
         super().__setstate__(state)
         _register(self)
 
+    def _apply(self, fn, recurse=True):
+        out = super()._apply(fn, recurse)
+        _bump_epoch()  # may have put new Parameter objects into _parameters
+        return out
+
 
 def invalidate_native_cache(module):
     """Force the next eval forward of every native module in ``module``'s tree
@@ -117,17 +123,38 @@ def _mark(y, *deps):
     return y
 
 
+# Structure epoch: bumped by torch's global registration hooks whenever ANY
+# module registers (or replaces) a parameter, buffer or submodule -- the
+# assignments nn.Module.__setattr__ / register_* make -- and by
+# _NativeModule._apply (.to(), .cuda(), .float() may put new Parameter objects
+# straight into _parameters).  A cached walk of a native module tree is valid
+# while the epoch it was taken at is current: an O(1) check per call instead
+# of one identity check per (module, name, tensor) entry.
+_STRUCT_EPOCH = [0]
+
+
+def _bump_epoch(*args, **kwargs):
+    _STRUCT_EPOCH[0] += 1
+
+
+for _reg in ("register_module_parameter_registration_hook", "register_module_buffer_registration_hook",
+             "register_module_module_registration_hook"):
+    getattr(torch.nn.modules.module, _reg)(_bump_epoch)
+
+
 class _TensorTree:
     """``list(root.parameters())`` and ``list(root.buffers())`` without
     torch's generator walk of the module tree (~1.3 ms for DSTDGCN's ~350
-    modules, paid per forward and per backward).  The walk is cached with
-    every (parent, name, child) edge and (module, name, tensor) entry it saw
-    and is reused only while all of them still hold -- a replaced submodule,
-    parameter or buffer invalidates it (one identity check per entry)."""
+    modules, paid per forward and per backward).  The walk is reused while the
+    structure epoch it was taken at is current (no module anywhere registered
+    or replaced a parameter, buffer or submodule since); a stale epoch falls
+    back to checking every (parent, name, child) edge and (module, name,
+    tensor) entry the walk saw, and walks again only if one of them changed."""
 
     def __init__(self):
         self.edges = self.pents = self.bents = None
         self.params = self.buffers = None
+        self.epoch = -1
 
     def _walk(self, root):
         mods, edges, seen = [], [], set()
@@ -167,9 +194,16 @@ class _TensorTree:
                 and all(m._buffers[n] is t for m, n, t in self.bents))
 
     def get(self, root):
+        if self.epoch == _STRUCT_EPOCH[0] and self.mods[0] is root:
+            return self.params, self.buffers
         if not self._valid(root):
             self._walk(root)
+        self.epoch = _STRUCT_EPOCH[0]
         return self.params, self.buffers
+
+
+_DATA_PTR = torch.Tensor.data_ptr
+_VERSION = operator.attrgetter("_version")
 
 
 def _needs_grad(*ts):
@@ -177,7 +211,14 @@ def _needs_grad(*ts):
 
 
 def _bn_modules(module):
-    return [m for m in module.modules() if isinstance(m, nn.BatchNorm1d)]
+    """The BatchNorm1d modules of ``module``'s tree; the walk (~1.4 ms on
+    DSTDGCN) is cached on the module for the current structure epoch."""
+    c = module.__dict__.get("_dstd_bn_cache")
+    if c is not None and c[0] == _STRUCT_EPOCH[0]:
+        return c[1]
+    bns = [m for m in module.modules() if isinstance(m, nn.BatchNorm1d)]
+    module.__dict__["_dstd_bn_cache"] = (_STRUCT_EPOCH[0], bns)
+    return bns
 
 
 def _bn_momentum(module):
@@ -737,9 +778,11 @@ class DSTDGCN(_NativeModule):
     # -- native parameter block ---------------------------------------------
     def _native_params(self):
         params, buffers = self._tree.get(self)
-        tensors = params + buffers
-        self._native_tensors = tensors
-        ptrs = [t.data_ptr() for t in tensors]
+        if self._native is not None and self._native[2] is params:
+            tensors = self._native_tensors
+        else:
+            tensors = self._native_tensors = params + buffers
+        ptrs = tuple(map(_DATA_PTR, tensors))
         if self._native is not None and self._native[0] == ptrs:
             return self._native[1]
         p = native.ModelParams()
@@ -758,7 +801,7 @@ class DSTDGCN(_NativeModule):
             p.enc_bn[i] = native.bn_struct(enc[1])
             p.enc_prelu[i] = native.ptr(enc[2].weight, f"encoders.{i}.2.weight")
         p.st_out = native.block_struct(self.conv_st_out.stgcn[0][0])
-        self._native = (ptrs, p)
+        self._native = (ptrs, p, params)
         return p
 
     def _native_grads(self, arena):
@@ -789,8 +832,16 @@ class DSTDGCN(_NativeModule):
             # train mode, or an eval-mode forward autograd differentiates (the
             # reference back-propagates through running-statistics BN there)
             return _ModelTrain.apply(self, False, x, *params)
-        return torch.ops.dstd.dstdgcn_forward(x, params + buffers, self._dstd_uid,
-                                              native.arith_flags(self.gc_arithmetic))
+        flags = native.arith_flags(self.gc_arithmetic)
+        if type(x) is not torch.Tensor or torch.compiler.is_compiling():
+            # tracing (torch.compile, FakeTensor): the custom op, whose inputs
+            # name every tensor the forward reads
+            return torch.ops.dstd.dstdgcn_forward(x, params + buffers, self._dstd_uid, flags)
+        # eager: the op's implementation without the dispatcher's per-call
+        # boxing of ~400 tensor arguments
+        y = torch.empty_like(x)
+        self._forward_native(x, y, arith=flags)
+        return y
 
     def forward_pair(self, x1, x2):
         """``(self(x1), self(x2))`` -- PredictionEngine.train's forward of a
@@ -868,8 +919,8 @@ class DSTDGCN(_NativeModule):
         p = self._native_params()
         flags = native.arith_flags(self.gc_arithmetic) if arith is None else arith
         try:
-            versions = tuple(tt._version for tt in self._native_tensors)
-            tag = (self._dstd_uid, self._dstd_gen, tuple(self._native[0]), n, flags, versions)
+            versions = tuple(map(_VERSION, self._native_tensors))
+            tag = (self._dstd_uid, self._dstd_gen, self._native[0], n, flags, versions)
         except RuntimeError:  # "Inference tensors do not track version counter"
             tag = None
         nbytes = L.dstd_model_workspace_bytes(n, t, v, self.num_feature, self.num_layers)

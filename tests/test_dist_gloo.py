@@ -42,7 +42,13 @@ def _worker(rank, world, port, fn_name, q):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        q.put((rank, _to_numpy(globals()[fn_name](rank, world))))
+        if ":" in fn_name:  # a body defined in another test module ("module:function")
+            import importlib
+            mod, fn = fn_name.split(":")
+            body = getattr(importlib.import_module(mod), fn)
+        else:
+            body = globals()[fn_name]
+        q.put((rank, _to_numpy(body(rank, world))))
     except Exception as e:  # surface worker failures in the parent
         q.put((rank, e))
     finally:

@@ -1,0 +1,140 @@
+"""The data-parallel path with the NATIVE model in more than one
+process: two ranks share the box's one GPU and talk over gloo on GPU tensors
+(RCCL refuses two ranks on one device; the 8-GPU RCCL run is the driver's).
+
+* config 4 (sharded eval): dstd_dist.sharded_forward of the native forward,
+  all-gathered, is bit-identical to the full-batch forward on every rank
+  (eval BatchNorm uses running statistics: no cross-sample coupling), after
+  the weights went out from rank 0 with broadcast_module;
+* config 5 (data-parallel training): one PredictionEngine.train step on each
+  rank's half of the batch, whose allreduce_grads reduces the native gradient
+  arena in place, hands Adam exactly the mean of the two ranks' own
+  single-process gradients (engine/prediction.py:198-317, 391-404)."""
+import pytest
+import torch
+
+from conftest import group, load_npz
+from test_dist_gloo import run_world
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _h36m_model():
+    from model import get_model
+    d = load_npz("model_h36m.npz")
+    opts = {k[4:]: d[k].item() for k in d.files if k.startswith("opt/")}
+    m = get_model("dstdgcn", dstdgcn=opts)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in group(d, "sd/").items()})
+    return m.to(DEV).eval(), opts
+
+
+def _sharded_native_body(rank, world):
+    import dstd_dist as D
+    torch.cuda.set_device(0)
+    m, opts = _h36m_model()
+    if rank != 0:  # rank 1 starts from other weights; the broadcast must fix them
+        with torch.no_grad():
+            for p in m.parameters():
+                p.mul_(0.5)
+    D.broadcast_module(m, src=0)
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(11, T, 22, 3, generator=g)  # ragged shards: 6 + 5
+    x[:, opts["input_time_frame"]:] = x[:, opts["input_time_frame"] - 1:opts["input_time_frame"]]
+    x = x.to(DEV)
+    with torch.no_grad():
+        y_sh = D.sharded_forward(m, x)
+        y_full = m(x)
+    torch.cuda.synchronize()
+    return {"equal": bool(torch.equal(y_sh, y_full)), "y": y_sh.cpu(),
+            "alias": m.conv_st_in.stgcn[0][0].A_s.data_ptr() == m.conv_st_in.stgcn[0][0].R_s.data_ptr()}
+
+
+def test_sharded_native_forward_equals_full_batch():
+    res = run_world("test_gpu_dist:_sharded_native_body")
+    for r in (0, 1):
+        assert res[r]["equal"], r
+    assert torch.equal(res[0]["y"], res[1]["y"])
+
+
+def _model_3dpw():
+    from model import get_model
+    from model.dstdgcn import DSTDGCB
+    d = load_npz("engine.npz")
+    opts = dict(input_channels=6, input_time_frame=10, output_time_frame=30, st_gcnn_dropout=0.0,
+                joints_to_consider=23, num_feature=64, num_layers=5, layout="3dpw")
+    m = get_model("dstdgcn", dstdgcn=opts)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in group(d, "train/sd0/").items()})
+    m = m.to(DEV)
+    for b in m.modules():  # the CPU fixture's A_s/R_s alias (test_gpu_train._realias)
+        if isinstance(b, DSTDGCB):
+            b.A_s.data = b.R_s.data
+    return m.train(), d
+
+
+def _dp_train_body(rank, world):
+    import torch.distributed as dist
+
+    import dstd_dist as D
+    from engine import PredictionEngine
+    torch.cuda.set_device(0)
+
+    class _Log:
+        def info(self, *a, **k):
+            pass
+
+    cfg = dict(learn=dict(opt="adam", lr=3e-3, weight_decay=0, gamma=0.9, step_size=5),
+               loss=dict(joint=["jl2", 1]), n_out=1, transform="tsc", use_weight=False, inverse=True)
+    d = load_npz("engine.npz")
+    batch = tuple(D.shard(torch.from_numpy(d[f"train/{n}0"]), world, rank).contiguous()
+                  for n in ("inp", "inv", "seq", "seq"))
+
+    # (1) this rank's own single-process gradient of its shard: the engine's
+    # step with the all-reduce left out (the process group is up, so take the
+    # single-process branch by hand)
+    m1, _ = _model_3dpw()
+    eng1 = PredictionEngine(cfg, m1, _Log())
+    local = {}
+    eng1.optimizer.step = lambda: local.update(
+        {n: p.grad.detach().clone() for n, p in m1.named_parameters() if p.grad is not None})
+    import engine.prediction as EP
+    saved_world = EP._world
+    EP._world = lambda: (0, 1)
+    try:
+        eng1.train([batch], 0, max_iter=1)
+    finally:
+        EP._world = saved_world
+
+    # (2) the data-parallel step: allreduce_grads over the native arena
+    m2, _ = _model_3dpw()
+    eng2 = PredictionEngine(cfg, m2, _Log())
+    seen = {}
+    step = eng2.optimizer.step
+
+    def capture():
+        seen.update({n: p.grad.detach().clone() for n, p in m2.named_parameters() if p.grad is not None})
+        seen["_arena"] = getattr(m2, "_dstd_grad_arena", None) is not None and all(
+            p.grad._base is m2._dstd_grad_arena.buf for p in m2.parameters() if p.grad is not None)
+        return step()
+
+    eng2.optimizer.step = capture
+    eng2.train([batch], 0, max_iter=1)
+    # the mean of the two ranks' own gradients, over the same gloo group
+    names = sorted(local)
+    flat = torch.cat([local[n].reshape(-1) for n in names])
+    both = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(both, flat)
+    mean = (both[0] + both[1]) / 2
+    got = torch.cat([seen[n].reshape(-1) for n in names])
+    return {"equal": bool(torch.equal(got, mean)), "maxdiff": float((got - mean).abs().max()),
+            "arena": bool(seen["_arena"]), "n": len(names),
+            "differs": bool(not torch.equal(both[0], both[1]))}
+
+
+def test_dp_training_step_averages_native_arena():
+    res = run_world("test_gpu_dist:_dp_train_body")
+    for r in (0, 1):
+        assert res[r]["arena"], "the engine's gradients were not slices of the native arena"
+        assert res[r]["differs"], "the two shards gave the same gradient: the test would prove nothing"
+        assert res[r]["equal"], (r, res[r]["maxdiff"])

@@ -261,7 +261,9 @@ def test_fast_eval_mode_backward():
             r.append((float(np.abs(named[k].grad.double().cpu().numpy() - ref).max()) / noise, k))
     r.sort(reverse=True)
     v = np.array([a for a, _ in r])
-    assert np.median(v) <= 1.5 and np.quantile(v, 0.9) <= 3.0 and v.max() <= 12.0, r[:8]
+    assert np.median(v) <= 1.5 and np.quantile(v, 0.9) <= 3.0, r[:8]
+    from test_gpu_train import check_tail
+    check_tail(r)
 
 
 def test_fast_model_in_the_engine():

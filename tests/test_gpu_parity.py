@@ -326,7 +326,9 @@ def test_eval_mode_backward_matches_oracle():
     keys = [k for k, p in P.items() if p.requires_grad]
     r = _grad_ratios(named, P, (P32, G32), keys)
     vals = np.array([v for v, _ in r])
-    assert np.median(vals) <= 1.5 and np.quantile(vals, 0.9) <= 3.0 and vals.max() <= 12.0, r[:8]
+    assert np.median(vals) <= 1.5 and np.quantile(vals, 0.9) <= 3.0, r[:8]
+    from test_gpu_train import check_tail
+    check_tail(r)
     xn = max(float(np.abs(x32.grad.double().numpy() - x64.grad.numpy()).max()),
              float(np.abs(xg32.grad.double().cpu().numpy() - x64.grad.numpy()).max()),
              1e-4 * float(np.abs(x64.grad.numpy()).max()))

@@ -10,12 +10,17 @@ Tolerances
                             fp32 error of two other fp32 implementations (the
                             reference's g32err and the CPU oracle in fp32) --
                             the 21-op stack is chaotic in fp32:
-                            median <= 1.5, 90th percentile <= 3, max <= 12
+                            median <= 1.5, 90th percentile <= 3; every
+                            tensor above 3x printed and required to be a
+                            global-sum gradient (GLOBAL_SUM: scalars and conv
+                            biases), those within 12x
                             (scripts/grad_noise.py prints the table)
   5-step loss curve       : within twice the reference's own fp32 deviation
                             from its fp64 curve
 """
 import os
+
+import re
 
 import numpy as np
 import pytest
@@ -214,6 +219,27 @@ def _bn_of(module, key):
 
 
 # ---- whole model: one engine step vs the reference's fp64 gradients ---------
+# Gradients that are one sum over every position of the batch: the scalars
+# (alpha_sm / alpha_tm, the PReLU slopes) and the conv biases (conv_f /
+# conv_m1 / conv_m2 / conv_rm / residual conv, each summed over all (n, t, v)
+# or (n, t, v, w)).  Their fp32 round-off is the heavy tail of the 21-op
+# stack's chaos: the reference's own fp32 run and the fp32
+# oracle land several times apart on them.  Every other tensor (conv weights,
+# W_s, R_s, R_t, BatchNorm weights and biases) must stay within 3x the fp32
+# noise of two other implementations; a global-sum tensor within 12x.
+GLOBAL_SUM = re.compile(r"(alpha_sm|alpha_tm|prelu\.weight|encoders\.\d+\.2\.weight|"
+                        r"conv_(f|m1|m2|rm)\.bias|residual\.0\.bias)$")
+
+
+def check_tail(ratios, bar=3.0, global_bar=12.0):
+    """ratios: (error / fp32 noise, tensor name).  Prints every tensor above
+    `bar`; those must all be global-sum gradients (GLOBAL_SUM), within
+    `global_bar`."""
+    above = sorted(((v, k) for v, k in ratios if v > bar), reverse=True)
+    print(f"gradient error / fp32 noise above {bar}x ({len(above)} of {len(ratios)}):",
+          [(round(v, 2), k) for v, k in above])
+    assert all(GLOBAL_SUM.search(k) for _, k in above), [(v, k) for v, k in above if not GLOBAL_SUM.search(k)]
+    assert all(v <= global_bar for v, _ in above), above[:4]
 def _realias(model):
     """Module.to() converts each parameter separately and so splits the
     A_s/R_s storage alias (the reference's runner does the same with
@@ -264,12 +290,11 @@ def test_model_step_gradients_vs_reference_fp64():
         ratios.append((err / noise, k, err, noise, scale))
     ratios.sort(reverse=True)
     r = np.array([x[0] for x in ratios])
-    # as accurate as a typical fp32 implementation, with the same heavy tail
-    # (the CPU oracle's own fp32 error reaches ~9x the reference's on the
-    # global-sum gradients: alpha_tm, conv_rm.bias)
+    # as accurate as a typical fp32 implementation (the CPU oracle's own fp32
+    # error reaches ~9x the reference's on global-sum gradients)
     assert np.median(r) <= 1.5, (np.median(r), ratios[:8])
     assert np.quantile(r, 0.9) <= 3.0, (np.quantile(r, 0.9), ratios[:8])
-    assert r.max() <= 12.0, ratios[:8]
+    check_tail([(x[0], x[1]) for x in ratios])
     assert named["conv_st_in.stgcn.0.0.A_s"].grad is None
 
 
