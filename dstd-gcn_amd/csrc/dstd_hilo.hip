@@ -764,29 +764,58 @@ struct TemporalStage {
   int rng[3];
 };
 
-template <int T, int EPI, int C, int VB>
-__device__ __forceinline__ void stage_temporal(const TemporalHLArgs& a, TemporalStage<T, EPI, C, VB>& st, int tid, int nt) {
+template <int T, int EPI, int C, int VB, int NTH>
+__device__ __forceinline__ void stage_temporal(const TemporalHLArgs& a, TemporalStage<T, EPI, C, VB>& st, int tid,
+                                               int oz = 0) {
   using S = TemporalStage<T, EPI, C, VB>;
   const bool has_pq = a.pq != nullptr;
-  for (int i = tid; i < S::WIMG; i += nt) st.wl[i] = a.wimg[i];
-  if (has_pq)
-    for (int i = tid; i < S::PIMG; i += nt) st.pql[i] = a.pqimg[i];
-  if constexpr (S::use_bn) {
-    // folded BN vectors [V][C] -> [c/4][v]
-    for (int i = tid; i < a.V * 4 * S::NCT; i += nt) {
-      const int v = i / (4 * S::NCT), c4 = i % (4 * S::NCT);
-      float e[2][4];
+  // every global load is issued before the first LDS write (one memory
+  // round trip instead of one per loop trip)
+  constexpr int NW = cdiv(S::WIMG, NTH), NP = cdiv(S::PIMG, NTH);
+  constexpr int NB = S::use_bn ? cdiv(VB * 4 * S::NCT, NTH) : 0;
+  uint4 wv[NW], pv[NP];
+  float4 bs[NB > 0 ? NB : 1], bh[NB > 0 ? NB : 1];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        e[0][q] = 4 * c4 + q < C ? a.bn_s[v * C + 4 * c4 + q] : 0.f;
-        e[1][q] = 4 * c4 + q < C ? a.bn_h[v * C + 4 * c4 + q] : 0.f;
-      }
-      st.bnl[0][c4 * a.V + v] = make_float4(e[0][0], e[0][1], e[0][2], e[0][3]);
-      st.bnl[1][c4 * a.V + v] = make_float4(e[1][0], e[1][1], e[1][2], e[1][3]);
+  // (oz: an opaque zero from a caller that stages once per loop trip, so
+  // that these loop-invariant loads are not hoisted out of its loop)
+  for (int it = 0; it < NW; ++it) wv[it] = a.wimg[min(tid + it * NTH + oz, S::WIMG - 1)];
+#pragma unroll
+  for (int it = 0; it < NP; ++it) pv[it] = has_pq ? a.pqimg[min(tid + it * NTH + oz, S::PIMG - 1)] : make_uint4(0, 0, 0, 0);
+  const int nbn = a.V * 4 * S::NCT;
+  if constexpr (S::use_bn) {
+    static_assert(C % 4 == 0, "folded BN rows load as float4");
+    // folded BN vectors [V][C] -> [c/4][v]
+#pragma unroll
+    for (int it = 0; it < NB; ++it) {
+      const int i = min(tid + it * NTH + oz, nbn - 1);
+      const int v = i / (4 * S::NCT), c4 = i - v * (4 * S::NCT);
+      bs[it] = ld4(a.bn_s + v * C + 4 * c4);
+      bh[it] = ld4(a.bn_h + v * C + 4 * c4);
     }
   }
-  if (tid < 16 * S::NCT) st.bfl[tid] = tid < C ? a.bf[tid] : 0.f;
-  if (tid < 8) st.bql[tid] = has_pq ? a.pqb[tid >> 1][tid & 1] : 0.f;
+  const float bf = tid < 16 * S::NCT && tid < C ? a.bf[tid] : 0.f;
+  const float bq = tid < 8 && has_pq ? a.pqb[tid >> 1][tid & 1] : 0.f;
+#pragma unroll
+  for (int it = 0; it < NW; ++it)
+    if (tid + it * NTH < S::WIMG) st.wl[tid + it * NTH] = wv[it];
+  if (has_pq) {
+#pragma unroll
+    for (int it = 0; it < NP; ++it)
+      if (tid + it * NTH < S::PIMG) st.pql[tid + it * NTH] = pv[it];
+  }
+  if constexpr (S::use_bn) {
+#pragma unroll
+    for (int it = 0; it < NB; ++it) {
+      const int i = tid + it * NTH;
+      if (i < nbn) {
+        const int v = i / (4 * S::NCT), c4 = i - v * (4 * S::NCT);
+        st.bnl[0][c4 * a.V + v] = bs[it];
+        st.bnl[1][c4 * a.V + v] = bh[it];
+      }
+    }
+  }
+  if (tid < 16 * S::NCT) st.bfl[tid] = bf;
+  if (tid < 8) st.bql[tid] = bq;
   if (tid == 0) {
     st.scl[0] = *a.wscale;
     st.scl[1] = has_pq ? *a.pqscale : 0.f;
@@ -1075,7 +1104,7 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
   using SM = SlotMap<T, false>;
   constexpr int SL = SM::SL, NS = SM::NS, NUT = cdiv(T, 16);
   __shared__ TemporalStage<T, EPI, C, 32> st;
-  stage_temporal<T, EPI, C, 32>(a, st, threadIdx.x, temporal_nt<T, C>());
+  stage_temporal<T, EPI, C, 32, temporal_nt<T, C>()>(a, st, threadIdx.x);
   __syncthreads();
   int uend;
   const int u0 = unit_range(a.B * a.V, uend);
@@ -1534,27 +1563,59 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         El[T * SE + i] = 1.f;
         Fl[T * SE + i] = 1.f;
       }
-      int bad = 0;
-      for (int i = tid; i < T * V; i += NT) {
-        const int t = i / V, v = i % V;
-        const float4 q4 = ld4(pqb + t * L.st + v * L.sv);  // (P_0, P_1, Q_0, Q_1)
-        const float ep0 = C2 * q4.x, ep1 = C2 * q4.y, eq0 = -C2 * q4.z, eq1 = -C2 * q4.w;
-        bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
-        El[t * SE + v] = __builtin_amdgcn_exp2f(ep0);
-        El[t * SE + V + v] = __builtin_amdgcn_exp2f(ep1);
-        Fl[t * SE + v] = __builtin_amdgcn_exp2f(eq0);
-        Fl[t * SE + V + v] = __builtin_amdgcn_exp2f(eq1);
+      // every global load of the prologue is issued before the first LDS
+      // write that needs one (one memory round trip, not one per loop trip)
+      constexpr int FULL = NS * 2 * 64;  // uint4 per row tile (full K-steps)
+      constexpr int NPQ = cdiv(T * V, NT), NWF = cdiv(RTC * FULL, NT), NWT = TAIL ? cdiv(RTC * 64, NT) : 0;
+      constexpr int NAS = cdiv(T * T, NT);
+      float4 q4[NPQ];
+      uint4 wf[NWF], wt[NWT > 0 ? NWT : 1];
+      float av[NAS];
+      // (the P/Q and Astat loads do not depend on the chunk: an opaque zero
+      // in their index keeps hipcc from hoisting them out of the chunk loop,
+      // where they would stay live through phase 2 and spill)
+      const int oz = Gm::NCHUNK > 1 ? opaque_zero() : 0;
+#pragma unroll
+      for (int it = 0; it < NPQ; ++it) {
+        const int i = min(tid + it * NT + oz, T * V - 1);  // clamped: no branch around the load
+        const int t = i / V, v = i - t * V;
+        q4[it] = ld4(pqb + t * L.st + v * L.sv);  // (P_0, P_1, Q_0, Q_1)
       }
       {
         const uint4* wg = j.wimg[0];
-        constexpr int FULL = NS * 2 * 64;  // uint4 per row tile (full K-steps)
-        for (int i = tid; i < RTC * FULL; i += NT) wl[i] = wg[rt0 * FULL + i];
-        if constexpr (TAIL)
-          for (int i = tid; i < RTC * 64; i += NT) wl[RTC * FULL + i] = wg[Gm::RTG * FULL + rt0 * 64 + i];
+#pragma unroll
+        for (int it = 0; it < NWF; ++it) wf[it] = wg[rt0 * FULL + min(tid + it * NT, RTC * FULL - 1)];
+#pragma unroll
+        for (int it = 0; it < NWT; ++it) wt[it] = wg[Gm::RTG * FULL + rt0 * 64 + min(tid + it * NT, RTC * 64 - 1)];
       }
-      for (int i = tid; i < T * T; i += NT) asl[i] = j.astat[0][i];
+#pragma unroll
+      for (int it = 0; it < NAS; ++it) av[it] = j.astat[0][min(tid + it * NT + oz, T * T - 1)];
+      const float bv = tid < 16 * RTC && 16 * rt0 + tid < V ? j.bias[0][16 * rt0 + tid] : 0.f;
+      int bad = 0;
+#pragma unroll
+      for (int it = 0; it < NPQ; ++it) {
+        const int i = tid + it * NT;
+        if (i < T * V) {
+          const int t = i / V, v = i - t * V;
+          const float ep0 = C2 * q4[it].x, ep1 = C2 * q4[it].y, eq0 = -C2 * q4[it].z, eq1 = -C2 * q4[it].w;
+          bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
+          El[t * SE + v] = __builtin_amdgcn_exp2f(ep0);
+          El[t * SE + V + v] = __builtin_amdgcn_exp2f(ep1);
+          Fl[t * SE + v] = __builtin_amdgcn_exp2f(eq0);
+          Fl[t * SE + V + v] = __builtin_amdgcn_exp2f(eq1);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < NWF; ++it)
+        if (tid + it * NT < RTC * FULL) wl[tid + it * NT] = wf[it];
+#pragma unroll
+      for (int it = 0; it < NWT; ++it)
+        if (tid + it * NT < RTC * 64) wl[RTC * FULL + tid + it * NT] = wt[it];
+#pragma unroll
+      for (int it = 0; it < NAS; ++it)
+        if (tid + it * NT < T * T) asl[tid + it * NT] = av[it];
       if (tid == 0) asl[T * T] = 0.f;
-      if (tid < 16 * RTC) bsl[tid] = 16 * rt0 + tid < V ? j.bias[0][16 * rt0 + tid] : 0.f;
+      if (tid < 16 * RTC) bsl[tid] = bv;
       const bool sep = __syncthreads_or(bad) == 0;
       __syncthreads();  // (__syncthreads_or alone did not order the LDS writes above before the reads below)
       if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0)
@@ -1735,7 +1796,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
 #endif
       // ---- phase 2: the stage, then the chunk's GC units ----
-      stage_temporal<T, EPI, C, V>(a, st, tid, NT);
+      stage_temporal<T, EPI, C, V, NT>(a, st, tid, Gm::NCHUNK > 1 ? opaque_zero() : 0);
       __syncthreads();
       const int ub = n * V + v0;
       auto load_adj = [&](int u, int s, uint4 (&bh)[NUT], uint4 (&bo)[NUT]) {

@@ -115,7 +115,9 @@ def lib():
         vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
         L.dstd_source_hash.restype = ctypes.c_char_p
         built, tree = L.dstd_source_hash().decode(), source_hash()
-        if tree is not None and built != tree:
+        # DSTD_AB_FOREIGN_LIB=1: A/B tooling (scripts/ab_kernels.py) loading a
+        # library built from an earlier revision on purpose
+        if tree is not None and built != tree and os.environ.get("DSTD_AB_FOREIGN_LIB") != "1":
             raise RuntimeError(f"{LIB_PATH} was built from other sources (hash {built}, this tree {tree}): "
                                "rebuild with `make -C dstd-gcn_amd`")
         L.dstd_version.restype = ctypes.c_char_p
