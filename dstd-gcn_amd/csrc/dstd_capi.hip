@@ -14,6 +14,18 @@
 
 using namespace dstd;
 
+#ifdef DSTD_SPRE_CHECK
+#include <stdio.h>
+// (debug builds: the planes phase 3 left in adj_s against a k_adj_hl<0> run
+// of the same block into a private buffer -- mismatching halves and the first)
+__global__ void k_cmp_u16(const uint16_t* a, const uint16_t* b, size_t n, unsigned* out) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    if (a[i] != b[i]) {
+      atomicAdd(&out[0], 1u);
+      atomicMin(&out[1], (unsigned)i);
+    }
+}
+#endif
 namespace {
 
 constexpr int kMaxT = 128;  // the generic kernels cover T <= 128 (adjacency row groups past 112)
@@ -94,10 +106,12 @@ struct BlockFold {
   float* hl_rbias;  // [2T + V]: fused conv_rm biases (HLJob::bias_out) of rms0, rms1, rmt
 };
 
-// Which GC launches of a block run the split-f16 kernels; tf: the temporal
-// one with its adjacency built in LDS (k_temporal_fused, no k_adj_hl<1>).
+// Which GC launches of a block run the split-f16 kernels; tf / sf: the
+// temporal / spatial one with its adjacency built in LDS (k_temporal_fused, no
+// k_adj_hl<1>; k_spatial_fused, no k_adj_hl<0>).
 struct BlockHL {
-  bool s, t, tf;
+  bool s, t, tf, sf;
+  bool s_pre = false;  // the spatial adjacency planes were built by the previous block's temporal launch
 };
 
 struct BlockScratch {
@@ -253,12 +267,15 @@ struct BlockTail {
   const float* bn_h;
   const float* prelu;
   const dstd_block_params* next;  // next block: its spatial P/Q are produced here
+  // the next block's spatial adjacency planes are built here too (k_temporal_fused phase 3)
+  const BlockFold* next_f = nullptr;
+  bool next_adj = false;
 };
 
 // Split-f16 GC kernels (dstd_hilo.hip) where the shape has them, unless the
 // call asks for exact fp32 (DSTD_FWD_EXACT_FP32).
 BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V, bool exact) {
-  BlockHL r{false, false, false};
+  BlockHL r{false, false, false, false, false};
   if (exact) return r;
   r.s = spatial_hl_supported(T, V) &&
         ((p->cin == 64 && p->cout == 64) || (p->cin == 6 && p->cout == 64) || (p->cin == 64 && p->cout == 3));
@@ -268,6 +285,12 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V
          (p->cout == 3 && (tail.epi == TEPI_OUT || tail.epi == TEPI_RAW) && !tail.next));
 #ifndef DSTD_NO_TFUSED
   r.tf = r.t && temporal_fused_supported(T, V);
+#endif
+#ifdef DSTD_SFUSED  // (opt-in: measured slower than k_adj_hl<0> + k_spatial_hl)
+  r.sf = r.s && spatial_fused_supported(T, V);
+#ifdef DSTD_SF_MASK  // (bisection builds: bit 0 64->64, bit 1 6->64, bit 2 64->3)
+  r.sf = r.sf && ((DSTD_SF_MASK >> (p->cin == 6 ? 1 : p->cout == 3 ? 2 : 0)) & 1);
+#endif
 #endif
   return r;
 }
@@ -345,10 +368,11 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     aa.out_sN = 2L * T * aa.ldo;
     aa.out_sG = (long)T * aa.ldo;
   }
-  pf.begin(DSTD_KIND_ADJ_S, s);
-  hipError_t e;
+  hipError_t e = hipSuccess;
+  AdjHLArgs ah{};
+  const bool adj_launch = !hl.sf && !hl.s_pre;
+  if (adj_launch) pf.begin(DSTD_KIND_ADJ_S, s);
   if (hl.s) {
-    AdjHLArgs ah{};
     ah.pq = aa.pq;
     ah.pql = aa.pql;
     ah.B = B;
@@ -373,11 +397,43 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
         ah.mb[g][1] = p->conv_s[g].bm2;
       }
     }
-    e = launch_adj_hl(ah, 0, T, V, s);
+    // else built in LDS by k_spatial_fused (step 2) or already in sc.adj_s (s_pre)
+    if (adj_launch) e = launch_adj_hl(ah, 0, T, V, s);
+#ifdef DSTD_SPRE_CHECK
+    if (hl.s_pre) {
+      const size_t n = (size_t)2 * adj_s_floats(B, T, V);  // halves
+      uint16_t* ref = nullptr;
+      unsigned* cnt = nullptr;
+      (void)hipMalloc(&ref, n * 2);
+      (void)hipMalloc(&cnt, 8);
+      const unsigned init[2] = {0u, 0xffffffffu};
+      (void)hipMemcpy(cnt, init, 8, hipMemcpyHostToDevice);
+      AdjHLArgs ac = ah;
+      ac.out = ref;
+      (void)hipStreamSynchronize(s);
+      (void)launch_adj_hl(ac, 0, T, V, s);
+      hipLaunchKernelGGL(k_cmp_u16, dim3(1024), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(sc.adj_s), ref,
+                         (size_t)B * ah.out_sN, cnt);
+      unsigned h[2];
+      (void)hipMemcpy(h, cnt, 8, hipMemcpyDeviceToHost);
+      uint16_t va = 0, vb = 0;
+      if (h[0]) {
+        (void)hipMemcpy(&va, reinterpret_cast<const uint16_t*>(sc.adj_s) + h[1], 2, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(&vb, ref + h[1], 2, hipMemcpyDeviceToHost);
+      }
+      const long i = h[1], per_n = ah.out_sN, per_g = ah.out_sG, ncol = V * hl_sl_spatial(V);
+      fprintf(stderr, "spre check cin %d cout %d: %u of %ld halves differ; first %ld (n %ld g %ld t %ld plane %ld col %ld) %04x vs %04x\n",
+              p->cin, p->cout, h[0], (long)B * per_n, h[0] ? i : -1L, h[0] ? i / per_n : -1L,
+              h[0] ? i % per_n / per_g : -1L, h[0] ? i % per_g / (2 * ncol) : -1L,
+              h[0] ? i % (2 * ncol) / ncol : -1L, h[0] ? i % ncol : -1L, va, vb);
+      (void)hipFree(ref);
+      (void)hipFree(cnt);
+    }
+#endif
   } else {
     e = launch_adj(aa, s);
   }
-  pf.end(s);
+  if (adj_launch) pf.end(s);
   if (e != hipSuccess) return e;
 
   // (2) spatial GC + bn + residual + prelu, P_t/Q_t of h
@@ -414,7 +470,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ha.pqb[1] = p->conv_t.bm2;
     ha.pq = sc.pq_t;
     pf.begin(DSTD_KIND_SPATIAL, s);
-    e = launch_spatial_hl(ha, s);
+    e = hl.sf ? launch_spatial_fused(ha, ah, s) : launch_spatial_hl(ha, s);
     pf.end(s);
     if (e != hipSuccess) return e;
   } else {
@@ -538,8 +594,30 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
       ht.pqb[3] = q->conv_s[1].bm2;
       ht.pq = sc.pq_s;
     }
+    // the next block's spatial adjacency (its launch_adj_hl mode 0 arguments)
+    AdjHLArgs sn{};
+    if (tail.next_adj) {
+      const dstd_block_params* q = tail.next;
+      const BlockFold& nf = *tail.next_f;
+      const int ncol = V * hl_sl_spatial(V);
+      sn.pq = sc.pq_s;
+      sn.pql = pq_layout_vt(8, T, V);
+      sn.B = B;
+      sn.ngroups = 2;
+      for (int g = 0; g < 2; ++g) {
+        sn.p_ch[g] = 4 * g;
+        sn.wimg[g] = nf.hl_rms[g];
+        sn.wscale[g] = hls(nf, 5 + g);
+        sn.bias[g] = nf.hl_rbias + g * T;
+        sn.astat[g] = nf.astat_s + g * V * V;
+      }
+      sn.alpha = q->alpha_sm;
+      sn.out = reinterpret_cast<uint16_t*>(sc.adj_s);
+      sn.out_sG = 2L * T * ncol;  // halves
+      sn.out_sN = 2 * sn.out_sG;
+    }
     pf.begin(DSTD_KIND_TEMPORAL, s);
-    e = hl.tf ? launch_temporal_fused(ht, aht, s) : launch_temporal_hl(ht, s);
+    e = hl.tf ? launch_temporal_fused(ht, aht, tail.next_adj ? &sn : nullptr, s) : launch_temporal_hl(ht, s);
     pf.end(s);
     return e;
   }
@@ -923,6 +1001,17 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
     hls[b] = block_hl(blk[b], tails[b], T, V, exact);
     add_block_hl_jobs(hj, blk[b], *fold[b], tails[b], hls[b], T, V);
   }
+#ifndef DSTD_NO_SPRE
+  // a block's spatial adjacency from the previous block's fused temporal
+  // launch (phase 3), which writes the P/Q it is built from
+  for (int b = 1; b < NB; ++b)
+    if (hls[b].s && hls[b - 1].tf && blk[b - 1]->cout == 64) {
+      hls[b].s_pre = true;
+      hls[b].sf = false;
+      tails[b - 1].next_f = fold[b];
+      tails[b - 1].next_adj = true;
+    }
+#endif
 
   // input prep: x6 = cat(x, x - x[:, -1]) and block-0 spatial P/Q (:298-305)
   PQArgs pa{};

@@ -302,8 +302,16 @@ bool spatial_hl_supported(int T, int V);
 bool temporal_hl_supported(int T, int V);
 // the temporal GC with its adjacency built in LDS (k_temporal_fused): g as for
 // launch_temporal_hl (g.adj unused), j the adjacency's inputs as for
-// launch_adj_hl mode 1 (j.out unused); hipErrorNotSupported off its shapes
-hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, hipStream_t s);
+// launch_adj_hl mode 1 (j.out unused); sn (optional, C = 64 with g.pq): the
+// next block's spatial adjacency as for launch_adj_hl mode 0 with sn->pq ==
+// g.pq, built by the same launch after the units (no launch_adj_hl of it);
+// hipErrorNotSupported off its shapes
+hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn, hipStream_t s);
 bool temporal_fused_supported(int T, int V);
+// the spatial GC with both graphs' adjacency built in LDS (k_spatial_fused): g
+// as for launch_spatial_hl (g.adj unused), j as for launch_adj_hl mode 0
+// (j.out unused); hipErrorNotSupported off its shapes
+hipError_t launch_spatial_fused(const SpatialHLArgs& g, const AdjHLArgs& j, hipStream_t s);
+bool spatial_fused_supported(int T, int V);
 
 }  // namespace dstd

@@ -42,7 +42,10 @@ extern "C" int dstd_debug_w(unsigned* host) {
 }
 #endif
 #ifdef DSTD_STAMPS
-__device__ unsigned long long g_tl_hl[2][2048][4];
+// modes: 0 k_adj_hl<0>, 1 k_adj_hl<1>, 2 k_temporal_fused phase 3 (start,
+// E/F ready, tiles issued, stores drained), 3 k_temporal_fused C = 64 (entry,
+// chunk 0 phase 1 done, units done, exit)
+__device__ unsigned long long g_tl_hl[4][2048][4];
 #define TLH(m, i) \
   if (threadIdx.x == 0 && blockIdx.x < 2048) g_tl_hl[m][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();
 #else
@@ -99,6 +102,7 @@ __device__ __forceinline__ int unit_range(int nunits, int& uend) {
 // stays exact across the loop back-edge (with branchy loads / stores it
 // waited for the previous unit's stores at the top of every unit).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t OOB = 0x80000000u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
@@ -354,58 +358,109 @@ __device__ __forceinline__ void stage_bnC(float4* dst, const float* src, int V, 
   }
 }
 
+// The stage (LDS images) and the unit loop of the spatial GC, shared by
+// k_spatial_hl (adjacency planes from HBM, written by k_adj_hl<0>) and
+// k_spatial_fused (planes built in LDS by the same launch).
 template <int V, int CIN, int COUT>
-__global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE, DSTD_HL_WPE))) void k_spatial_hl(
-    SpatialHLArgs a) {
+struct SpatialStage {
+  static constexpr bool RES = CIN != COUT;
+  static constexpr int KSI = cdiv(CIN, 32), NCT = cdiv(COUT, 16), KSO = cdiv(NCT, 2);
+  static constexpr int WIMG = NCT * KSI * 2 * 64, PIMG = KSO * 2 * 64;
+  uint4 wl[RES ? 3 : 2][WIMG];  // conv (graphs 0, 1), residual conv
+  uint4 pql[PIMG];
+  float4 bnl[RES ? 4 : 2][4 * NCT * V];
+  float bfl[3][16 * NCT];
+  float bql[4];
+  float scl[4];
+  int rng[3];
+};
+
+// every global load before the first LDS write (one memory round trip)
+template <int V, int CIN, int COUT, int NTH>
+__device__ __forceinline__ void stage_spatial(const SpatialHLArgs& a, SpatialStage<V, CIN, COUT>& st, int tid) {
+  using S = SpatialStage<V, CIN, COUT>;
+  constexpr bool RES = S::RES;
+  constexpr int NCT = S::NCT, WIMG = S::WIMG, PIMG = S::PIMG, NIMG = (RES ? 3 : 2) * WIMG;
+  constexpr int NW = cdiv(NIMG, NTH), NP = cdiv(PIMG, NTH), NBN = cdiv(V * 4 * NCT, NTH);
+  constexpr int NBV = RES ? 4 : 2;
+  uint4 wv[NW], pv[NP];
+  float4 bv[NBV][NBN];
+#pragma unroll
+  for (int it = 0; it < NW; ++it) {
+    const int i = min(tid + it * NTH, NIMG - 1);
+    wv[it] = a.wimg[i / WIMG][i % WIMG];
+  }
+#pragma unroll
+  for (int it = 0; it < NP; ++it) pv[it] = a.pqimg[min(tid + it * NTH, PIMG - 1)];
+  const float* bsrc[4] = {a.bn_s, a.bn_h, a.rbn_s, a.rbn_h};
+#pragma unroll
+  for (int q = 0; q < NBV; ++q)
+#pragma unroll
+    for (int it = 0; it < NBN; ++it) {
+      const int i = min(tid + it * NTH, V * 4 * NCT - 1);
+      const int v = i / (4 * NCT), c4 = i % (4 * NCT);
+      if constexpr (COUT % 4 == 0) {
+        bv[q][it] = ld4(bsrc[q] + v * COUT + 4 * c4);
+      } else {  // thin output (3 channels): element loads, zero past COUT
+        float e[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) e[r] = 4 * c4 + r < COUT ? bsrc[q][v * COUT + 4 * c4 + r] : 0.f;
+        bv[q][it] = make_float4(e[0], e[1], e[2], e[3]);
+      }
+    }
+  const int nbf = (RES ? 3 : 2) * 16 * NCT;
+  static_assert((RES ? 3 : 2) * 16 * NCT <= NTH, "one conv bias per thread");
+  const float bf = tid < nbf && tid % (16 * NCT) < COUT ? a.bf[tid / (16 * NCT)][tid % (16 * NCT)] : 0.f;
+#pragma unroll
+  for (int it = 0; it < NW; ++it) {
+    const int i = tid + it * NTH;
+    if (i < NIMG) st.wl[i / WIMG][i % WIMG] = wv[it];
+  }
+#pragma unroll
+  for (int it = 0; it < NP; ++it)
+    if (tid + it * NTH < PIMG) st.pql[tid + it * NTH] = pv[it];
+#pragma unroll
+  for (int q = 0; q < NBV; ++q)
+#pragma unroll
+    for (int it = 0; it < NBN; ++it) {
+      const int i = tid + it * NTH;
+      if (i < V * 4 * NCT) {
+        const int v = i / (4 * NCT), c4 = i % (4 * NCT);
+        st.bnl[q][c4 * V + v] = bv[q][it];
+      }
+    }
+  if (tid < nbf) st.bfl[tid / (16 * NCT)][tid % (16 * NCT)] = bf;
+  if (tid < 4) st.bql[tid] = a.pqb[tid >> 1][tid & 1];
+  if (tid == 0) {
+    st.scl[0] = *a.wscale[0];
+    st.scl[1] = *a.wscale[1];
+    st.scl[2] = *a.pqscale;
+    st.scl[3] = RES ? *a.wscale[2] : 0.f;
+    // range: |W_f|_inf and max|b_f| over both graphs, the planes' shared shift
+    st.rng[0] = fexp_bits(__float_as_uint(fmaxf(1.f, fmaxf(a.wscale[0][HLS_BOUND], a.wscale[1][HLS_BOUND]))));
+    st.rng[1] = fexp_bits(__float_as_uint(fmaxf(a.wscale[0][HLS_BMAX], a.wscale[1][HLS_BMAX])));
+    st.rng[2] = hl_range_shift(fexp_bits(__float_as_uint(fmaxf(a.adjb[0][HLS_BOUND], a.adjb[1][HLS_BOUND]))));
+  }
+}
+
+// The spatial GC units u, u + ustep, ... < uend (unit = (sample, frame) =
+// n * T + t); load_adj_g(u, g, ab[NWT][2]) fetches the unit's graph-g
+// adjacency B fragments (hi, lo planes) for its two w tiles.
+template <int V, int CIN, int COUT, typename AdjLoad>
+__device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const SpatialStage<V, CIN, COUT>& st, int u,
+                                              int uend, int ustep, AdjLoad load_adj_g) {
   using SM = SlotMap<V, true>;
   constexpr bool RES = CIN != COUT;
-  constexpr int SL = SM::SL, NG = SM::NG, NWT = cdiv(V, 16);
+  constexpr int NWT = cdiv(V, 16);
   constexpr int KSI = cdiv(CIN, 32);   // conv k-steps
   constexpr int NCT = cdiv(COUT, 16);  // output channel tiles
   constexpr int KSO = cdiv(NCT, 2);    // P/Q k-steps
-  constexpr int WIMG = NCT * KSI * 2 * 64, PIMG = KSO * 2 * 64;
   static_assert(SM::MT == 2 && SM::NS == 1, "one K-step of two tiles per frame");
-  __shared__ uint4 wl[RES ? 3 : 2][WIMG];  // conv (graphs 0, 1), residual conv
-  __shared__ uint4 pql[PIMG];
-  __shared__ float4 bnl[RES ? 4 : 2][4 * NCT * V];
-  __shared__ float bfl[3][16 * NCT];
-  __shared__ float bql[4];
-  __shared__ float scl[4];
-  __shared__ int rng[3];
-
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int lane = threadIdx.x & 63;
   const int kl = lane >> 4, cl = lane & 15;
   const int T = a.T;
-  constexpr int NT = spatial_nt();
-  for (int i = tid; i < (RES ? 3 : 2) * WIMG; i += NT) wl[i / WIMG][i % WIMG] = a.wimg[i / WIMG][i % WIMG];
-  for (int i = tid; i < PIMG; i += NT) pql[i] = a.pqimg[i];
-  stage_bnC<COUT, NCT>(bnl[0], a.bn_s, V, tid);
-  stage_bnC<COUT, NCT>(bnl[1], a.bn_h, V, tid);
-  if constexpr (RES) {
-    stage_bnC<COUT, NCT>(bnl[2], a.rbn_s, V, tid);
-    stage_bnC<COUT, NCT>(bnl[3], a.rbn_h, V, tid);
-  }
-  for (int i = tid; i < (RES ? 3 : 2) * 16 * NCT; i += NT) {
-    const int g = i / (16 * NCT), c = i % (16 * NCT);
-    bfl[g][c] = c < COUT ? a.bf[g][c] : 0.f;
-  }
-  if (tid < 4) bql[tid] = a.pqb[tid >> 1][tid & 1];
-  if (tid == 0) {
-    scl[0] = *a.wscale[0];
-    scl[1] = *a.wscale[1];
-    scl[2] = *a.pqscale;
-    scl[3] = RES ? *a.wscale[2] : 0.f;
-    // range: |W_f|_inf and max|b_f| over both graphs, the planes' shared shift
-    rng[0] = fexp_bits(__float_as_uint(fmaxf(1.f, fmaxf(a.wscale[0][HLS_BOUND], a.wscale[1][HLS_BOUND]))));
-    rng[1] = fexp_bits(__float_as_uint(fmaxf(a.wscale[0][HLS_BMAX], a.wscale[1][HLS_BMAX])));
-    rng[2] = hl_range_shift(fexp_bits(__float_as_uint(fmaxf(a.adjb[0][HLS_BOUND], a.adjb[1][HLS_BOUND]))));
-  }
-  __syncthreads();
-  const int efb = __builtin_amdgcn_readfirstlane(rng[0]), eb = __builtin_amdgcn_readfirstlane(rng[1]);
-  const int sa = __builtin_amdgcn_readfirstlane(rng[2]);
-
-  int uend;
-  int u = unit_range(a.B * T, uend);
+  const int efb = __builtin_amdgcn_readfirstlane(st.rng[0]), eb = __builtin_amdgcn_readfirstlane(st.rng[1]);
+  const int sa = __builtin_amdgcn_readfirstlane(st.rng[2]);
   const float pw = *a.prelu;
   // conv rows: joint of tile m, row cl
   // (padding slots read past the unit's range: zero rows, no memory traffic)
@@ -413,11 +468,9 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
   const int jr1 = SM::row_idx(1, cl) < V ? SM::row_idx(1, cl) : 1 << 20;
   constexpr uint32_t xunit = V * CIN * 4;         // one frame of x
   constexpr uint32_t yunit = V * COUT * 4;        // one frame of y
-  constexpr uint32_t adj_bytes = 2 * V * SL * 2;  // one (n, g, t) adjacency: 2 planes of V x SL halves
   // this lane's output joint w = 16wt + cl: joints past V fall outside the
-  // unit's buffer range by themselves; adjacency lane groups past NG and
-  // P/Q lanes other than kl == 0 get an explicit out-of-range offset
-  const uint32_t wadj0 = kl < NG ? (uint32_t)(cl * SL + 8 * kl) * 2 : OOB;  // + wt * 32 * SL
+  // unit's buffer range by themselves; P/Q lanes other than kl == 0 get an
+  // explicit out-of-range offset
   const uint32_t wpq0 = kl == 0 ? (uint32_t)cl * 16 : OOB;                  // + wt * 256
 
   // xmodel (CIN == 6 only): x is the model input [B][T][V][3] and the rows
@@ -439,19 +492,9 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
     }
   };
   uint4 ab[2][NWT][2];  // adjacency B fragments [graph][w tile][plane]
-  auto load_adj_g = [&](int uu, int g) {
-    const int n = uu / T, t = uu - n * T;
-    const uint16_t* base = a.adj + ((size_t)(n * 2 + g) * T + t) * (adj_bytes / 2);
-    const auto rh = rsrc(base, adj_bytes / 2), rl = rsrc(base + V * SL, adj_bytes / 2);  // one plane each
-#pragma unroll
-    for (int wt = 0; wt < NWT; ++wt) {
-      ab[g][wt][0] = bldu4(rh, wadj0 + wt * 32 * SL);
-      ab[g][wt][1] = bldu4(rl, wadj0 + wt * 32 * SL);
-    }
-  };
   if (u < uend) load_x(u);
   while (u < uend) {
-    const int un = u + 1;
+    const int un = u + ustep;
     const int lz = lane + opaque_zero();
     const auto rx = frame_rsrc(u), rxl = last_rsrc(u);
     // residual: identity -> x at the output positions (w, channels 16ct + 4kl ..);
@@ -471,7 +514,7 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
     }
     // this unit's graph-0 adjacency now, graph 1 after the first conv (a
     // whole-unit-ahead prefetch of both measured 6% slower: registers)
-    load_adj_g(u, 0);
+    load_adj_g(u, 0, ab[0]);
     __builtin_amdgcn_sched_barrier(0);
     // range shift of the unit's rows (0 unless a half could overflow)
     float xm = 0.f;
@@ -517,8 +560,8 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
           f16x8 wh[Q2], wo[Q2];
 #pragma unroll
           for (int q = 0; q < Q2; ++q) {
-            wh[q] = as_h8(wl[g][(((c2 + q) * KSI + ks) * 2 + 0) * 64 + lz]);
-            wo[q] = as_h8(wl[g][(((c2 + q) * KSI + ks) * 2 + 1) * 64 + lz]);
+            wh[q] = as_h8(st.wl[g][(((c2 + q) * KSI + ks) * 2 + 0) * 64 + lz]);
+            wo[q] = as_h8(st.wl[g][(((c2 + q) * KSI + ks) * 2 + 1) * 64 + lz]);
           }
 #pragma unroll
           for (int q = 0; q < Q2; ++q)
@@ -535,7 +578,7 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
         }
       if (g == 0) {
         __builtin_amdgcn_sched_barrier(0);
-        load_adj_g(u, 1);
+        load_adj_g(u, 1, ab[1]);
         __builtin_amdgcn_sched_barrier(0);
       }
       // x is dead after the second conv: prefetch the next unit's rows
@@ -543,15 +586,15 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
       // branch hides the loads from hipcc's vmcnt bookkeeping)
       if (g == 1) {
         __builtin_amdgcn_sched_barrier(0);  // keep the prefetch here: its registers free up only now
-        load_x(min(un, uend - 1));
+        load_x(un < uend ? un : u);
         __builtin_amdgcn_sched_barrier(0);
       }
       // ---- aggregation: O[c][w] += sum_v D[v][c] Adj[v][w] ----
-      const float s = scl[g];
+      const float s = st.scl[g];
       f16x8 dh[NCT], dl[NCT];
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
-        const float b = bfl[g][16 * ct + cl] * dnx;  // F_s = 2^-sx F
+        const float b = st.bfl[g][16 * ct + cl] * dnx;  // F_s = 2^-sx F
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -592,8 +635,8 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
         }
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) {
-          const f16x8 ah = as_h8(wl[2][((ct * KSI + ks) * 2 + 0) * 64 + lz]);
-          const f16x8 ao = as_h8(wl[2][((ct * KSI + ks) * 2 + 1) * 64 + lz]);
+          const f16x8 ah = as_h8(st.wl[2][((ct * KSI + ks) * 2 + 0) * 64 + lz]);
+          const f16x8 ao = as_h8(st.wl[2][((ct * KSI + ks) * 2 + 1) * 64 + lz]);
 #pragma unroll
           for (int wt = 0; wt < NWT; ++wt) rc[ct][wt] = mfma32(ao, bh[wt], rc[ct][wt]);
 #pragma unroll
@@ -621,14 +664,14 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
       for (int ct = 0; ct < NCT; ++ct) {
         f32x4& o = O[ct][wt];
         const int c4 = (4 * ct + kl) * V + wc;
-        const float4 sc = bnl[0][c4], sh = bnl[1][c4];
+        const float4 sc = st.bnl[0][c4], sh = st.bnl[1][c4];
         float r[4];
         if constexpr (RES) {
-          const float4 rs = bnl[2][c4], rh = bnl[3][c4];
-          const float s3 = scl[3] * pow2f(sx);  // the residual conv ran on 2^-sx x
+          const float4 rs = st.bnl[2][c4], rh = st.bnl[3][c4];
+          const float s3 = st.scl[3] * pow2f(sx);  // the residual conv ran on 2^-sx x
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const float b = bfl[2][16 * ct + 4 * kl + q];
+            const float b = st.bfl[2][16 * ct + 4 * kl + q];
             const float rv = fmaf(rc[ct][wt][q], s3, b);
             r[q] = fmaf(rv, q == 0 ? rs.x : q == 1 ? rs.y : q == 2 ? rs.z : rs.w,
                         q == 0 ? rh.x : q == 1 ? rh.y : q == 2 ? rh.z : rh.w);
@@ -677,7 +720,7 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
     for (int wt = 0; wt < NWT; ++wt) acc[wt] = zero4();
 #pragma unroll
     for (int ks = 0; ks < KSO; ++ks) {
-      const f16x8 qh = as_h8(pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(pql[(ks * 2 + 1) * 64 + lz]);
+      const f16x8 qh = as_h8(st.pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(st.pql[(ks * 2 + 1) * 64 + lz]);
       f16x8 hh[NWT], hl[NWT];
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt)
@@ -690,16 +733,44 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
       for (int wt = 0; wt < NWT; ++wt) acc[wt] = mfma32(qh, hh[wt], acc[wt]);
     }
     {
-      const float s = scl[2] * pow2f(sh);
+      const float s = st.scl[2] * pow2f(sh);
       const auto rp = rsrc(a.pq + (size_t)u * V * 4, V * 16);
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt)
         bst4(rp, wpq0 + wt * 256,
-             make_float4(fmaf(acc[wt][0], s, bql[0]), fmaf(acc[wt][1], s, bql[1]), fmaf(acc[wt][2], s, bql[2]),
-                         fmaf(acc[wt][3], s, bql[3])));
+             make_float4(fmaf(acc[wt][0], s, st.bql[0]), fmaf(acc[wt][1], s, st.bql[1]), fmaf(acc[wt][2], s, st.bql[2]),
+                         fmaf(acc[wt][3], s, st.bql[3])));
     }
     u = un;
   }
+}
+
+template <int V, int CIN, int COUT>
+__global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DSTD_HL_WPE, DSTD_HL_WPE))) void k_spatial_hl(
+    SpatialHLArgs a) {
+  using SM = SlotMap<V, true>;
+  constexpr int SL = SM::SL, NG = SM::NG, NWT = cdiv(V, 16);
+  __shared__ SpatialStage<V, CIN, COUT> st;
+  stage_spatial<V, CIN, COUT, spatial_nt()>(a, st, threadIdx.x);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, kl = lane >> 4, cl = lane & 15;
+  const int T = a.T;
+  constexpr uint32_t adj_bytes = 2 * V * SL * 2;  // one (n, g, t) adjacency: 2 planes of V x SL halves
+  // adjacency lane groups past NG get an out-of-range offset (zero fragments)
+  const uint32_t wadj0 = kl < NG ? (uint32_t)(cl * SL + 8 * kl) * 2 : OOB;  // + wt * 32 * SL
+  auto load_adj_g = [&](int uu, int g, uint4 (&ab)[NWT][2]) {
+    const int n = uu / T, t = uu - n * T;
+    const uint16_t* base = a.adj + ((size_t)(n * 2 + g) * T + t) * (adj_bytes / 2);
+    const auto rh = rsrc(base, adj_bytes / 2), rl = rsrc(base + V * SL, adj_bytes / 2);  // one plane each
+#pragma unroll
+    for (int wt = 0; wt < NWT; ++wt) {
+      ab[wt][0] = bldu4(rh, wadj0 + wt * 32 * SL);
+      ab[wt][1] = bldu4(rl, wadj0 + wt * 32 * SL);
+    }
+  };
+  int uend;
+  const int u = unit_range(a.B * T, uend);
+  spatial_units<V, CIN, COUT>(a, st, u, uend, 1, load_adj_g);
 }
 
 // ===========================================================================
@@ -1486,6 +1557,11 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
 // VALU-bound (the tanh), phase 2 MFMA / memory; the one workgroup per CU the
 // LDS allows runs them back to back.  Grid = B (a persistent sample loop kept
 // its loop-carried state live through phase 2 and spilled).
+// Round 3 tried the phases overlapped (k_temporal_pipe: 4 waves building the
+// next chunk's planes while 4 run the GC units of this one; all variants
+// bit-exact): 38% slower at H36M, 24% at CMU, 34% at 3DPW -- the units are
+// latency-bound streaming and lost half their loads in flight
+// (profiles/r03f_pipe_ab.txt).  Retired.
 // ===========================================================================
 constexpr int kLdsBudget = 160 * 1024;
 
@@ -1518,7 +1594,232 @@ struct TFusedGeom {
 struct TemporalFusedArgs {
   TemporalHLArgs g;  // the GC launch (adj unused)
   AdjHLArgs j;       // P/Q (pq, pql), HLJ_RM image (wimg[0], wscale[0]), bias[0], alpha, astat[0]
+  AdjHLArgs sn;      // out != null: the next block's spatial adjacency planes (launch_adj_hl mode 0 args;
+                     // pq = g.pq, the P/Q this launch writes), built after the units (phase 3)
 };
+
+// ---- phase 3 of k_temporal_fused: the NEXT block's spatial adjacency planes
+// of sample n (k_adj_hl<0>'s GEMM and epilogue, transposed as in phase 1:
+// A = tanh columns, B = conv_rm rows).  The workgroup has just written every
+// (t, v) P/Q of the sample in its units' epilogues, so the planes follow in
+// the same launch: no k_adj_hl<0> launch (its prologue round trip and tail),
+// the P/Q read back from L2 by the CU that wrote them.  LDS: both graphs' E/F
+// rows and Astat (the planes and the stage of phases 1-2 are dead by then).
+template <int T, int V>
+struct SAdjGeom {
+  using SM = SlotMap<V, true>;
+  static constexpr int K = 2 * T, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL, SE = KP + 4;
+  static constexpr int SL = SM::SL, NCOL = V * SL, NCTC = cdiv(NCOL, 16), RT = cdiv(T, 16), FULL = NS * 2 * 64;
+  static constexpr int WIMG = RT * (FULL + TAIL * 64);  // uint4 of one graph's HLJ_RM image
+  static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
+  static constexpr size_t EF = al16(2 * (size_t)(V + 1) * SE * 4);  // one graph's E rows then F rows
+  static constexpr size_t AS = al16(((size_t)V * V + 1) * 4);       // one graph's Astat (+ a zero)
+  static constexpr size_t WB = (size_t)WIMG * 16;                   // one graph's image
+  static constexpr size_t BB = al16((size_t)16 * RT * 4);           // one graph's conv_rm bias (rows padded)
+  static constexpr size_t LDS = 2 * (EF + AS + WB + BB);
+};
+
+template <int T, int V, int NT>
+__device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, unsigned char* dsm) {
+  using Gm = SAdjGeom<T, V>;
+  using SM = typename Gm::SM;
+  constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
+  constexpr int RT = Gm::RT, FULL = Gm::FULL, WIMG = Gm::WIMG, NW = NT / 64, NCTC = Gm::NCTC;
+  constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
+  // LDS: [E/F g0][E/F g1][Astat g0][Astat g1][image g0][image g1][bias g0][bias g1]
+  auto Elg = [&](int g) { return reinterpret_cast<float*>(dsm + g * Gm::EF); };  // F rows at + (V + 1) * SE
+  auto asg = [&](int g) { return reinterpret_cast<float*>(dsm + 2 * Gm::EF + g * Gm::AS); };
+  uint4* wl = reinterpret_cast<uint4*>(dsm + 2 * (Gm::EF + Gm::AS));  // both images, graph-major
+  float* bl = reinterpret_cast<float*>(dsm + 2 * (Gm::EF + Gm::AS + Gm::WB));  // [g][16 RT]
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = lane >> 4, cl = lane & 15;
+
+  // ---- prologue: both graphs' P/Q -> E/F rows, conv_rm images, Astat, bias;
+  // every global load before the first LDS write ----
+  const PQLayout L = j.pql;
+  constexpr int NPQ = cdiv(T * V, NT), NWI = cdiv(2 * WIMG, NT), NAS = cdiv(2 * V * V, NT);
+  auto pq_at = [&](int g, int i) __attribute__((always_inline)) -> float4 {  // (P_0, P_1, Q_0, Q_1) of element i (joint-major)
+    const int t = i % T, v = i / T;
+    return ld4(j.pq + (size_t)n * L.sn + j.p_ch[g] + t * L.st + v * L.sv);
+  };
+  float4 q4[2][NPQ];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int it = 0; it < NPQ; ++it) q4[g][it] = pq_at(g, min(tid + it * NT, T * V - 1));
+  uint4 wv[NWI];
+  float av[NAS];
+#pragma unroll
+  for (int it = 0; it < NWI; ++it) {
+    const int i = min(tid + it * NT, 2 * WIMG - 1);
+    wv[it] = (i >= WIMG ? j.wimg[1] : j.wimg[0])[i >= WIMG ? i - WIMG : i];
+  }
+#pragma unroll
+  for (int it = 0; it < NAS; ++it) {
+    const int i = min(tid + it * NT, 2 * V * V - 1);
+    av[it] = (i >= V * V ? j.astat[1] : j.astat[0])[i >= V * V ? i - V * V : i];
+  }
+  const int bg = tid >= 16 * RT, br = tid - bg * 16 * RT;
+  const float bv = tid < 2 * 16 * RT && br < T ? (bg ? j.bias[1] : j.bias[0])[br] : 0.f;
+#pragma unroll
+  for (int it = 0; it < NWI; ++it)
+    if (tid + it * NT < 2 * WIMG) wl[tid + it * NT] = wv[it];
+#pragma unroll
+  for (int it = 0; it < NAS; ++it) {
+    const int i = tid + it * NT;
+    if (i < 2 * V * V) asg(i >= V * V)[i >= V * V ? i - V * V : i] = av[it];
+  }
+  if (tid < 2) asg(tid)[V * V] = 0.f;
+  if (tid < 2 * 16 * RT) bl[tid] = bv;
+  auto ef_pad = [&](float val) __attribute__((always_inline)) {  // padding k and the row p = q = V: tanh 0
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      float* El = Elg(g);
+      float* Fl = El + (V + 1) * SE;
+      for (int i = tid; i < (V + 1) * (KP - K); i += NT) {
+        const int r = i / (KP - K), k = K + i % (KP - K);
+        El[r * SE + k] = val;
+        Fl[r * SE + k] = val;
+      }
+      for (int i = tid; i < K; i += NT) {
+        El[V * SE + i] = val;
+        Fl[V * SE + i] = val;
+      }
+    }
+  };
+  ef_pad(1.f);
+  int bad = 0;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float* El = Elg(g);
+    float* Fl = El + (V + 1) * SE;
+#pragma unroll
+    for (int it = 0; it < NPQ; ++it) {
+      const int i = tid + it * NT;
+      if (i < T * V) {
+        const int t = i % T, v = i / T;
+        const float ep0 = C2 * q4[g][it].x, ep1 = C2 * q4[g][it].y, eq0 = -C2 * q4[g][it].z, eq1 = -C2 * q4[g][it].w;
+        bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
+        El[v * SE + t] = __builtin_amdgcn_exp2f(ep0);
+        El[v * SE + T + t] = __builtin_amdgcn_exp2f(ep1);
+        Fl[v * SE + t] = __builtin_amdgcn_exp2f(eq0);
+        Fl[v * SE + T + t] = __builtin_amdgcn_exp2f(eq1);
+      }
+    }
+  }
+  const bool sep = __syncthreads_or(bad) == 0;
+  if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0)
+    __syncthreads();
+    ef_pad(0.f);
+    for (int g = 0; g < 2; ++g) {
+      float* El = Elg(g);
+      float* Fl = El + (V + 1) * SE;
+      for (int i = tid; i < T * V; i += NT) {
+        const int t = i % T, v = i / T;
+        const float4 p4 = pq_at(g, i);
+        El[v * SE + t] = p4.x;
+        El[v * SE + T + t] = p4.y;
+        Fl[v * SE + t] = p4.z;
+        Fl[v * SE + T + t] = p4.w;
+      }
+    }
+    __syncthreads();
+  }
+  const float dna = pow2f(-hl_range_shift(
+      fexp_bits(__float_as_uint(fmaxf(j.wscale[0][HLS_BOUND], j.wscale[1][HLS_BOUND])))));
+  const float alpha = *j.alpha * dna;
+  const float inv0 = *j.wscale[0], inv1 = *j.wscale[1];
+  TLH(2, 1)
+
+  auto tiles = [&](auto sep_c) __attribute__((always_inline)) {
+    constexpr bool SEP = decltype(sep_c)::value;
+    // one tile space over both graphs (2 NCTC column tiles): the waves split
+    // it evenly instead of rounding up twice
+    f16x8 wh[RT][NS], wo[RT][NS];  // the current graph's conv_rm rows as B fragments
+    f16x4 wth[RT], wto[RT];        // (lane = row 16 rt + cl, k group kg)
+    float b[RT];
+    int gcur = -1;
+#pragma unroll 1
+    for (int ti = wave; ti < 2 * NCTC; ti += NW) {
+      const int g = ti >= NCTC ? 1 : 0, ct = ti - g * NCTC;
+      if (g != gcur) {  // (wave-uniform: at most once per wave)
+        gcur = g;
+        const uint4* wg = wl + g * WIMG;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            wh[rt][s] = as_h8(wg[((rt * NS + s) * 2 + 0) * 64 + lane]);
+            wo[rt][s] = as_h8(wg[((rt * NS + s) * 2 + 1) * 64 + lane]);
+          }
+          if constexpr (TAIL) {
+            const uint2* w16 = reinterpret_cast<const uint2*>(wg + RT * FULL);
+            wth[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
+            wto[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
+          }
+          b[rt] = bl[g * 16 * RT + 16 * rt + cl];
+        }
+      }
+      const float inv = g ? inv1 : inv0;
+      const float* El = Elg(g);
+      const float* Fl = El + (V + 1) * SE;
+      const float* as = asg(g);
+      const auto ro = rsrc(j.out + (size_t)n * j.out_sN + (size_t)g * j.out_sG, 2u * T * 2 * NCOL);
+      // this lane's A-operand row = column ct * 16 + cl of the planes
+      const int col = ct * 16 + cl;
+      const int qa = col / SL, pa = SM::slot_idx(col - qa * SL);
+      const bool va = col < NCOL && pa < V;
+      f16x8 bh[NS], bo[NS];
+      f16x4 th, to;
+      tanh_frags<SEP, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
+      // the accumulator's 4 columns colb .. colb + 3 (one joint q, slots slot0 ..)
+      const int colb = ct * 16 + 4 * kg, q = colb / SL, slot0 = colb - q * SL;
+      float asv[4], al[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int pi = SM::slot_idx(slot0 + r);
+        const bool valid = colb + r < NCOL && pi < V;
+        asv[r] = as[valid ? pi * V + q : V * V] * dna;
+        al[r] = valid ? alpha : 0.f;
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          acc = mfma32(bh[s], wo[rt][s], acc);
+          acc = mfma32(bo[s], wh[rt][s], acc);
+          acc = mfma32(bh[s], wh[rt][s], acc);
+        }
+        if constexpr (TAIL) {  // on an accumulator of its own (dstd_hilo.h: mixed-shape MFMA chains)
+          f32x4 tac = __builtin_amdgcn_mfma_f32_16x16x16f16(th, wto[rt], zero4(), 0, 0, 0);
+          tac = __builtin_amdgcn_mfma_f32_16x16x16f16(to, wth[rt], tac, 0, 0, 0);
+          tac = __builtin_amdgcn_mfma_f32_16x16x16f16(th, wth[rt], tac, 0, 0, 0);
+          acc += tac;
+        }
+        float vv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) vv[r] = fmaf(al[r], fmaf(acc[r], inv, b[rt]), asv[r]);
+        uint4 hi, lo;
+        split8(make_float4(vv[0], vv[1], vv[2], vv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+        // frame t = 16 rt + cl: the hi plane at [t][0][col], lo at [t][1][col]
+        const int t = 16 * rt + cl;
+        const uint32_t off = t < T && colb < NCOL ? 2u * (uint32_t)(t * 2 * NCOL + colb) : OOB;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_uint2(hi.x, hi.y)), ro, off, 0,
+                                              DSTD_ADJ_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_uint2(lo.x, lo.y)), ro,
+                                              off + 2u * NCOL, 0, DSTD_ADJ_ST_AUX);
+      }
+    }
+  };
+  if (sep) tiles(std::true_type{});
+  else tiles(std::false_type{});
+#ifdef DSTD_STAMPS
+  TLH(2, 2)
+  __builtin_amdgcn_s_waitcnt(0);
+  TLH(2, 3)
+#endif
+}
 
 template <int T, int V, int EPI, int C>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_temporal_fused(TemporalFusedArgs fa) {
@@ -1546,6 +1847,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, cl = lane & 15;
   const int n = blockIdx.x;  // one sample per workgroup
+  if constexpr (C == 64) { TLH(3, 0) }
 
   {
     for (int ch = 0; ch < Gm::NCHUNK; ++ch) {
@@ -1617,7 +1919,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if (tid == 0) asl[T * T] = 0.f;
       if (tid < 16 * RTC) bsl[tid] = bv;
       const bool sep = __syncthreads_or(bad) == 0;
-      __syncthreads();  // (__syncthreads_or alone did not order the LDS writes above before the reads below)
+      // (__syncthreads_or already orders the LDS writes above: __ockl_wgred_or_i32
+      // waits lgkmcnt(0) before its first barrier, checked in the ISA; round
+      // 2's "did not order" was the mixed-shape MFMA hazard)
+      __syncthreads();
       if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0)
         for (int i = tid; i < T * V; i += NT) {
           const int t = i / V, v = i % V;
@@ -1788,6 +2093,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
 #endif
       __syncthreads();  // planes complete; the phase-1 scratch is free
+      if constexpr (C == 64) {
+        if (ch == 0) { TLH(3, 1) }
+      }
 #ifdef DSTD_TF_DUMPP
       // (bisection build: workgroup 0's planes of chunk 0 to g_dbg_planes)
       if (blockIdx.x == 0 && ch == 0) {
@@ -1816,6 +2124,316 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       temporal_units<T, EPI, C, V, true>(a, st, ub + wave, ub + nv, NW, load_adj);
 #endif
     }
+  }
+  // ---- phase 3: the next block's spatial adjacency planes of this sample ----
+  if constexpr (C == 64) {
+    static_assert(SAdjGeom<T, V>::LDS <= Gm::LDS, "phase 3 reuses the launch's LDS");
+    TLH(3, 2)
+    if (fa.sn.out) {
+      __syncthreads();  // every unit's P/Q written (one CU: the workgroup-scope fences of the barrier suffice)
+      TLH(2, 0)
+      spatial_adj_sample<T, V, NT>(fa.sn, n, dsm);
+    }
+    TLH(3, 3)
+  }
+}
+
+// ===========================================================================
+// Spatial DSTDGC with its adjacency built in LDS (DSTDGC.forward model/
+// dstdgcn.py:83-87 feeding 95-97; round 3): one workgroup per sample, 8 waves.
+// The sample's frames go in chunks of F (a multiple of 8, <= 16: one row tile
+// of the conv_rm GEMM): phase 1, every wave builds both graphs' split-f16
+// planes of the chunk in LDS -- k_adj_hl<0>'s tanh GEMM and epilogue, the same
+// products in the same order, so the planes are bit-identical to the ones
+// k_adj_hl<0> wrote to HBM -- then phase 2, every wave runs GC units (frames)
+// of the chunk (spatial_units, the unit loop of k_spatial_hl) with its
+// adjacency B fragments from LDS.  The planes never reach HBM: k_adj_hl<0>
+// wrote B x 2 x T x 2 planes x V x SL halves (148 KB per sample at H36M) and
+// k_spatial_hl read them back.  Cost: the tanh operand is regenerated per
+// chunk (cdiv(T, F) x k_adj_hl<0>'s).
+// Phases, not producer / consumer waves: a 4 + 4 wave pipeline of this
+// kernel (round 3, profiles/r03f_pipe_ab.txt) ran 43% slower than k_adj_hl<0>
+// + k_spatial_hl -- the GC units are latency-bound streaming and 4 waves per
+// CU keep half the loads in flight that 8 do.
+// LDS: one plane buffer, both graphs' E/F rows and Astat, the GC stage.
+// ===========================================================================
+template <int T, int V, int CIN, int COUT>
+struct SFusedGeom {
+  using SM = SlotMap<V, true>;
+  static constexpr int K = 2 * T, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL, SE = KP + 4;
+  static constexpr int SL = SM::SL, NCOL = V * SL, NCTC = cdiv(NCOL, 16);
+  static constexpr int PG = 2 * V * SL;  // halves per (frame, graph): hi plane, lo plane ([V rows][SL] each)
+  static constexpr int RTG = cdiv(T, 16);
+  static constexpr int FULL = NS * 2 * 64;  // uint4 per row tile of the HLJ_RM image (full K-steps)
+  static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
+  static constexpr size_t EF = al16(2 * (size_t)(V + 1) * SE * 4);  // one graph's E rows then F rows
+  static constexpr size_t AS = al16(((size_t)V * V + 1) * 4);       // one graph's Astat (+ a zero)
+  static constexpr size_t fixed_bytes() { return 2 * EF + 2 * AS + al16(sizeof(SpatialStage<V, CIN, COUT>)); }
+  static constexpr size_t lds(int f) { return al16((size_t)f * 2 * PG * 2) + fixed_bytes(); }
+  // frames per chunk: the fewest chunks whose plane buffer fits (DSTD_SF_F overrides)
+  static constexpr int pick_nch() {
+    for (int nch = 1; nch <= T; ++nch)
+      if (lds(cdiv(T, nch)) <= kLdsBudget) return nch;
+    return T;
+  }
+#ifdef DSTD_SF_F
+  static constexpr int F = DSTD_SF_F < T && lds(DSTD_SF_F) <= kLdsBudget ? DSTD_SF_F : cdiv(T, pick_nch());
+#else
+  static constexpr int F = cdiv(T, pick_nch());
+#endif
+  static constexpr int NCH = cdiv(T, F), RTC = cdiv(F, 16);  // chunks, row tiles per chunk
+  static constexpr size_t PLANES = al16((size_t)F * 2 * PG * 2), LDS = lds(F);
+  static_assert(LDS <= kLdsBudget, "one plane buffer of a chunk must fit");
+};
+
+struct SpatialFusedArgs {
+  SpatialHLArgs g;  // the GC launch (adj unused)
+  AdjHLArgs j;      // P/Q (pq, pql, p_ch or xin/mw/mb), HLJ_RM images, wscale, bias, alpha, astat of both graphs
+};
+
+template <int T, int V, int CIN, int COUT>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_spatial_fused(SpatialFusedArgs fa) {
+  using Gm = SFusedGeom<T, V, CIN, COUT>;
+  using SM = typename Gm::SM;
+  constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
+  constexpr int PG = Gm::PG, F = Gm::F, NCH = Gm::NCH, FULL = Gm::FULL, NT = 512, NW = NT / 64, NWT = cdiv(V, 16);
+  constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
+  const SpatialHLArgs& a = fa.g;
+  const AdjHLArgs& j = fa.j;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  _Float16* planes = reinterpret_cast<_Float16*>(dsm);  // [frame][graph][plane][V][SL]
+  unsigned char* fx = dsm + Gm::PLANES;
+  auto Elg = [&](int g) { return reinterpret_cast<float*>(fx + g * Gm::EF); };  // F rows at + (V + 1) * SE
+  auto asg = [&](int g) { return reinterpret_cast<float*>(fx + 2 * Gm::EF + g * Gm::AS); };
+  auto& st = *reinterpret_cast<SpatialStage<V, CIN, COUT>*>(fx + 2 * Gm::EF + 2 * Gm::AS);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kg = lane >> 4, cl = lane & 15;
+  const int n = blockIdx.x;  // one sample per workgroup
+
+  // ---- prologue: both graphs' P/Q -> E/F rows and Astat, the GC stage; the
+  // P/Q and Astat loads go out before the stage's ----
+  const PQLayout L = j.pql;
+  constexpr int NPQ = cdiv(T * V, NT), NAS = cdiv(V * V, NT);
+  // (P_0, P_1, Q_0, Q_1) of graph g at element i (memory order: joint-major)
+  auto pq_at = [&](int g, int i) -> float4 {
+    const int t = i % T, v = i / T;
+    if constexpr (CIN == 6) {
+      if (j.xin) {  // conv_st_in (model/dstdgcn.py:298-305): P/Q of x6 = cat(x, x - x[:, -1])
+        const float* xn = j.xin + (size_t)n * T * V * 3;
+        const float* xc = xn + (t * V + v) * 3;
+        const float* xl = xn + ((T - 1) * V + v) * 3;
+        const float x6v[6] = {xc[0], xc[1], xc[2], xc[0] - xl[0], xc[1] - xl[1], xc[2] - xl[2]};
+        float pq[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float acc = j.mb[g][r >> 1][r & 1];
+#pragma unroll
+          for (int c = 0; c < 6; ++c) acc = fmaf(j.mw[g][r >> 1][(r & 1) * 6 + c], x6v[c], acc);
+          pq[r] = acc;
+        }
+        return make_float4(pq[0], pq[1], pq[2], pq[3]);
+      }
+    }
+    return ld4(j.pq + (size_t)n * L.sn + j.p_ch[g] + t * L.st + v * L.sv);
+  };
+  float4 q4[2][NPQ];
+  float av[2][NAS];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+#pragma unroll
+    for (int it = 0; it < NPQ; ++it) q4[g][it] = pq_at(g, min(tid + it * NT, T * V - 1));
+#pragma unroll
+    for (int it = 0; it < NAS; ++it) av[g][it] = j.astat[g][min(tid + it * NT, V * V - 1)];
+  }
+  stage_spatial<V, CIN, COUT, NT>(a, st, tid);
+  auto ef_pad = [&](float val) {  // padding k and the row p = q = V: tanh 0
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      float* El = Elg(g);
+      float* Fl = El + (V + 1) * SE;
+      for (int i = tid; i < (V + 1) * (KP - K); i += NT) {
+        const int r = i / (KP - K), k = K + i % (KP - K);
+        El[r * SE + k] = val;
+        Fl[r * SE + k] = val;
+      }
+      for (int i = tid; i < K; i += NT) {
+        El[V * SE + i] = val;
+        Fl[V * SE + i] = val;
+      }
+    }
+  };
+  ef_pad(1.f);
+  int bad = 0;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    float* El = Elg(g);
+    float* Fl = El + (V + 1) * SE;
+#pragma unroll
+    for (int it = 0; it < NPQ; ++it) {
+      const int i = tid + it * NT;
+      if (i < T * V) {
+        const int t = i % T, v = i / T;
+        const float ep0 = C2 * q4[g][it].x, ep1 = C2 * q4[g][it].y, eq0 = -C2 * q4[g][it].z, eq1 = -C2 * q4[g][it].w;
+        bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
+        El[v * SE + t] = __builtin_amdgcn_exp2f(ep0);
+        El[v * SE + T + t] = __builtin_amdgcn_exp2f(ep1);
+        Fl[v * SE + t] = __builtin_amdgcn_exp2f(eq0);
+        Fl[v * SE + T + t] = __builtin_amdgcn_exp2f(eq1);
+      }
+    }
+    float* as = asg(g);
+#pragma unroll
+    for (int it = 0; it < NAS; ++it)
+      if (tid + it * NT < V * V) as[tid + it * NT] = av[g][it];
+    if (tid == 0) as[V * V] = 0.f;
+  }
+  const bool sep = __syncthreads_or(bad) == 0;
+  if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0); P/Q fetched again
+    __syncthreads();
+    ef_pad(0.f);
+    for (int g = 0; g < 2; ++g) {
+      float* El = Elg(g);
+      float* Fl = El + (V + 1) * SE;
+      for (int i = tid; i < T * V; i += NT) {
+        const int t = i % T, v = i / T;
+        const float4 p4 = pq_at(g, i);
+        El[v * SE + t] = p4.x;
+        El[v * SE + T + t] = p4.y;
+        Fl[v * SE + t] = p4.z;
+        Fl[v * SE + T + t] = p4.w;
+      }
+    }
+    __syncthreads();
+  }
+  const float dna = pow2f(-hl_range_shift(
+      fexp_bits(__float_as_uint(fmaxf(j.wscale[0][HLS_BOUND], j.wscale[1][HLS_BOUND])))));
+  const float alpha = *j.alpha * dna;
+
+  // ---- phase 1: both graphs' planes of chunk c (k_adj_hl<0> on the RTC row
+  // tiles of frames t0 .. t0 + F - 1: A = conv_rm rows, B = tanh columns) ----
+  constexpr int RTC = Gm::RTC;
+  auto produce = [&](int c, auto sep_c) __attribute__((always_inline)) {
+    constexpr bool SEP = decltype(sep_c)::value;
+    const int t0 = c * F, nf = min(F, T - t0);
+#pragma unroll 1
+    for (int g = 0; g < 2; ++g) {
+      // (selects, not j.x[g]: a run-time index into the kernel arguments puts them in scratch)
+      const uint4* wg = g ? j.wimg[1] : j.wimg[0];
+      const float* bg = g ? j.bias[1] : j.bias[0];
+      f16x8 ah[RTC][NS], ao[RTC][NS];
+      f16x4 tah[RTC], tao[RTC];
+      float b[RTC][4];  // conv_rm bias of this lane's output rows (frames t0 + 16 rt + 4kg + r)
+#pragma unroll
+      for (int rt = 0; rt < RTC; ++rt) {
+        // this lane's A-operand row cl = frame t0 + 16 rt + cl of the image
+        // (rows past the chunk read a valid row, their outputs are dropped)
+        const int tr = min(t0 + 16 * rt + cl, T - 1), rtw = tr >> 4, lw = (tr & 15) + 16 * kg;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          ah[rt][s] = as_h8(wg[((rtw * NS + s) * 2 + 0) * 64 + lw]);
+          ao[rt][s] = as_h8(wg[((rtw * NS + s) * 2 + 1) * 64 + lw]);
+        }
+        if constexpr (TAIL) {
+          const uint2* w16 = reinterpret_cast<const uint2*>(wg + Gm::RTG * FULL);
+          tah[rt] = __builtin_bit_cast(f16x4, w16[(rtw * 2 + 0) * 64 + lw]);
+          tao[rt] = __builtin_bit_cast(f16x4, w16[(rtw * 2 + 1) * 64 + lw]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[rt][r] = bg[min(t0 + 16 * rt + 4 * kg + r, T - 1)];
+      }
+      const float inv = *(g ? j.wscale[1] : j.wscale[0]);
+      const float* El = Elg(g);
+      const float* Fl = El + (V + 1) * SE;
+      const float* as = asg(g);
+      for (int ct = wave; ct < Gm::NCTC; ct += NW) {
+        // this lane's B-operand column = column ct * 16 + cl of the planes
+        const int col = ct * 16 + cl;
+        const int q = col / SL, slot = col - q * SL, pi = SM::slot_idx(slot);
+        const bool valid = col < NCOL && pi < V;
+        f16x8 bh[NS], bo[NS];
+        f16x4 th, to;
+        tanh_frags<SEP, NS, TAIL, SE>(El, Fl, valid ? pi : V, col < NCOL ? q : V, kg, bh, bo, th, to);
+        f32x4 acc[RTC];
+#pragma unroll
+        for (int rt = 0; rt < RTC; ++rt) acc[rt] = zero4();
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+#pragma unroll
+          for (int rt = 0; rt < RTC; ++rt) acc[rt] = mfma32(ao[rt][s], bh[s], acc[rt]);
+#pragma unroll
+          for (int rt = 0; rt < RTC; ++rt) acc[rt] = mfma32(ah[rt][s], bo[s], acc[rt]);
+#pragma unroll
+          for (int rt = 0; rt < RTC; ++rt) acc[rt] = mfma32(ah[rt][s], bh[s], acc[rt]);
+        }
+        if constexpr (TAIL) {  // on an accumulator of its own (dstd_hilo.h: mixed-shape MFMA chains)
+          f32x4 tac[RTC];
+#pragma unroll
+          for (int rt = 0; rt < RTC; ++rt) tac[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(tao[rt], th, zero4(), 0, 0, 0);
+#pragma unroll
+          for (int rt = 0; rt < RTC; ++rt) tac[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(tah[rt], to, tac[rt], 0, 0, 0);
+#pragma unroll
+          for (int rt = 0; rt < RTC; ++rt) tac[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(tah[rt], th, tac[rt], 0, 0, 0);
+#pragma unroll
+          for (int rt = 0; rt < RTC; ++rt) acc[rt] += tac[rt];
+        }
+        // epilogue (k_adj_hl's): alpha * (acc + b) + Astat, 0 on padding slots
+        const float asv = as[valid ? pi * V + q : V * V] * dna, al = valid ? alpha : 0.f;
+        if (col < NCOL) {
+          _Float16* d = planes + g * PG + q * SL + slot;
+#pragma unroll
+          for (int rt = 0; rt < RTC; ++rt) {
+            float vv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) vv[r] = fmaf(al, fmaf(acc[rt][r], inv, b[rt][r]), asv);
+            uint4 hi, lo;
+            split8(make_float4(vv[0], vv[1], vv[2], vv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+            const uint32_t hw[2] = {hi.x, hi.y}, lw2[2] = {lo.x, lo.y};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int f = 16 * rt + 4 * kg + r;
+              if (f < nf) {
+                const uint32_t sh = 16 * (r & 1);
+                d[f * 2 * PG] = __builtin_bit_cast(_Float16, (uint16_t)(hw[r >> 1] >> sh));
+                d[f * 2 * PG + V * SL] = __builtin_bit_cast(_Float16, (uint16_t)(lw2[r >> 1] >> sh));
+              }
+            }
+          }
+        }
+      }
+    }
+  };
+  // ---- phase 2: the GC units (frames) of chunk c ----
+  auto consume = [&](int c) __attribute__((always_inline)) {
+    const int t0 = c * F, nf = min(F, T - t0);
+    const int ub = n * T + t0;
+    auto load_adj_g = [&](int uu, int g, uint4 (&ab)[NWT][2]) {
+      const _Float16* base = planes + (uu - ub) * 2 * PG + g * PG;
+#pragma unroll
+      for (int wt = 0; wt < NWT; ++wt) {
+        const int w = 16 * wt + cl;  // output joint (plane row), slot group kg
+        const bool ok = w < V && kg < SM::NG;
+        const int off = ok ? w * SL + 8 * kg : 0;
+        const uint4 h = *reinterpret_cast<const uint4*>(base + off);
+        const uint4 l = *reinterpret_cast<const uint4*>(base + V * SL + off);
+        ab[wt][0] = ok ? h : make_uint4(0u, 0u, 0u, 0u);
+        ab[wt][1] = ok ? l : make_uint4(0u, 0u, 0u, 0u);
+      }
+    };
+    spatial_units<V, CIN, COUT>(a, st, ub + wave, ub + nf, NW, load_adj_g);
+  };
+
+#pragma unroll 1
+  for (int c = 0; c < NCH; ++c) {
+#ifndef DSTD_SF_NOPROD  // (timing experiments: phase 2 alone)
+    if (sep) produce(c, std::true_type{});
+    else produce(c, std::false_type{});
+#endif
+    __syncthreads();  // chunk c's planes
+#ifndef DSTD_SF_NOCONS  // (timing experiments: prologue + phase 1 alone)
+    consume(c);
+#endif
+    __syncthreads();  // the plane buffer is free
   }
 }
 
@@ -1961,13 +2579,50 @@ hipError_t tfused_tv(const TemporalFusedArgs& a, hipStream_t s) {
   }
 }
 
+template <int T, int V, int CIN, int COUT>
+hipError_t sfused_run(const SpatialFusedArgs& a, hipStream_t s) {
+  using Gm = SFusedGeom<T, V, CIN, COUT>;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)k_spatial_fused<T, V, CIN, COUT>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::LDS);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_spatial_fused<T, V, CIN, COUT>), dim3(a.g.B), dim3(512), Gm::LDS, s, a);
+  return hipGetLastError();
+}
+
+template <int T, int V>
+hipError_t sfused_tv(const SpatialFusedArgs& a, hipStream_t s) {
+  if (a.g.Cin == 64 && a.g.Cout == 64) return sfused_run<T, V, 64, 64>(a, s);
+  if (a.g.Cin == 6 && a.g.Cout == 64) return sfused_run<T, V, 6, 64>(a, s);
+  if (a.g.Cin == 64 && a.g.Cout == 3) return sfused_run<T, V, 64, 3>(a, s);
+  return hipErrorNotSupported;
+}
+
+bool spatial_fused_supported(int T, int V) { return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23); }
+
+hipError_t launch_spatial_fused(const SpatialHLArgs& g, const AdjHLArgs& j, hipStream_t s) {
+  if (!spatial_fused_supported(g.T, g.V) || j.ngroups != 2 || (g.xmodel && g.Cin != 6) || (g.xmodel != (j.xin != nullptr)))
+    return hipErrorNotSupported;
+  if (!j.xin && (j.pql.sch != 1 || ((uintptr_t)j.pq & 15) || (j.pql.st & 3) || (j.pql.sv & 3) || (j.pql.sn & 3) ||
+                 (j.p_ch[0] & 3) || (j.p_ch[1] & 3)))
+    return hipErrorNotSupported;
+  const SpatialFusedArgs a{g, j};
+  if (g.T == 35 && g.V == 22) return sfused_tv<35, 22>(a, s);
+  if (g.T == 35 && g.V == 25) return sfused_tv<35, 25>(a, s);
+  if (g.T == 40 && g.V == 23) return sfused_tv<40, 23>(a, s);
+  return hipErrorNotSupported;
+}
+
 bool temporal_fused_supported(int T, int V) { return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23); }
 
-hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, hipStream_t s) {
+hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn, hipStream_t s) {
   if (!temporal_fused_supported(g.T, g.V) || g.V != (int)(j.pql.st / 4) || j.pql.sch != 1 || j.pql.sv != 4 ||
       ((uintptr_t)j.pq & 15))
     return hipErrorNotSupported;
-  const TemporalFusedArgs a{g, j};
+  if (sn && (g.C != 64 || !g.pq || sn->pq != g.pq || sn->ngroups != 2 || sn->xin || sn->pql.sch != 1 ||
+             (sn->pql.st & 3) || (sn->pql.sv & 3) || (sn->pql.sn & 3) || (sn->p_ch[0] & 3) || (sn->p_ch[1] & 3) ||
+             !sn->out))
+    return hipErrorNotSupported;
+  const TemporalFusedArgs a{g, j, sn ? *sn : AdjHLArgs{}};
   if (g.T == 35 && g.V == 22) return tfused_tv<35, 22>(a, s);
   if (g.T == 35 && g.V == 25) return tfused_tv<35, 25>(a, s);
   if (g.T == 40 && g.V == 23) return tfused_tv<40, 23>(a, s);
@@ -1988,7 +2643,7 @@ hipError_t launch_temporal_hl(const TemporalHLArgs& a, hipStream_t s) {
 
 #ifdef DSTD_STAMPS
 extern "C" int dstd_debug_timeline_hl(int mode, unsigned long long* host, int n) {
-  if (mode < 0 || mode > 1 || n > 2048 * 4) return 1;
+  if (mode < 0 || mode > 3 || n > 2048 * 4) return 1;
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tl_hl), n * sizeof(unsigned long long),
                                   mode * 2048 * 4 * sizeof(unsigned long long));
 }

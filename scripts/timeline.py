@@ -36,18 +36,23 @@ def main():
             model(x)
         torch.cuda.synchronize()
     buf = np.zeros(2048 * 4, dtype=np.uint64)
-    for mode in (0, 1):
+    names = {0: "k_adj_hl<0>", 1: "k_adj_hl<1>", 2: "k_temporal_fused phase 3 (start, E/F, tiles, drained)",
+             3: "k_temporal_fused C=64 (entry, chunk-0 phase 1, units, exit)"}
+    for mode in ((0, 1, 2, 3) if "--hl" in sys.argv else (0, 1)):
         fn(mode, buf.ctypes.data, buf.size)
         raw = buf.reshape(2048, 4).copy()
         raw = raw[raw[:, 0] > 0]
         hw = None
-        if "--hl" in sys.argv:  # slot 3 holds (XCC_ID << 32) | HW_ID: placement per workgroup
+        if not len(raw):
+            print(f"mode {mode} ({names.get(mode)}): no stamps")
+            continue
+        if "--hl" in sys.argv and mode < 2:  # slot 3 holds (XCC_ID << 32) | HW_ID: placement per workgroup
             hw = raw[:, 3].copy()
             raw[:, 3] = raw[:, 2]
         tl = raw.astype(np.float64)
         t0 = tl[:, 0].min()
         us = (tl - t0) / 100.0  # 100 MHz -> us
-        print(f"mode {mode}: {len(tl)} workgroups, span {us[:, 3].max():.2f} us")
+        print(f"mode {mode} ({names.get(mode)}): {len(tl)} workgroups, span {us[:, 3].max():.2f} us")
         for name, col in (("entry", 0), ("staged", 1), ("computed", 2), ("exit", 3)):
             c = us[:, col]
             print(f"   {name:9s} min {c.min():6.2f}  p50 {np.median(c):6.2f}  p90 {np.percentile(c, 90):6.2f}  max {c.max():6.2f}")
