@@ -161,6 +161,18 @@ def model_compulsory_bytes(opts):
     return sum(T * V * (a + b) * 4 for a, b in [(cin0, C)] + [(C, C)] * L + [(C, cout_last)])
 
 
+def phase3_moves(blocks, opts, split_on):
+    """Blocks 1.. of a split forward at a FUSED_TEMPORAL shape get their
+    spatial adjacency from the previous block's fused temporal launch
+    (k_temporal_fused phase 3): that family's work moves there."""
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    if split_on and (T, opts["joints_to_consider"]) in FUSED_TEMPORAL:
+        for i in range(len(blocks) - 1):
+            blocks[i][native.KIND_TEMPORAL] += blocks[i + 1][native.KIND_ADJ_S]
+            blocks[i + 1][native.KIND_ADJ_S] = 0
+    return blocks
+
+
 def model_block_bytes(opts, split_on):
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V, C, L = opts["joints_to_consider"], opts["num_feature"], opts["num_layers"]
@@ -170,16 +182,16 @@ def model_block_bytes(opts, split_on):
     for cin, cout, tail in spec:
         split = (split_on and cin == 64 and cout == 64, split_on and cout == 64)
         out.append(block_bytes(cin, cout, T, V, tail, split))
-    return out
+    return phase3_moves(out, opts, split_on)
 
 
-def model_block_flops(opts):
+def model_block_flops(opts, split_on=False):
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V, C, L = opts["joints_to_consider"], opts["num_feature"], opts["num_layers"]
     blocks = [block_flops(opts["input_channels"], C, T, V, "in")]
     blocks += [block_flops(C, C, T, V, "enc") for _ in range(L)]
     blocks.append(block_flops(C, opts["input_channels"] // 2, T, V, "out"))
-    return blocks
+    return phase3_moves(blocks, opts, split_on)
 
 
 class Profiler:
@@ -437,7 +449,7 @@ def main():
     x = x_cpu.to(device)
     y = torch.empty_like(x)
     L = native.lib()
-    fl = model_block_flops(opts)
+    fl = model_block_flops(opts, model.gc_arithmetic == "split")
 
     def barrier():
         if dist is not None:
@@ -508,7 +520,8 @@ def main():
     traffic = load_traffic(kname + "_split" if split_blk else kname, split_instance(dominant, T, V) if split_blk else None)
     total_flop_per_seq = sum(sum(b.values()) for b in fl)
     # algorithmic FLOPs of the probed launch (the fused temporal launch also
-    # builds its adjacency: the adjacency family's FLOPs count to it)
+    # builds its own adjacency and, phase 3, the next block's spatial one:
+    # those families' FLOPs count to it -- phase3_moves did the latter)
     fused_t = split_on and (T, V) in FUSED_TEMPORAL
     launch_flop = fl[1][dominant] + (fl[1][native.KIND_ADJ_T] if fused_t and dominant == native.KIND_TEMPORAL else 0)
     flops = launch_flop * B / avg_launch_s / 1e12 if kernel_ms > 0 else 0.0

@@ -106,11 +106,10 @@ struct BlockFold {
   float* hl_rbias;  // [2T + V]: fused conv_rm biases (HLJob::bias_out) of rms0, rms1, rmt
 };
 
-// Which GC launches of a block run the split-f16 kernels; tf / sf: the
-// temporal / spatial one with its adjacency built in LDS (k_temporal_fused, no
-// k_adj_hl<1>; k_spatial_fused, no k_adj_hl<0>).
+// Which GC launches of a block run the split-f16 kernels; tf: the temporal
+// one with its adjacency built in LDS (k_temporal_fused, no k_adj_hl<1>).
 struct BlockHL {
-  bool s, t, tf, sf;
+  bool s, t, tf;
   bool s_pre = false;  // the spatial adjacency planes were built by the previous block's temporal launch
 };
 
@@ -275,7 +274,7 @@ struct BlockTail {
 // Split-f16 GC kernels (dstd_hilo.hip) where the shape has them, unless the
 // call asks for exact fp32 (DSTD_FWD_EXACT_FP32).
 BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V, bool exact) {
-  BlockHL r{false, false, false, false, false};
+  BlockHL r{false, false, false, false};
   if (exact) return r;
   r.s = spatial_hl_supported(T, V) &&
         ((p->cin == 64 && p->cout == 64) || (p->cin == 6 && p->cout == 64) || (p->cin == 64 && p->cout == 3));
@@ -285,12 +284,6 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V
          (p->cout == 3 && (tail.epi == TEPI_OUT || tail.epi == TEPI_RAW) && !tail.next));
 #ifndef DSTD_NO_TFUSED
   r.tf = r.t && temporal_fused_supported(T, V);
-#endif
-#ifdef DSTD_SFUSED  // (opt-in: measured slower than k_adj_hl<0> + k_spatial_hl)
-  r.sf = r.s && spatial_fused_supported(T, V);
-#ifdef DSTD_SF_MASK  // (bisection builds: bit 0 64->64, bit 1 6->64, bit 2 64->3)
-  r.sf = r.sf && ((DSTD_SF_MASK >> (p->cin == 6 ? 1 : p->cout == 3 ? 2 : 0)) & 1);
-#endif
 #endif
   return r;
 }
@@ -370,7 +363,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   }
   hipError_t e = hipSuccess;
   AdjHLArgs ah{};
-  const bool adj_launch = !hl.sf && !hl.s_pre;
+  const bool adj_launch = !hl.s_pre;
   if (adj_launch) pf.begin(DSTD_KIND_ADJ_S, s);
   if (hl.s) {
     ah.pq = aa.pq;
@@ -397,7 +390,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
         ah.mb[g][1] = p->conv_s[g].bm2;
       }
     }
-    // else built in LDS by k_spatial_fused (step 2) or already in sc.adj_s (s_pre)
+    // (s_pre: already in sc.adj_s, built by the previous block's temporal launch)
     if (adj_launch) e = launch_adj_hl(ah, 0, T, V, s);
 #ifdef DSTD_SPRE_CHECK
     if (hl.s_pre) {
@@ -470,7 +463,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ha.pqb[1] = p->conv_t.bm2;
     ha.pq = sc.pq_t;
     pf.begin(DSTD_KIND_SPATIAL, s);
-    e = hl.sf ? launch_spatial_fused(ha, ah, s) : launch_spatial_hl(ha, s);
+    e = launch_spatial_hl(ha, s);
     pf.end(s);
     if (e != hipSuccess) return e;
   } else {
@@ -920,7 +913,7 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
   StreamDeviceGuard dev_guard_(stream, x);
   const bool reuse = (flags & DSTD_FWD_REUSE_CONSTANTS) != 0;
   const bool exact = (flags & DSTD_FWD_EXACT_FP32) != 0;
-  if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32)) return DSTD_EINVAL;
+  if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32 | DSTD_FWD_SEPARATE_ADJ)) return DSTD_EINVAL;
   if (!p || !x || !y || !workspace) return DSTD_EINVAL;
   if (prof && (prof->capacity < 0 || (prof->capacity > 0 && (!prof->events || !prof->kinds)))) return DSTD_EINVAL;
   Prof pf;
@@ -1004,10 +997,9 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
 #ifndef DSTD_NO_SPRE
   // a block's spatial adjacency from the previous block's fused temporal
   // launch (phase 3), which writes the P/Q it is built from
-  for (int b = 1; b < NB; ++b)
+  for (int b = 1; b < NB && !(flags & DSTD_FWD_SEPARATE_ADJ); ++b)
     if (hls[b].s && hls[b - 1].tf && blk[b - 1]->cout == 64) {
       hls[b].s_pre = true;
-      hls[b].sf = false;
       tails[b - 1].next_f = fold[b];
       tails[b - 1].next_adj = true;
     }

@@ -308,10 +308,5 @@ bool temporal_hl_supported(int T, int V);
 // hipErrorNotSupported off its shapes
 hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn, hipStream_t s);
 bool temporal_fused_supported(int T, int V);
-// the spatial GC with both graphs' adjacency built in LDS (k_spatial_fused): g
-// as for launch_spatial_hl (g.adj unused), j as for launch_adj_hl mode 0
-// (j.out unused); hipErrorNotSupported off its shapes
-hipError_t launch_spatial_fused(const SpatialHLArgs& g, const AdjHLArgs& j, hipStream_t s);
-bool spatial_fused_supported(int T, int V);
 
 }  // namespace dstd

@@ -358,9 +358,9 @@ __device__ __forceinline__ void stage_bnC(float4* dst, const float* src, int V, 
   }
 }
 
-// The stage (LDS images) and the unit loop of the spatial GC, shared by
-// k_spatial_hl (adjacency planes from HBM, written by k_adj_hl<0>) and
-// k_spatial_fused (planes built in LDS by the same launch).
+// The stage (LDS images) and the unit loop of the spatial GC (k_spatial_hl;
+// factored out in round 3 for the fused-spatial experiments of DESIGN.md §4,
+// whose kernels read the adjacency B fragments from LDS through load_adj_g).
 template <int V, int CIN, int COUT>
 struct SpatialStage {
   static constexpr bool RES = CIN != COUT;
@@ -1671,24 +1671,22 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
   }
   if (tid < 2) asg(tid)[V * V] = 0.f;
   if (tid < 2 * 16 * RT) bl[tid] = bv;
-  auto ef_pad = [&](float val) __attribute__((always_inline)) {  // padding k and the row p = q = V: tanh 0
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      float* El = Elg(g);
-      float* Fl = El + (V + 1) * SE;
-      for (int i = tid; i < (V + 1) * (KP - K); i += NT) {
-        const int r = i / (KP - K), k = K + i % (KP - K);
-        El[r * SE + k] = val;
-        Fl[r * SE + k] = val;
-      }
-      for (int i = tid; i < K; i += NT) {
-        El[V * SE + i] = val;
-        Fl[V * SE + i] = val;
-      }
+  auto ef_pad = [&](int g, float val) __attribute__((always_inline)) {  // padding k and the row p = q = V: tanh 0
+    float* El = Elg(g);
+    float* Fl = El + (V + 1) * SE;
+    for (int i = tid; i < (V + 1) * (KP - K); i += NT) {
+      const int r = i / (KP - K), k = K + i % (KP - K);
+      El[r * SE + k] = val;
+      Fl[r * SE + k] = val;
+    }
+    for (int i = tid; i < K; i += NT) {
+      El[V * SE + i] = val;
+      Fl[V * SE + i] = val;
     }
   };
-  ef_pad(1.f);
-  int bad = 0;
+  ef_pad(0, 1.f);
+  ef_pad(1, 1.f);
+  int bad[2] = {0, 0};
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     float* El = Elg(g);
@@ -1699,7 +1697,7 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
       if (i < T * V) {
         const int t = i % T, v = i / T;
         const float ep0 = C2 * q4[g][it].x, ep1 = C2 * q4[g][it].y, eq0 = -C2 * q4[g][it].z, eq1 = -C2 * q4[g][it].w;
-        bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
+        bad[g] |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
         El[v * SE + t] = __builtin_amdgcn_exp2f(ep0);
         El[v * SE + T + t] = __builtin_amdgcn_exp2f(ep1);
         Fl[v * SE + t] = __builtin_amdgcn_exp2f(eq0);
@@ -1707,11 +1705,13 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
       }
     }
   }
-  const bool sep = __syncthreads_or(bad) == 0;
-  if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0)
+  // separable or direct tanh per graph, as k_adj_hl<0> decides per (sample, graph) workgroup
+  const bool sep0 = __syncthreads_or(bad[0]) == 0, sep1 = __syncthreads_or(bad[1]) == 0;
+  if (!sep0 || !sep1) {  // direct path: E / F hold P / Q themselves (padding 0)
     __syncthreads();
-    ef_pad(0.f);
     for (int g = 0; g < 2; ++g) {
+      if (g ? sep1 : sep0) continue;
+      ef_pad(g, 0.f);
       float* El = Elg(g);
       float* Fl = El + (V + 1) * SE;
       for (int i = tid; i < T * V; i += NT) {
@@ -1731,8 +1731,7 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
   const float inv0 = *j.wscale[0], inv1 = *j.wscale[1];
   TLH(2, 1)
 
-  auto tiles = [&](auto sep_c) __attribute__((always_inline)) {
-    constexpr bool SEP = decltype(sep_c)::value;
+  {
     // one tile space over both graphs (2 NCTC column tiles): the waves split
     // it evenly instead of rounding up twice
     f16x8 wh[RT][NS], wo[RT][NS];  // the current graph's conv_rm rows as B fragments
@@ -1771,7 +1770,8 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
       const bool va = col < NCOL && pa < V;
       f16x8 bh[NS], bo[NS];
       f16x4 th, to;
-      tanh_frags<SEP, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
+      if (g ? sep1 : sep0) tanh_frags<true, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
+      else tanh_frags<false, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
       // the accumulator's 4 columns colb .. colb + 3 (one joint q, slots slot0 ..)
       const int colb = ct * 16 + 4 * kg, q = colb / SL, slot0 = colb - q * SL;
       float asv[4], al[4];
@@ -1811,9 +1811,7 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
                                               off + 2u * NCOL, 0, DSTD_ADJ_ST_AUX);
       }
     }
-  };
-  if (sep) tiles(std::true_type{});
-  else tiles(std::false_type{});
+  }
 #ifdef DSTD_STAMPS
   TLH(2, 2)
   __builtin_amdgcn_s_waitcnt(0);
@@ -2139,305 +2137,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 // ===========================================================================
-// Spatial DSTDGC with its adjacency built in LDS (DSTDGC.forward model/
-// dstdgcn.py:83-87 feeding 95-97; round 3): one workgroup per sample, 8 waves.
-// The sample's frames go in chunks of F (a multiple of 8, <= 16: one row tile
-// of the conv_rm GEMM): phase 1, every wave builds both graphs' split-f16
-// planes of the chunk in LDS -- k_adj_hl<0>'s tanh GEMM and epilogue, the same
-// products in the same order, so the planes are bit-identical to the ones
-// k_adj_hl<0> wrote to HBM -- then phase 2, every wave runs GC units (frames)
-// of the chunk (spatial_units, the unit loop of k_spatial_hl) with its
-// adjacency B fragments from LDS.  The planes never reach HBM: k_adj_hl<0>
-// wrote B x 2 x T x 2 planes x V x SL halves (148 KB per sample at H36M) and
-// k_spatial_hl read them back.  Cost: the tanh operand is regenerated per
-// chunk (cdiv(T, F) x k_adj_hl<0>'s).
-// Phases, not producer / consumer waves: a 4 + 4 wave pipeline of this
-// kernel (round 3, profiles/r03f_pipe_ab.txt) ran 43% slower than k_adj_hl<0>
-// + k_spatial_hl -- the GC units are latency-bound streaming and 4 waves per
-// CU keep half the loads in flight that 8 do.
-// LDS: one plane buffer, both graphs' E/F rows and Astat, the GC stage.
-// ===========================================================================
-template <int T, int V, int CIN, int COUT>
-struct SFusedGeom {
-  using SM = SlotMap<V, true>;
-  static constexpr int K = 2 * T, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL, SE = KP + 4;
-  static constexpr int SL = SM::SL, NCOL = V * SL, NCTC = cdiv(NCOL, 16);
-  static constexpr int PG = 2 * V * SL;  // halves per (frame, graph): hi plane, lo plane ([V rows][SL] each)
-  static constexpr int RTG = cdiv(T, 16);
-  static constexpr int FULL = NS * 2 * 64;  // uint4 per row tile of the HLJ_RM image (full K-steps)
-  static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
-  static constexpr size_t EF = al16(2 * (size_t)(V + 1) * SE * 4);  // one graph's E rows then F rows
-  static constexpr size_t AS = al16(((size_t)V * V + 1) * 4);       // one graph's Astat (+ a zero)
-  static constexpr size_t fixed_bytes() { return 2 * EF + 2 * AS + al16(sizeof(SpatialStage<V, CIN, COUT>)); }
-  static constexpr size_t lds(int f) { return al16((size_t)f * 2 * PG * 2) + fixed_bytes(); }
-  // frames per chunk: the fewest chunks whose plane buffer fits (DSTD_SF_F overrides)
-  static constexpr int pick_nch() {
-    for (int nch = 1; nch <= T; ++nch)
-      if (lds(cdiv(T, nch)) <= kLdsBudget) return nch;
-    return T;
-  }
-#ifdef DSTD_SF_F
-  static constexpr int F = DSTD_SF_F < T && lds(DSTD_SF_F) <= kLdsBudget ? DSTD_SF_F : cdiv(T, pick_nch());
-#else
-  static constexpr int F = cdiv(T, pick_nch());
-#endif
-  static constexpr int NCH = cdiv(T, F), RTC = cdiv(F, 16);  // chunks, row tiles per chunk
-  static constexpr size_t PLANES = al16((size_t)F * 2 * PG * 2), LDS = lds(F);
-  static_assert(LDS <= kLdsBudget, "one plane buffer of a chunk must fit");
-};
-
-struct SpatialFusedArgs {
-  SpatialHLArgs g;  // the GC launch (adj unused)
-  AdjHLArgs j;      // P/Q (pq, pql, p_ch or xin/mw/mb), HLJ_RM images, wscale, bias, alpha, astat of both graphs
-};
-
-template <int T, int V, int CIN, int COUT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_spatial_fused(SpatialFusedArgs fa) {
-  using Gm = SFusedGeom<T, V, CIN, COUT>;
-  using SM = typename Gm::SM;
-  constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
-  constexpr int PG = Gm::PG, F = Gm::F, NCH = Gm::NCH, FULL = Gm::FULL, NT = 512, NW = NT / 64, NWT = cdiv(V, 16);
-  constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
-  const SpatialHLArgs& a = fa.g;
-  const AdjHLArgs& j = fa.j;
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  _Float16* planes = reinterpret_cast<_Float16*>(dsm);  // [frame][graph][plane][V][SL]
-  unsigned char* fx = dsm + Gm::PLANES;
-  auto Elg = [&](int g) { return reinterpret_cast<float*>(fx + g * Gm::EF); };  // F rows at + (V + 1) * SE
-  auto asg = [&](int g) { return reinterpret_cast<float*>(fx + 2 * Gm::EF + g * Gm::AS); };
-  auto& st = *reinterpret_cast<SpatialStage<V, CIN, COUT>*>(fx + 2 * Gm::EF + 2 * Gm::AS);
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int kg = lane >> 4, cl = lane & 15;
-  const int n = blockIdx.x;  // one sample per workgroup
-
-  // ---- prologue: both graphs' P/Q -> E/F rows and Astat, the GC stage; the
-  // P/Q and Astat loads go out before the stage's ----
-  const PQLayout L = j.pql;
-  constexpr int NPQ = cdiv(T * V, NT), NAS = cdiv(V * V, NT);
-  // (P_0, P_1, Q_0, Q_1) of graph g at element i (memory order: joint-major)
-  auto pq_at = [&](int g, int i) -> float4 {
-    const int t = i % T, v = i / T;
-    if constexpr (CIN == 6) {
-      if (j.xin) {  // conv_st_in (model/dstdgcn.py:298-305): P/Q of x6 = cat(x, x - x[:, -1])
-        const float* xn = j.xin + (size_t)n * T * V * 3;
-        const float* xc = xn + (t * V + v) * 3;
-        const float* xl = xn + ((T - 1) * V + v) * 3;
-        const float x6v[6] = {xc[0], xc[1], xc[2], xc[0] - xl[0], xc[1] - xl[1], xc[2] - xl[2]};
-        float pq[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float acc = j.mb[g][r >> 1][r & 1];
-#pragma unroll
-          for (int c = 0; c < 6; ++c) acc = fmaf(j.mw[g][r >> 1][(r & 1) * 6 + c], x6v[c], acc);
-          pq[r] = acc;
-        }
-        return make_float4(pq[0], pq[1], pq[2], pq[3]);
-      }
-    }
-    return ld4(j.pq + (size_t)n * L.sn + j.p_ch[g] + t * L.st + v * L.sv);
-  };
-  float4 q4[2][NPQ];
-  float av[2][NAS];
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-#pragma unroll
-    for (int it = 0; it < NPQ; ++it) q4[g][it] = pq_at(g, min(tid + it * NT, T * V - 1));
-#pragma unroll
-    for (int it = 0; it < NAS; ++it) av[g][it] = j.astat[g][min(tid + it * NT, V * V - 1)];
-  }
-  stage_spatial<V, CIN, COUT, NT>(a, st, tid);
-  auto ef_pad = [&](float val) {  // padding k and the row p = q = V: tanh 0
-#pragma unroll
-    for (int g = 0; g < 2; ++g) {
-      float* El = Elg(g);
-      float* Fl = El + (V + 1) * SE;
-      for (int i = tid; i < (V + 1) * (KP - K); i += NT) {
-        const int r = i / (KP - K), k = K + i % (KP - K);
-        El[r * SE + k] = val;
-        Fl[r * SE + k] = val;
-      }
-      for (int i = tid; i < K; i += NT) {
-        El[V * SE + i] = val;
-        Fl[V * SE + i] = val;
-      }
-    }
-  };
-  ef_pad(1.f);
-  int bad = 0;
-#pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    float* El = Elg(g);
-    float* Fl = El + (V + 1) * SE;
-#pragma unroll
-    for (int it = 0; it < NPQ; ++it) {
-      const int i = tid + it * NT;
-      if (i < T * V) {
-        const int t = i % T, v = i / T;
-        const float ep0 = C2 * q4[g][it].x, ep1 = C2 * q4[g][it].y, eq0 = -C2 * q4[g][it].z, eq1 = -C2 * q4[g][it].w;
-        bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
-        El[v * SE + t] = __builtin_amdgcn_exp2f(ep0);
-        El[v * SE + T + t] = __builtin_amdgcn_exp2f(ep1);
-        Fl[v * SE + t] = __builtin_amdgcn_exp2f(eq0);
-        Fl[v * SE + T + t] = __builtin_amdgcn_exp2f(eq1);
-      }
-    }
-    float* as = asg(g);
-#pragma unroll
-    for (int it = 0; it < NAS; ++it)
-      if (tid + it * NT < V * V) as[tid + it * NT] = av[g][it];
-    if (tid == 0) as[V * V] = 0.f;
-  }
-  const bool sep = __syncthreads_or(bad) == 0;
-  if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0); P/Q fetched again
-    __syncthreads();
-    ef_pad(0.f);
-    for (int g = 0; g < 2; ++g) {
-      float* El = Elg(g);
-      float* Fl = El + (V + 1) * SE;
-      for (int i = tid; i < T * V; i += NT) {
-        const int t = i % T, v = i / T;
-        const float4 p4 = pq_at(g, i);
-        El[v * SE + t] = p4.x;
-        El[v * SE + T + t] = p4.y;
-        Fl[v * SE + t] = p4.z;
-        Fl[v * SE + T + t] = p4.w;
-      }
-    }
-    __syncthreads();
-  }
-  const float dna = pow2f(-hl_range_shift(
-      fexp_bits(__float_as_uint(fmaxf(j.wscale[0][HLS_BOUND], j.wscale[1][HLS_BOUND])))));
-  const float alpha = *j.alpha * dna;
-
-  // ---- phase 1: both graphs' planes of chunk c (k_adj_hl<0> on the RTC row
-  // tiles of frames t0 .. t0 + F - 1: A = conv_rm rows, B = tanh columns) ----
-  constexpr int RTC = Gm::RTC;
-  auto produce = [&](int c, auto sep_c) __attribute__((always_inline)) {
-    constexpr bool SEP = decltype(sep_c)::value;
-    const int t0 = c * F, nf = min(F, T - t0);
-#pragma unroll 1
-    for (int g = 0; g < 2; ++g) {
-      // (selects, not j.x[g]: a run-time index into the kernel arguments puts them in scratch)
-      const uint4* wg = g ? j.wimg[1] : j.wimg[0];
-      const float* bg = g ? j.bias[1] : j.bias[0];
-      f16x8 ah[RTC][NS], ao[RTC][NS];
-      f16x4 tah[RTC], tao[RTC];
-      float b[RTC][4];  // conv_rm bias of this lane's output rows (frames t0 + 16 rt + 4kg + r)
-#pragma unroll
-      for (int rt = 0; rt < RTC; ++rt) {
-        // this lane's A-operand row cl = frame t0 + 16 rt + cl of the image
-        // (rows past the chunk read a valid row, their outputs are dropped)
-        const int tr = min(t0 + 16 * rt + cl, T - 1), rtw = tr >> 4, lw = (tr & 15) + 16 * kg;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          ah[rt][s] = as_h8(wg[((rtw * NS + s) * 2 + 0) * 64 + lw]);
-          ao[rt][s] = as_h8(wg[((rtw * NS + s) * 2 + 1) * 64 + lw]);
-        }
-        if constexpr (TAIL) {
-          const uint2* w16 = reinterpret_cast<const uint2*>(wg + Gm::RTG * FULL);
-          tah[rt] = __builtin_bit_cast(f16x4, w16[(rtw * 2 + 0) * 64 + lw]);
-          tao[rt] = __builtin_bit_cast(f16x4, w16[(rtw * 2 + 1) * 64 + lw]);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) b[rt][r] = bg[min(t0 + 16 * rt + 4 * kg + r, T - 1)];
-      }
-      const float inv = *(g ? j.wscale[1] : j.wscale[0]);
-      const float* El = Elg(g);
-      const float* Fl = El + (V + 1) * SE;
-      const float* as = asg(g);
-      for (int ct = wave; ct < Gm::NCTC; ct += NW) {
-        // this lane's B-operand column = column ct * 16 + cl of the planes
-        const int col = ct * 16 + cl;
-        const int q = col / SL, slot = col - q * SL, pi = SM::slot_idx(slot);
-        const bool valid = col < NCOL && pi < V;
-        f16x8 bh[NS], bo[NS];
-        f16x4 th, to;
-        tanh_frags<SEP, NS, TAIL, SE>(El, Fl, valid ? pi : V, col < NCOL ? q : V, kg, bh, bo, th, to);
-        f32x4 acc[RTC];
-#pragma unroll
-        for (int rt = 0; rt < RTC; ++rt) acc[rt] = zero4();
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-#pragma unroll
-          for (int rt = 0; rt < RTC; ++rt) acc[rt] = mfma32(ao[rt][s], bh[s], acc[rt]);
-#pragma unroll
-          for (int rt = 0; rt < RTC; ++rt) acc[rt] = mfma32(ah[rt][s], bo[s], acc[rt]);
-#pragma unroll
-          for (int rt = 0; rt < RTC; ++rt) acc[rt] = mfma32(ah[rt][s], bh[s], acc[rt]);
-        }
-        if constexpr (TAIL) {  // on an accumulator of its own (dstd_hilo.h: mixed-shape MFMA chains)
-          f32x4 tac[RTC];
-#pragma unroll
-          for (int rt = 0; rt < RTC; ++rt) tac[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(tao[rt], th, zero4(), 0, 0, 0);
-#pragma unroll
-          for (int rt = 0; rt < RTC; ++rt) tac[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(tah[rt], to, tac[rt], 0, 0, 0);
-#pragma unroll
-          for (int rt = 0; rt < RTC; ++rt) tac[rt] = __builtin_amdgcn_mfma_f32_16x16x16f16(tah[rt], th, tac[rt], 0, 0, 0);
-#pragma unroll
-          for (int rt = 0; rt < RTC; ++rt) acc[rt] += tac[rt];
-        }
-        // epilogue (k_adj_hl's): alpha * (acc + b) + Astat, 0 on padding slots
-        const float asv = as[valid ? pi * V + q : V * V] * dna, al = valid ? alpha : 0.f;
-        if (col < NCOL) {
-          _Float16* d = planes + g * PG + q * SL + slot;
-#pragma unroll
-          for (int rt = 0; rt < RTC; ++rt) {
-            float vv[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) vv[r] = fmaf(al, fmaf(acc[rt][r], inv, b[rt][r]), asv);
-            uint4 hi, lo;
-            split8(make_float4(vv[0], vv[1], vv[2], vv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
-            const uint32_t hw[2] = {hi.x, hi.y}, lw2[2] = {lo.x, lo.y};
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int f = 16 * rt + 4 * kg + r;
-              if (f < nf) {
-                const uint32_t sh = 16 * (r & 1);
-                d[f * 2 * PG] = __builtin_bit_cast(_Float16, (uint16_t)(hw[r >> 1] >> sh));
-                d[f * 2 * PG + V * SL] = __builtin_bit_cast(_Float16, (uint16_t)(lw2[r >> 1] >> sh));
-              }
-            }
-          }
-        }
-      }
-    }
-  };
-  // ---- phase 2: the GC units (frames) of chunk c ----
-  auto consume = [&](int c) __attribute__((always_inline)) {
-    const int t0 = c * F, nf = min(F, T - t0);
-    const int ub = n * T + t0;
-    auto load_adj_g = [&](int uu, int g, uint4 (&ab)[NWT][2]) {
-      const _Float16* base = planes + (uu - ub) * 2 * PG + g * PG;
-#pragma unroll
-      for (int wt = 0; wt < NWT; ++wt) {
-        const int w = 16 * wt + cl;  // output joint (plane row), slot group kg
-        const bool ok = w < V && kg < SM::NG;
-        const int off = ok ? w * SL + 8 * kg : 0;
-        const uint4 h = *reinterpret_cast<const uint4*>(base + off);
-        const uint4 l = *reinterpret_cast<const uint4*>(base + V * SL + off);
-        ab[wt][0] = ok ? h : make_uint4(0u, 0u, 0u, 0u);
-        ab[wt][1] = ok ? l : make_uint4(0u, 0u, 0u, 0u);
-      }
-    };
-    spatial_units<V, CIN, COUT>(a, st, ub + wave, ub + nf, NW, load_adj_g);
-  };
-
-#pragma unroll 1
-  for (int c = 0; c < NCH; ++c) {
-#ifndef DSTD_SF_NOPROD  // (timing experiments: phase 2 alone)
-    if (sep) produce(c, std::true_type{});
-    else produce(c, std::false_type{});
-#endif
-    __syncthreads();  // chunk c's planes
-#ifndef DSTD_SF_NOCONS  // (timing experiments: prologue + phase 1 alone)
-    consume(c);
-#endif
-    __syncthreads();  // the plane buffer is free
-  }
-}
-
-// ===========================================================================
 // dispatch
 // ===========================================================================
 namespace {
@@ -2577,39 +2276,6 @@ hipError_t tfused_tv(const TemporalFusedArgs& a, hipStream_t s) {
     case TEPI_RAW: return tfused_run<T, V, TEPI_RAW, 64>(a, s);
     default: return hipErrorNotSupported;
   }
-}
-
-template <int T, int V, int CIN, int COUT>
-hipError_t sfused_run(const SpatialFusedArgs& a, hipStream_t s) {
-  using Gm = SFusedGeom<T, V, CIN, COUT>;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)k_spatial_fused<T, V, CIN, COUT>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::LDS);
-  if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_spatial_fused<T, V, CIN, COUT>), dim3(a.g.B), dim3(512), Gm::LDS, s, a);
-  return hipGetLastError();
-}
-
-template <int T, int V>
-hipError_t sfused_tv(const SpatialFusedArgs& a, hipStream_t s) {
-  if (a.g.Cin == 64 && a.g.Cout == 64) return sfused_run<T, V, 64, 64>(a, s);
-  if (a.g.Cin == 6 && a.g.Cout == 64) return sfused_run<T, V, 6, 64>(a, s);
-  if (a.g.Cin == 64 && a.g.Cout == 3) return sfused_run<T, V, 64, 3>(a, s);
-  return hipErrorNotSupported;
-}
-
-bool spatial_fused_supported(int T, int V) { return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23); }
-
-hipError_t launch_spatial_fused(const SpatialHLArgs& g, const AdjHLArgs& j, hipStream_t s) {
-  if (!spatial_fused_supported(g.T, g.V) || j.ngroups != 2 || (g.xmodel && g.Cin != 6) || (g.xmodel != (j.xin != nullptr)))
-    return hipErrorNotSupported;
-  if (!j.xin && (j.pql.sch != 1 || ((uintptr_t)j.pq & 15) || (j.pql.st & 3) || (j.pql.sv & 3) || (j.pql.sn & 3) ||
-                 (j.p_ch[0] & 3) || (j.p_ch[1] & 3)))
-    return hipErrorNotSupported;
-  const SpatialFusedArgs a{g, j};
-  if (g.T == 35 && g.V == 22) return sfused_tv<35, 22>(a, s);
-  if (g.T == 35 && g.V == 25) return sfused_tv<35, 25>(a, s);
-  if (g.T == 40 && g.V == 23) return sfused_tv<40, 23>(a, s);
-  return hipErrorNotSupported;
 }
 
 bool temporal_fused_supported(int T, int V) { return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23); }

@@ -179,6 +179,11 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
  * (tests/test_gpu_parity.py).  No counterpart in the reference (pure fp32
  * ATen, model/dstdgcn.py:80-94). */
 #define DSTD_FWD_EXACT_FP32 2u
+/* Launch schedule, for A/B and the bit-identity test (same results either
+ * way): every block's spatial adjacency planes in a launch of their own
+ * (k_adj_hl<0>) instead of built by the previous block's fused temporal
+ * launch after its units (k_temporal_fused phase 3, the default). */
+#define DSTD_FWD_SEPARATE_ADJ 4u
 int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof);
 int dstd_events_create(int n, void** events);

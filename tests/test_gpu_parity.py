@@ -238,6 +238,30 @@ def test_constant_reuse_tracks_parameter_updates():
         assert torch.equal(m5(xi), y0) and torch.equal(m5(xi), y0)
 
 
+@pytest.mark.parametrize("tag", ["h36m", "cmu", "3dpw"])
+def test_phase3_spatial_adjacency_bit_identical(tag):
+    """The default schedule builds each block's spatial adjacency planes in
+    the previous block's fused temporal launch (k_temporal_fused phase 3);
+    DSTD_FWD_SEPARATE_ADJ builds them in k_adj_hl<0> launches as before.  Same
+    products, same order, and the separable / direct tanh chosen per (sample,
+    graph) in both -- bit-identical outputs, also for inputs large enough to
+    send some (sample, graph) through the direct tanh (round 3: deciding it
+    per sample for both graphs at once gave 1-ulp plane differences)."""
+    import dstd_native as native
+    m, _, _, opts = load_model(tag)
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    V = opts["joints_to_consider"]
+    for scale in (1.0, 40.0):
+        x = (synth(64, T, V, opts["input_time_frame"], 7) * scale).to(DEV)
+        y0, y1 = torch.empty_like(x), torch.empty_like(x)
+        with torch.no_grad():
+            m._forward_native(x, y0)
+            m._forward_native(x, y1, arith=native.FWD_SEPARATE_ADJ)
+        torch.cuda.synchronize()
+        assert torch.isfinite(y0).all()
+        assert torch.equal(y0, y1), (scale, float((y0 - y1).abs().max()))
+
+
 @pytest.mark.parametrize("B", [4, 32])
 def test_graphed_forward_matches_eager(B):
     """DSTDGCN.graphed (a HIP graph of the eval forward):
