@@ -400,9 +400,30 @@ def train_leg(device, B, steps, warmup):
         opt.step()
 
     ms, host = timed_calls(step, steps, warmup)
-    return {"workload": f"3DPW-shape synthetic T=40 V=23, B={B}: forward pair + 2 mpjpe + backward + Adam (fp32)",
-            "value": round(B / ms * 1e3, 2), "unit": "train seq/s", "ms_per_step": round(ms, 4),
-            "host_us_per_step": round(host, 2)}
+    out = {"workload": f"3DPW-shape synthetic T=40 V=23, B={B}: forward pair + 2 mpjpe + backward + Adam (fp32)",
+           "value": round(B / ms * 1e3, 2), "unit": "train seq/s", "ms_per_step": round(ms, 4),
+           "host_us_per_step": round(host, 2)}
+    # the same step captured as one HIP graph (engine/graphed.py; what
+    # PredictionEngine runs with learn.graph): capturable Adam, tensor lr
+    from engine.graphed import GraphedStep
+    torch.manual_seed(0)
+    m2 = get_model("dstdgcn", dstdgcn=opts).to(device).train()
+    m2._dstd_inplace_grads = True
+    opt2 = torch.optim.Adam(m2.parameters(), lr=torch.tensor(3e-3, device=device), capturable=True)
+
+    def step2(a, b, s, si):
+        out2, out2_i = m2.forward_pair(a.view(B, 40, 23, 3), b.view(B, 40, 23, 3))
+        loss2 = (mpjpe_error_3d(out2.reshape(B, 40, 69), s) + mpjpe_error_3d(out2_i.reshape(B, 40, 69), si)) / 2
+        opt2.zero_grad()
+        loss2.backward()
+        opt2.step()
+        return (loss2.detach(),)
+
+    g = GraphedStep(step2, (inp, inv, seq, seq_inv), m2, opt2)
+    gms, ghost = timed_calls(lambda: g(inp, inv, seq, seq_inv), steps, warmup)
+    out["graph_replay"] = {"value": round(B / gms * 1e3, 2), "ms_per_step": round(gms, 4),
+                           "host_us_per_step": round(ghost, 2)}
+    return out
 
 
 def main():

@@ -273,7 +273,8 @@ struct BlockTail {
 
 // Split-f16 GC kernels (dstd_hilo.hip) where the shape has them, unless the
 // call asks for exact fp32 (DSTD_FWD_EXACT_FP32).
-BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V, bool exact) {
+BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int B, int T, int V, unsigned flags) {
+  const bool exact = (flags & DSTD_FWD_EXACT_FP32) != 0;
   BlockHL r{false, false, false, false};
   if (exact) return r;
   r.s = spatial_hl_supported(T, V) &&
@@ -283,7 +284,10 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int T, int V
           (!tail.next || tail.next->cin == 64)) ||
          (p->cout == 3 && (tail.epi == TEPI_OUT || tail.epi == TEPI_RAW) && !tail.next));
 #ifndef DSTD_NO_TFUSED
-  r.tf = r.t && temporal_fused_supported(T, V);
+  // one workgroup per sample: below one sample per CU the fused kernel leaves
+  // CUs idle and the unit-parallel pair (k_adj_hl<1> + k_temporal_hl) wins
+  // (B = 16..128: 25-30% faster forward; B = 256: 8% slower, profiles/r03m_small_batch_ab.txt)
+  r.tf = r.t && temporal_fused_supported(T, V) && (B >= hl_device_cus() || (flags & DSTD_FWD_FUSED_TEMPORAL));
 #endif
   return r;
 }
@@ -874,7 +878,7 @@ int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int
 int dstd_block_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags) {
   StreamDeviceGuard dev_guard_(stream, x);
-  if (flags & ~DSTD_FWD_EXACT_FP32) return DSTD_EINVAL;
+  if (flags & ~(DSTD_FWD_EXACT_FP32 | DSTD_FWD_FUSED_TEMPORAL)) return DSTD_EINVAL;
   if (!x || !y || !workspace || !block_ok(p) || !shape_ok(B, T, V)) return DSTD_EINVAL;
   if (!limits_ok(T, V, p->cin, p->cout)) return DSTD_ELIMIT;
   if (workspace_bytes < dstd_block_workspace_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
@@ -888,7 +892,7 @@ int dstd_block_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, 
   DSTD_TRY(to_layout(x, L.xin, B, p->cin, T * V, 1, s));
   DSTD_TRY(spatial_pq(p, L.xin, B, T, V, L.sc.pq_s, s));
   BlockTail tail{TEPI_RAW, nullptr, nullptr, nullptr, nullptr, nullptr};
-  const BlockHL hl = block_hl(p, tail, T, V, (flags & DSTD_FWD_EXACT_FP32) != 0);
+  const BlockHL hl = block_hl(p, tail, B, T, V, flags);
   HLList hj;
   add_block_hl_jobs(hj, p, L.f, tail, hl, T, V);
   DSTD_TRY(run_hl_prep(hj, s));
@@ -913,7 +917,8 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
   StreamDeviceGuard dev_guard_(stream, x);
   const bool reuse = (flags & DSTD_FWD_REUSE_CONSTANTS) != 0;
   const bool exact = (flags & DSTD_FWD_EXACT_FP32) != 0;
-  if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32 | DSTD_FWD_SEPARATE_ADJ)) return DSTD_EINVAL;
+  if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32 | DSTD_FWD_SEPARATE_ADJ | DSTD_FWD_FUSED_TEMPORAL))
+    return DSTD_EINVAL;
   if (!p || !x || !y || !workspace) return DSTD_EINVAL;
   if (prof && (prof->capacity < 0 || (prof->capacity > 0 && (!prof->events || !prof->kinds)))) return DSTD_EINVAL;
   Prof pf;
@@ -991,7 +996,7 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
   }
   HLList hj;
   for (int b = 0; b < NB; ++b) {
-    hls[b] = block_hl(blk[b], tails[b], T, V, exact);
+    hls[b] = block_hl(blk[b], tails[b], B, T, V, flags);
     add_block_hl_jobs(hj, blk[b], *fold[b], tails[b], hls[b], T, V);
   }
 #ifndef DSTD_NO_SPRE

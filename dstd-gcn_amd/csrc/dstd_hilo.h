@@ -293,6 +293,7 @@ struct AdjHLArgs {
 };
 
 hipError_t launch_hl_prep(const HLPrepArgs& a, hipStream_t s);
+int hl_device_cus();  // compute units of the current device
 // mode 0 spatial, 1 temporal
 hipError_t launch_adj_hl(const AdjHLArgs& a, int mode, int T, int V, hipStream_t s);
 // hipErrorNotSupported when the shape has no instantiation

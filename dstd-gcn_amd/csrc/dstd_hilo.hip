@@ -2190,6 +2190,8 @@ hipError_t temporal_hl_t(const TemporalHLArgs& a, hipStream_t s) {
 
 }  // namespace
 
+int hl_device_cus() { return hl_num_cus(); }
+
 hipError_t launch_hl_prep(const HLPrepArgs& a, hipStream_t s) {
   if (a.njobs <= 0) return hipSuccess;
   if (a.njobs > kMaxHLJobs) return hipErrorInvalidValue;

@@ -186,7 +186,9 @@ hipError_t out_ntvc_bwd(const float* dy, int B, int T, int V, int C, float* dO, 
 
 // Inverted dropout with a counter-based hash mask: out[i] = keep(seed, i) ? in[i] / (1 - p) : 0.
 // Applying it to the upstream gradient with the same seed is the backward.
-hipError_t dropout(const float* in, float* out, size_t n, float p, unsigned long long seed, hipStream_t s);
+// seed_on_device: `seed` is the address of a device uint64 holding the seed
+hipError_t dropout(const float* in, float* out, size_t n, float p, unsigned long long seed, hipStream_t s,
+                   bool seed_on_device = false);
 
 // mpjpe_error_3d (engine/utils/loss.py:52-65): loss = mean_k ||p_k - q_k||_2
 // over K = n / 3 points.  fwd: out[0] (=); bwd: dp = g * (p - q) / ||p - q|| / K

@@ -6,6 +6,7 @@
 #include "dstd_train.h"
 
 #include <algorithm>
+#include <stdio.h>
 
 namespace dstd {
 namespace train {
@@ -861,7 +862,9 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
   return z ^ (z >> 31);
 }
 
-__global__ void k_dropout(const float* in, float* out, size_t n, float p, unsigned long long seed) {
+__global__ void k_dropout(const float* in, float* out, size_t n, float p, unsigned long long seed,
+                          const unsigned long long* seedp) {
+  if (seedp) seed = *seedp;  // DSTD_TRAIN_SEED_DEVICE (a seed drawn on the device: graph replays)
   const float keep_scale = 1.f / (1.f - p);
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
     const unsigned long long h = mix64(seed * 0x9e3779b97f4a7c15ULL + e);
@@ -956,6 +959,11 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   }
   dim3 grid(cdiv(g.N, TN), cdiv(g.M, TM), g.reduce ? nsplit : nbat);
   float* part = nsplit > 1 ? scratch : nullptr;
+#ifdef DSTD_GEMM_LOG  // (debug builds: the shape mix of a training step)
+  fprintf(stderr, "gemm M %d N %d K %d nb %d reduce %d nsplit %d a_m %lld a_k %lld b_k %lld b_n %lld c_m %lld c_n %lld "
+          "d_out %d nseg %d bias %d beta %g\n", g.M, g.N, g.K, nbat, g.reduce, nsplit, g.a_m, g.a_k, g.b_k, g.b_n, g.c_m,
+          g.c_n, g.d_out != nullptr, g.nseg, g.bias_m != nullptr, g.beta);
+#endif
   if (TM == 32 && TN == 32) k_gemm<32, 32><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
   else if (TM == 32) k_gemm<32, 64><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
   else if (TN == 32) k_gemm<64, 32><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
@@ -1119,8 +1127,10 @@ hipError_t out_ntvc_bwd(const float* dy, int B, int T, int V, int C, float* dO, 
   return hipGetLastError();
 }
 
-hipError_t dropout(const float* in, float* out, size_t n, float p, unsigned long long seed, hipStream_t s) {
-  k_dropout<<<grid_for(n), 256, 0, s>>>(in, out, n, p, seed);
+hipError_t dropout(const float* in, float* out, size_t n, float p, unsigned long long seed, hipStream_t s,
+                   bool seed_on_device) {
+  const unsigned long long* seedp = seed_on_device ? reinterpret_cast<const unsigned long long*>(seed) : nullptr;
+  k_dropout<<<grid_for(n), 256, 0, s>>>(in, out, n, p, seedp ? 0ULL : seed, seedp);
   return hipGetLastError();
 }
 

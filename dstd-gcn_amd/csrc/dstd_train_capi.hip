@@ -28,6 +28,7 @@ constexpr int kMaxV = 32;
 constexpr int kMaxC = 64;
 constexpr int kMaxRed = 8;  // red_channels of one DSTDGC (P / Q channels each)
 constexpr unsigned kTrainFlags = DSTD_TRAIN_RUNNING_STATS | DSTD_TRAIN_PAIRED;
+constexpr unsigned kModelTrainFlags = kTrainFlags | DSTD_TRAIN_SEED_DEVICE;
 
 struct Carver {
   char* base;
@@ -659,7 +660,8 @@ int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, f
                             unsigned flags) {
   StreamDeviceGuard dev_guard_(stream, x);
   if (!model_ok(p) || !x || !y || !saved || !(dropout_p >= 0.f && dropout_p < 1.f)) return DSTD_EINVAL;
-  if (flags & ~kTrainFlags) return DSTD_EINVAL;
+  if (flags & ~kModelTrainFlags) return DSTD_EINVAL;
+  if ((flags & DSTD_TRAIN_SEED_DEVICE) && dropout_p > 0.f && !seed) return DSTD_EINVAL;
   if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
   const int run = (int)flags;
   const int T = p->T, V = p->V, C = p->num_feature, L = p->num_layers;
@@ -690,7 +692,7 @@ int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, f
   b0.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
   b0.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
   DSTD_TRY(bn_train_fwd(b0, B, C, T, V, S.red, s));
-  if (dropout_p > 0.f) DSTD_TRY(dropout(S.hp0, S.h[0], act, dropout_p, seed, s));  // do_in
+  if (dropout_p > 0.f) DSTD_TRY(dropout(S.hp0, S.h[0], act, dropout_p, seed, s, (flags & DSTD_TRAIN_SEED_DEVICE) != 0));  // do_in
   for (int i = 0; i < L; ++i) {                                                  // :310-311
     DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s, run));
     BnFwd be;  // BN(block(h) + h) -> PReLU  (:278-285, Identity residual :247-248)
@@ -728,7 +730,8 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
   StreamDeviceGuard dev_guard_(stream, x);
   if (!model_ok(p) || !g || !x || !dy || !saved || !workspace || !(dropout_p >= 0.f && dropout_p < 1.f))
     return DSTD_EINVAL;
-  if (flags & ~kTrainFlags) return DSTD_EINVAL;
+  if (flags & ~kModelTrainFlags) return DSTD_EINVAL;
+  if ((flags & DSTD_TRAIN_SEED_DEVICE) && dropout_p > 0.f && !seed) return DSTD_EINVAL;
   if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
   const int run = (int)flags;
   const int T = p->T, V = p->V, C = p->num_feature, L = p->num_layers;
@@ -773,7 +776,7 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
     DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s, run, true, W.du));
     std::swap(dha, dhb);
   }
-  if (dropout_p > 0.f) DSTD_TRY(dropout(dha, dha, act, dropout_p, seed, s));
+  if (dropout_p > 0.f) DSTD_TRY(dropout(dha, dha, act, dropout_p, seed, s, (flags & DSTD_TRAIN_SEED_DEVICE) != 0));
   BnBwd b0;
   b0.x = S.y0;
   b0.zsave = S.z0;

@@ -75,9 +75,11 @@ class ModelGrads(ctypes.Structure):
 
 TRAIN_RUNNING_STATS = 1  # include/dstd_gcn_train.h DSTD_TRAIN_RUNNING_STATS
 TRAIN_PAIRED = 2  # DSTD_TRAIN_PAIRED: two BatchNorm batches of B/2 (a forward pair)
+TRAIN_SEED_DEVICE = 4  # DSTD_TRAIN_SEED_DEVICE: the dropout seed is read from device memory
 FWD_REUSE_CONSTANTS = 1  # include/dstd_gcn.h DSTD_FWD_REUSE_CONSTANTS
 FWD_EXACT_FP32 = 2  # include/dstd_gcn.h DSTD_FWD_EXACT_FP32
 FWD_SEPARATE_ADJ = 4  # include/dstd_gcn.h DSTD_FWD_SEPARATE_ADJ
+FWD_FUSED_TEMPORAL = 8  # include/dstd_gcn.h DSTD_FWD_FUSED_TEMPORAL
 KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL = range(6)
 KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temporal_gc")
 

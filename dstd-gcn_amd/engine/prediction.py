@@ -115,6 +115,12 @@ class PredictionEngine:
             return x
         return [self.inverse_func(s) for s in x] if isinstance(x, list) else self.inverse_func(x)
 
+    def _graphed(self):
+        """learn.graph: capture the training step as a HIP graph (engine/graphed.py)
+        -- one process per GPU without a process group (a gloo all-reduce
+        cannot be captured)."""
+        return bool(self.config["learn"].get("graph", False)) and self.device.type == "cuda" and _world()[1] == 1
+
     def reset(self):
         self.lr = self.config["learn"]["lr"]
         self.best_err = float("inf")
@@ -147,7 +153,15 @@ class PredictionEngine:
     def _setup_learn(self, params, opt_type="adam"):
         if opt_type != "adam":
             raise NotImplementedError(f"optimizer '{opt_type}' (shipped configs use adam)")
-        optimizer = optim.Adam(params, lr=self.config["learn"]["lr"], weight_decay=self.config["learn"]["weight_decay"])
+        if self._graphed():
+            # replayable step (engine/graphed.py): device-side step count and a
+            # tensor learning rate that StepLR updates in place
+            optimizer = optim.Adam(params, lr=torch.tensor(float(self.config["learn"]["lr"]), device=self.device),
+                                   weight_decay=self.config["learn"]["weight_decay"], capturable=True)
+        else:
+            optimizer = optim.Adam(params, lr=self.config["learn"]["lr"],
+                                   weight_decay=self.config["learn"]["weight_decay"])
+        self._graph_step = None
         scheduler = optim.lr_scheduler.StepLR(optimizer, step_size=self.config["learn"]["step_size"],
                                               gamma=self.config["learn"]["gamma"])
         return optimizer, scheduler
@@ -176,59 +190,23 @@ class PredictionEngine:
         for i, (inputs, inputs_inv, targets, all_seqs) in enumerate(train_loader):
             inputs, inputs_inv, targets = _to_dev(inputs, dev), _to_dev(inputs_inv, dev), _to_dev(targets, dev)
             N = inputs[0].shape[0] if isinstance(inputs, list) else inputs.shape[0]
-            if time_tsfm is not None:
-                inputs = time_tsfm.transform(inputs)
-            inputs = self.transform(inputs)
-            # the batch and its time reversal as one native forward pair
-            # (DSTDGCN.forward_pair: per-half BatchNorm statistics, so the same
-            # step as the two calls of the reference, with half the launches)
-            pair = self.config["inverse"] and hasattr(self.model.model, "forward_pair")
-            if pair:
-                if time_tsfm is not None:
-                    inputs_inv = time_tsfm.transform(inputs_inv)
-                inputs_inv = self.transform(inputs_inv)
-                out_pair = self.model.model.forward_pair(inputs, inputs_inv)
-                outputs = self.inverse(out_pair[0])
+
+            def step(inp, inp_inv, targ):
+                return self._step(inp, inp_inv, targ, time_tsfm, scale_tsfm, weights, distributed)
+
+            tensors = not isinstance(inputs, list) and torch.is_tensor(inputs_inv)
+            if self._graphed() and tensors:
+                g = self._graph_step
+                if g is None:
+                    from .graphed import GraphedStep
+                    g = self._graph_step = GraphedStep(step, (inputs, inputs_inv, targets), self.model.model,
+                                                       self.optimizer)
+                losses = g(inputs, inputs_inv, targets) if g.matches(inputs, inputs_inv, targets) else \
+                    step(inputs, inputs_inv, targets)  # (a ragged last batch runs eagerly)
             else:
-                outputs = self.inverse(self.model(inputs, False))
-            if scale_tsfm is not None:
-                outputs = scale_tsfm.inverse(outputs)
-            if time_tsfm is not None:
-                outputs = time_tsfm.inverse(outputs)
-            t = outputs.shape[1]
-            targets_l = targets[:, -t:] if t != targets.shape[1] else targets
-            loss = self.model.calc_loss(outputs, targets_l, "all", weights)
-            all_loss = 0
-            for ls in loss:
-                all_loss = all_loss + loss[ls]
-                t_l[ls].update(loss[ls] * N, N)
-            if self.config["inverse"]:  # time-reversed augmentation pass (:267-287)
-                if pair:
-                    outputs_inv = self.inverse(out_pair[1])
-                else:
-                    if time_tsfm is not None:
-                        inputs_inv = time_tsfm.transform(inputs_inv)
-                    inputs_inv = self.transform(inputs_inv)
-                    outputs_inv = self.inverse(self.model(inputs_inv, True))
-                targets_inv = targets.flip(1)
-                t = outputs_inv.shape[1]
-                targets_il = targets_inv[:, -t:] if t != targets_inv.shape[1] else targets_inv
-                if time_tsfm is not None:
-                    outputs_inv = time_tsfm.inverse(outputs_inv)
-                if scale_tsfm is not None:
-                    outputs_inv = scale_tsfm.inverse(outputs_inv)
-                loss_inv = self.model.calc_loss(outputs_inv, targets_il, "all", weights)
-                for ls in loss_inv:
-                    all_loss = all_loss + loss_inv[ls]
-                all_loss = all_loss / 2
-            self.optimizer.zero_grad()
-            all_loss.backward()
-            if distributed:
-                from dstd_dist import allreduce_grads
-                allreduce_grads(self.model.parameters())
-            if self.config.get("clip", -1) > 0:
-                nn.utils.clip_grad_norm_(self.model.model.parameters(), max_norm=self.config["clip"])
-            self.optimizer.step()
+                losses = step(inputs, inputs_inv, targets)
+            for ls, v in zip(t_l, losses):
+                t_l[ls].update(v * N, N)
             if i >= num_iter - 1:
                 break
         if distributed:  # global averages: one all-reduce of (loss sums, sample counts)
@@ -246,8 +224,66 @@ class PredictionEngine:
         # the decayed rate decayed once more -- the value its checkpoints store
         with warnings.catch_warnings():
             warnings.simplefilter("ignore", UserWarning)
-            self.lr = self.scheduler.get_lr()[0]
+            self.lr = float(self.scheduler.get_lr()[0])
         return sum(avg.values())
+
+    def _step(self, inputs, inputs_inv, targets, time_tsfm, scale_tsfm, weights, distributed):
+        """One training step (:231-294): forward (pair), losses, backward,
+        gradient all-reduce / clip, Adam.  Returns the forward pass's losses
+        (one per loss type, in config order) for the epoch averages."""
+        if time_tsfm is not None:
+            inputs = time_tsfm.transform(inputs)
+        inputs = self.transform(inputs)
+        # the batch and its time reversal as one native forward pair
+        # (DSTDGCN.forward_pair: per-half BatchNorm statistics, so the same
+        # step as the two calls of the reference, with half the launches)
+        pair = self.config["inverse"] and hasattr(self.model.model, "forward_pair")
+        if pair:
+            if time_tsfm is not None:
+                inputs_inv = time_tsfm.transform(inputs_inv)
+            inputs_inv = self.transform(inputs_inv)
+            out_pair = self.model.model.forward_pair(inputs, inputs_inv)
+            outputs = self.inverse(out_pair[0])
+        else:
+            outputs = self.inverse(self.model(inputs, False))
+        if scale_tsfm is not None:
+            outputs = scale_tsfm.inverse(outputs)
+        if time_tsfm is not None:
+            outputs = time_tsfm.inverse(outputs)
+        t = outputs.shape[1]
+        targets_l = targets[:, -t:] if t != targets.shape[1] else targets
+        loss = self.model.calc_loss(outputs, targets_l, "all", weights)
+        all_loss = 0
+        for ls in loss:
+            all_loss = all_loss + loss[ls]
+        if self.config["inverse"]:  # time-reversed augmentation pass (:267-287)
+            if pair:
+                outputs_inv = self.inverse(out_pair[1])
+            else:
+                if time_tsfm is not None:
+                    inputs_inv = time_tsfm.transform(inputs_inv)
+                inputs_inv = self.transform(inputs_inv)
+                outputs_inv = self.inverse(self.model(inputs_inv, True))
+            targets_inv = targets.flip(1)
+            t = outputs_inv.shape[1]
+            targets_il = targets_inv[:, -t:] if t != targets_inv.shape[1] else targets_inv
+            if time_tsfm is not None:
+                outputs_inv = time_tsfm.inverse(outputs_inv)
+            if scale_tsfm is not None:
+                outputs_inv = scale_tsfm.inverse(outputs_inv)
+            loss_inv = self.model.calc_loss(outputs_inv, targets_il, "all", weights)
+            for ls in loss_inv:
+                all_loss = all_loss + loss_inv[ls]
+            all_loss = all_loss / 2
+        self.optimizer.zero_grad()
+        all_loss.backward()
+        if distributed:
+            from dstd_dist import allreduce_grads
+            allreduce_grads(self.model.parameters())
+        if self.config.get("clip", -1) > 0:
+            nn.utils.clip_grad_norm_(self.model.model.parameters(), max_norm=self.config["clip"])
+        self.optimizer.step()
+        return tuple(loss[ls].detach() for ls in self.config["loss"])
 
     # ------------------------------------------------------------------
     def test(self, test_loader, input_n=10, eval_frame=None, dim_used=None, joint_to_ignore=None, joint_equal=None,

@@ -94,6 +94,10 @@ def _register(mod):
 
 
 class _NativeModule(nn.Module):
+    # extra per-call launch-schedule flags of the eval forwards (include/dstd_gcn.h
+    # DSTD_FWD_SEPARATE_ADJ / DSTD_FWD_FUSED_TEMPORAL: same results, for tests and A/B)
+    _dstd_fwd_flags = 0
+
     def __setstate__(self, state):
         super().__setstate__(state)
         _register(self)
@@ -375,7 +379,15 @@ class _ModelTrain(torch.autograd.Function):
         # paired: x is two train-mode batches of B/2 (DSTDGCN.forward_pair)
         flags = _bn_flags(model) | (native.TRAIN_PAIRED if paired else 0)
         drop = float(model.do_in.p) if model.do_in.training else 0.0
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if drop > 0 else 0
+        seed, ctx.seed_t = 0, None
+        if drop > 0:
+            # the dropout seed is drawn on the device and read there
+            # (DSTD_TRAIN_SEED_DEVICE): no host round trip, and a captured HIP
+            # graph (engine.GraphedStep) draws a fresh mask per replay; the
+            # tensor lives in ctx until the backward has regenerated the mask
+            ctx.seed_t = torch.randint(0, 2 ** 62, (1,), device=x.device, dtype=torch.int64)
+            seed = ctx.seed_t.data_ptr()
+            flags |= native.TRAIN_SEED_DEVICE
         y, saved = torch.ops.dstd.dstdgcn_train_forward(x, list(params), model._tree.get(model)[1], model._dstd_uid,
                                                         flags, _bn_momentum(model), drop, seed)
         if not flags & native.TRAIN_RUNNING_STATS:
@@ -407,11 +419,11 @@ class _ModelTrain(torch.autograd.Function):
                 if g is None:  # the persistent arena: its pointer table is reused
                     g = arena.model_grads = model._native_grads(arena)
                 dx = _model_train_bwd_native(model, x, ctx.saved_buf, dy, ctx.flags, ctx.drop, ctx.seed, g, need_dx)
-                ctx.saved_buf = None
+                ctx.saved_buf = ctx.seed_t = None
                 return (None, None, dx, *([None] * len(arena.params)))
         dx, flat = torch.ops.dstd.dstdgcn_train_backward(x, ctx.saved_buf, dy, ctx.params, model._dstd_uid, ctx.flags,
                                                          ctx.drop, ctx.seed, need_dx)
-        ctx.saved_buf = None
+        ctx.saved_buf = ctx.seed_t = None
         arena = native.GradArena(ctx.params, dev, buf=flat)
         return (None, None, dx if need_dx else None, *arena.views())
 
@@ -560,8 +572,9 @@ class DSTDGCB(_NativeModule):
             # native training path (running-statistics BN in eval mode)
             return _BlockTrain.apply(self, x, *params)
         tensors = params + list(self.buffers())
+        # _dstd_fwd_flags: extra per-call schedule flags (tests / A-B: include/dstd_gcn.h DSTD_FWD_*)
         return torch.ops.dstd.dstdgcb_forward(x, tensors, self._dstd_uid, self.out_channels,
-                                              native.arith_flags(self.gc_arithmetic))
+                                              native.arith_flags(self.gc_arithmetic) | self._dstd_fwd_flags)
 
     def _eval_native(self, x, flags):
         """dstd_block_fwd_ex (torch.ops.dstd.dstdgcb_forward)."""
@@ -917,7 +930,7 @@ class DSTDGCN(_NativeModule):
         if prof is None:  # event brackets requested through the module (bench.py probes model(x) itself)
             prof = getattr(self, "_dstd_profile", None)
         p = self._native_params()
-        flags = native.arith_flags(self.gc_arithmetic) if arith is None else arith
+        flags = (native.arith_flags(self.gc_arithmetic) if arith is None else arith) | self._dstd_fwd_flags
         try:
             versions = tuple(map(_VERSION, self._native_tensors))
             tag = (self._dstd_uid, self._dstd_gen, self._native[0], n, flags, versions)

@@ -122,7 +122,7 @@ int dstd_dstdgc_fwd(int mode, const float* x, int B, int cin, int cout, int T, i
 /* y = DSTDGCB(x) in eval mode; x [B][cin][T][V] -> y [B][cout][T][V]. */
 int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float* y,
                    void* workspace, size_t workspace_bytes, void* stream);
-/* dstd_block_fwd with flags (DSTD_FWD_EXACT_FP32 only). */
+/* dstd_block_fwd with flags (DSTD_FWD_EXACT_FP32, DSTD_FWD_FUSED_TEMPORAL). */
 int dstd_block_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float* y,
                       void* workspace, size_t workspace_bytes, void* stream, unsigned flags);
 
@@ -184,6 +184,13 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
  * (k_adj_hl<0>) instead of built by the previous block's fused temporal
  * launch after its units (k_temporal_fused phase 3, the default). */
 #define DSTD_FWD_SEPARATE_ADJ 4u
+/* Launch schedule: the temporal graph convolutions with their adjacency
+ * built in LDS (k_temporal_fused, one workgroup per sample) at any batch
+ * size where the shape has the kernel.  Default: only when B >= the device's
+ * compute units -- below that the unit-parallel pair (k_adj_hl + k_temporal_hl)
+ * is faster.  Same results either way; for testing and A/B.  Also accepted by
+ * dstd_block_fwd_ex. */
+#define DSTD_FWD_FUSED_TEMPORAL 8u
 int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof);
 int dstd_events_create(int n, void** events);

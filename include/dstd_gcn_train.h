@@ -126,6 +126,12 @@ int dstd_block_train_bwd(const dstd_block_params* p, const float* x, int B, int 
  * (the engine's batch and its time reversal, engine/prediction.py:231-287)
  * in one launch sequence.  Pass the same flags to the backward. */
 #define DSTD_TRAIN_PAIRED 2u
+/* DSTD_TRAIN_SEED_DEVICE (model train fwd / bwd only): `seed` is the address
+ * of a device uint64 that holds the dropout seed, read by the kernels -- a
+ * seed drawn on the device (no host synchronisation, and a captured HIP graph
+ * draws a fresh one per replay).  Pass the same flags and address to the
+ * backward before the value changes. */
+#define DSTD_TRAIN_SEED_DEVICE 4u
 int dstd_block_train_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum,
                             float* y, void* saved, size_t saved_bytes, void* stream, unsigned flags);
 int dstd_block_train_bwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, const void* saved,

@@ -249,6 +249,7 @@ def test_phase3_spatial_adjacency_bit_identical(tag):
     per sample for both graphs at once gave 1-ulp plane differences)."""
     import dstd_native as native
     m, _, _, opts = load_model(tag)
+    m._dstd_fwd_flags = native.FWD_FUSED_TEMPORAL  # (phase 3 rides on the fused temporal launch)
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V = opts["joints_to_consider"]
     for scale in (1.0, 40.0):
@@ -260,6 +261,49 @@ def test_phase3_spatial_adjacency_bit_identical(tag):
         torch.cuda.synchronize()
         assert torch.isfinite(y0).all()
         assert torch.equal(y0, y1), (scale, float((y0 - y1).abs().max()))
+
+
+@pytest.mark.parametrize("tag", ["h36m", "cmu", "3dpw"])
+def test_fused_temporal_schedule_bit_identical(tag):
+    """Below one sample per CU the forward runs the unit-parallel temporal pair
+    (k_adj_hl<1> + k_temporal_hl); DSTD_FWD_FUSED_TEMPORAL forces the fused
+    kernel (and phase 3) at any batch.  Both schedules are the same arithmetic:
+    bit-identical at small batches, ragged B, the fixture input and inputs
+    x1000 (range-scaled planes) -- so every oracle test of the default
+    schedule covers the fused kernels too."""
+    import dstd_native as native
+    m, d, _, opts = load_model(tag)
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    V = opts["joints_to_consider"]
+    xs = [t(d["x"]), synth(5, T, V, opts["input_time_frame"], 3).to(DEV),
+          (synth(16, T, V, opts["input_time_frame"], 4) * 1000.0).to(DEV)]
+    for x in xs:
+        with torch.no_grad():
+            m._dstd_fwd_flags = 0
+            y0 = m(x)
+            m._dstd_fwd_flags = native.FWD_FUSED_TEMPORAL
+            y1 = m(x)
+        assert torch.equal(y0, y1), (tag, x.shape[0], float((y0 - y1).abs().max()))
+
+
+@pytest.mark.parametrize("cin,cout", [(64, 64), (6, 64), (64, 3)])
+def test_fused_temporal_schedule_bit_identical_block(cin, cout):
+    """The same at block level (dstd_block_fwd_ex), with a large adjacency
+    (|alpha| ~ 1e4: range-shifted planes)."""
+    import dstd_native as native
+    torch.manual_seed(7 + cin + cout)
+    blk = DSTDGCB(cin, cout, 35, 22, "h36m")
+    with torch.no_grad():
+        blk.alpha_tm.fill_(-2.0e4)
+        blk.alpha_sm.fill_(1.5e4)
+    blk = blk.to(DEV).eval()
+    x = torch.randn(6, cin, 35, 22, device=DEV)
+    with torch.no_grad():
+        y0 = blk(x)
+        blk._dstd_fwd_flags = native.FWD_FUSED_TEMPORAL
+        y1 = blk(x)
+    assert torch.isfinite(y0).all()
+    assert torch.equal(y0, y1), float((y0 - y1).abs().max())
 
 
 @pytest.mark.parametrize("B", [4, 32])

@@ -449,6 +449,43 @@ def test_training_curve_matches_reference():
     assert blk.A_s.data_ptr() == blk.R_s.data_ptr()
 
 
+def test_graphed_engine_step_equals_eager():
+    """learn.graph: the engine's step captured as a HIP graph (engine/graphed.py)
+    and replayed -- after the warm-up is undone, replay k is eager step k bit
+    for bit (the same capturable Adam both ways), across StepLR boundaries
+    (the tensor learning rate updated in place) and a ragged last batch that
+    runs eagerly; and the replays really are graph launches."""
+    from engine import PredictionEngine
+
+    class _Log:
+        def info(self, *a, **k):
+            pass
+
+    d = load_npz("engine.npz")
+    batches = [tuple(torch.from_numpy(d[f"train/{n}{i}"]) for n in ("inp", "inv", "seq", "seq")) for i in range(4)]
+    ragged = tuple(t[:6] for t in batches[3])
+    engines = []
+    for graphed in (True, False):
+        m, _ = _model_3dpw()
+        cfg = dict(learn=dict(opt="adam", lr=3e-3, weight_decay=0, gamma=0.5, step_size=2, graph=True),
+                   loss=dict(joint=["jl2", 1]), n_out=1, transform="tsc", use_weight=False, inverse=True)
+        eng = PredictionEngine(cfg, m, _Log())
+        if not graphed:
+            eng._graphed = lambda: False  # same capturable Adam, eager steps
+        losses = [eng.train(batches[:3] + [ragged], e) for e in range(3)]
+        engines.append((eng, m, losses))
+    (eg, mg, lg), (ee, me, le) = engines
+    assert eg._graph_step is not None and ee._graph_step is None
+    assert lg == le, (lg, le)
+    for (n, a), b in zip(mg.named_parameters(), me.parameters()):
+        assert torch.equal(a, b), n
+    for (n, a), b in zip(mg.named_buffers(), me.buffers()):
+        assert torch.equal(a, b), n
+    lr_g, lr_e = (float(e.optimizer.param_groups[0]["lr"]) for e in (eg, ee))
+    assert lr_g == lr_e and abs(lr_g - 1.5e-3) < 1e-9, (lr_g, lr_e)
+    assert lg[-1] < lg[0]
+
+
 def test_dropout_mask_is_regenerated_in_backward():
     """do_in dropout (p > 0): the forward mask is a hash of (seed, element),
     so the backward regenerates it; the gradient matches a finite difference
