@@ -790,7 +790,7 @@ constexpr int temporal_hl_wpe() {
 #ifdef DSTD_T_WPE
   return DSTD_T_WPE * (C == 3 ? 2 : 1);
 #endif
-  return (T <= 48 ? 2 : 1) * (C == 3 ? 2 : 1);
+  return (T <= 48 || C == 64 ? 2 : 1) * (C == 3 ? 2 : 1);
 }
 // one workgroup per CU at the kernel's waves per SIMD (4 waves at one per
 // SIMD: an 8-wave workgroup would force two per SIMD and spill), at most 8
@@ -1077,7 +1077,10 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     // that no branch hides the loads from hipcc's vmcnt bookkeeping)
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (EPI == TEPI_ENC && late_res) load_res_enc();
-    load_x(un < uend ? un : u);
+    // (long sequences: the next unit's rows after the epilogue, so that they,
+    // the output accumulators and the residual are not live at once)
+    constexpr bool late_x = LAZY && T > 48;
+    if constexpr (!late_x) load_x(un < uend ? un : u);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- epilogue ----
@@ -1163,6 +1166,10 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
                          fmaf(acc[ut][3], s, bql[b4 + 3])));
       }
     }
+    if constexpr (late_x) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_x(un < uend ? un : u);
+    }
     u = un;
   }
 }
@@ -1195,7 +1202,26 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
         bo[s][ut] = bldu4(rl, off);
       }
   };
-  temporal_units<T, EPI, C, 32, false>(a, st, u0, uend, 1, load_adj);
+  if constexpr (T > 48) {
+    // long sequences (T = 75): the unit's NS x NUT fragment pairs held through
+    // the conv took 120 VGPRs and left one wave per SIMD (256 VGPRs + 184
+    // AGPRs); fetched per aggregation K-step instead (LAZY), the kernel runs
+    // two waves per SIMD
+    auto load_adj_s = [&](int u, int s, uint4 (&bh)[NUT], uint4 (&bo)[NUT]) {
+      const auto rh = rsrc(a.adj + (size_t)u * (adj_bytes / 2), adj_bytes / 2);  // hi plane
+      const auto rl = rsrc(a.adj + (size_t)u * (adj_bytes / 2) + T * SL, adj_bytes / 2);
+#pragma unroll
+      for (int ut = 0; ut < NUT; ++ut) {
+        const int uo = 16 * ut + cl;
+        const uint32_t off = uo < T && kl < SM::ng(s) ? (uint32_t)(uo * SL + 8 * (SM::goff(s) + kl)) * 2 : OOB;
+        bh[ut] = bldu4(rh, off);
+        bo[ut] = bldu4(rl, off);
+      }
+    };
+    temporal_units<T, EPI, C, 32, true>(a, st, u0, uend, 1, load_adj_s);
+  } else {
+    temporal_units<T, EPI, C, 32, false>(a, st, u0, uend, 1, load_adj);
+  }
 }
 
 // ===========================================================================
