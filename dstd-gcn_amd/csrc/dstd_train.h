@@ -56,6 +56,25 @@ struct Gemm {
 size_t gemm_scratch_floats(int M, int N);
 hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s);
 
+// The DSTDGC aggregation products per sample n (model/dstdgcn.py:87 / :93),
+// NCTV operands with channel stride T*V and per-sample strides fs / ys / dys /
+// dfs; (a, i) = (t, v) for the spatial op, (v, t) for the temporal one;
+// D [B][A][NN][NN] (A = T, NN = V spatial; A = V, NN = T temporal):
+//   agg_fwd  y[c][(a,j)] (beta 0: = / 1: +=) sum_i F[c][(a,i)] D[a][i][j]
+//   agg_bwd  dF[c][(a,i)] = sum_j dy[c][(a,j)] D[a][i][j]
+//            dD[a][i][j] = sum_c F[c][(a,i)] dy[c][(a,j)]
+// agg_bwd reports how dD was produced in *nparts: 1 -- in dD; k > 1 -- as k
+// channel-chunk partials dDpart[p][B][A][NN][NN] (dDpart >= agg_parts(C) *
+// B*A*NN*NN floats; pass them to adj_bwd); 0 -- not at all (DSTD_AGG_FORM=0:
+// the caller's strided GEMM).  hipErrorNotSupported (nothing launched)
+// outside C <= 64, NN <= 64: the caller runs the strided GEMMs instead.
+hipError_t agg_fwd(const float* F, long long fs, const float* D, float* y, long long ys, float beta, int B, int C,
+                   int T, int V, int temporal, hipStream_t s);
+hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys, const float* D, float* dF,
+                   long long dfs, float* dD, int B, int C, int T, int V, int temporal, hipStream_t s, float* dDpart,
+                   int* nparts);
+inline int agg_parts(int C) { return (C + 15) / 16; }
+
 // P / Q element (n, r, a, i) lives at n*sn + r*sr + a*sa + i*si.
 struct PQView {
   long long sn, sr, sa, si;
@@ -72,9 +91,11 @@ hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int 
 // place, and dalpha += <dD, E>, dA[ij] += sum_{n,a} dD, dbrm[a] += sum_{n,ij} dE.
 // scratch >= adj_bwd_scratch_floats(B, A, NN2).
 size_t adj_bwd_scratch_floats(int B, int A, int NN2);
-// assign_dA: dA (=) instead of (+=)
+// assign_dA: dA (=) instead of (+=).  nparts > 1: dD is the fixed-order sum
+// of the partials dDpart[p][B][A][NN2] (agg_bwd), dE written to dD.
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
-                   float* dalpha, float* scratch, hipStream_t s, int assign_dA = 0);
+                   float* dalpha, float* scratch, hipStream_t s, int assign_dA = 0, const float* dDpart = nullptr,
+                   int nparts = 1);
 
 // Batched strided 2-D copies in one launch: dst[r*dst_ld + c] (+)= src[r*src_ld + c].
 struct CopyJob {

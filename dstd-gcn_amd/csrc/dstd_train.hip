@@ -6,7 +6,9 @@
 #include "dstd_train.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <stdio.h>
+#include <stdlib.h>
 
 namespace dstd {
 namespace train {
@@ -218,6 +220,538 @@ __global__ __launch_bounds__(256) void k_gemm_finish(Gemm g, int nsplit, const f
 constexpr int kMaxSplit = 128;
 
 // ---------------------------------------------------------------------------
+// Per-sample aggregation over slabs: the DSTDGC products (model/dstdgcn.py:87
+// spatial, :93 temporal) and their gradients,
+//   fwd  y[c][(a,j)]  (+)= sum_i F[c][(a,i)] D[a][i][j]
+//   bwd  dD[a][i][j]   (=) sum_c F[c][(a,i)] dy[c][(a,j)]
+//        dF[c][(a,i)]  (=) sum_j dy[c][(a,j)] D[a][i][j]
+// where (a,i) is frame-major a*V + i for the spatial op (a = t, i = v) and
+// i*V + a for the temporal one (a = v, i = t).  Workgroup = (sample, chunk
+// of AC consecutive a); the chunk's slab -- every channel's AC x NN values,
+// contiguous runs of AC (temporal) or AC*NN (spatial) floats -- is staged in
+// LDS with coalesced loads.  Each wave owns whole a's: it stages D[n][a]
+// (zero padded, transposed for dF) in its own LDS region and runs the
+// products on fp32 MFMA from LDS; outputs laid out like the slab overwrite
+// the a's slots in place and leave as one coalesced store.  This replaces a
+// one-batch-per-workgroup strided GEMM whose operand gathers (stride V for
+// the temporal products) made it L2-request bound.
+// ---------------------------------------------------------------------------
+struct AggArgs {
+  const float* X;  // fwd: F; bwd: F (rows [0, C) of the packed conv output)
+  long long xs;
+  const float* Y0;  // bwd: dy
+  long long y0s;
+  const float* Dm;  // [B][A][NN][NN]
+  float* O;         // fwd: y; bwd: dF
+  long long os;
+  float* dD;  // bwd: [B][A][NN][NN]
+  float beta;
+  int C, A, NN, V, TV, AC, QP, RK, P;
+  int vec;  // k_aggc: 16-byte loads / stores (T*V, strides and bases 4-aligned)
+  int B;    // k_aggc_bwd: samples (stride of the dD partials)
+};
+constexpr int kAggMaxC = 64, kAggMaxNN = 64;
+
+// x / d for x < 2^16 by a multiply-high: m = ceil(2^32 / d) (m = 2^32, i.e.
+// hi set, for d = 1); exact since x * (m - 2^32 / d) / 2^32 < 1 / d.
+struct FastDiv {
+  uint32_t m, hi;
+  __device__ explicit FastDiv(uint32_t d) {
+    const uint64_t M = 0xFFFFFFFFull / d + 1;
+    m = (uint32_t)M;
+    hi = (uint32_t)(M >> 32);
+  }
+  __device__ int operator()(int x) const { return (int)(__umulhi((uint32_t)x, m) + (hi ? (uint32_t)x : 0u)); }
+};
+
+template <bool TEMP, bool BWD, int MF, int JF, bool DF = true>  // DF: bwd also computes dF
+__global__ __launch_bounds__(256) void k_agg(AggArgs g) {
+  extern __shared__ float agg_sm[];
+  constexpr int U = BWD ? 24 : 32;  // loads in flight per thread in the staging loops
+  const int nth = blockDim.x, nw = nth >> 6, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = g.C, NN = g.NN, V = g.V, AC = g.AC, QP = g.QP, P = g.P;
+  const int chunks = cdiv(g.A, AC);
+  const int n = blockIdx.x / chunks, a0 = (blockIdx.x - n * chunks) * AC;
+  const int ac = min(AC, g.A - a0);
+  float* SX = agg_sm;                                // C x QP
+  float* SY = agg_sm + C * QP;                       // bwd: dy slab
+  float* DL = agg_sm + (BWD ? 2 : 1) * C * QP;       // ac x [RK][P]: D of the chunk's a
+  const float* Xn = g.X + n * g.xs;
+  const float* Yn = BWD ? g.Y0 + n * g.y0s : nullptr;
+  // slab element e (memory order within each channel row) -> its offset in
+  // the sample / its LDS slot
+  const int per = ac * NN, tot = C * per;
+  const FastDiv div_per(per), div_ac(ac), div_nn(NN), div_nn2(NN * NN);
+  auto slot = [&](int e, int& go, int& q) __attribute__((always_inline)) {
+    const int c = div_per(e), r = e - c * per;
+    if (TEMP) {
+      const int i = div_ac(r), al = r - i * ac;
+      go = c * g.TV + i * V + a0 + al;
+      q = c * QP + i * AC + al;
+    } else {
+      go = c * g.TV + a0 * V + r;
+      q = c * QP + r;
+    }
+  };
+  auto lq = [&](int al, int i) __attribute__((always_inline)) { return TEMP ? i * AC + al : al * NN + i; };
+
+  // stage the slab(s) and D[n][a0 .. a0+ac) (contiguous): U loads per thread
+  // in flight, then the LDS writes
+  const int NN2 = NN * NN, dtot = (BWD && !DF) ? 0 : ac * NN2;
+  const float* Dn = g.Dm + ((long long)n * g.A + a0) * NN2;
+  for (int e0 = tid; e0 < tot; e0 += U * nth) {
+    float vx[U], vy[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // (clamped: the last element is re-staged with its own value)
+      int go, q;
+      slot(min(e0 + u * nth, tot - 1), go, q);
+      vx[u] = Xn[go];
+      if (BWD) vy[u] = Yn[go];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // (slots recomputed: U loads in flight, not U addresses)
+      int go, q;
+      slot(min(e0 + u * nth, tot - 1), go, q);
+      SX[q] = vx[u];
+      if (BWD) SY[q] = vy[u];
+    }
+  }
+  for (int e0 = tid; e0 < dtot; e0 += U * nth) {
+    float vd[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) vd[u] = Dn[min(e0 + u * nth, dtot - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // Dl[i][j] (fwd: B operand rows i) or Dl[j][i] (dF: rows j)
+      const int e = min(e0 + u * nth, dtot - 1);
+      const int al = div_nn2(e), r = e - al * NN2, i = div_nn(r), j = r - i * NN;
+      DL[al * g.RK * P + (BWD ? j * P + i : i * P + j)] = vd[u];
+    }
+  }
+  // pad rows NN .. RK-1 of every D tile: zero (the K tail of the products)
+  for (int e = tid; e < ((BWD && !DF) ? 0 : ac * (g.RK - NN) * P); e += nth) {
+    const int al = e / ((g.RK - NN) * P), r = e - al * ((g.RK - NN) * P);
+    DL[al * g.RK * P + NN * P + r] = 0.f;
+  }
+  __syncthreads();
+
+  // Fragment rows / columns beyond C or NN hold garbage that only reaches
+  // output rows / columns that are never stored; the K tail (k >= NN, or
+  // c >= C for dD) is masked on the A side and zero on the B side.
+  const int lr = lane & 15, lk = lane >> 4;
+  for (int al = wave; al < ac; al += nw) {
+    const float* Dl = DL + al * g.RK * P;
+    if (BWD) {  // dD[a] = F^T dy over the channels: rows i, columns j
+      f32x4 acc[JF][JF];
+#pragma unroll
+      for (int x = 0; x < JF; ++x)
+#pragma unroll
+        for (int y = 0; y < JF; ++y) acc[x][y] = zero4();
+      int sl[JF];  // LDS slot of (a, i = x*16 + lr) within a channel row
+#pragma unroll
+      for (int x = 0; x < JF; ++x) sl[x] = lq(al, x * 16 + lr);
+      for (int c = lk; c < C; c += 4) {
+        float av[JF], bv[JF];
+#pragma unroll
+        for (int x = 0; x < JF; ++x) {
+          av[x] = SX[c * QP + sl[x]];
+          bv[x] = SY[c * QP + sl[x]];
+        }
+#pragma unroll
+        for (int x = 0; x < JF; ++x)
+#pragma unroll
+          for (int y = 0; y < JF; ++y) acc[x][y] = mfma16x16x4(av[x], bv[y], acc[x][y]);
+      }
+      if (C & 3) {  // channel tail: lanes past C contribute zero
+        const int c = (C & ~3) + lk;
+        float av[JF], bv[JF];
+#pragma unroll
+        for (int x = 0; x < JF; ++x) {
+          av[x] = c < C ? SX[c * QP + sl[x]] : 0.f;
+          bv[x] = c < C ? SY[c * QP + sl[x]] : 0.f;
+        }
+#pragma unroll
+        for (int x = 0; x < JF; ++x)
+#pragma unroll
+          for (int y = 0; y < JF; ++y) acc[x][y] = mfma16x16x4(av[x], bv[y], acc[x][y]);
+      }
+      float* dDa = g.dD + ((long long)n * g.A + a0 + al) * NN2;
+#pragma unroll
+      for (int x = 0; x < JF; ++x)
+#pragma unroll
+        for (int y = 0; y < JF; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = x * 16 + lk * 4 + r, j = y * 16 + lr;
+            if (i < NN && j < NN) dDa[i * NN + j] = acc[x][y][r];
+          }
+      if (!DF) continue;
+    }
+    // out[c][(a, col)] = sum_k In[c][(a, k)] Dl[k][col]: In = F (fwd) / dy (dF)
+    const float* In = BWD ? SY : SX;
+    f32x4 acc[MF][JF];
+#pragma unroll
+    for (int x = 0; x < MF; ++x)
+#pragma unroll
+      for (int y = 0; y < JF; ++y) acc[x][y] = zero4();
+    auto kstep = [&](int k, bool tail) __attribute__((always_inline)) {
+      const int kq = lq(al, k);
+      float av[MF], bv[JF];
+#pragma unroll
+      for (int x = 0; x < MF; ++x) {
+        av[x] = In[(x * 16 + lr) * QP + kq];
+        if (tail) av[x] = k < NN ? av[x] : 0.f;
+      }
+#pragma unroll
+      for (int y = 0; y < JF; ++y) bv[y] = Dl[k * P + y * 16 + lr];
+#pragma unroll
+      for (int x = 0; x < MF; ++x)
+#pragma unroll
+        for (int y = 0; y < JF; ++y) acc[x][y] = mfma16x16x4(av[x], bv[y], acc[x][y]);
+    };
+    int k = lk;
+    for (; k < (NN & ~3); k += 4) kstep(k, false);
+    if (NN & 3) kstep(k, true);
+    // in place: the a's slots of SX (its F values are no longer needed)
+#pragma unroll
+    for (int x = 0; x < MF; ++x)
+#pragma unroll
+      for (int y = 0; y < JF; ++y) {
+        const int j = y * 16 + lr;
+        if (j < NN) {
+          const int q = lq(al, j);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = x * 16 + lk * 4 + r;
+            if (c < C) SX[c * QP + q] = acc[x][y][r];
+          }
+        }
+      }
+  }
+  if (BWD && !DF) return;
+  __syncthreads();
+  float* On = g.O + n * g.os;
+  const bool acc_out = !BWD && g.beta != 0.f;
+  for (int e0 = tid; e0 < tot; e0 += U * nth) {
+    float old[U];
+    int gos[U], qs[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * nth;
+      if (e < tot) {
+        slot(e, gos[u], qs[u]);
+        old[u] = acc_out ? On[gos[u]] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (e0 + u * nth < tot) On[gos[u]] = acc_out ? fmaf(g.beta, old[u], SX[qs[u]]) : SX[qs[u]];
+  }
+}
+
+// Channel-chunk form of the per-a products without a channel reduction:
+//   fwd  out[c][(a,j)] (+)= sum_i In[c][(a,i)] D[a][i][j]   (In = F)
+//   dF   out[c][(a,i)]  (=) sum_j In[c][(a,j)] D[a][i][j]   (In = dy; TRANS)
+// Workgroup = (sample, 16 channels) over ALL a: the slab is 16 whole channel
+// rows, T*V contiguous floats, staged with 16-byte loads; each wave streams
+// D[n][a] of its a's through its own LDS tile, the next a's D loaded into
+// registers while the current a's MFMAs run.  Outputs overwrite the a's
+// slots in place and leave as one contiguous store.  The LDS row pitch is
+// = 4 mod 64 so the 16 rows x 4 k of an A fragment hit distinct banks for
+// both k strides (1: spatial, V: temporal).
+constexpr int kAggcThreads = 512;
+template <bool TEMP, bool TRANS, int JF>
+__global__ __launch_bounds__(kAggcThreads) void k_aggc(AggArgs g) {
+  extern __shared__ float agg_sm[];
+  constexpr int DR = JF * JF * 4;  // >= ceil(NN^2 / 64): D values per lane
+  constexpr int NW = kAggcThreads / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
+  const int C = g.C, NN = g.NN, V = g.V, TV = g.TV, TVP = g.QP, P = g.P, RK = g.RK;
+  const int cch = cdiv(C, 16);
+  const int n = blockIdx.x / cch, c0 = (blockIdx.x - n * cch) * 16;
+  const int cv = min(16, C - c0);
+  float* S = agg_sm;  // [16][TVP]
+  float* Dl = agg_sm + 16 * TVP + wave * RK * P;
+  const float* In = g.X + n * g.xs + (long long)c0 * TV;
+  float* Out = g.O + n * g.os + (long long)c0 * TV;
+  const int NN2 = NN * NN;
+  const FastDiv div_nn(NN);
+  auto off = [&](int a, int i) __attribute__((always_inline)) { return TEMP ? i * V + a : a * V + i; };
+
+  // first D tile of this wave into registers (its latency overlaps the slab)
+  float dv[DR];
+  auto load_d = [&](int a) __attribute__((always_inline)) {
+    const float* Da = g.Dm + ((long long)n * g.A + a) * NN2;
+#pragma unroll
+    for (int r = 0; r < DR; ++r) dv[r] = Da[min(lane + 64 * r, NN2 - 1)];
+  };
+  if (wave < g.A) load_d(wave);
+  // the 16 channel rows are contiguous in memory
+  if (g.vec) {
+    constexpr int U = 8;
+    const int tv4 = TV >> 2, tot4 = cv * tv4;
+    const FastDiv div_tv4(tv4);
+    const f32x4* In4 = reinterpret_cast<const f32x4*>(In);
+    for (int e0 = tid; e0 < tot4; e0 += U * kAggcThreads) {
+      f32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = In4[min(e0 + u * kAggcThreads, tot4 - 1)];  // (clamped: no branch)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // (a clamped element is rewritten with its own value)
+        const int e = min(e0 + u * kAggcThreads, tot4 - 1);
+        const int c = div_tv4(e), q = e - c * tv4;
+        *reinterpret_cast<f32x4*>(S + c * TVP + 4 * q) = v[u];
+      }
+    }
+  } else {
+    constexpr int U = 16;
+    const int tot = cv * TV;
+    const FastDiv div_tv(TV);
+    for (int e0 = tid; e0 < tot; e0 += U * kAggcThreads) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = In[min(e0 + u * kAggcThreads, tot - 1)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = min(e0 + u * kAggcThreads, tot - 1);
+        const int c = div_tv(e);
+        S[c * TVP + e - c * TV] = v[u];
+      }
+    }
+  }
+  for (int e = lane; e < (RK - NN) * P; e += 64) Dl[NN * P + e] = 0.f;  // K-tail rows
+  __syncthreads();
+
+  for (int a = wave; a < g.A; a += NW) {
+#pragma unroll
+    for (int r = 0; r < DR; ++r) {  // D[a] -> Dl[i][j] (fwd) / Dl[j][i] (dF)
+      const int e = min(lane + 64 * r, NN2 - 1);
+      const int i = div_nn(e), j = e - i * NN;
+      Dl[TRANS ? j * P + i : i * P + j] = dv[r];
+    }
+    if (a + NW < g.A) load_d(a + NW);
+    __builtin_amdgcn_wave_barrier();
+    f32x4 acc[JF];
+#pragma unroll
+    for (int y = 0; y < JF; ++y) acc[y] = zero4();
+    auto kstep = [&](int k, bool tail) __attribute__((always_inline)) {
+      float av = S[lr * TVP + off(a, k)];
+      if (tail) av = k < NN ? av : 0.f;
+      float bv[JF];
+#pragma unroll
+      for (int y = 0; y < JF; ++y) bv[y] = Dl[k * P + y * 16 + lr];
+#pragma unroll
+      for (int y = 0; y < JF; ++y) acc[y] = mfma16x16x4(av, bv[y], acc[y]);
+    };
+    int k = lk;
+    for (; k < (NN & ~3); k += 4) kstep(k, false);
+    if (NN & 3) kstep(k, true);
+#pragma unroll
+    for (int y = 0; y < JF; ++y) {
+      const int j = y * 16 + lr;
+      if (j < NN) {
+        const int q = off(a, j);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[(lk * 4 + r) * TVP + q] = acc[y][r];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  const bool acc_out = g.beta != 0.f;
+  if (g.vec) {
+    const int tv4 = TV >> 2, tot4 = cv * tv4;
+    const FastDiv div_tv4(tv4);
+    f32x4* Out4 = reinterpret_cast<f32x4*>(Out);
+    for (int e = tid; e < tot4; e += kAggcThreads) {
+      const int c = div_tv4(e), q = e - c * tv4;
+      f32x4 v = *reinterpret_cast<const f32x4*>(S + c * TVP + 4 * q);
+      if (acc_out) v += g.beta * Out4[e];
+      Out4[e] = v;
+    }
+  } else {
+    const int tot = cv * TV;
+    const FastDiv div_tv(TV);
+    for (int e = tid; e < tot; e += kAggcThreads) {
+      const int c = div_tv(e);
+      float v = S[c * TVP + e - c * TV];
+      if (acc_out) v = fmaf(g.beta, Out[e], v);
+      Out[e] = v;
+    }
+  }
+}
+
+// Channel-chunk backward of one op's aggregation in one pass over dy:
+//   dF[c][(a,i)] (=) sum_j dy[c][(a,j)] D[a][i][j]
+//   dD_p[a][i][j] (=) sum_{c in chunk p} F[c][(a,i)] dy[c][(a,j)]
+// Workgroup = (sample, 16-channel chunk p) over all a, dy and F slabs of the
+// chunk in LDS (16-byte loads); per a, the wave first forms the chunk's
+// partial dD (K = 16 channels), then dF (D[a]^T through its LDS tile) in
+// place of the a's dy slots.  The cdiv(C, 16) partials are summed in a fixed
+// order by adj_bwd (deterministic).
+constexpr int kAggcbThreads = 256;
+template <bool TEMP, int JF>
+__global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
+  extern __shared__ float agg_sm[];
+  constexpr int DR = JF * JF * 4;  // >= ceil(NN^2 / 64): D values per lane
+  constexpr int NW = kAggcbThreads / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
+  const int C = g.C, NN = g.NN, V = g.V, TV = g.TV, TVP = g.QP, P = g.P, RK = g.RK;
+  const int cch = cdiv(C, 16);
+  const int n = blockIdx.x / cch, p = blockIdx.x - n * cch, c0 = p * 16;
+  const int cv = min(16, C - c0);
+  float* SY = agg_sm;              // [16][TVP] dy, then dF
+  float* SF = agg_sm + 16 * TVP;   // [16][TVP] F
+  float* Dl = agg_sm + 32 * TVP + wave * RK * P;
+  const float* Yn = g.Y0 + n * g.y0s + (long long)c0 * TV;
+  const float* Fn = g.X + n * g.xs + (long long)c0 * TV;
+  float* Out = g.O + n * g.os + (long long)c0 * TV;
+  const int NN2 = NN * NN;
+  const FastDiv div_nn(NN);
+  auto off = [&](int a, int i) __attribute__((always_inline)) { return TEMP ? i * V + a : a * V + i; };
+
+  float dv[DR];
+  auto load_d = [&](int a) __attribute__((always_inline)) {
+    const float* Da = g.Dm + ((long long)n * g.A + a) * NN2;
+#pragma unroll
+    for (int r = 0; r < DR; ++r) dv[r] = Da[min(lane + 64 * r, NN2 - 1)];
+  };
+  if (wave < g.A) load_d(wave);
+  if (g.vec) {
+    constexpr int U = 8;
+    const int tv4 = TV >> 2, tot4 = cv * tv4;
+    const FastDiv div_tv4(tv4);
+    const f32x4* Y4 = reinterpret_cast<const f32x4*>(Yn);
+    const f32x4* F4 = reinterpret_cast<const f32x4*>(Fn);
+    for (int e0 = tid; e0 < tot4; e0 += U * kAggcbThreads) {
+      f32x4 vy[U], vf[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = min(e0 + u * kAggcbThreads, tot4 - 1);
+        vy[u] = Y4[e];
+        vf[u] = F4[e];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {  // (a clamped element is rewritten with its own value)
+        const int e = min(e0 + u * kAggcbThreads, tot4 - 1);
+        const int c = div_tv4(e), q = c * TVP + 4 * (e - c * tv4);
+        *reinterpret_cast<f32x4*>(SY + q) = vy[u];
+        *reinterpret_cast<f32x4*>(SF + q) = vf[u];
+      }
+    }
+  } else {
+    constexpr int U = 8;
+    const int tot = cv * TV;
+    const FastDiv div_tv(TV);
+    for (int e0 = tid; e0 < tot; e0 += U * kAggcbThreads) {
+      float vy[U], vf[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = min(e0 + u * kAggcbThreads, tot - 1);
+        vy[u] = Yn[e];
+        vf[u] = Fn[e];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = min(e0 + u * kAggcbThreads, tot - 1);
+        const int c = div_tv(e), q = c * TVP + e - c * TV;
+        SY[q] = vy[u];
+        SF[q] = vf[u];
+      }
+    }
+  }
+  for (int e = lane; e < (RK - NN) * P; e += 64) Dl[NN * P + e] = 0.f;  // K-tail rows
+  __syncthreads();
+
+  float* dDp = g.dD + (long long)p * g.B * g.A * NN2;
+  for (int a = wave; a < g.A; a += NW) {
+    {  // partial dD[a] over the chunk's channels: rows i, columns j, K = c
+      f32x4 acc[JF][JF];
+#pragma unroll
+      for (int x = 0; x < JF; ++x)
+#pragma unroll
+        for (int y = 0; y < JF; ++y) acc[x][y] = zero4();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int c = ks * 4 + lk;
+        float av[JF], bv[JF];
+#pragma unroll
+        for (int x = 0; x < JF; ++x) {
+          const int q = c * TVP + off(a, x * 16 + lr);
+          av[x] = c < cv ? SF[q] : 0.f;
+          bv[x] = c < cv ? SY[q] : 0.f;
+        }
+#pragma unroll
+        for (int x = 0; x < JF; ++x)
+#pragma unroll
+          for (int y = 0; y < JF; ++y) acc[x][y] = mfma16x16x4(av[x], bv[y], acc[x][y]);
+      }
+      float* dDa = dDp + ((long long)n * g.A + a) * NN2;
+#pragma unroll
+      for (int x = 0; x < JF; ++x)
+#pragma unroll
+        for (int y = 0; y < JF; ++y) {
+          const int j = y * 16 + lr;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = x * 16 + lk * 4 + r;
+            if (i < NN && j < NN) dDa[i * NN + j] = acc[x][y][r];
+          }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < DR; ++r) {  // D[a]^T -> Dl[j][i]
+      const int e = min(lane + 64 * r, NN2 - 1);
+      const int i = div_nn(e), j = e - i * NN;
+      Dl[j * P + i] = dv[r];
+    }
+    if (a + NW < g.A) load_d(a + NW);
+    __builtin_amdgcn_wave_barrier();
+    f32x4 acc[JF];
+#pragma unroll
+    for (int y = 0; y < JF; ++y) acc[y] = zero4();
+    auto kstep = [&](int k, bool tail) __attribute__((always_inline)) {
+      float av = SY[lr * TVP + off(a, k)];
+      if (tail) av = k < NN ? av : 0.f;
+      float bv[JF];
+#pragma unroll
+      for (int y = 0; y < JF; ++y) bv[y] = Dl[k * P + y * 16 + lr];
+#pragma unroll
+      for (int y = 0; y < JF; ++y) acc[y] = mfma16x16x4(av, bv[y], acc[y]);
+    };
+    int k = lk;
+    for (; k < (NN & ~3); k += 4) kstep(k, false);
+    if (NN & 3) kstep(k, true);
+#pragma unroll
+    for (int y = 0; y < JF; ++y) {
+      const int i = y * 16 + lr;
+      if (i < NN) {
+        const int q = off(a, i);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) SY[(lk * 4 + r) * TVP + q] = acc[y][r];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  if (g.vec) {
+    const int tv4 = TV >> 2, tot4 = cv * tv4;
+    const FastDiv div_tv4(tv4);
+    f32x4* Out4 = reinterpret_cast<f32x4*>(Out);
+    for (int e = tid; e < tot4; e += kAggcbThreads) {
+      const int c = div_tv4(e);
+      Out4[e] = *reinterpret_cast<const f32x4*>(SY + c * TVP + 4 * (e - c * tv4));
+    }
+  } else {
+    const int tot = cv * TV;
+    const FastDiv div_tv(TV);
+    for (int e = tid; e < tot; e += kAggcbThreads) {
+      const int c = div_tv(e);
+      Out[e] = SY[c * TVP + e - c * TV];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // tanh outer difference
 // ---------------------------------------------------------------------------
 constexpr int kTanhMaxNN = 128;  // the frame envelope (T <= 128; V <= 64)
@@ -278,7 +812,8 @@ __global__ void k_tanh_outer_bwd(const float* __restrict__ M, const float* __res
 __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, const float* __restrict__ E,
                                                       const float* __restrict__ alpha, int B, int A, int NN2, int nch,
                                                       float* __restrict__ pdA, float* __restrict__ pbr,
-                                                      float* __restrict__ pal) {
+                                                      float* __restrict__ pal, const float* __restrict__ dDp,
+                                                      int np) {
   __shared__ float red[4];
   const int a = blockIdx.x, ch = blockIdx.y;
   const int per = (B + nch - 1) / nch, n0 = ch * per, n1 = min(B, n0 + per);
@@ -291,7 +826,14 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const size_t i = ((size_t)(nb + u) * A + a) * NN2 + ij;
-        dv[u] = nb + u < n1 ? dD[i] : 0.f;
+        if (np > 1) {  // channel-chunk partials, summed in chunk order
+          const size_t ps = (size_t)B * A * NN2;
+          float t = 0.f;
+          for (int q = 0; q < np; ++q) t += nb + u < n1 ? dDp[q * ps + i] : 0.f;
+          dv[u] = t;
+        } else {
+          dv[u] = nb + u < n1 ? dD[i] : 0.f;
+        }
         ev[u] = nb + u < n1 ? E[i] : 0.f;
       }
 #pragma unroll
@@ -974,6 +1516,189 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   return hipGetLastError();
 }
 
+namespace {
+// a-chunk per workgroup: the widest chunk (<= 4, one a per wave) whose slabs
+// and D tiles fit 80 KB of LDS (two workgroups per CU)
+constexpr size_t kAggLds = 80 * 1024;
+void agg_tile(int NN, int& RK, int& P) {
+  RK = rup(NN, 4);
+  const int jf = cdiv(NN, 16);
+  P = 16 * ((jf & 1) ? jf : jf + 1);  // 4 B-operand rows of 16 hit distinct banks
+}
+size_t agg_lds(bool bwd, bool df, int C, int NN, int ac, int& QP, int& RK, int& P) {
+  QP = (ac * NN) | 1;
+  agg_tile(NN, RK, P);
+  return sizeof(float) * ((size_t)(bwd ? 2 : 1) * C * QP + (df ? (size_t)ac * RK * P : 0));
+}
+int env_int(const char* name) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : 0;
+}
+int agg_env_ac() {
+  static const int v = env_int("DSTD_AGG_AC");
+  return v;
+}
+// DSTD_AGG_FORM (A/B of the aggregation kernels): 2 (default) fwd and dF on
+// the channel-chunk kernels, dD as per-chunk partials of the fused backward;
+// 1 every product on the a-chunk kernel; 0 channel-chunk fwd / dF, dD left to
+// the caller's strided GEMM; 3 channel-chunk fwd / dF, a-chunk dD
+int agg_form() {
+  static const int v = [] {
+    const char* e = getenv("DSTD_AGG_FORM");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+template <class K>
+void agg_go(K kern, dim3 grid, dim3 block, size_t lds, const AggArgs& g, hipStream_t s) {
+  static bool attr = false;  // (per instantiation) allow > 64 KB of dynamic LDS
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  kern<<<grid, block, lds, s>>>(g);
+}
+bool agg_ok(const AggArgs& g) {
+  return g.C > 0 && g.C <= kAggMaxC && g.NN > 0 && g.NN <= kAggMaxNN && g.A > 0;
+}
+// a-chunk kernel: fwd, bwd dD + dF (df) or bwd dD only
+hipError_t agg_launch_a(bool bwd, bool df, AggArgs g, int B, int temporal, hipStream_t s) {
+  if (!agg_ok(g)) return hipErrorNotSupported;
+  int ac = std::min(g.A, 4);
+  if (agg_env_ac() > 0) ac = std::min(std::min(g.A, agg_env_ac()), 8);  // (FastDiv: slab sizes < 2^16)
+  size_t lds = agg_lds(bwd, df, g.C, g.NN, ac, g.QP, g.RK, g.P);
+  while (ac > 1 && lds > kAggLds) lds = agg_lds(bwd, df, g.C, g.NN, --ac, g.QP, g.RK, g.P);
+  if (lds > 160 * 1024) return hipErrorNotSupported;
+  g.AC = ac;
+  const dim3 grid(B * cdiv(g.A, ac)), block(64 * std::min(ac, 4));
+  // channel fragments 1, 2, 4 (3 runs as 4); column fragments 1-4
+  const int mf = cdiv(g.C, 16) == 3 ? 4 : cdiv(g.C, 16), jf = cdiv(g.NN, 16);
+  auto pick_jf = [&](auto tb, auto bb, auto mfc, auto dfc) {
+    constexpr bool T_ = decltype(tb)::value, B_ = decltype(bb)::value, D_ = decltype(dfc)::value;
+    constexpr int M_ = decltype(mfc)::value;
+    switch (jf) {
+      case 1: agg_go(k_agg<T_, B_, M_, 1, D_>, grid, block, lds, g, s); break;
+      case 2: agg_go(k_agg<T_, B_, M_, 2, D_>, grid, block, lds, g, s); break;
+      case 3: agg_go(k_agg<T_, B_, M_, 3, D_>, grid, block, lds, g, s); break;
+      default: agg_go(k_agg<T_, B_, M_, 4, D_>, grid, block, lds, g, s); break;
+    }
+  };
+  using T1 = std::true_type;
+  using F0 = std::false_type;
+  auto pick_mf = [&](auto tb, auto bb, auto dfc) {
+    if (mf == 1) pick_jf(tb, bb, std::integral_constant<int, 1>(), dfc);
+    else if (mf == 2) pick_jf(tb, bb, std::integral_constant<int, 2>(), dfc);
+    else pick_jf(tb, bb, std::integral_constant<int, 4>(), dfc);
+  };
+  if (!bwd) temporal ? pick_mf(T1(), F0(), T1()) : pick_mf(F0(), F0(), T1());
+  else if (df) temporal ? pick_mf(T1(), T1(), T1()) : pick_mf(F0(), T1(), T1());
+  else temporal ? pick_mf(T1(), T1(), F0()) : pick_mf(F0(), T1(), F0());
+  return hipGetLastError();
+}
+// channel-chunk kernel: fwd (trans 0) or dF (trans 1)
+hipError_t agg_launch_c(bool trans, AggArgs g, int B, int temporal, hipStream_t s) {
+  if (!agg_ok(g)) return hipErrorNotSupported;
+  agg_tile(g.NN, g.RK, g.P);
+  g.QP = g.TV;
+  while ((g.QP & 63) != 4) ++g.QP;
+  const size_t lds = sizeof(float) * ((size_t)16 * g.QP + (size_t)(kAggcThreads / 64) * g.RK * g.P);
+  if (lds > 160 * 1024) return hipErrorNotSupported;
+  g.vec = (g.TV % 4 == 0 && g.xs % 4 == 0 && g.os % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
+           ((uintptr_t)g.O & 15) == 0);
+  const dim3 grid(B * cdiv(g.C, 16)), block(kAggcThreads);
+  const int jf = cdiv(g.NN, 16);
+  auto pick = [&](auto tb, auto rb) {
+    constexpr bool T_ = decltype(tb)::value, R_ = decltype(rb)::value;
+    switch (jf) {
+      case 1: agg_go(k_aggc<T_, R_, 1>, grid, block, lds, g, s); break;
+      case 2: agg_go(k_aggc<T_, R_, 2>, grid, block, lds, g, s); break;
+      case 3: agg_go(k_aggc<T_, R_, 3>, grid, block, lds, g, s); break;
+      default: agg_go(k_aggc<T_, R_, 4>, grid, block, lds, g, s); break;
+    }
+  };
+  using T1 = std::true_type;
+  using F0 = std::false_type;
+  if (temporal) trans ? pick(T1(), T1()) : pick(T1(), F0());
+  else trans ? pick(F0(), T1()) : pick(F0(), F0());
+  return hipGetLastError();
+}
+AggArgs agg_geom(int C, int T, int V, int temporal) {
+  AggArgs g{};
+  g.C = C;
+  g.A = temporal ? V : T;
+  g.NN = temporal ? T : V;
+  g.V = V;
+  g.TV = T * V;
+  return g;
+}
+}  // namespace
+
+hipError_t agg_fwd(const float* F, long long fs, const float* D, float* y, long long ys, float beta, int B, int C,
+                   int T, int V, int temporal, hipStream_t s) {
+  AggArgs g = agg_geom(C, T, V, temporal);
+  g.X = F, g.xs = fs, g.Dm = D, g.O = y, g.os = ys, g.beta = beta;
+  return agg_form() == 1 ? agg_launch_a(false, true, g, B, temporal, s) : agg_launch_c(false, g, B, temporal, s);
+}
+
+hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys, const float* D, float* dF,
+                   long long dfs, float* dD, int B, int C, int T, int V, int temporal, hipStream_t s, float* dDpart,
+                   int* nparts) {
+  AggArgs g = agg_geom(C, T, V, temporal);
+  g.X = F, g.xs = fs, g.Y0 = dy, g.y0s = dys, g.Dm = D, g.O = dF, g.os = dfs, g.dD = dD;
+  *nparts = 0;
+  if (!agg_ok(g)) return hipErrorNotSupported;
+  const int form = agg_form(), cch = cdiv(C, 16);
+  *nparts = 1;
+  if (form == 1) {
+    const hipError_t e = agg_launch_a(true, true, g, B, temporal, s);
+    if (e == hipErrorNotSupported) *nparts = 0;
+    return e;
+  }
+  if (form == 2 && (cch == 1 || dDpart)) {
+    if (cch > 1) g.dD = dDpart, *nparts = cch;
+    g.B = B;
+    agg_tile(g.NN, g.RK, g.P);
+    g.QP = g.TV;
+    while ((g.QP & 63) != 4) ++g.QP;
+    const size_t lds = sizeof(float) * ((size_t)32 * g.QP + (size_t)(kAggcbThreads / 64) * g.RK * g.P);
+    if (lds <= 160 * 1024) {
+      g.vec = (g.TV % 4 == 0 && g.xs % 4 == 0 && g.os % 4 == 0 && g.y0s % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
+               ((uintptr_t)g.O & 15) == 0 && ((uintptr_t)g.Y0 & 15) == 0);
+      const dim3 grid(B * cch), block(kAggcbThreads);
+      const int jf = cdiv(g.NN, 16);
+      auto pick = [&](auto tb) {
+        constexpr bool T_ = decltype(tb)::value;
+        switch (jf) {
+          case 1: agg_go(k_aggc_bwd<T_, 1>, grid, block, lds, g, s); break;
+          case 2: agg_go(k_aggc_bwd<T_, 2>, grid, block, lds, g, s); break;
+          case 3: agg_go(k_aggc_bwd<T_, 3>, grid, block, lds, g, s); break;
+          default: agg_go(k_aggc_bwd<T_, 4>, grid, block, lds, g, s); break;
+        }
+      };
+      temporal ? pick(std::true_type()) : pick(std::false_type());
+      return hipGetLastError();
+    }
+    *nparts = 1;
+    g.dD = dD;
+  }
+  AggArgs c = agg_geom(C, T, V, temporal);  // dF = dy . D^T per a
+  c.X = dy, c.xs = dys, c.Dm = D, c.O = dF, c.os = dfs;
+  const hipError_t e = agg_launch_c(true, c, B, temporal, s);
+  if (e != hipSuccess) {
+    *nparts = 0;  // (NotSupported: the caller runs both products)
+    return e;
+  }
+  if (form == 0) {
+    *nparts = 0;  // dD: the caller's
+    return hipSuccess;
+  }
+  const hipError_t ed = agg_launch_a(true, false, g, B, temporal, s);  // dD
+  if (ed == hipErrorNotSupported) *nparts = 0;  // (dF is done; the caller recomputes both)
+  return ed;
+}
+
+
+
 hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int R, int A, int NN, float* M,
                           hipStream_t s) {
   if (NN > kTanhMaxNN) return hipErrorInvalidValue;
@@ -999,12 +1724,13 @@ size_t adj_bwd_scratch_floats(int B, int A, int NN2) {
 }
 
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
-                   float* dalpha, float* scratch, hipStream_t s, int assign_dA) {
+                   float* dalpha, float* scratch, hipStream_t s, int assign_dA, const float* dDpart, int nparts) {
+  if (nparts > 1 && !dDpart) return hipErrorInvalidValue;
   const int nch = adj_bwd_chunks(B, A);
   float* pdA = scratch;
   float* pbr = pdA + (size_t)nch * A * NN2;
   float* pal = pbr + (size_t)nch * A;
-  k_adj_bwd_part<<<dim3(A, nch), 256, 0, s>>>(dD, E, alpha, B, A, NN2, nch, pdA, pbr, pal);
+  k_adj_bwd_part<<<dim3(A, nch), 256, 0, s>>>(dD, E, alpha, B, A, NN2, nch, pdA, pbr, pal, dDpart, nparts);
   k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(pdA, pbr, pal, A, NN2, nch, dA, dbrm, dalpha, assign_dA);
   return hipGetLastError();
 }

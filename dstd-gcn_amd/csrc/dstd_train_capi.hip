@@ -9,6 +9,7 @@
 // An NCTV activation X[n][c][t][v] is addressed as n*C*TV + c*TV + a*ps_a +
 // i*ps_i with (ps_a, ps_i) = (V, 1) spatial and (1, V) temporal, so every
 // step below is one strided GEMM or element-wise kernel for either mode.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -88,11 +89,21 @@ bool model_ok(const dstd_model_params* p) {
 // ---------------------------------------------------------------------------
 // one DSTDGC
 // ---------------------------------------------------------------------------
+// The aggregation products run on the slab kernels (agg_fwd / agg_bwd);
+// DSTD_TRAIN_AGG_GEMM=1 routes them through the strided GEMMs instead (A/B).
+bool use_agg() {
+  static const bool v = [] {
+    const char* e = getenv("DSTD_TRAIN_AGG_GEMM");
+    return !(e && atoi(e) != 0);
+  }();
+  return v;
+}
 struct OpGeom {
   int B, cin, cout, T, V, TV;
   int R;  // red_channels: P / Q channels per op (2 in every block of the reference)
   int A, NN, NN2;
   long long ps_a, ps_i;
+  int temporal;
   OpGeom(int mode, int B_, int cin_, int cout_, int T_, int V_, int R_ = 2)
       : B(B_), cin(cin_), cout(cout_), T(T_), V(V_), TV(T_ * V_), R(R_) {
     const bool sp = mode == DSTD_MODE_SPATIAL;
@@ -101,6 +112,7 @@ struct OpGeom {
     NN2 = NN * NN;
     ps_a = sp ? V : 1;
     ps_i = sp ? 1 : V;
+    temporal = !sp;
   }
   int CG() const { return cout + 2 * R; }  // rows of the packed conv output G = [F; P; Q]
   // P (Q) rows of G: element (n, r, a, i) at n*CG*TV + r*TV + a*ps_a + i*ps_i
@@ -133,6 +145,7 @@ bool pack_jobs(CopyJobs& js, const dstd_gc_weights* w, const OpSaved& sv, const 
 
 struct OpWs {
   float *dG, *dD, *dM, *gW, *gs, *part, *red;
+  float* dDp;  // channel-chunk partials of dD (agg_bwd), null when one chunk suffices
 };
 // Reduction / BatchNorm / adjacency-backward scratch for a geometry.
 size_t red_floats(const OpGeom& g) {
@@ -143,10 +156,11 @@ size_t red_floats(const OpGeom& g) {
 // Sized for the largest of the given op geometries (one workspace serves every
 // op of a block / model in turn).
 void carve_op_ws(Carver& cv, OpWs& w, const std::vector<OpGeom>& gl) {
-  size_t nG = 0, nD = 0, nM = 0, nW = 0, nmn = 0, nred = 0;
+  size_t nG = 0, nD = 0, nM = 0, nW = 0, nmn = 0, nred = 0, nDp = 0;
   for (const OpGeom& g : gl) {
     nG = std::max(nG, (size_t)g.B * g.CG() * g.TV);
     nD = std::max(nD, (size_t)g.B * g.A * g.NN2);
+    if (agg_parts(g.cout) > 1) nDp = std::max(nDp, (size_t)agg_parts(g.cout) * g.B * g.A * g.NN2);
     nM = std::max(nM, (size_t)g.B * g.R * g.A * g.NN2);
     nW = std::max(nW, (size_t)g.CG() * (g.cin + 1));
     nmn = std::max(nmn, (size_t)std::max(std::max(g.CG() * (g.cin + 1), g.R * g.A * g.A), g.cout * g.cin));
@@ -159,6 +173,7 @@ void carve_op_ws(Carver& cv, OpWs& w, const std::vector<OpGeom>& gl) {
   w.gs = cv.take(gemm_scratch_floats((int)nmn, 1));
   w.part = cv.take(std::max(dot_partials(), mpjpe_partials()));
   w.red = cv.take(nred);
+  w.dDp = nDp ? cv.take(nDp) : nullptr;
 }
 
 // 1x1 conv as GEMMs over NCTV (W [cout][cin]).
@@ -222,6 +237,11 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   e.d_W = W0;
   e.d_R = R0;
   DSTD_TRYH(gemm(e, nullptr, s));
+  if (use_agg()) {  // y[c][(a,j)] = sum_i F[c][(a,i)] D[a][i][j]     :87 / :93
+    const hipError_t e = agg_fwd(sv.G, (long long)g.CG() * g.TV, sv.D, y, (long long)g.cout * g.TV, beta_y, g.B,
+                                 g.cout, g.T, g.V, g.temporal, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   Gemm a;  // y[c][j] = sum_i F[c][i] D[i][j] per (n, a)               :87 / :93
   a.M = g.cout, a.N = g.NN, a.K = g.NN, a.nb1 = g.B, a.nb2 = g.A;
   a.A = sv.G, a.a_b1 = (long long)g.CG() * g.TV, a.a_b2 = g.ps_a, a.a_m = g.TV, a.a_k = g.ps_i;
@@ -237,20 +257,32 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
                   const float* dy, float* dx, const dstd_gc_grads* gr, float* dA, float* dalpha, const OpWs& ws,
                   hipStream_t s, float dx_beta = 1.f, int assign_dA = 0) {
   const long long ldG = (long long)g.CG() * g.TV;
-  Gemm f;  // dF[c][i] = sum_j dy[c][j] D[i][j]  -> rows [0, cout) of dG
-  f.M = g.cout, f.N = g.NN, f.K = g.NN, f.nb1 = g.B, f.nb2 = g.A;
-  f.A = dy, f.a_b1 = (long long)g.cout * g.TV, f.a_b2 = g.ps_a, f.a_m = g.TV, f.a_k = g.ps_i;
-  f.B = sv.D, f.b_b1 = (long long)g.A * g.NN2, f.b_b2 = g.NN2, f.b_k = 1, f.b_n = g.NN;
-  f.C = ws.dG, f.c_b1 = ldG, f.c_b2 = g.ps_a, f.c_m = g.TV, f.c_n = g.ps_i;
-  DSTD_TRYH(gemm(f, nullptr, s));
-  Gemm d;  // dD[i][j] = sum_c F[c][i] dy[c][j]
-  d.M = g.NN, d.N = g.NN, d.K = g.cout, d.nb1 = g.B, d.nb2 = g.A;
-  d.A = sv.G, d.a_b1 = ldG, d.a_b2 = g.ps_a, d.a_m = g.ps_i, d.a_k = g.TV;
-  d.B = dy, d.b_b1 = (long long)g.cout * g.TV, d.b_b2 = g.ps_a, d.b_k = g.TV, d.b_n = g.ps_i;
-  d.C = ws.dD, d.c_b1 = (long long)g.A * g.NN2, d.c_b2 = g.NN2, d.c_m = g.NN, d.c_n = 1;
-  DSTD_TRYH(gemm(d, nullptr, s));
+  // dF -> rows [0, cout) of dG; dD in place or as channel-chunk partials
+  hipError_t ae = hipErrorNotSupported;
+  int nparts = 0;
+  if (use_agg())
+    ae = agg_bwd(sv.G, ldG, dy, (long long)g.cout * g.TV, sv.D, ws.dG, ldG, ws.dD, g.B, g.cout, g.T, g.V,
+                 g.temporal, s, ws.dDp, &nparts);
+  if (ae != hipErrorNotSupported) DSTD_TRYH(ae);
+  if (ae == hipErrorNotSupported) {
+    Gemm f;  // dF[c][i] = sum_j dy[c][j] D[i][j]  -> rows [0, cout) of dG
+    f.M = g.cout, f.N = g.NN, f.K = g.NN, f.nb1 = g.B, f.nb2 = g.A;
+    f.A = dy, f.a_b1 = (long long)g.cout * g.TV, f.a_b2 = g.ps_a, f.a_m = g.TV, f.a_k = g.ps_i;
+    f.B = sv.D, f.b_b1 = (long long)g.A * g.NN2, f.b_b2 = g.NN2, f.b_k = 1, f.b_n = g.NN;
+    f.C = ws.dG, f.c_b1 = ldG, f.c_b2 = g.ps_a, f.c_m = g.TV, f.c_n = g.ps_i;
+    DSTD_TRYH(gemm(f, nullptr, s));
+  }
+  if (nparts == 0) {
+    Gemm d;  // dD[i][j] = sum_c F[c][i] dy[c][j]
+    d.M = g.NN, d.N = g.NN, d.K = g.cout, d.nb1 = g.B, d.nb2 = g.A;
+    d.A = sv.G, d.a_b1 = ldG, d.a_b2 = g.ps_a, d.a_m = g.ps_i, d.a_k = g.TV;
+    d.B = dy, d.b_b1 = (long long)g.cout * g.TV, d.b_b2 = g.ps_a, d.b_k = g.TV, d.b_n = g.ps_i;
+    d.C = ws.dD, d.c_b1 = (long long)g.A * g.NN2, d.c_b2 = g.NN2, d.c_m = g.NN, d.c_n = 1;
+    DSTD_TRYH(gemm(d, nullptr, s));
+    nparts = 1;
+  }
   // Adj = alpha * (conv_rm(M)) + A:  dalpha, dA, d b_rm, and dE = alpha dD in place
-  DSTD_TRYH(adj_bwd(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, dA, gr->brm, dalpha, ws.red, s, assign_dA));
+  DSTD_TRYH(adj_bwd(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, dA, gr->brm, dalpha, ws.red, s, assign_dA, ws.dDp, nparts));
   const float* dE = ws.dD;
   Gemm wr;  // dWrm[a][k] = sum_{n,ij} dE[n][a][ij] M[n][k][ij]
   wr.M = g.A, wr.N = g.R * g.A, wr.K = g.NN2, wr.nb1 = g.B, wr.reduce = 1;
