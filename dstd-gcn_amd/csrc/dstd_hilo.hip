@@ -1230,7 +1230,7 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
 //   out[row][q][slot] = alpha * (sum_k W[row][k] tanh(P[k][p] - Q[k][q]) + b[row]) + Astat[p][q]
 // with p = slot_idx(slot).  MODE 0 (spatial): row = t, (p, q) = joints,
 // k = r*T + t'.  MODE 1 (temporal): row = v, (p, q) = frames, k = r*V + v'.
-// tanh separably, as in dstd_fast.hip: E = 2^(c P), F = 2^(-c Q) once per
+// tanh separably, as in dstd_adj.hip: E = 2^(c P), F = 2^(-c Q) once per
 // workgroup in LDS ([p][k] rows, k contiguous so a lane's 8 k of a K-step are
 // two 16-byte reads), tanh = 1 - 2 / (E F + 1); a sample with |cP| or |cQ|
 // above 120 takes the direct tanh(P - Q) path.  The B fragments (tanh
@@ -2225,7 +2225,7 @@ hipError_t launch_hl_prep(const HLPrepArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// the shapes whose adjacency kernels (dstd_fast.hip) have a split-f16 writer
+// the shapes whose adjacency kernels (dstd_adj.hip) have a split-f16 writer
 static bool hl_shape(int T, int V) {
   return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23) || (T == 75 && V == 22);
 }

@@ -156,12 +156,11 @@ hipError_t launch_spatial(SpatialArgs a, hipStream_t s);
 hipError_t launch_temporal(TemporalArgs a, hipStream_t s);
 hipError_t launch_transpose(const TransposeArgs& a, hipStream_t s);
 
-// shape-specialised variants (dstd_fast.hip); hipErrorNotSupported when the
+// shape-specialised adjacency (dstd_adj.hip); hipErrorNotSupported when the
 // shape has no instantiation and the generic kernel must run
 hipError_t launch_adj_fast(const AdjArgs& a, hipStream_t s, int nblocks);
-hipError_t launch_spatial_fast(const SpatialArgs& a, hipStream_t s);
-hipError_t launch_temporal_fast(const TemporalArgs& a, hipStream_t s);
-// wave-independent 64 -> 64 kernels (dstd_wave.hip), tried first
+// exact-fp32 block kernels for the model's channel configurations
+// (dstd_wave.hip), tried first; the generic kernels take every other shape
 hipError_t launch_spatial_wave(const SpatialArgs& a, hipStream_t s);
 hipError_t launch_temporal_wave(const TemporalArgs& a, hipStream_t s);
 

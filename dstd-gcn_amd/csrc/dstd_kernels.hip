@@ -599,8 +599,6 @@ hipError_t launch_spatial(SpatialArgs a, hipStream_t s) {
   if (a.Tt <= 0) {
     const hipError_t we = launch_spatial_wave(a, s);
     if (we != hipErrorNotSupported) return we;
-    const hipError_t fe = launch_spatial_fast(a, s);
-    if (fe != hipErrorNotSupported) return fe;
   }
   if (a.Tt <= 0) a.Tt = spatial_frames_per_wg(a.T, a.V, a.Cin, a.Cout, a.G);
   int NP16, SX, Cp, SP, lf;
@@ -620,8 +618,6 @@ hipError_t launch_temporal(TemporalArgs a, hipStream_t s) {
   if (a.Vt <= 0) {
     const hipError_t we = launch_temporal_wave(a, s);
     if (we != hipErrorNotSupported) return we;
-    const hipError_t fe = launch_temporal_fast(a, s);
-    if (fe != hipErrorNotSupported) return fe;
   }
   if (a.Vt <= 0) a.Vt = temporal_joints_per_wg(a.T, a.V, a.Cin, a.Cout);
   int NP16, SX, Cp, SP, lf;

@@ -1,7 +1,7 @@
 // Training-path primitives: a strided batched fp32-MFMA
 // GEMM plus the element-wise / reduction kernels that the DSTDGC, BatchNorm
 // and PReLU backward passes are composed of.  The fused inference kernels
-// (dstd_wave.hip, dstd_fast.hip) keep nothing for a backward pass; training
+// (dstd_wave.hip, dstd_hilo.hip) keep nothing for a backward pass; training
 // instead materialises F, P, Q, M, E and D per op (a few MB per op at the
 // config-5 batch of 32) and runs the backward as GEMMs over those saved
 // tensors.  All launchers enqueue on the given stream and return the launch

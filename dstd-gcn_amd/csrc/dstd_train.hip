@@ -178,6 +178,28 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
   }
   const int b1 = g.reduce ? 0 : blockIdx.z / g.nb2, b2 = g.reduce ? 0 : blockIdx.z - b1 * g.nb2;
   float* Cb = g.C + b1 * g.c_b1 + b2 * g.c_b2;
+  if (!g.d_out && !g.nseg) {  // plain store: one uniform branch, not one per element
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+        if (gm >= g.M) continue;
+        float* row = Cb + gm * g.c_m;
+        const float bm = g.bias_m ? g.bias_m[gm] : 0.f;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int gn = n0 + wn + j * 16 + (lane & 15);
+          if (gn < g.N) {
+            float* c = row + gn * g.c_n;
+            float v = fmaf(g.alpha, acc[i][j][r], bm);
+            if (g.beta != 0.f) v = fmaf(g.beta, *c, v);
+            *c = v;
+          }
+        }
+      }
+    return;
+  }
   float* Db = g.d_out ? g.d_out + b1 * g.c_b1 + b2 * g.c_b2 : nullptr;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -219,6 +241,179 @@ __global__ __launch_bounds__(256) void k_gemm_finish(Gemm g, int nsplit, const f
 
 constexpr int kMaxSplit = 128;
 
+// x / d for x < 2^16 by a multiply-high: m = ceil(2^32 / d) (m = 2^32, i.e.
+// hi set, for d = 1); exact since x * (m - 2^32 / d) / 2^32 < 1 / d.
+struct FastDiv {
+  uint32_t m, hi;
+  __device__ explicit FastDiv(uint32_t d) {
+    const uint64_t M = 0xFFFFFFFFull / d + 1;
+    m = (uint32_t)M;
+    hi = (uint32_t)(M >> 32);
+  }
+  __device__ int operator()(int x) const { return (int)(__umulhi((uint32_t)x, m) + (hi ? (uint32_t)x : 0u)); }
+};
+
+// ---------------------------------------------------------------------------
+// Skinny GEMM of the training step's 1x1 convolutions: a small weight matrix
+// (M, K <= 80) times a wide panel of contiguous rows.  gemm() routes the
+// matching shapes here; the whole K extent of both operands sits in LDS.
+// ---------------------------------------------------------------------------
+constexpr int kSkMax = 80;     // M, K <= 5 fragments of 16
+constexpr int kSkPT = 128;     // panel columns per workgroup
+__host__ __device__ constexpr int sk_pitch(int n, int want) {  // >= n, = want mod 64
+  int s = n;
+  while ((s & 63) != want) ++s;
+  return s;
+}
+
+// C[b][m][p] = alpha * sum_k A[m][k] B[b][k][p] (+ bias, beta, d_out, nseg:
+// gemm_store), B and C rows contiguous (b_n = c_n = 1).  Workgroup = (batch,
+// 128 columns): A (any strides) and the B panel in LDS, zero-padded to whole
+// fragments; 4 waves x 32 columns x MF row fragments.
+template <int MF>
+__global__ __launch_bounds__(256) void k_skinny_panel(Gemm g, int KP, int BP, int vec) {
+  extern __shared__ float sk_sm[];
+  float* As = sk_sm;                   // [MF*16][KP]
+  float* Bs = sk_sm + MF * 16 * KP;    // [K4][BP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
+  const int ntile = cdiv(g.N, kSkPT);
+  const int b = blockIdx.x / ntile, p0 = (blockIdx.x - b * ntile) * kSkPT;
+  const int b1 = b / g.nb2, b2 = b - b1 * g.nb2;
+  const int K = g.K, K4 = rup(K, 4);
+  const float* Bb = g.B + b1 * g.b_b1 + b2 * g.b_b2;
+  // every load of the staging in flight at once (clamped indices, no
+  // branches): A (zero rows >= M, columns >= K), then the B panel
+  constexpr int UA = cdiv(MF * 16 * kSkMax, 256);
+  const int ta = MF * 16 * K4;
+  const FastDiv div_k4(K4);
+  float va[UA];
+#pragma unroll
+  for (int u = 0; u < UA; ++u) {
+    const int e = min(tid + u * 256, ta - 1), m = div_k4(e), k = e - m * K4;
+    const bool in = m < g.M && k < K;
+    const float x = g.A[in ? m * g.a_m + k * g.a_k : 0];
+    va[u] = in ? x : 0.f;
+  }
+  if (vec) {  // 16-byte loads: K4 rows x 32 float4 (b_k, N, batch strides 4-aligned)
+    constexpr int UB = cdiv(kSkMax * kSkPT / 4, 256);
+    const int tb = K4 * (kSkPT / 4);
+    f32x4 vb[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int e = min(tid + u * 256, tb - 1), k = e >> 5, p = p0 + 4 * (e & 31);
+      const bool in = k < K && p < g.N;
+      const f32x4 x = *reinterpret_cast<const f32x4*>(Bb + (in ? k * g.b_k + p : 0));
+      vb[u] = in ? x : zero4();
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int e = min(tid + u * 256, tb - 1);
+      *reinterpret_cast<f32x4*>(Bs + (e >> 5) * BP + 4 * (e & 31)) = vb[u];
+    }
+  } else {
+    constexpr int U = 20;
+    const int tot = K4 * kSkPT;
+    for (int e0 = tid; e0 < tot; e0 += U * 256) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = min(e0 + u * 256, tot - 1), k = e >> 7, p = p0 + (e & (kSkPT - 1));
+        const bool in = k < K && p < g.N;
+        const float x = Bb[in ? k * g.b_k + p : 0];
+        v[u] = in ? x : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = min(e0 + u * 256, tot - 1);
+        Bs[(e >> 7) * BP + (e & (kSkPT - 1))] = v[u];
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < UA; ++u) {
+    const int e = min(tid + u * 256, ta - 1), m = div_k4(e);
+    As[m * KP + e - m * K4] = va[u];
+  }
+  __syncthreads();
+  f32x4 acc[MF][2];
+#pragma unroll
+  for (int x = 0; x < MF; ++x) acc[x][0] = acc[x][1] = zero4();
+  const int cw = wave * 32;
+  for (int k = lk; k < K4; k += 4) {
+    float av[MF], bv[2];
+#pragma unroll
+    for (int x = 0; x < MF; ++x) av[x] = As[(x * 16 + lr) * KP + k];
+#pragma unroll
+    for (int y = 0; y < 2; ++y) bv[y] = Bs[k * BP + cw + y * 16 + lr];
+#pragma unroll
+    for (int x = 0; x < MF; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[x][y] = mfma16x16x4(av[x], bv[y], acc[x][y]);
+  }
+  float* Cb = g.C + b1 * g.c_b1 + b2 * g.c_b2;
+  if (!g.d_out && !g.nseg) {  // plain store: one uniform branch, not one per element
+#pragma unroll
+    for (int x = 0; x < MF; ++x)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = x * 16 + lk * 4 + r;
+        if (m >= g.M) continue;
+        float* row = Cb + m * g.c_m;
+        const float bm = g.bias_m ? g.bias_m[m] : 0.f;
+#pragma unroll
+        for (int y = 0; y < 2; ++y) {
+          const int p = p0 + cw + y * 16 + lr;
+          if (p < g.N) {
+            float v = fmaf(g.alpha, acc[x][y][r], bm);
+            if (g.beta != 0.f) v = fmaf(g.beta, row[p], v);
+            row[p] = v;
+          }
+        }
+      }
+    return;
+  }
+  float* Db = g.d_out ? g.d_out + b1 * g.c_b1 + b2 * g.c_b2 : nullptr;
+  if (Db && !g.nseg) {  // C and the adjacency D = alpha_d * C + (A (* W) (+ R)) per column
+    const float ad = *g.d_alpha;
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int p = p0 + cw + y * 16 + lr;
+      if (p >= g.N) continue;
+      float ac = g.d_A[p];
+      if (g.d_W) ac *= g.d_W[p];
+      if (g.d_R) ac += g.d_R[p];
+#pragma unroll
+      for (int x = 0; x < MF; ++x)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = x * 16 + lk * 4 + r;
+          if (m < g.M) {
+            float v = g.alpha * acc[x][y][r];
+            if (g.bias_m) v += g.bias_m[m];
+            Db[m * g.c_m + p] = fmaf(ad, v, ac);
+            float* c = Cb + m * g.c_m + p;
+            if (g.beta != 0.f) v += g.beta * *c;
+            *c = v;
+          }
+        }
+    }
+    return;
+  }
+#pragma unroll
+  for (int x = 0; x < MF; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = x * 16 + lk * 4 + r, p = p0 + cw + y * 16 + lr;
+        if (m < g.M && p < g.N) {
+          float v = g.alpha * acc[x][y][r];
+          if (g.bias_m) v += g.bias_m[m];
+          gemm_store(g, Cb, Db, m, p, v);
+        }
+      }
+}
+
 // ---------------------------------------------------------------------------
 // Per-sample aggregation over slabs: the DSTDGC products (model/dstdgcn.py:87
 // spatial, :93 temporal) and their gradients,
@@ -252,17 +447,6 @@ struct AggArgs {
 };
 constexpr int kAggMaxC = 64, kAggMaxNN = 64;
 
-// x / d for x < 2^16 by a multiply-high: m = ceil(2^32 / d) (m = 2^32, i.e.
-// hi set, for d = 1); exact since x * (m - 2^32 / d) / 2^32 < 1 / d.
-struct FastDiv {
-  uint32_t m, hi;
-  __device__ explicit FastDiv(uint32_t d) {
-    const uint64_t M = 0xFFFFFFFFull / d + 1;
-    m = (uint32_t)M;
-    hi = (uint32_t)(M >> 32);
-  }
-  __device__ int operator()(int x) const { return (int)(__umulhi((uint32_t)x, m) + (hi ? (uint32_t)x : 0u)); }
-};
 
 template <bool TEMP, bool BWD, int MF, int JF, bool DF = true>  // DF: bwd also computes dF
 __global__ __launch_bounds__(256) void k_agg(AggArgs g) {
@@ -818,23 +1002,30 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
   const int a = blockIdx.x, ch = blockIdx.y;
   const int per = (B + nch - 1) / nch, n0 = ch * per, n1 = min(B, n0 + per);
   const float al = *alpha;
+  // dD, or the sum of its np <= 4 channel-chunk partials in chunk order
+  const float* src = np > 1 ? dDp : dD;
+  const int nq = np > 1 ? np : 1;
+  const size_t qs = np > 1 ? (size_t)B * A * NN2 : 0;
   float sbr = 0.f, sal = 0.f;
   for (int ij = threadIdx.x; ij < NN2; ij += blockDim.x) {
     float sa = 0.f;
     for (int nb = n0; nb < n1; nb += 4) {  // 4 samples' loads in flight, then use in order
       float dv[4], ev[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const size_t i = ((size_t)(nb + u) * A + a) * NN2 + ij;
-        if (np > 1) {  // channel-chunk partials, summed in chunk order
-          const size_t ps = (size_t)B * A * NN2;
+      for (int u = 0; u < 4; ++u) {  // (clamped sample: loads without branches)
+        const size_t i = ((size_t)min(nb + u, n1 - 1) * A + a) * NN2 + ij;
+        if (nq > 1) {
+          float pv[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pv[q] = src[min(q, nq - 1) * qs + i];
           float t = 0.f;
-          for (int q = 0; q < np; ++q) t += nb + u < n1 ? dDp[q * ps + i] : 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) t += q < nq ? pv[q] : 0.f;
           dv[u] = t;
         } else {
-          dv[u] = nb + u < n1 ? dD[i] : 0.f;
+          dv[u] = src[i];
         }
-        ev[u] = nb + u < n1 ? E[i] : 0.f;
+        ev[u] = E[i];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -1482,9 +1673,58 @@ int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 4096); }
 
 size_t gemm_scratch_floats(int M, int N) { return (size_t)kMaxSplit * M * N; }
 
+namespace {
+// DSTD_GEMM_GENERIC=1: every GEMM on k_gemm (A/B of the skinny kernel)
+bool gemm_generic() {
+  static const bool v = [] {
+    const char* e = getenv("DSTD_GEMM_GENERIC");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+template <class K, class... Args>
+void sk_go(K kern, int grid, size_t lds, hipStream_t s, Args... args) {
+  static bool attr = false;  // (per instantiation) allow > 64 KB of dynamic LDS
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  kern<<<grid, 256, lds, s>>>(args...);
+}
+// hipErrorNotSupported: not a skinny shape (nothing launched)
+hipError_t gemm_skinny(const Gemm& g, float* scratch, hipStream_t s) {
+  const int nbat = g.nb1 * g.nb2;
+  // Only the shape class where it measured faster than k_gemm (the 1x1-conv
+  // forward, K = Cin = 64: 20.5 vs 25.5 us at the config-5 batch,
+  // profiles/r03v_skinny_micro.txt); conv dx (K = 68, beta 1), conv_rm (d_out)
+  // and its transposed product (K = A) stay on k_gemm.
+  if (!g.reduce && g.b_n == 1 && g.c_n == 1 && !g.b_ones_last && !g.d_out && !g.nseg && g.beta == 0.f &&
+      g.M <= kSkMax && g.K <= kSkMax && g.K >= 48 && g.N >= 64) {
+    const int MF = cdiv(g.M, 16), K4 = rup(g.K, 4), KP = sk_pitch(K4, 4), BP = sk_pitch(kSkPT, 16);
+    const size_t lds = sizeof(float) * ((size_t)MF * 16 * KP + (size_t)K4 * BP);
+    const int grid = nbat * cdiv(g.N, kSkPT);
+    const int vec = g.N % 4 == 0 && g.b_k % 4 == 0 && g.b_b1 % 4 == 0 && g.b_b2 % 4 == 0 &&
+                    ((uintptr_t)g.B & 15) == 0;
+    switch (MF) {
+      case 1: sk_go(k_skinny_panel<1>, grid, lds, s, g, KP, BP, vec); break;
+      case 2: sk_go(k_skinny_panel<2>, grid, lds, s, g, KP, BP, vec); break;
+      case 3: sk_go(k_skinny_panel<3>, grid, lds, s, g, KP, BP, vec); break;
+      case 4: sk_go(k_skinny_panel<4>, grid, lds, s, g, KP, BP, vec); break;
+      default: sk_go(k_skinny_panel<5>, grid, lds, s, g, KP, BP, vec); break;
+    }
+    return hipGetLastError();
+  }
+  return hipErrorNotSupported;
+}
+}  // namespace
+
 hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.d_out && (g.reduce || !g.d_A || !g.d_alpha)) return hipErrorInvalidValue;
+  if (!gemm_generic()) {
+    const hipError_t e = gemm_skinny(g, scratch, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   const int TM = g.M <= 32 ? 32 : 64, TN = g.N <= 32 ? 32 : 64;
   const int tiles = cdiv(g.M, TM) * cdiv(g.N, TN);
   const int nbat = g.nb1 * g.nb2;

@@ -3,8 +3,8 @@
 // with their residual conv; temporal 64->64 and the 3->3 output tail).
 //
 // Why a second design (profiles/r01_*, scripts/ab_kernels.py): the persistent
-// 8-wave kernels of dstd_fast.hip spend ~60% of their time outside the MFMA
-// pipe -- four barriers per tile, index arithmetic for the LDS staging, the
+// 8-wave kernels of round 1 (dstd_fast.hip, retired in round 3) spent ~60% of
+// their time outside the MFMA pipe -- four barriers per tile, index arithmetic for the LDS staging, the
 // conv output round trip through LDS.  Here every wave owns a whole unit of
 // work and never meets a barrier after the prologue:
 //
@@ -737,7 +737,7 @@ int wave_occupancy(K k) {
 }
 
 // (compile-time only: a -DDSTD_NO_WAVE build routes the exact-fp32 block
-// launches to the dstd_fast.hip kernels; no process-wide switch)
+// launches to the generic kernels; no process-wide switch)
 bool wave_disabled() {
 #ifdef DSTD_NO_WAVE
   return true;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Per-kernel VGPR / spill / occupancy / LDS summary of a HIP source (gfx950).
-# usage: scripts/kres.sh dstd-gcn_amd/csrc/dstd_fast.hip [extra hipcc flags]
+# usage: scripts/kres.sh dstd-gcn_amd/csrc/dstd_adj.hip [extra hipcc flags]
 src=$1; shift
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c "$src" -o /tmp/kres.o "$@" \
   -Rpass-analysis=kernel-resource-usage 2>&1 | sed -n 's/.*remark: *//p' | sed 's/ \[-Rpass.*//' | awk '

@@ -3,3 +3,5 @@
 cd "$(dirname "$0")" || exit 2
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 agg_micro.cpp -o agg_micro \
   -L../../dstd-gcn_amd -ldstd_gcn -Wl,-rpath,'$ORIGIN/../../dstd-gcn_amd'
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 skinny_micro.cpp -o skinny_micro \
+  -L../../dstd-gcn_amd -ldstd_gcn -Wl,-rpath,'$ORIGIN/../../dstd-gcn_amd'

@@ -1,0 +1,35 @@
+"""Summarise a rocprofv3 kernel trace (run_kernel_trace.csv): per-kernel-name
+totals, busy time (union of kernel intervals) vs wall span, per step.
+usage: trace_summary.py TRACE.csv STEPS [TOP]"""
+import collections
+import csv
+import sys
+
+
+def main(path, steps, top=25):
+    rows = list(csv.DictReader(open(path)))
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    tot = collections.defaultdict(lambda: [0, 0])
+    for s, e, k in iv:
+        t = tot[k.replace("(anonymous namespace)::", "").split("(")[0][-70:]]
+        t[0] += e - s
+        t[1] += 1
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, _ in iv:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    span = iv[-1][1] - iv[0][0]
+    ksum = sum(v[0] for v in tot.values())
+    print(f"launches/step {len(iv) / steps:.0f}  kernel-sum/step {ksum / steps / 1e3:.1f} us  "
+          f"busy/step {busy / steps / 1e3:.1f} us  span/step {span / steps / 1e3:.1f} us")
+    for k, (t, c) in sorted(tot.items(), key=lambda kv: -kv[1][0])[:top]:
+        print(f"{t / steps / 1e3:9.1f} us/step {c / steps:6.1f}/step {t / c / 1e3:8.2f} us  {k}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]) if len(sys.argv) > 3 else 25)
