@@ -232,11 +232,12 @@ def _bn_momentum(module):
     return float(moms.pop())
 
 
-def _count_batch(module):
-    """nn.BatchNorm1d bumps num_batches_tracked once per train forward."""
+def _count_batch(module, calls=1):
+    """nn.BatchNorm1d bumps num_batches_tracked once per train forward
+    (``calls``: a forward pair counts as two)."""
     t = [m.num_batches_tracked for m in _bn_modules(module) if m.num_batches_tracked is not None]
     if t:
-        torch._foreach_add_(t, 1)
+        torch._foreach_add_(t, calls)
 
 
 def _op_train_fwd_native(mod, mode, x, A, alpha):
@@ -370,9 +371,10 @@ class _ModelTrain(torch.autograd.Function):
     """DSTDGCN forward + native backward (reference :293-317): train mode, or
     an eval-mode model under autograd (running-statistics BN, no dropout).
     Both directions are torch.library ops (dstd::dstdgcn_train_forward /
-    dstdgcn_train_backward, below) over the C ABI; the opt-in in-place
-    gradient arena calls the C ABI directly (it writes .grad as a side
-    effect, which an op cannot)."""
+    dstdgcn_train_backward, below) over the C ABI; eager forwards call the
+    forward op's implementation directly (as the eval forward does), and the
+    opt-in in-place gradient arena calls the C ABI directly (it writes .grad
+    as a side effect, which an op cannot)."""
 
     @staticmethod
     def forward(ctx, model, paired, x, *params):
@@ -388,12 +390,21 @@ class _ModelTrain(torch.autograd.Function):
             ctx.seed_t = torch.randint(0, 2 ** 62, (1,), device=x.device, dtype=torch.int64)
             seed = ctx.seed_t.data_ptr()
             flags |= native.TRAIN_SEED_DEVICE
-        y, saved = torch.ops.dstd.dstdgcn_train_forward(x, list(params), model._tree.get(model)[1], model._dstd_uid,
-                                                        flags, _bn_momentum(model), drop, seed)
+        buffers = model._tree.get(model)[1]
+        if type(x) is torch.Tensor and not torch.compiler.is_compiling():
+            # eager: the op's implementation without the dispatcher's boxing
+            # of ~300 tensor arguments (~0.3 ms of host time per step); the
+            # running statistics it updates get the version bump the op's
+            # mutates_args declares (the eval forward's constant cache keys
+            # on versions)
+            y, saved = _model_train_fwd_native(model, x, flags, _bn_momentum(model), drop, seed)
+            if not flags & native.TRAIN_RUNNING_STATS:
+                torch.autograd.graph.increment_version(buffers)
+        else:
+            y, saved = torch.ops.dstd.dstdgcn_train_forward(x, list(params), buffers, model._dstd_uid,
+                                                            flags, _bn_momentum(model), drop, seed)
         if not flags & native.TRAIN_RUNNING_STATS:
-            _count_batch(model)
-            if paired:
-                _count_batch(model)
+            _count_batch(model, 2 if paired else 1)
         ctx.model, ctx.saved_buf, ctx.drop, ctx.seed, ctx.flags = model, saved, drop, seed, flags
         ctx.params = list(params)  # the backward reuses them (a module walk costs ~0.7 ms)
         ctx.save_for_backward(x)
