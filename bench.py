@@ -382,7 +382,7 @@ def train_leg(device, B, steps, warmup):
     torch.manual_seed(0)
     m = get_model("dstdgcn", dstdgcn=opts).to(device).train()
     m._dstd_inplace_grads = True  # as engine.PredictionEngine.train opts in
-    opt = torch.optim.Adam(m.parameters(), lr=3e-3)
+    opt = torch.optim.Adam(m.parameters(), lr=3e-3, fused=True)  # the engine's optimizer (eager steps)
     g = torch.Generator().manual_seed(1234)
     seq = torch.randn(B, 40, 69, generator=g)
     inp = seq.clone()

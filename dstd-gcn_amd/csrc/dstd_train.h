@@ -86,29 +86,6 @@ hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int R
 // dZ = dM * (1 - M^2);  dP(n,r,a,i) = sum_j dZ;  dQ(n,r,a,j) = -sum_i dZ.
 hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int R, int A, int NN, float* dP,
                           float* dQ, hipStream_t s);
-// M = tanh(P_i - Q_j) (stored), E = Wrm M + b_rm, D = alpha E + (A0 (* W0)
-// (+ R0)) in one launch; hipErrorNotSupported (nothing launched) outside
-// A, R*A <= 80.
-struct TanhRmArgs {
-  const float* P;
-  const float* Q;
-  PQView v;
-  int R, A, NN;
-  const float* wrm;
-  const float* brm;
-  float* M;
-  float* E;
-  float* D;
-  const float* alpha;
-  const float* A0;
-  const float* W0;
-  const float* R0;
-};
-hipError_t tanh_rm_fwd(const TanhRmArgs& a, int B, hipStream_t s);
-// dM = Wrm^T dE (conv_rm's input gradient, Wrm [A][R*A]) fused with
-// tanh_outer_bwd: dM never materialised.
-hipError_t dm_tanh_bwd(const float* Wrm, const float* dE, const float* M, PQView v, int B, int R, int A, int NN,
-                       float* dP, float* dQ, hipStream_t s);
 
 // Backward of adj_combine + the conv_rm bias, fused: dD -> dE = alpha * dD in
 // place, and dalpha += <dD, E>, dA[ij] += sum_{n,a} dD, dbrm[a] += sum_{n,ij} dE.

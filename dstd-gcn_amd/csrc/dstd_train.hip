@@ -415,94 +415,6 @@ __global__ __launch_bounds__(256) void k_skinny_panel(Gemm g, int KP, int BP, in
 }
 
 // ---------------------------------------------------------------------------
-// conv_rm of the tanh outer difference in one pass (model/dstdgcn.py:84-86 /
-// :90-92; replaces k_tanh_outer_fwd + the conv_rm GEMM and M's read-back):
-// workgroup = (sample n, 128 columns ij of the NN x NN plane).  The K = R*A
-// rows M[k][ij] = tanh(P[k][i] - Q[k][j]) of the panel are formed from the
-// sample's Q rows and the panel's P values staged in LDS (the same tanhf as
-// k_tanh_outer_fwd: bit-identical M), stored once (the backward's saved M)
-// and kept in LDS as the B panel; then k_skinny_panel's MFMA loop and its
-// adjacency epilogue: E = Wrm M + b_rm, D = alpha E + (A (* W) (+ R)).
-// ---------------------------------------------------------------------------
-template <int MF>
-__global__ __launch_bounds__(256) void k_tanh_rm_fwd(TanhRmArgs g, int KP, int BP, int NI) {
-  extern __shared__ float sk_sm[];
-  const int RA = g.R * g.A, K4 = rup(RA, 4), NN = g.NN, NN2 = NN * NN;
-  float* As = sk_sm;                   // [MF*16][KP]: Wrm rows (zero padded)
-  float* Bs = As + MF * 16 * KP;       // [K4][BP]: the M panel
-  float* Qs = Bs + K4 * BP;            // [RA][NN]
-  float* Ps = Qs + RA * NN;            // [RA][NI]: P[k][i0 + ii]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
-  const int ntile = cdiv(NN2, kSkPT);
-  const int n = blockIdx.x / ntile, p0 = (blockIdx.x - n * ntile) * kSkPT, i0 = p0 / NN;
-  const float* P = g.P + n * g.v.sn;
-  const float* Q = g.Q + n * g.v.sn;
-  const FastDiv div_a(g.A), div_nn(NN), div_k4(K4), div_ni(NI);
-  for (int e = tid; e < MF * 16 * K4; e += 256) {
-    const int m = div_k4(e), k = e - m * K4;
-    As[m * KP + k] = m < g.A && k < RA ? g.wrm[m * RA + k] : 0.f;
-  }
-  for (int e = tid; e < RA * NN; e += 256) {
-    const int k = div_nn(e), j = e - k * NN, r = div_a(k), a = k - r * g.A;
-    Qs[e] = Q[r * g.v.sr + a * g.v.sa + j * g.v.si];
-  }
-  for (int e = tid; e < RA * NI; e += 256) {
-    const int k = div_ni(e), ii = e - k * NI, r = div_a(k), a = k - r * g.A;
-    Ps[e] = i0 + ii < NN ? P[r * g.v.sr + a * g.v.sa + (i0 + ii) * g.v.si] : 0.f;
-  }
-  __syncthreads();
-  float* Mn = g.M + (size_t)n * RA * NN2;
-  for (int e = tid; e < K4 * kSkPT; e += 256) {
-    const int k = e >> 7, p = e & (kSkPT - 1), col = p0 + p;
-    float val = 0.f;
-    if (k < RA && col < NN2) {
-      const int i = div_nn(col), j = col - i * NN;
-      val = tanhf(Ps[k * NI + i - i0] - Qs[k * NN + j]);
-      Mn[(size_t)k * NN2 + col] = val;
-    }
-    Bs[k * BP + p] = val;
-  }
-  __syncthreads();
-  f32x4 acc[MF][2];
-#pragma unroll
-  for (int x = 0; x < MF; ++x) acc[x][0] = acc[x][1] = zero4();
-  const int cw = wave * 32;
-  for (int k = lk; k < K4; k += 4) {
-    float av[MF], bv[2];
-#pragma unroll
-    for (int x = 0; x < MF; ++x) av[x] = As[(x * 16 + lr) * KP + k];
-#pragma unroll
-    for (int y = 0; y < 2; ++y) bv[y] = Bs[k * BP + cw + y * 16 + lr];
-#pragma unroll
-    for (int x = 0; x < MF; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y) acc[x][y] = mfma16x16x4(av[x], bv[y], acc[x][y]);
-  }
-  float* Eb = g.E + (size_t)n * g.A * NN2;
-  float* Db = g.D + (size_t)n * g.A * NN2;
-  const float ad = *g.alpha;
-#pragma unroll
-  for (int y = 0; y < 2; ++y) {
-    const int p = p0 + cw + y * 16 + lr;
-    if (p >= NN2) continue;
-    float ac = g.A0[p];
-    if (g.W0) ac *= g.W0[p];
-    if (g.R0) ac += g.R0[p];
-#pragma unroll
-    for (int x = 0; x < MF; ++x)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = x * 16 + lk * 4 + r;
-        if (m < g.A) {
-          const float v = acc[x][y][r] + (g.brm ? g.brm[m] : 0.f);
-          Eb[m * NN2 + p] = v;
-          Db[m * NN2 + p] = fmaf(ad, v, ac);
-        }
-      }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Per-sample aggregation over slabs: the DSTDGC products (model/dstdgcn.py:87
 // spatial, :93 temporal) and their gradients,
 //   fwd  y[c][(a,j)]  (+)= sum_i F[c][(a,i)] D[a][i][j]
@@ -1073,79 +985,6 @@ __global__ void k_tanh_outer_bwd(const float* __restrict__ M, const float* __res
     } else {
       const int j = i - NN;
       for (int k = 0; k < NN; ++k) s += dz[k * (NN + 1) + j];
-      dQ[base + j * v.si] = -s;
-    }
-  }
-}
-
-
-// dM = conv_rm's input gradient and the tanh-outer backward in one pass
-// (replaces the dM GEMM + k_tanh_outer_bwd pair, and dM's HBM round trip):
-//   dM[n][k][ij] = sum_a' Wrm[a'][k] dE[n][a'][ij]        (k = r*A + a)
-//   dZ = dM * (1 - M^2);  dP(n,r,a,i) = sum_j dZ;  dQ(n,r,a,j) = -sum_i dZ
-// Workgroup = (sample n, KB consecutive k): each thread forms dZ for its
-// columns ij (the dE column's A loads in flight, KB FMA chains against the
-// Wrm columns in LDS) into an LDS block per k, then the row / column sums in
-// k_tanh_outer_bwd's order.  The workgroups of one sample are adjacent in
-// the grid, so the dE slab they share is read from L2.
-constexpr int kDmRows = 8;
-__global__ __launch_bounds__(256) void k_dm_tanh_bwd(const float* __restrict__ Wrm, const float* __restrict__ dE,
-                                                     const float* __restrict__ M, PQView v, int R, int A, int NN,
-                                                     int KB, float* __restrict__ dP, float* __restrict__ dQ) {
-  extern __shared__ float dmz[];
-  const int RA = R * A, NN2 = NN * NN, ZP = NN2 + 1, nkb = cdiv(RA, KB);
-  const int n = blockIdx.x / nkb, k0 = (blockIdx.x - n * nkb) * KB, nk = min(KB, RA - k0);
-  float* w = dmz;                     // [A][kDmRows]: Wrm[a'][k0 + kk] (0 past nk)
-  float* dz = dmz + A * kDmRows;      // [KB][ZP]
-  for (int e = threadIdx.x; e < A * kDmRows; e += blockDim.x) {
-    const int ap = e / kDmRows, kk = e - ap * kDmRows;
-    w[e] = kk < nk ? Wrm[(size_t)ap * RA + k0 + kk] : 0.f;
-  }
-  __syncthreads();
-  const float* de = dE + (size_t)n * A * NN2;
-  const float* m = M + ((size_t)n * RA + k0) * NN2;
-  for (int ij = threadIdx.x; ij < NN2; ij += blockDim.x) {
-    float acc[kDmRows];
-#pragma unroll
-    for (int kk = 0; kk < kDmRows; ++kk) acc[kk] = 0.f;
-    for (int a0 = 0; a0 < A; a0 += 8) {  // 8 loads in flight, then the FMAs in a' order
-      float d[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) d[u] = de[(size_t)min(a0 + u, A - 1) * NN2 + ij];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (a0 + u >= A) break;
-        const float4 w0 = *reinterpret_cast<const float4*>(w + (a0 + u) * kDmRows);
-        const float4 w1 = *reinterpret_cast<const float4*>(w + (a0 + u) * kDmRows + 4);
-        acc[0] = fmaf(w0.x, d[u], acc[0]);
-        acc[1] = fmaf(w0.y, d[u], acc[1]);
-        acc[2] = fmaf(w0.z, d[u], acc[2]);
-        acc[3] = fmaf(w0.w, d[u], acc[3]);
-        acc[4] = fmaf(w1.x, d[u], acc[4]);
-        acc[5] = fmaf(w1.y, d[u], acc[5]);
-        acc[6] = fmaf(w1.z, d[u], acc[6]);
-        acc[7] = fmaf(w1.w, d[u], acc[7]);
-      }
-    }
-    float t[kDmRows];
-#pragma unroll
-    for (int kk = 0; kk < kDmRows; ++kk) t[kk] = kk < nk ? m[(size_t)kk * NN2 + ij] : 0.f;
-#pragma unroll
-    for (int kk = 0; kk < kDmRows; ++kk)
-      if (kk < nk) dz[kk * ZP + ij] = acc[kk] * (1.f - t[kk] * t[kk]);
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < nk * 2 * NN; e += blockDim.x) {
-    const int kk = e / (2 * NN), i = e - kk * 2 * NN, k = k0 + kk, r = k / A, a = k - r * A;
-    const size_t base = n * v.sn + r * v.sr + a * v.sa;
-    const float* z = dz + kk * ZP;
-    float s = 0.f;
-    if (i < NN) {
-      for (int j = 0; j < NN; ++j) s += z[i * NN + j];
-      dP[base + i * v.si] = s;
-    } else {
-      const int j = i - NN;
-      for (int q = 0; q < NN; ++q) s += z[q * NN + j];
       dQ[base + j * v.si] = -s;
     }
   }
@@ -2113,42 +1952,6 @@ hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int 
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_tanh_outer_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   k_tanh_outer_bwd<<<B * R * A, 256, lds, s>>>(M, dM, v, R, A, NN, dP, dQ);
-  return hipGetLastError();
-}
-
-
-hipError_t dm_tanh_bwd(const float* Wrm, const float* dE, const float* M, PQView v, int B, int R, int A, int NN,
-                       float* dP, float* dQ, hipStream_t s) {
-  const size_t zrow = (size_t)(NN * NN + 1) * sizeof(float), wb = (size_t)A * kDmRows * sizeof(float);
-  const int KB = (int)std::min<size_t>(kDmRows, (96 * 1024) / zrow);
-  if (NN > kTanhMaxNN || KB < 1 || R * A <= 0) return hipErrorInvalidValue;
-  const size_t lds = wb + (size_t)KB * zrow;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  static bool attr = false;  // allow > 64 KB of dynamic LDS (the T = 128 envelope top)
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k_dm_tanh_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  k_dm_tanh_bwd<<<B * cdiv(R * A, KB), 256, lds, s>>>(Wrm, dE, M, v, R, A, NN, KB, dP, dQ);
-  return hipGetLastError();
-}
-
-
-hipError_t tanh_rm_fwd(const TanhRmArgs& a, int B, hipStream_t s) {
-  const int RA = a.R * a.A, NN2 = a.NN * a.NN;
-  if (a.A > kSkMax || RA > kSkMax || a.NN > kTanhMaxNN || RA <= 0 || !a.alpha || !a.A0) return hipErrorNotSupported;
-  const int MF = cdiv(a.A, 16), K4 = rup(RA, 4), KP = sk_pitch(K4, 4), BP = sk_pitch(kSkPT, 16);
-  const int NI = std::min(a.NN, cdiv(kSkPT - 1, a.NN) + 1);  // i values one 128-column panel touches
-  const size_t lds = sizeof(float) * ((size_t)MF * 16 * KP + (size_t)K4 * BP + (size_t)RA * a.NN + (size_t)RA * NI);
-  if (lds > 160 * 1024) return hipErrorNotSupported;
-  const int grid = B * cdiv(NN2, kSkPT);
-  switch (MF) {
-    case 1: sk_go(k_tanh_rm_fwd<1>, grid, lds, s, a, KP, BP, NI); break;
-    case 2: sk_go(k_tanh_rm_fwd<2>, grid, lds, s, a, KP, BP, NI); break;
-    case 3: sk_go(k_tanh_rm_fwd<3>, grid, lds, s, a, KP, BP, NI); break;
-    case 4: sk_go(k_tanh_rm_fwd<4>, grid, lds, s, a, KP, BP, NI); break;
-    default: sk_go(k_tanh_rm_fwd<5>, grid, lds, s, a, KP, BP, NI); break;
-  }
   return hipGetLastError();
 }
 

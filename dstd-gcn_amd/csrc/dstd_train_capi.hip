@@ -89,16 +89,6 @@ bool model_ok(const dstd_model_params* p) {
 // ---------------------------------------------------------------------------
 // one DSTDGC
 // ---------------------------------------------------------------------------
-// DSTD_TRAIN_TANH_FUSED=1: the tanh planes and conv_rm run as one kernel each
-// way (tanh_rm_fwd, dm_tanh_bwd) instead of the tanh kernels + conv_rm GEMMs
-// (opt-in until measured on the GPU).
-bool use_dm_gemm() {
-  static const bool v = [] {
-    const char* e = getenv("DSTD_TRAIN_TANH_FUSED");
-    return !(e && atoi(e) != 0);
-  }();
-  return v;
-}
 // The aggregation products run on the slab kernels (agg_fwd / agg_bwd);
 // DSTD_TRAIN_AGG_GEMM=1 routes them through the strided GEMMs instead (A/B).
 bool use_agg() {
@@ -234,27 +224,19 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   DSTD_TRYH(gemm(conv_fwd(sv.Wp, sv.bp, x, sv.G, g.B, g.cin, g.CG(), g.TV), nullptr, s));
   const float* P = sv.G + (size_t)g.cout * g.TV;
   const float* Q = P + (size_t)g.R * g.TV;
-  hipError_t te = hipErrorNotSupported;
-  if (!use_dm_gemm()) {  // M, E = conv_rm(M), D in one launch            :84-86 / :90-92
-    TanhRmArgs ta{P, Q, g.pq(), g.R, g.A, g.NN, w->wrm, w->brm, sv.M, sv.E, sv.D, alpha, A0, W0, R0};
-    te = tanh_rm_fwd(ta, g.B, s);
-    if (te != hipErrorNotSupported) DSTD_TRYH(te);
-  }
-  if (te == hipErrorNotSupported) {
-    DSTD_TRYH(tanh_outer_fwd(P, Q, g.pq(), g.B, g.R, g.A, g.NN, sv.M, s));                   // :84 / :90
-    Gemm e;  // E = conv_rm(M): [A x RA] . [RA x NN^2] + b_rm           :85 / :91
-    e.M = g.A, e.N = g.NN2, e.K = g.R * g.A, e.nb1 = g.B;
-    e.A = w->wrm, e.a_m = g.R * g.A, e.a_k = 1;
-    e.B = sv.M, e.b_b1 = (long long)g.R * g.A * g.NN2, e.b_k = g.NN2, e.b_n = 1;
-    e.C = sv.E, e.c_b1 = (long long)g.A * g.NN2, e.c_m = g.NN2, e.c_n = 1;
-    e.bias_m = w->brm;
-    e.d_out = sv.D;  // D = alpha * E + Acomb                          :86 / :92
-    e.d_alpha = alpha;
-    e.d_A = A0;
-    e.d_W = W0;
-    e.d_R = R0;
-    DSTD_TRYH(gemm(e, nullptr, s));
-  }
+  DSTD_TRYH(tanh_outer_fwd(P, Q, g.pq(), g.B, g.R, g.A, g.NN, sv.M, s));                   // :84 / :90
+  Gemm e;  // E = conv_rm(M): [A x RA] . [RA x NN^2] + b_rm           :85 / :91
+  e.M = g.A, e.N = g.NN2, e.K = g.R * g.A, e.nb1 = g.B;
+  e.A = w->wrm, e.a_m = g.R * g.A, e.a_k = 1;
+  e.B = sv.M, e.b_b1 = (long long)g.R * g.A * g.NN2, e.b_k = g.NN2, e.b_n = 1;
+  e.C = sv.E, e.c_b1 = (long long)g.A * g.NN2, e.c_m = g.NN2, e.c_n = 1;
+  e.bias_m = w->brm;
+  e.d_out = sv.D;  // D = alpha * E + Acomb                          :86 / :92
+  e.d_alpha = alpha;
+  e.d_A = A0;
+  e.d_W = W0;
+  e.d_R = R0;
+  DSTD_TRYH(gemm(e, nullptr, s));
   if (use_agg()) {  // y[c][(a,j)] = sum_i F[c][(a,i)] D[a][i][j]     :87 / :93
     const hipError_t e = agg_fwd(sv.G, (long long)g.CG() * g.TV, sv.D, y, (long long)g.cout * g.TV, beta_y, g.B,
                                  g.cout, g.T, g.V, g.temporal, s);
@@ -309,19 +291,15 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   wr.C = gr->wrm, wr.c_m = g.R * g.A, wr.c_n = 1;
   wr.beta = 1.f;
   DSTD_TRYH(gemm(wr, ws.gs, s));
+  Gemm dm;  // dM[n][k][ij] = sum_a Wrm[a][k] dE[n][a][ij]
+  dm.M = g.R * g.A, dm.N = g.NN2, dm.K = g.A, dm.nb1 = g.B;
+  dm.A = w->wrm, dm.a_m = 1, dm.a_k = g.R * g.A;
+  dm.B = dE, dm.b_b1 = (long long)g.A * g.NN2, dm.b_k = g.NN2, dm.b_n = 1;
+  dm.C = ws.dM, dm.c_b1 = (long long)g.R * g.A * g.NN2, dm.c_m = g.NN2, dm.c_n = 1;
+  DSTD_TRYH(gemm(dm, nullptr, s));
   // dP, dQ -> rows [cout, cout + 2R) of dG
   float* dP = ws.dG + (size_t)g.cout * g.TV;
-  if (use_dm_gemm()) {
-    Gemm dm;  // dM[n][k][ij] = sum_a Wrm[a][k] dE[n][a][ij]
-    dm.M = g.R * g.A, dm.N = g.NN2, dm.K = g.A, dm.nb1 = g.B;
-    dm.A = w->wrm, dm.a_m = 1, dm.a_k = g.R * g.A;
-    dm.B = dE, dm.b_b1 = (long long)g.A * g.NN2, dm.b_k = g.NN2, dm.b_n = 1;
-    dm.C = ws.dM, dm.c_b1 = (long long)g.R * g.A * g.NN2, dm.c_m = g.NN2, dm.c_n = 1;
-    DSTD_TRYH(gemm(dm, nullptr, s));
-    DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.R, g.A, g.NN, dP, dP + (size_t)g.R * g.TV, s));
-  } else {  // dM formed per sample in LDS, never stored
-    DSTD_TRYH(dm_tanh_bwd(w->wrm, dE, sv.M, g.pq(), g.B, g.R, g.A, g.NN, dP, dP + (size_t)g.R * g.TV, s));
-  }
+  DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.R, g.A, g.NN, dP, dP + (size_t)g.R * g.TV, s));
   // the three 1x1 convs at once: dx += Wp^T dG;  [dWp | dbp] = sum dG [x; 1]^T
   if (dx) {
     Gemm gx = conv_dx(sv.Wp, ws.dG, dx, g.B, g.cin, g.CG(), g.TV);

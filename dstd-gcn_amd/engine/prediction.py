@@ -159,8 +159,13 @@ class PredictionEngine:
             optimizer = optim.Adam(params, lr=torch.tensor(float(self.config["learn"]["lr"]), device=self.device),
                                    weight_decay=self.config["learn"]["weight_decay"], capturable=True)
         else:
+            # the reference's Adam (:188-192) as torch's single-kernel
+            # implementation on the GPU: same update, ~30 foreach launches and
+            # ~0.8 ms of host time per step fewer (scripts/train_host_probe.py)
+            params = list(params)
+            fused = all(p.is_cuda for p in params)
             optimizer = optim.Adam(params, lr=self.config["learn"]["lr"],
-                                   weight_decay=self.config["learn"]["weight_decay"])
+                                   weight_decay=self.config["learn"]["weight_decay"], fused=fused or None)
         self._graph_step = None
         scheduler = optim.lr_scheduler.StepLR(optimizer, step_size=self.config["learn"]["step_size"],
                                               gamma=self.config["learn"]["gamma"])

@@ -18,7 +18,7 @@ def main(B=32, steps=10):
     torch.manual_seed(0)
     m = get_model("dstdgcn", dstdgcn=opts).to(dev).train()
     m._dstd_inplace_grads = True
-    opt = torch.optim.Adam(m.parameters(), lr=3e-3)
+    opt = torch.optim.Adam(m.parameters(), lr=3e-3, fused=True)  # as bench.train_leg
     g = torch.Generator().manual_seed(1234)
     seq = torch.randn(B, 40, 69, generator=g)
     inp = seq.clone()
