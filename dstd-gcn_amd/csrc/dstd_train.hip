@@ -1671,7 +1671,10 @@ int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 4096); }
 
 }  // namespace
 
-size_t gemm_scratch_floats(int M, int N) { return (size_t)kMaxSplit * M * N; }
+// reduce GEMMs on 96-wide tiles split up to twice as far (one tile, e.g. the
+// 68 x 65 packed-conv [W | b] gradient, must still fill the chip)
+constexpr int kMaxSplit96 = 2 * kMaxSplit;
+size_t gemm_scratch_floats(int M, int N) { return (size_t)kMaxSplit96 * M * N; }
 
 namespace {
 // DSTD_GEMM_GENERIC=1: every GEMM on k_gemm (A/B of the skinny kernel)
@@ -1690,6 +1693,13 @@ void sk_go(K kern, int grid, size_t lds, hipStream_t s, Args... args) {
     attr = true;
   }
   kern<<<grid, 256, lds, s>>>(args...);
+}
+bool gemm_96() {
+  static const bool v = [] {
+    const char* e = getenv("DSTD_GEMM_96");
+    return e && atoi(e) != 0;
+  }();
+  return v;
 }
 // hipErrorNotSupported: not a skinny shape (nothing launched)
 hipError_t gemm_skinny(const Gemm& g, float* scratch, hipStream_t s) {
@@ -1725,7 +1735,13 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
     const hipError_t e = gemm_skinny(g, scratch, s);
     if (e != hipErrorNotSupported) return e;
   }
-  const int TM = g.M <= 32 ? 32 : 64, TN = g.N <= 32 ? 32 : 64;
+  // tile edge per operand: 32 / 64, and 96 for a reduce GEMM's 65..96 extent
+  // (the packed conv's [W | b] gradient is 68 x 65: one 96 x 96 tile instead
+  // of four 64 x 64 ones, each operand read once instead of twice;
+  // opt-in DSTD_GEMM_96=1 until measured on the GPU)
+  const bool t96 = g.reduce && scratch && gemm_96();
+  auto edge = [&](int x) { return x <= 32 ? 32 : (x <= 64 || !t96 || x > 96) ? 64 : 96; };
+  const int TM = edge(g.M), TN = edge(g.N);
   const int tiles = cdiv(g.M, TM) * cdiv(g.N, TN);
   const int nbat = g.nb1 * g.nb2;
   int nsplit = 1, kch = 1, kc_len = rup(std::max(g.K, 1), 16);
@@ -1733,7 +1749,7 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
     // ~1024 workgroups, each reducing >= 64 values of K: split the K range of
     // every batch into kch chunks so small batch counts still fill the chip
     const int ksteps = cdiv(g.K, 16);
-    nsplit = std::max(1, std::min(kMaxSplit, 512 / tiles));
+    nsplit = std::max(1, std::min(TM == 96 || TN == 96 ? kMaxSplit96 : kMaxSplit, 512 / tiles));
     kch = std::max(1, std::min(cdiv(nsplit, nbat), cdiv(ksteps, 4)));
     kc_len = cdiv(ksteps, kch) * 16;
     kch = cdiv(g.K, kc_len);
@@ -1746,10 +1762,12 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
           "d_out %d nseg %d bias %d beta %g\n", g.M, g.N, g.K, nbat, g.reduce, nsplit, g.a_m, g.a_k, g.b_k, g.b_n, g.c_m,
           g.c_n, g.d_out != nullptr, g.nseg, g.bias_m != nullptr, g.beta);
 #endif
-  if (TM == 32 && TN == 32) k_gemm<32, 32><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
-  else if (TM == 32) k_gemm<32, 64><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
-  else if (TN == 32) k_gemm<64, 32><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
-  else k_gemm<64, 64><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part);
+#define DSTD_GEMM_GO(tm, tn) \
+  if (TM == tm && TN == tn) k_gemm<tm, tn><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part)
+  DSTD_GEMM_GO(32, 32); else DSTD_GEMM_GO(32, 64); else DSTD_GEMM_GO(64, 32); else DSTD_GEMM_GO(64, 64);
+  else DSTD_GEMM_GO(96, 96); else DSTD_GEMM_GO(96, 64); else DSTD_GEMM_GO(64, 96); else DSTD_GEMM_GO(96, 32);
+  else DSTD_GEMM_GO(32, 96);
+#undef DSTD_GEMM_GO
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nsplit == 1) return e;
   k_gemm_finish<<<cdiv(g.M * g.N, 16), 256, 0, s>>>(g, nsplit, part);
