@@ -1697,7 +1697,7 @@ void sk_go(K kern, int grid, size_t lds, hipStream_t s, Args... args) {
 bool gemm_96() {
   static const bool v = [] {
     const char* e = getenv("DSTD_GEMM_96");
-    return e && atoi(e) != 0;
+    return !(e && atoi(e) == 0);
   }();
   return v;
 }
@@ -1738,7 +1738,8 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   // tile edge per operand: 32 / 64, and 96 for a reduce GEMM's 65..96 extent
   // (the packed conv's [W | b] gradient is 68 x 65: one 96 x 96 tile instead
   // of four 64 x 64 ones, each operand read once instead of twice;
-  // opt-in DSTD_GEMM_96=1 until measured on the GPU)
+  // B=32 training step 5.95 -> 5.69 ms, profiles/r03y_gemm96_ab.txt;
+  // DSTD_GEMM_96=0 keeps 64-wide tiles, A/B)
   const bool t96 = g.reduce && scratch && gemm_96();
   auto edge = [&](int x) { return x <= 32 ? 32 : (x <= 64 || !t96 || x > 96) ? 64 : 96; };
   const int TM = edge(g.M), TN = edge(g.N);
