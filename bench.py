@@ -298,27 +298,22 @@ def cpu_model():
     return None
 
 
-def variant_throughput(config, B, device, steps, warmup):
-    """Side measurement at N=1 (not `value`): the same eval forward on another
-    shape of the H36M model -- BASELINE.json's metric names "22J x 50T" while
-    the shipped yaml (dstdgcn_h36m.yaml:137-138) runs 10 + 25 frames; the
-    '50 in / 25 out' T=75 variant is timed here so both are on the line."""
+def config_leg(config, B, device, steps, warmup):
+    """Side measurement at N=1 (not `value`): the eval forward of another
+    BASELINE.json config through the drop-in call model(x), fixture weights of
+    that layout.  "h36m75": BASELINE.json's metric names "22J x 50T" while the
+    shipped yaml (dstdgcn_h36m.yaml:137-138) runs 10 + 25 frames, so the
+    '50 in / 25 out' T=75 variant is on the line too; "cmu" / "3dpw": configs
+    3 and the 3DPW shape at B=256."""
     model, opts, _ = load_model(config, device)
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V = opts["joints_to_consider"]
     x = synth_input(B, T, V, opts["input_time_frame"], 1234).to(device)
-    y = torch.empty_like(x)
     with torch.no_grad():
-        for _ in range(max(warmup, 2)):
-            model._forward_native(x, y)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            model._forward_native(x, y)
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-    return {"workload": CONFIGS[config][1] + f", B={B}, eval forward", "seq_len": T,
-            "value": round(B * steps / el, 2), "unit": "seq/s", "ms_per_step": round(el / steps * 1e3, 4)}
+        ms, host = timed_calls(lambda: model(x), steps, max(warmup, 2))
+    return {"workload": CONFIGS[config][1] + f", B={B}, eval forward", "seq_len": T, "joints": V,
+            "value": round(B / ms * 1e3, 2), "unit": "seq/s", "ms_per_step": round(ms, 4),
+            "host_us_per_call": round(host, 2), "timed_call": "model(x)"}
 
 
 def timed_calls(fn, steps, warmup):
@@ -438,7 +433,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variant", action="store_true",
-                    help="skip the side measurement of the '50 in / 25 out' (T=75) H36M variant at N=1")
+                    help="skip the side measurements of the other configs at N=1 (H36M '50 in / 25 out' T=75, "
+                         "CMU and 3DPW at B=256)")
     ap.add_argument("--no-side", action="store_true",
                     help="skip the N=1 side legs (exact fp32, B=32 eval, B=32 3DPW training step)")
     ap.add_argument("--probe-every", type=int, default=5,
@@ -595,7 +591,9 @@ def main():
             "timed_call": "model(x): DSTDGCN.forward -> torch.ops.dstd.dstdgcn_forward (the drop-in path)",
         }
         if world == 1 and args.config == "h36m" and not args.no_variant:
-            out["variant_t75"] = variant_throughput("h36m75", B, device, args.steps, args.warmup)
+            out["variant_t75"] = config_leg("h36m75", B, device, args.steps, args.warmup)
+            out["cmu_b256"] = config_leg("cmu", B, device, args.steps, args.warmup)
+            out["3dpw_b256"] = config_leg("3dpw", B, device, args.steps, args.warmup)
         if world == 1 and not args.no_side:
             out["exact_fp32"] = arithmetic_leg(model, x, "fp32", args.steps, args.warmup)
             out["eval_b32"] = small_batch_leg(model, x, 32, max(args.steps, 100), args.warmup)

@@ -748,6 +748,7 @@ const char* dstd_error_string(int code) {
     case DSTD_EINVAL: return "invalid argument (null pointer or bad shape)";
     case DSTD_EWORKSPACE: return "workspace too small";
     case DSTD_ELIMIT: return "shape outside the supported envelope (T<=128, V<=32, C<=64)";
+    case DSTD_ECOLLECTIVE: return "the dstd_bn_sync collective returned an error (SyncBN)";
     default: return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
   }
 }

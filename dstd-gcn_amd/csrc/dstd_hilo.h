@@ -80,6 +80,38 @@ __device__ __forceinline__ void split8(const float4& a, const float4& b, f16x8& 
   hi = __builtin_bit_cast(f16x8, h);
   lo = __builtin_bit_cast(f16x8, l);
 }
+// 4 values (the other four halves of an 8-half fragment are zero): split8
+// without the four fma_mix on zeros, which the asm block hides from hipcc
+__device__ __forceinline__ void split4(const float4& a, uint2& hi, uint2& lo) {
+  hi.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a.x, a.y}, f16x2_t));
+  hi.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a.z, a.w}, f16x2_t));
+  asm("v_fma_mixlo_f16 %0, %2, 1.0, -%6 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %3, 1.0, -%6 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixlo_f16 %1, %4, 1.0, -%7 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %5, 1.0, -%7 op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+      "s_nop 1"
+      : "=&v"(lo.x), "=&v"(lo.y)
+      : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(hi.x), "v"(hi.y));
+}
+
+// max(m, |a|, |b|) as ONE v_max3_f32 with abs source modifiers.  fmaxf on
+// loaded values costs three instructions per two values here: in IEEE mode
+// hipcc first canonicalises each operand (v_max_f32 x, |x|, |x|).  Operands
+// must be loads or VALU results, never an MFMA accumulator read directly: the
+// hazard recognizer does not look into inline asm, so it would not pad the
+// MFMA -> VALU read.
+__device__ __forceinline__ float amax2(float m, float a, float b) {
+  float r;
+  asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+
+// PReLU as one median: w <= 1 gives max(x, w x), w > 1 gives min(x, w x),
+// i.e. med3(x, w x, c) with the wave-uniform c = +inf / -inf (prelu_cap).
+// Equal to prelu_f bit for bit up to the sign of a zero; two VALU per value
+// instead of three (max, min, fma).
+__device__ __forceinline__ float prelu_cap(float w) { return w <= 1.f ? __builtin_inff() : -__builtin_inff(); }
+__device__ __forceinline__ float prelu_m(float x, float w, float c) { return __builtin_amdgcn_fmed3f(x, w * x, c); }
 
 template <int N, bool IL>
 struct SlotMap {

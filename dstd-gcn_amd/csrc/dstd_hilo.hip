@@ -76,6 +76,13 @@ __device__ __forceinline__ f32x4 mfma32(const f16x8& a, const f16x8& b, f32x4 c)
 __device__ __forceinline__ void split_acc(const f32x4& a, const f32x4& b, f16x8& hi, f16x8& lo) {
   split8(make_float4(a[0], a[1], a[2], a[3]), make_float4(b[0], b[1], b[2], b[3]), hi, lo);
 }
+// the same with no second tile (slots 4..7 zero)
+__device__ __forceinline__ void split_acc(const f32x4& a, f16x8& hi, f16x8& lo) {
+  uint2 h, l;
+  split4(make_float4(a[0], a[1], a[2], a[3]), h, l);
+  hi = __builtin_bit_cast(f16x8, make_uint4(h.x, h.y, 0u, 0u));
+  lo = __builtin_bit_cast(f16x8, make_uint4(l.x, l.y, 0u, 0u));
+}
 
 // A zero the compiler cannot see through: added to LDS fragment addresses
 // inside the unit loop it stops hipcc from hoisting the (loop-invariant)
@@ -159,10 +166,11 @@ __device__ __forceinline__ uint32_t wave_max_bits(float v) {
   const uint32_t r2 = __builtin_amdgcn_readlane(b, 32), r3 = __builtin_amdgcn_readlane(b, 48);
   return max(max(r0, r1), max(r2, r3));
 }
-__device__ __forceinline__ float amax4(float m, const float4& v) {
-  return fmaxf(fmaxf(m, fmaxf(fabsf(v.x), fabsf(v.y))), fmaxf(fabsf(v.z), fabsf(v.w)));
-}
-__device__ __forceinline__ float amax4(float m, const f32x4& v) {
+__device__ __forceinline__ float amax4(float m, const float4& v) { return amax2(amax2(m, v.x, v.y), v.z, v.w); }
+// (f32x4 operands: accumulators after a VALU epilogue; amax4_mfma for ones
+// that may come straight from an MFMA, see amax2)
+__device__ __forceinline__ float amax4(float m, const f32x4& v) { return amax2(amax2(m, v[0], v[1]), v[2], v[3]); }
+__device__ __forceinline__ float amax4_mfma(float m, const f32x4& v) {
   return fmaxf(fmaxf(m, fmaxf(fabsf(v[0]), fabsf(v[1]))), fmaxf(fabsf(v[2]), fabsf(v[3])));
 }
 __device__ __forceinline__ float4 mul4(const float4& v, float s) { return make_float4(v.x * s, v.y * s, v.z * s, v.w * s); }
@@ -461,7 +469,7 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
   const int T = a.T;
   const int efb = __builtin_amdgcn_readfirstlane(st.rng[0]), eb = __builtin_amdgcn_readfirstlane(st.rng[1]);
   const int sa = __builtin_amdgcn_readfirstlane(st.rng[2]);
-  const float pw = *a.prelu;
+  const float pw = *a.prelu, pc = prelu_cap(pw);
   // conv rows: joint of tile m, row cl
   // (padding slots read past the unit's range: zero rows, no memory traffic)
   const int jr0 = SM::row_idx(0, cl) < V ? SM::row_idx(0, cl) : 1 << 20;
@@ -682,10 +690,10 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
           r[2] = R[ct][wt].z;
           r[3] = R[ct][wt].w;
         }
-        o[0] = prelu_f(fmaf(o[0], sc.x, sh.x) + r[0], pw);
-        o[1] = prelu_f(fmaf(o[1], sc.y, sh.y) + r[1], pw);
-        o[2] = prelu_f(fmaf(o[2], sc.z, sh.z) + r[2], pw);
-        o[3] = prelu_f(fmaf(o[3], sc.w, sh.w) + r[3], pw);
+        o[0] = prelu_m(fmaf(o[0], sc.x, sh.x) + r[0], pw, pc);
+        o[1] = prelu_m(fmaf(o[1], sc.y, sh.y) + r[1], pw, pc);
+        o[2] = prelu_m(fmaf(o[2], sc.z, sh.z) + r[2], pw, pc);
+        o[3] = prelu_m(fmaf(o[3], sc.w, sh.w) + r[3], pw, pc);
         if constexpr (COUT % 4 == 0) {
           bst4(ry, (uint32_t)((16 * wt + cl) * COUT + 16 * ct + 4 * kl) * 4, make_float4(o[0], o[1], o[2], o[3]));
         } else {
@@ -723,8 +731,10 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
       const f16x8 qh = as_h8(st.pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(st.pql[(ks * 2 + 1) * 64 + lz]);
       f16x8 hh[NWT], hl[NWT];
 #pragma unroll
-      for (int wt = 0; wt < NWT; ++wt)
-        split_acc(O[2 * ks][wt], 2 * ks + 1 < NCT ? O[2 * ks + 1][wt] : zero4(), hh[wt], hl[wt]);
+      for (int wt = 0; wt < NWT; ++wt) {
+        if (2 * ks + 1 < NCT) split_acc(O[2 * ks][wt], O[2 * ks + 1 < NCT ? 2 * ks + 1 : 0][wt], hh[wt], hl[wt]);
+        else split_acc(O[2 * ks][wt], hh[wt], hl[wt]);
+      }
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt) acc[wt] = mfma32(qo, hh[wt], acc[wt]);
 #pragma unroll
@@ -927,7 +937,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
   const bool has_pq = a.pq != nullptr;
   const int efb = __builtin_amdgcn_readfirstlane(st.rng[0]), eb = __builtin_amdgcn_readfirstlane(st.rng[1]);
   const int sa = __builtin_amdgcn_readfirstlane(st.rng[2]);
-  const float pw = use_bn ? *a.prelu : 0.f;
+  const float pw = use_bn ? *a.prelu : 0.f, pc = prelu_cap(pw);
   // a unit's rows: frame t of joint v at t * V * C floats from the unit base
   const uint32_t col_bytes = (uint32_t)((T - 1) * V + 1) * C * 4;
   const uint32_t frame_bytes = (uint32_t)V * C * 4;
@@ -1059,7 +1069,10 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
       if constexpr (LAZY) load_adj(u, s, bh[0], bo[0]);
       f16x8 dh[NCT], dl[NCT];
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct) split_acc(D[2 * s][ct], 2 * s + 1 < MT ? D[2 * s + 1][ct] : zero4(), dh[ct], dl[ct]);
+      for (int ct = 0; ct < NCT; ++ct) {
+        if (2 * s + 1 < MT) split_acc(D[2 * s][ct], D[2 * s + 1 < MT ? 2 * s + 1 : 0][ct], dh[ct], dl[ct]);
+        else split_acc(D[2 * s][ct], dh[ct], dl[ct]);
+      }
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
@@ -1106,10 +1119,10 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
         }
         if constexpr (use_bn) {
           const float4 sc = st.bnl[0][(4 * ct + kl) * V + v], sh = st.bnl[1][(4 * ct + kl) * V + v];
-          o[0] = prelu_f(fmaf(o[0], sc.x, sh.x), pw);
-          o[1] = prelu_f(fmaf(o[1], sc.y, sh.y), pw);
-          o[2] = prelu_f(fmaf(o[2], sc.z, sh.z), pw);
-          o[3] = prelu_f(fmaf(o[3], sc.w, sh.w), pw);
+          o[0] = prelu_m(fmaf(o[0], sc.x, sh.x), pw, pc);
+          o[1] = prelu_m(fmaf(o[1], sc.y, sh.y), pw, pc);
+          o[2] = prelu_m(fmaf(o[2], sc.z, sh.z), pw, pc);
+          o[3] = prelu_m(fmaf(o[3], sc.w, sh.w), pw, pc);
         }
         if constexpr (C % 4 == 0) {
           bst4(ry, uoff[ut] + 64 * ct, make_float4(o[0], o[1], o[2], o[3]));
@@ -1130,7 +1143,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) hm = amax4(hm, O[ct][ut]);
+        for (int ut = 0; ut < NUT; ++ut) hm = use_bn || use_res ? amax4(hm, O[ct][ut]) : amax4_mfma(hm, O[ct][ut]);
       const int sh = hl_range_shift(fexp_bits(wave_max_bits(hm)));
       if (sh) {
         const float dn = pow2f(-sh);
@@ -1147,8 +1160,10 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
         const f16x8 qh = as_h8(pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(pql[(ks * 2 + 1) * 64 + lz]);
         f16x8 hh[NUT], hl[NUT];
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut)
-          split_acc(O[2 * ks][ut], 2 * ks + 1 < NCT ? O[2 * ks + 1][ut] : zero4(), hh[ut], hl[ut]);
+        for (int ut = 0; ut < NUT; ++ut) {
+          if (2 * ks + 1 < NCT) split_acc(O[2 * ks][ut], O[2 * ks + 1 < NCT ? 2 * ks + 1 : 0][ut], hh[ut], hl[ut]);
+          else split_acc(O[2 * ks][ut], hh[ut], hl[ut]);
+        }
 #pragma unroll
         for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma32(qo, hh[ut], acc[ut]);
 #pragma unroll
@@ -1284,10 +1299,10 @@ __device__ __forceinline__ void tanh_frags(const float* El, const float* Fl, int
   if constexpr (TAIL) {
     float tv[8];
     tanh_run<SEP, 4>(El + pr * SE + 32 * NS + 4 * kg, Fl + qr * SE + 32 * NS + 4 * kg, tv);
-    uint4 hi, lo;
-    split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
-    th = __builtin_bit_cast(f16x4, make_uint2(hi.x, hi.y));
-    to = __builtin_bit_cast(f16x4, make_uint2(lo.x, lo.y));
+    uint2 hi, lo;
+    split4(make_float4(tv[0], tv[1], tv[2], tv[3]), hi, lo);
+    th = __builtin_bit_cast(f16x4, hi);
+    to = __builtin_bit_cast(f16x4, lo);
   }
 }
 
@@ -1596,8 +1611,9 @@ struct TFusedGeom {
   using SM = SlotMap<T, false>;
   static constexpr int K = 2 * V, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL, SE = KP + 4;
   static constexpr int SL = SM::SL, NCOL = T * SL, NCTC = cdiv(NCOL, 16);
-  // halves per joint in LDS: two planes + 8 (a joint 4 rows down lands on other banks)
-  static constexpr int PJ = 2 * T * SL + 8;
+  // halves per joint in LDS: two planes + 8 (a joint 4 rows down lands on
+  // other banks), the 8 kept zero: the B fragment of a padding slot (ZPAD)
+  static constexpr int PJ = 2 * T * SL + 8, ZPAD = 2 * T * SL;
   static constexpr int RTG = cdiv(V, 16);  // row tiles of the whole HLJ_RM image
   static constexpr size_t stage_bytes = sizeof(TemporalStage<T, EPI, C, V>);
   static constexpr size_t p1_bytes(int rtc) {
@@ -1826,15 +1842,13 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
         float vv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) vv[r] = fmaf(al[r], fmaf(acc[r], inv, b[rt]), asv[r]);
-        uint4 hi, lo;
-        split8(make_float4(vv[0], vv[1], vv[2], vv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+        uint2 hi, lo;
+        split4(make_float4(vv[0], vv[1], vv[2], vv[3]), hi, lo);
         // frame t = 16 rt + cl: the hi plane at [t][0][col], lo at [t][1][col]
         const int t = 16 * rt + cl;
         const uint32_t off = t < T && colb < NCOL ? 2u * (uint32_t)(t * 2 * NCOL + colb) : OOB;
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_uint2(hi.x, hi.y)), ro, off, 0,
-                                              DSTD_ADJ_ST_AUX);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_uint2(lo.x, lo.y)), ro,
-                                              off + 2u * NCOL, 0, DSTD_ADJ_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hi), ro, off, 0, DSTD_ADJ_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lo), ro, off + 2u * NCOL, 0, DSTD_ADJ_ST_AUX);
       }
     }
   }
@@ -1942,6 +1956,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (tid + it * NT < T * T) asl[tid + it * NT] = av[it];
       if (tid == 0) asl[T * T] = 0.f;
       if (tid < 16 * RTC) bsl[tid] = bv;
+      if (tid < Gm::jn(RC)) *reinterpret_cast<uint4*>(planes + tid * PJ + Gm::ZPAD) = make_uint4(0u, 0u, 0u, 0u);
       const bool sep = __syncthreads_or(bad) == 0;
       // (__syncthreads_or already orders the LDS writes above: __ockl_wgred_or_i32
       // waits lgkmcnt(0) before its first barrier, checked in the ISA; round
@@ -2081,12 +2096,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
               float vv[4];
 #pragma unroll
               for (int r = 0; r < 4; ++r) vv[r] = fmaf(al[i][r], fmaf(acc[i][r], inv, b), as[i][r]);
-              uint4 hi, lo;
-              split8(make_float4(vv[0], vv[1], vv[2], vv[3]), make_float4(0.f, 0.f, 0.f, 0.f), hi, lo);
+              uint2 hi, lo;
+              split4(make_float4(vv[0], vv[1], vv[2], vv[3]), hi, lo);
               if (jv < nv && colb[i] < NCOL) {
                 _Float16* dst = planes + jv * PJ + q[i] * SL + slot0[i];
-                *reinterpret_cast<uint2*>(dst) = make_uint2(hi.x, hi.y);
-                *reinterpret_cast<uint2*>(dst + T * SL) = make_uint2(lo.x, lo.y);
+                *reinterpret_cast<uint2*>(dst) = hi;
+                *reinterpret_cast<uint2*>(dst + T * SL) = lo;
               }
             }
           }
@@ -2131,17 +2146,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       stage_temporal<T, EPI, C, V, NT>(a, st, tid, Gm::NCHUNK > 1 ? opaque_zero() : 0);
       __syncthreads();
       const int ub = n * V + v0;
+      // (a lane outside the planes -- frame past T, slot group past ng(s) --
+      // reads the joint block's zeroed 16-byte pad instead: no exec-masked
+      // read, no select)
       auto load_adj = [&](int u, int s, uint4 (&bh)[NUT], uint4 (&bo)[NUT]) {
         const _Float16* base = planes + (u - ub) * PJ;
+        // (the offsets are lane constants: recomputed per call from an opaque
+        // lane index instead of 12 registers held through the unit loop)
+        const int clz = cl + opaque_zero();
 #pragma unroll
         for (int ut = 0; ut < NUT; ++ut) {
-          const int uo = 16 * ut + cl;
+          const int uo = 16 * ut + clz;
           const bool ok = uo < T && kg < SM::ng(s);
-          const int off = ok ? uo * SL + 8 * (SM::goff(s) + kg) : 0;
-          const uint4 h = *reinterpret_cast<const uint4*>(base + off);
-          const uint4 l = *reinterpret_cast<const uint4*>(base + T * SL + off);
-          bh[ut] = ok ? h : make_uint4(0u, 0u, 0u, 0u);
-          bo[ut] = ok ? l : make_uint4(0u, 0u, 0u, 0u);
+          const int off = uo * SL + 8 * (SM::goff(s) + kg);
+          bh[ut] = *reinterpret_cast<const uint4*>(base + (ok ? off : Gm::ZPAD));
+          bo[ut] = *reinterpret_cast<const uint4*>(base + (ok ? T * SL + off : Gm::ZPAD));
         }
       };
 #ifndef DSTD_TF_SKIP_P2  // (timing experiments: phase 1 alone)

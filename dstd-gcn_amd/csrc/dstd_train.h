@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+#include "../../include/dstd_gcn_train.h"
+
 namespace dstd {
 namespace train {
 
@@ -65,8 +67,8 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s);
 //            dD[a][i][j] = sum_c F[c][(a,i)] dy[c][(a,j)]
 // agg_bwd reports how dD was produced in *nparts: 1 -- in dD; k > 1 -- as k
 // channel-chunk partials dDpart[p][B][A][NN][NN] (dDpart >= agg_parts(C) *
-// B*A*NN*NN floats; pass them to adj_bwd); 0 -- not at all (DSTD_AGG_FORM=0:
-// the caller's strided GEMM).  hipErrorNotSupported (nothing launched)
+// B*A*NN*NN floats; pass them to adj_bwd); 0 -- not at all (the a-chunk
+// kernel does not fit: the caller's strided GEMM).  hipErrorNotSupported (nothing launched)
 // outside C <= 64, NN <= 64: the caller runs the strided GEMMs instead.
 hipError_t agg_fwd(const float* F, long long fs, const float* D, float* y, long long ys, float beta, int B, int C,
                    int T, int V, int temporal, hipStream_t s);
@@ -142,6 +144,17 @@ hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStre
 // mean / rstd ([C*V], index c*V + v) are saved for the backward; running
 // stats are updated with `momentum` and the unbiased variance when
 // running_mean != null.
+// SyncBN (dstd_bn_sync, include/dstd_gcn_train.h): a collective that failed
+// surfaces as DSTD_ECOLLECTIVE through the hipError_t paths (the C entry
+// points return (int)error; -5 is outside hipError_t's own range, hence the
+// representation copy instead of a cast)
+static_assert(sizeof(hipError_t) == sizeof(int), "hipError_t carries the DSTD error code");
+inline hipError_t collective_failed() {
+  const int v = DSTD_ECOLLECTIVE;
+  hipError_t e;
+  __builtin_memcpy(&e, &v, sizeof e);
+  return e;
+}
 struct BnFwd {
   const float* x;
   const float* x2 = nullptr;
@@ -163,6 +176,11 @@ struct BnFwd {
   // updates in order; mean / rstd hold groups x C*V) -- the engine's forward
   // of a batch and of its time reversal as ONE launch sequence
   int groups = 1;
+  // cross-rank statistics (null: this rank's batch only); gath / world are
+  // set by bn_train_fwd from it: every rank's (mean, M2, count) per group
+  const dstd_bn_sync* sync = nullptr;
+  const float* gath = nullptr;
+  int world = 1;
 };
 hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s);
 
@@ -185,6 +203,10 @@ struct BnBwd {
   float* dbeta;
   int use_running = 0;  // mean / rstd are constants (eval-mode BN): du = gamma * rstd * dz
   int groups = 1;       // as BnFwd::groups (the forward's grouping)
+  // cross-rank sums (null: this rank's); gsum is set by bn_train_bwd from it:
+  // the all-reduced [groups][C*V][2] (sum dz, sum dz*xhat), then the groups' row counts
+  const dstd_bn_sync* sync = nullptr;
+  const float* gsum = nullptr;
 };
 // scratch (both directions) >= bn_scratch_floats(B, C, T, V) (any groups)
 size_t bn_scratch_floats(int B, int C, int T, int V);

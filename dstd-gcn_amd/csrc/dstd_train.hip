@@ -1307,32 +1307,60 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_stats_part(BnFwd a, int B, i
 constexpr int kBnMaxV = 64;
 constexpr int kBnMaxSplits = 16;  // bn_splits() never exceeds it
 // rows: rows per group; g: the group whose split partials merge
+// this rank's (mean, M2) of channel ch, group g: Chan merge of the split partials in split order
+__device__ __forceinline__ void bn_local_merge(int cv, int ch, int rows, int splits, const float* part, int g,
+                                               float& mean, float& m2) {
+  const int per = (rows + splits - 1) / splits;
+  part += (size_t)g * splits * cv * 2;
+  float m = 0.f;
+  for (int sp = 0; sp < splits; ++sp) {
+    const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+    m += cnt * part[((size_t)sp * cv + ch) * 2];
+  }
+  m /= rows;
+  float q = 0.f;
+  for (int sp = 0; sp < splits; ++sp) {
+    const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
+    const float* p = part + ((size_t)sp * cv + ch) * 2;
+    const float d = p[0] - m;
+    q += p[1] + cnt * d * d;
+  }
+  mean = m;
+  m2 = q;
+}
+
 __device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows, int splits, const float* part, int g,
                                                float& mean, float& rstd, bool store) {
   if (a.use_running) {
     mean = a.running_mean[ch];
     rstd = 1.f / sqrtf(a.running_var[ch] + a.eps);
   } else {
-    const int per = (rows + splits - 1) / splits;
-    part += (size_t)g * splits * a.cv * 2;
-    float m = 0.f;
-    for (int sp = 0; sp < splits; ++sp) {
-      const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
-      m += cnt * part[((size_t)sp * a.cv + ch) * 2];
+    float m, m2, n = (float)rows;
+    if (a.gath) {
+      // SyncBN: every rank's (mean, M2, count), Chan-merged in rank order
+      // (every rank computes the same values)
+      const size_t rs = (size_t)a.groups * a.cv * 3;
+      const float* q = a.gath + ((size_t)g * a.cv + ch) * 3;
+      n = 0.f;
+      m = 0.f;
+      for (int w = 0; w < a.world; ++w) {
+        n += q[w * rs + 2];
+        m += q[w * rs + 2] * q[w * rs];
+      }
+      m /= n;
+      m2 = 0.f;
+      for (int w = 0; w < a.world; ++w) {
+        const float d = q[w * rs] - m;
+        m2 += q[w * rs + 1] + q[w * rs + 2] * d * d;
+      }
+    } else {
+      bn_local_merge(a.cv, ch, rows, splits, part, g, m, m2);
     }
-    m /= rows;
-    float m2 = 0.f;
-    for (int sp = 0; sp < splits; ++sp) {
-      const int cnt = max(min(rows, (sp + 1) * per) - sp * per, 0);
-      const float* p = part + ((size_t)sp * a.cv + ch) * 2;
-      const float d = p[0] - m;
-      m2 += p[1] + cnt * d * d;
-    }
-    const float var = m2 / rows;
+    const float var = m2 / n;
     mean = m;
     rstd = 1.f / sqrtf(var + a.eps);
     if (store && a.running_mean) {
-      const float unb = rows > 1 ? m2 / (rows - 1) : var;
+      const float unb = n > 1.f ? m2 / (n - 1.f) : var;
       a.running_mean[ch] = (1.f - a.momentum) * a.running_mean[ch] + a.momentum * m;
       a.running_var[ch] = (1.f - a.momentum) * a.running_var[ch] + a.momentum * unb;
     }
@@ -1341,6 +1369,19 @@ __device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows,
     a.mean[g * a.cv + ch] = mean;
     a.rstd[g * a.cv + ch] = rstd;
   }
+}
+
+// SyncBN: this rank's (mean, M2, count) per (group, channel) into its slot of
+// the gather buffer (dst = buf + rank * groups * C*V * 3)
+__global__ __launch_bounds__(256) void k_bn_local_stats(int cv, int rows, int splits, const float* part, float* dst) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x, g = blockIdx.y;
+  if (ch >= cv) return;
+  float m, m2;
+  bn_local_merge(cv, ch, rows, splits, part, g, m, m2);
+  float* d = dst + ((size_t)g * cv + ch) * 3;
+  d[0] = m;
+  d[1] = m2;
+  d[2] = (float)rows;
 }
 
 // workgroup (c, y) covers samples [ns*y, ns*y + ns) (one group: ns divides B/groups)
@@ -1446,6 +1487,23 @@ __global__ __launch_bounds__(kRedThreads) void k_bn_bwd_part(BnBwd a, int B, int
   }
 }
 
+// SyncBN: this rank's (sum dz, sum dz*xhat) per (group, channel), split order,
+// then the groups' row counts -- the buffer the all-reduce sums
+__global__ __launch_bounds__(256) void k_bn_bwd_local_sums(int cv, int groups, int splits, int rows, const float* part,
+                                                           float* dst) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x, g = blockIdx.y;
+  if (ch == 0) dst[(size_t)groups * cv * 2 + g] = (float)rows;
+  if (ch >= cv) return;
+  float sd = 0.f, sdx = 0.f;
+  for (int sp = 0; sp < splits; ++sp) {
+    const float* p = part + ((size_t)(g * splits + sp) * cv + ch) * 2;
+    sd += p[0];
+    sdx += p[1];
+  }
+  dst[((size_t)g * cv + ch) * 2] = sd;
+  dst[((size_t)g * cv + ch) * 2 + 1] = sdx;
+}
+
 // Merge + apply of the backward in one launch: workgroup (c, n) sums the
 // split partials of its V channels (split order), the n == 0 one accumulates
 // dgamma / dbeta (and workgroup (0, 0) the PReLU slope: the partials in the
@@ -1479,8 +1537,10 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int
           sdx += pv[sp].y;
         }
       if (gg == grp) {
-        sdl[tid] = sd;
-        sxl[tid] = sdx;
+        // SyncBN: the input gradient takes every rank's sums; dgamma / dbeta
+        // (below) stay this rank's
+        sdl[tid] = a.gsum ? a.gsum[((size_t)grp * CV + ch) * 2] : sd;
+        sxl[tid] = a.gsum ? a.gsum[((size_t)grp * CV + ch) * 2 + 1] : sdx;
       }
       tb += sd;
       tg += sdx;
@@ -1498,7 +1558,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int
   }
   __syncthreads();
   const float w = a.prelu ? *a.prelu : 0.f;
-  const float inv = 1.f / (Bg * T);
+  const float inv = 1.f / (a.gsum ? a.gsum[(size_t)a.groups * CV * 2 + grp] : (float)(Bg * T));
   constexpr int EB = 4;  // elements per thread per batch, loads issued first
   for (int k = 0; k < ns; ++k)
   for (int e0 = tid; e0 < T * V; e0 += EB * 256) {
@@ -1677,14 +1737,6 @@ constexpr int kMaxSplit96 = 2 * kMaxSplit;
 size_t gemm_scratch_floats(int M, int N) { return (size_t)kMaxSplit96 * M * N; }
 
 namespace {
-// DSTD_GEMM_GENERIC=1: every GEMM on k_gemm (A/B of the skinny kernel)
-bool gemm_generic() {
-  static const bool v = [] {
-    const char* e = getenv("DSTD_GEMM_GENERIC");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
 template <class K, class... Args>
 void sk_go(K kern, int grid, size_t lds, hipStream_t s, Args... args) {
   static bool attr = false;  // (per instantiation) allow > 64 KB of dynamic LDS
@@ -1693,13 +1745,6 @@ void sk_go(K kern, int grid, size_t lds, hipStream_t s, Args... args) {
     attr = true;
   }
   kern<<<grid, 256, lds, s>>>(args...);
-}
-bool gemm_96() {
-  static const bool v = [] {
-    const char* e = getenv("DSTD_GEMM_96");
-    return !(e && atoi(e) == 0);
-  }();
-  return v;
 }
 // hipErrorNotSupported: not a skinny shape (nothing launched)
 hipError_t gemm_skinny(const Gemm& g, float* scratch, hipStream_t s) {
@@ -1731,16 +1776,15 @@ hipError_t gemm_skinny(const Gemm& g, float* scratch, hipStream_t s) {
 hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.d_out && (g.reduce || !g.d_A || !g.d_alpha)) return hipErrorInvalidValue;
-  if (!gemm_generic()) {
+  {
     const hipError_t e = gemm_skinny(g, scratch, s);
     if (e != hipErrorNotSupported) return e;
   }
   // tile edge per operand: 32 / 64, and 96 for a reduce GEMM's 65..96 extent
   // (the packed conv's [W | b] gradient is 68 x 65: one 96 x 96 tile instead
   // of four 64 x 64 ones, each operand read once instead of twice;
-  // B=32 training step 5.95 -> 5.69 ms, profiles/r03y_gemm96_ab.txt;
-  // DSTD_GEMM_96=0 keeps 64-wide tiles, A/B)
-  const bool t96 = g.reduce && scratch && gemm_96();
+  // B=32 training step 5.95 -> 5.69 ms, profiles/r03y_gemm96_ab.txt)
+  const bool t96 = g.reduce && scratch;
   auto edge = [&](int x) { return x <= 32 ? 32 : (x <= 64 || !t96 || x > 96) ? 64 : 96; };
   const int TM = edge(g.M), TN = edge(g.N);
   const int tiles = cdiv(g.M, TM) * cdiv(g.N, TN);
@@ -1789,25 +1833,6 @@ size_t agg_lds(bool bwd, bool df, int C, int NN, int ac, int& QP, int& RK, int& 
   agg_tile(NN, RK, P);
   return sizeof(float) * ((size_t)(bwd ? 2 : 1) * C * QP + (df ? (size_t)ac * RK * P : 0));
 }
-int env_int(const char* name) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : 0;
-}
-int agg_env_ac() {
-  static const int v = env_int("DSTD_AGG_AC");
-  return v;
-}
-// DSTD_AGG_FORM (A/B of the aggregation kernels): 2 (default) fwd and dF on
-// the channel-chunk kernels, dD as per-chunk partials of the fused backward;
-// 1 every product on the a-chunk kernel; 0 channel-chunk fwd / dF, dD left to
-// the caller's strided GEMM; 3 channel-chunk fwd / dF, a-chunk dD
-int agg_form() {
-  static const int v = [] {
-    const char* e = getenv("DSTD_AGG_FORM");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
 template <class K>
 void agg_go(K kern, dim3 grid, dim3 block, size_t lds, const AggArgs& g, hipStream_t s) {
   static bool attr = false;  // (per instantiation) allow > 64 KB of dynamic LDS
@@ -1824,7 +1849,6 @@ bool agg_ok(const AggArgs& g) {
 hipError_t agg_launch_a(bool bwd, bool df, AggArgs g, int B, int temporal, hipStream_t s) {
   if (!agg_ok(g)) return hipErrorNotSupported;
   int ac = std::min(g.A, 4);
-  if (agg_env_ac() > 0) ac = std::min(std::min(g.A, agg_env_ac()), 8);  // (FastDiv: slab sizes < 2^16)
   size_t lds = agg_lds(bwd, df, g.C, g.NN, ac, g.QP, g.RK, g.P);
   while (ac > 1 && lds > kAggLds) lds = agg_lds(bwd, df, g.C, g.NN, --ac, g.QP, g.RK, g.P);
   if (lds > 160 * 1024) return hipErrorNotSupported;
@@ -1896,7 +1920,7 @@ hipError_t agg_fwd(const float* F, long long fs, const float* D, float* y, long 
                    int T, int V, int temporal, hipStream_t s) {
   AggArgs g = agg_geom(C, T, V, temporal);
   g.X = F, g.xs = fs, g.Dm = D, g.O = y, g.os = ys, g.beta = beta;
-  return agg_form() == 1 ? agg_launch_a(false, true, g, B, temporal, s) : agg_launch_c(false, g, B, temporal, s);
+  return agg_launch_c(false, g, B, temporal, s);
 }
 
 hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys, const float* D, float* dF,
@@ -1906,14 +1930,12 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
   g.X = F, g.xs = fs, g.Y0 = dy, g.y0s = dys, g.Dm = D, g.O = dF, g.os = dfs, g.dD = dD;
   *nparts = 0;
   if (!agg_ok(g)) return hipErrorNotSupported;
-  const int form = agg_form(), cch = cdiv(C, 16);
+  // dF on the channel-chunk backward kernel, dD as its per-chunk partials
+  // (dDpart; one chunk: dD itself); else dF on the channel-chunk kernel and
+  // dD on the a-chunk kernel
+  const int cch = cdiv(C, 16);
   *nparts = 1;
-  if (form == 1) {
-    const hipError_t e = agg_launch_a(true, true, g, B, temporal, s);
-    if (e == hipErrorNotSupported) *nparts = 0;
-    return e;
-  }
-  if (form == 2 && (cch == 1 || dDpart)) {
+  if (cch == 1 || dDpart) {
     if (cch > 1) g.dD = dDpart, *nparts = cch;
     g.B = B;
     agg_tile(g.NN, g.RK, g.P);
@@ -1946,10 +1968,6 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
   if (e != hipSuccess) {
     *nparts = 0;  // (NotSupported: the caller runs both products)
     return e;
-  }
-  if (form == 0) {
-    *nparts = 0;  // dD: the caller's
-    return hipSuccess;
   }
   const hipError_t ed = agg_launch_a(true, false, g, B, temporal, s);  // dD
   if (ed == hipErrorNotSupported) *nparts = 0;  // (dF is done; the caller recomputes both)
@@ -2075,6 +2093,17 @@ hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scrat
   b.cv = C * V;
   if (!a.use_running)
     k_bn_stats_part<<<dim3(C, splits * a.groups), kRedThreads, 0, s>>>(b, B, C, T, V, splits, scratch);
+  if (a.sync && !a.use_running) {  // SyncBN: gather every rank's statistics
+    const dstd_bn_sync& y = *a.sync;
+    const long long n = (long long)a.groups * b.cv * 3;
+    k_bn_local_stats<<<dim3(cdiv(b.cv, 256), a.groups), 256, 0, s>>>(b.cv, (B / a.groups) * T, splits, scratch,
+                                                                     y.buf + (size_t)y.rank * n);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (y.fn(y.ctx, DSTD_COLL_ALLGATHER, y.buf, n, (void*)s) != 0) return collective_failed();
+    b.gath = y.buf;
+    b.world = y.world;
+  }
   const int ns = bn_apply_samples(B / a.groups, B, C);
   k_bn_apply_merged<<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, scratch, ns);
   return hipGetLastError();
@@ -2087,8 +2116,20 @@ hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scrat
   float* part = scratch;
   float* wpart = part + (size_t)a.groups * splits * C * V * 2;
   k_bn_bwd_part<<<dim3(C, splits * a.groups), kRedThreads, 0, s>>>(a, B, C, T, V, splits, part, wpart);
+  BnBwd b = a;
+  if (a.sync && !a.use_running) {  // SyncBN: sum every rank's sums and row counts
+    const dstd_bn_sync& y = *a.sync;
+    const int cv = C * V;
+    k_bn_bwd_local_sums<<<dim3(cdiv(cv, 256), a.groups), 256, 0, s>>>(cv, a.groups, splits, (B / a.groups) * T, part,
+                                                                      y.buf);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (y.fn(y.ctx, DSTD_COLL_ALLREDUCE_SUM, y.buf, (long long)a.groups * cv * 2 + a.groups, (void*)s) != 0)
+      return collective_failed();
+    b.gsum = y.buf;
+  }
   const int ns = bn_apply_samples(B / a.groups, B, C);
-  k_bn_bwd_apply_merged<<<dim3(C, B / ns), 256, 0, s>>>(a, B, C, T, V, splits, part, wpart, dprelu, ns);
+  k_bn_bwd_apply_merged<<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, part, wpart, dprelu, ns);
   return hipGetLastError();
 }
 

@@ -89,15 +89,8 @@ bool model_ok(const dstd_model_params* p) {
 // ---------------------------------------------------------------------------
 // one DSTDGC
 // ---------------------------------------------------------------------------
-// The aggregation products run on the slab kernels (agg_fwd / agg_bwd);
-// DSTD_TRAIN_AGG_GEMM=1 routes them through the strided GEMMs instead (A/B).
-bool use_agg() {
-  static const bool v = [] {
-    const char* e = getenv("DSTD_TRAIN_AGG_GEMM");
-    return !(e && atoi(e) != 0);
-  }();
-  return v;
-}
+// The aggregation products run on the slab kernels (agg_fwd / agg_bwd); the
+// strided GEMMs take the shapes those do not support.
 struct OpGeom {
   int B, cin, cout, T, V, TV;
   int R;  // red_channels: P / Q channels per op (2 in every block of the reference)
@@ -237,7 +230,7 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   e.d_W = W0;
   e.d_R = R0;
   DSTD_TRYH(gemm(e, nullptr, s));
-  if (use_agg()) {  // y[c][(a,j)] = sum_i F[c][(a,i)] D[a][i][j]     :87 / :93
+  {  // y[c][(a,j)] = sum_i F[c][(a,i)] D[a][i][j]     :87 / :93
     const hipError_t e = agg_fwd(sv.G, (long long)g.CG() * g.TV, sv.D, y, (long long)g.cout * g.TV, beta_y, g.B,
                                  g.cout, g.T, g.V, g.temporal, s);
     if (e != hipErrorNotSupported) return e;
@@ -258,10 +251,8 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
                   hipStream_t s, float dx_beta = 1.f, int assign_dA = 0) {
   const long long ldG = (long long)g.CG() * g.TV;
   // dF -> rows [0, cout) of dG; dD in place or as channel-chunk partials
-  hipError_t ae = hipErrorNotSupported;
   int nparts = 0;
-  if (use_agg())
-    ae = agg_bwd(sv.G, ldG, dy, (long long)g.cout * g.TV, sv.D, ws.dG, ldG, ws.dD, g.B, g.cout, g.T, g.V,
+  const hipError_t ae = agg_bwd(sv.G, ldG, dy, (long long)g.cout * g.TV, sv.D, ws.dG, ldG, ws.dD, g.B, g.cout, g.T, g.V,
                  g.temporal, s, ws.dDp, &nparts);
   if (ae != hipErrorNotSupported) DSTD_TRYH(ae);
   if (ae == hipErrorNotSupported) {
@@ -373,7 +364,7 @@ void carve_block_ws(Carver& cv, BlockWs& w, int B, int T, int V, std::initialize
 }
 
 hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum, float* y,
-                     const BlockSaved& S, hipStream_t s, int run = 0) {
+                     const BlockSaved& S, hipStream_t s, int run = 0, const dstd_bn_sync* sync = nullptr) {
   const int cin = p->cin, cout = p->cout, TV = T * V;
   const bool res = cin != cout;
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
@@ -401,7 +392,8 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.mean = S.rmean;
     rb.rstd = S.rrstd;
     rb.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
-  rb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+    rb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+    rb.sync = sync;
     DSTD_TRYH(bn_train_fwd(rb, B, cout, T, V, S.red, s));
     r = S.r;
   }
@@ -421,6 +413,7 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.rstd = S.rstd;
   bb.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
   bb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+  bb.sync = sync;
   DSTD_TRYH(bn_train_fwd(bb, B, cout, T, V, S.red, s));
   return op_fwd(gt, S.h, &p->conv_t, p->A_t, nullptr, p->R_t, p->alpha_tm, y, 0.f, S.op[2], s);  // :156-162
 }
@@ -430,7 +423,8 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
 // encoders' identity path of the model backward).
 hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, int V, const BlockSaved& S,
                      const float* dy, float* dx, const dstd_block_grads* g, const BlockWs& W, hipStream_t s,
-                     int run = 0, bool dx_init = false, const float* dx_extra = nullptr) {
+                     int run = 0, bool dx_init = false, const float* dx_extra = nullptr,
+                     const dstd_bn_sync* sync = nullptr) {
   const int cin = p->cin, cout = p->cout, TV = T * V;
   const bool res = cin != cout;
   const size_t act = (size_t)B * cout * TV;
@@ -452,6 +446,7 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.dbeta = g->bn.bias;
   bb.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
   bb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+  bb.sync = sync;
   DSTD_TRYH(bn_train_bwd(bb, B, cout, T, V, W.op.red, g->prelu, s));
   if (res) {
     BnBwd rb;
@@ -464,7 +459,8 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.dgamma = g->res_bn.weight;
     rb.dbeta = g->res_bn.bias;
     rb.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
-  rb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+    rb.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+    rb.sync = sync;
     DSTD_TRYH(bn_train_bwd(rb, B, cout, T, V, W.op.red, nullptr, s));
     if (dx_extra) return hipErrorInvalidValue;
     DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, W.op.red, s,
@@ -687,11 +683,30 @@ size_t dstd_model_train_workspace_bytes(int B, int T, int V, int num_feature, in
   return cv.off + 256;
 }
 
+size_t dstd_bn_sync_buffer_floats(int world, int num_feature, int V) {
+  // forward gather: world x (<= 2 groups) x C*V x (mean, M2, count); backward:
+  // 2 x C*V x 2 sums + 2 counts
+  const size_t cv = (size_t)std::max(num_feature, 6) * V;
+  return std::max((size_t)std::max(world, 1) * 2 * cv * 3, 2 * cv * 2 + 2);
+}
+
+static bool sync_ok(const dstd_bn_sync* y, int C, int V) {
+  return !y || (y->fn && y->buf && y->world >= 1 && y->rank >= 0 && y->rank < y->world &&
+                y->buf_floats >= (long long)dstd_bn_sync_buffer_floats(y->world, C, V));
+}
+
 int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, float momentum, float dropout_p,
                             unsigned long long seed, float* y, void* saved, size_t saved_bytes, void* stream,
                             unsigned flags) {
+  return dstd_model_train_fwd_sync(p, x, B, momentum, dropout_p, seed, y, saved, saved_bytes, stream, flags, nullptr);
+}
+
+int dstd_model_train_fwd_sync(const dstd_model_params* p, const float* x, int B, float momentum, float dropout_p,
+                              unsigned long long seed, float* y, void* saved, size_t saved_bytes, void* stream,
+                              unsigned flags, const dstd_bn_sync* sync) {
   StreamDeviceGuard dev_guard_(stream, x);
   if (!model_ok(p) || !x || !y || !saved || !(dropout_p >= 0.f && dropout_p < 1.f)) return DSTD_EINVAL;
+  if (!sync_ok(sync, p->num_feature, p->V)) return DSTD_EINVAL;
   if (flags & ~kModelTrainFlags) return DSTD_EINVAL;
   if ((flags & DSTD_TRAIN_SEED_DEVICE) && dropout_p > 0.f && !seed) return DSTD_EINVAL;
   if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
@@ -707,7 +722,7 @@ int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, f
   carve_model_saved(cv, S, B, T, V, C, L);
   const size_t act = (size_t)B * C * T * V;
   DSTD_TRY(prep_nctv(x, B, T, V, 3, S.X0, s));                                   // :298-303
-  DSTD_TRY(block_fwd(&p->st_in, S.X0, B, T, V, momentum, S.y0, S.st_in, s, run));  // :305
+  DSTD_TRY(block_fwd(&p->st_in, S.X0, B, T, V, momentum, S.y0, S.st_in, s, run, sync));  // :305
   BnFwd b0;                                                                      // :306-308
   b0.x = S.y0;
   b0.gamma = p->bn_in.weight;
@@ -723,10 +738,11 @@ int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, f
   b0.rstd = S.r0;
   b0.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
   b0.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+  b0.sync = sync;
   DSTD_TRY(bn_train_fwd(b0, B, C, T, V, S.red, s));
   if (dropout_p > 0.f) DSTD_TRY(dropout(S.hp0, S.h[0], act, dropout_p, seed, s, (flags & DSTD_TRAIN_SEED_DEVICE) != 0));  // do_in
   for (int i = 0; i < L; ++i) {                                                  // :310-311
-    DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s, run));
+    DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s, run, sync));
     BnFwd be;  // BN(block(h) + h) -> PReLU  (:278-285, Identity residual :247-248)
     be.x = S.yb[i];
     be.x2 = S.h[i];
@@ -742,10 +758,11 @@ int dstd_model_train_fwd_ex(const dstd_model_params* p, const float* x, int B, f
     be.mean = S.me[i];
     be.rstd = S.re[i];
     be.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
-  be.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+    be.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+    be.sync = sync;
     DSTD_TRY(bn_train_fwd(be, B, C, T, V, S.red, s));
   }
-  DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s, run));  // :313
+  DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s, run, sync));  // :313
   DSTD_TRY(out_ntvc(S.o, x, B, T, V, 3, y, s));                                       // :314-315
   return DSTD_OK;
 }
@@ -759,9 +776,18 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
                             unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
                             const dstd_model_grads* g, float* dx, void* workspace, size_t workspace_bytes,
                             void* stream, unsigned flags) {
+  return dstd_model_train_bwd_sync(p, x, B, dropout_p, seed, saved, saved_bytes, dy, g, dx, workspace,
+                                   workspace_bytes, stream, flags, nullptr);
+}
+
+int dstd_model_train_bwd_sync(const dstd_model_params* p, const float* x, int B, float dropout_p,
+                              unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
+                              const dstd_model_grads* g, float* dx, void* workspace, size_t workspace_bytes,
+                              void* stream, unsigned flags, const dstd_bn_sync* sync) {
   StreamDeviceGuard dev_guard_(stream, x);
   if (!model_ok(p) || !g || !x || !dy || !saved || !workspace || !(dropout_p >= 0.f && dropout_p < 1.f))
     return DSTD_EINVAL;
+  if (!sync_ok(sync, p->num_feature, p->V)) return DSTD_EINVAL;
   if (flags & ~kModelTrainFlags) return DSTD_EINVAL;
   if ((flags & DSTD_TRAIN_SEED_DEVICE) && dropout_p > 0.f && !seed) return DSTD_EINVAL;
   if ((flags & DSTD_TRAIN_PAIRED) && (B & 1)) return DSTD_EINVAL;
@@ -787,7 +813,8 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
   DSTD_TRY(out_ntvc_bwd(dy, B, T, V, 3, W.dO, s));
   float* dha = W.dha;
   float* dhb = W.dhb;
-  DSTD_TRY(block_bwd(&p->st_out, S.h[L], B, T, V, S.st_out, W.dO, dha, &g->st_out, W.blk, s, run, true));
+  DSTD_TRY(block_bwd(&p->st_out, S.h[L], B, T, V, S.st_out, W.dO, dha, &g->st_out, W.blk, s, run, true, nullptr,
+                     sync));
   for (int i = L - 1; i >= 0; --i) {
     BnBwd be;
     be.x = S.yb[i];
@@ -802,10 +829,12 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
     be.dgamma = g->enc_bn[i].weight;
     be.dbeta = g->enc_bn[i].bias;
     be.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
-  be.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+    be.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+    be.sync = sync;
     DSTD_TRY(bn_train_bwd(be, B, C, T, V, W.blk.op.red, g->enc_prelu[i], s));
     // u = block(h) + h: dh = du (identity path) + block backward
-    DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s, run, true, W.du));
+    DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s, run, true, W.du,
+                       sync));
     std::swap(dha, dhb);
   }
   if (dropout_p > 0.f) DSTD_TRY(dropout(dha, dha, act, dropout_p, seed, s, (flags & DSTD_TRAIN_SEED_DEVICE) != 0));
@@ -822,8 +851,10 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
   b0.dbeta = g->bn_in.bias;
   b0.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
   b0.groups = (run & DSTD_TRAIN_PAIRED) ? 2 : 1;
+  b0.sync = sync;
   DSTD_TRY(bn_train_bwd(b0, B, C, T, V, W.blk.op.red, g->prelu, s));
-  DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, dx ? W.dX0 : nullptr, &g->st_in, W.blk, s, run, true));
+  DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, dx ? W.dX0 : nullptr, &g->st_in, W.blk, s, run, true,
+                     nullptr, sync));
   if (dx) DSTD_TRY(prep_nctv_bwd(W.dX0, dy, B, T, V, 3, dx, s));  // :298-303, 315
   return DSTD_OK;
 }

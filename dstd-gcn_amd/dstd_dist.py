@@ -17,10 +17,20 @@ forward.  The only collectives are outside it:
 Training (config 5) has one real exchange per step: the data-parallel
 gradient average, ``allreduce_grads`` -- one flat bucket (~0.75 MB for the
 3DPW model), a single ring all-reduce over xGMI.  Train-mode BatchNorm keeps
-per-rank batch statistics (the DDP default).
+per-rank batch statistics (the DDP default) unless ``convert_sync_batchnorm``
+opts the model into cross-rank BatchNorm (SURVEY §8(e) SyncBN: every BatchNorm
+of the native train forward normalises with all ranks' statistics -- one
+all-gather of (mean, M2, count) per BatchNorm forward, one all-reduce of
+(sum dz, sum dz*xhat) per BatchNorm backward, issued by the library through
+``BnSync``'s collective on the call's stream).
 """
+import ctypes
+import sys
+
 import torch
 import torch.distributed as dist
+
+import dstd_native as native
 
 
 def shard_bounds(n, world, rank):
@@ -121,3 +131,66 @@ def allreduce_grads(params, group=None):
     for g in grads:
         g.copy_(flat[off:off + g.numel()].view_as(g))
         off += g.numel()
+
+
+class BnSync:
+    """The dstd_bn_sync of one model (include/dstd_gcn_train.h): this rank's
+    place in ``group``, a device buffer sized by dstd_bn_sync_buffer_floats,
+    and the collective the library calls at every BatchNorm -- an all-gather
+    of the per-rank statistics (forward) or an all-reduce of the gradient
+    sums (backward) over torch.distributed on the current stream (RCCL / NCCL
+    in place on the device; gloo through host copies)."""
+
+    def __init__(self, num_feature, V, device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        n = native.lib().dstd_bn_sync_buffer_floats(self.world, num_feature, V)
+        self.buf = torch.zeros(n, dtype=torch.float32, device=device)
+        self.host = dist.get_backend(group) == "gloo" and self.buf.is_cuda
+        self._fn = native.COLLECTIVE_FN(self._collective)  # kept alive with the struct
+        self._s = native.BnSyncStruct(self.world, self.rank, self._fn, None, self.buf.data_ptr(), n)
+        self.calls = 0
+
+    def struct_ref(self):
+        return ctypes.byref(self._s)
+
+    def _collective(self, ctx, op, buf, count, stream):
+        try:
+            if buf != self.buf.data_ptr():
+                raise RuntimeError("dstd_bn_sync: foreign buffer")
+            self.calls += 1
+            if op == native.COLL_ALLGATHER:
+                out = self.buf[:count * self.world]
+                mine = out[self.rank * count:(self.rank + 1) * count].clone()
+                if self.host:
+                    o = torch.empty(out.shape, dtype=out.dtype)
+                    dist.all_gather_into_tensor(o, mine.cpu(), group=self.group)
+                    out.copy_(o)
+                else:
+                    dist.all_gather_into_tensor(out, mine, group=self.group)
+            elif op == native.COLL_ALLREDUCE_SUM:
+                t = self.buf[:count]
+                if self.host:
+                    c = t.cpu()
+                    dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group)
+                    t.copy_(c)
+                else:
+                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            else:
+                raise ValueError(f"dstd_bn_sync: unknown collective {op}")
+            return 0
+        except Exception as e:  # the library returns DSTD_ECOLLECTIVE
+            print(f"dstd_bn_sync collective failed: {e!r}", file=sys.stderr)
+            return 1
+
+
+def convert_sync_batchnorm(model, group=None):
+    """Opt ``model`` (a DSTDGCN on its device, in a process group) into
+    cross-rank BatchNorm for its native train-mode forward and backward --
+    torch.nn.SyncBatchNorm.convert_sync_batchnorm's semantics without
+    replacing modules (the state-dict schema is unchanged).  Returns the
+    model; ``model._dstd_bn_sync = None`` goes back to per-rank statistics."""
+    dev = next(model.parameters()).device
+    model._dstd_bn_sync = BnSync(model.num_feature, model.joints_to_consider, dev, group)
+    return model

@@ -73,6 +73,17 @@ class ModelGrads(ctypes.Structure):
                 ("enc_prelu", ctypes.c_void_p * MAX_LAYERS), ("st_out", BlockGrads)]
 
 
+# include/dstd_gcn_train.h dstd_bn_sync: cross-rank BatchNorm (dstd_dist.BnSync)
+COLL_ALLGATHER, COLL_ALLREDUCE_SUM = 0, 1
+COLLECTIVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong,
+                                 ctypes.c_void_p)
+
+
+class BnSyncStruct(ctypes.Structure):
+    _fields_ = [("world", ctypes.c_int), ("rank", ctypes.c_int), ("fn", COLLECTIVE_FN), ("ctx", ctypes.c_void_p),
+                ("buf", ctypes.c_void_p), ("buf_floats", ctypes.c_longlong)]
+
+
 TRAIN_RUNNING_STATS = 1  # include/dstd_gcn_train.h DSTD_TRAIN_RUNNING_STATS
 TRAIN_PAIRED = 2  # DSTD_TRAIN_PAIRED: two BatchNorm batches of B/2 (a forward pair)
 TRAIN_SEED_DEVICE = 4  # DSTD_TRAIN_SEED_DEVICE: the dropout seed is read from device memory
@@ -192,6 +203,12 @@ def lib():
         L.dstd_model_train_bwd_ex.restype = ci
         L.dstd_model_train_bwd_ex.argtypes = [ctypes.POINTER(ModelParams), vp, ci, f32, u64, vp, sz, vp,
                                               ctypes.POINTER(ModelGrads), vp, vp, sz, vp, uf]
+        L.dstd_bn_sync_buffer_floats.restype = sz
+        L.dstd_bn_sync_buffer_floats.argtypes = [ci, ci, ci]
+        L.dstd_model_train_fwd_sync.restype = ci
+        L.dstd_model_train_fwd_sync.argtypes = L.dstd_model_train_fwd_ex.argtypes + [ctypes.POINTER(BnSyncStruct)]
+        L.dstd_model_train_bwd_sync.restype = ci
+        L.dstd_model_train_bwd_sync.argtypes = L.dstd_model_train_bwd_ex.argtypes + [ctypes.POINTER(BnSyncStruct)]
         L.dstd_loss_workspace_bytes.restype = sz
         L.dstd_loss_workspace_bytes.argtypes = []
         L.dstd_mpjpe_fwd.restype = ci
@@ -228,7 +245,8 @@ TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_b
                  "dstd_loss_workspace_bytes", "dstd_mpjpe_fwd", "dstd_mpjpe_bwd", "dstd_frame_mpjpe",
                  "dstd_block_train_fwd_ex", "dstd_block_train_bwd_ex", "dstd_model_train_fwd_ex",
                  "dstd_model_train_bwd_ex", "dstd_dstdgc_train_saved_bytes_r",
-                 "dstd_dstdgc_train_workspace_bytes_r", "dstd_dstdgc_train_fwd_r", "dstd_dstdgc_train_bwd_r")
+                 "dstd_dstdgc_train_workspace_bytes_r", "dstd_dstdgc_train_fwd_r", "dstd_dstdgc_train_bwd_r",
+                 "dstd_bn_sync_buffer_floats", "dstd_model_train_fwd_sync", "dstd_model_train_bwd_sync")
 AUX_EXPORTS = ("dstd_ctg_workspace_bytes", "dstd_ctg_fwd", "dstd_ctg_bwd", "dstd_conv2d_workspace_bytes",
                "dstd_conv2d_fwd", "dstd_conv2d_bwd")
 

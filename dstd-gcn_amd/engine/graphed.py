@@ -25,6 +25,9 @@ is exactly eager step k.
 """
 import torch
 
+import dstd_native as native
+from model.dstdgcn import invalidate_native_cache
+
 
 def _opt_state_tensors(optimizer):
     out = []
@@ -57,9 +60,15 @@ class GraphedStep:
                 step_fn(*self.static)
         torch.cuda.current_stream(dev).wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        cap = torch.cuda.Stream(device=dev)  # a stream of its own: its workspace is private to this graph
+        with torch.cuda.graph(self.graph, stream=cap):
             self.outputs = step_fn(*self.static)
         torch.cuda.synchronize(dev)
+        # the capture's native workspace lives in the graph's memory pool: keep
+        # it with the graph and out of the eager cache, where a later, larger
+        # claim on the same stream would free it under the graph
+        self._workspace = native._ws_cache.pop((str(dev), cap.cuda_stream), (None, None))[0]
+        self.model = model
         # undo the warm-up: replay 1 is step 1
         with torch.no_grad():
             for t, s in zip(list(model.parameters()) + list(model.buffers()), snap_model):
@@ -79,4 +88,8 @@ class GraphedStep:
         for dst, src in zip(self.static, args):
             dst.copy_(src, non_blocking=True)
         self.graph.replay()
+        # the replay updated parameters and BatchNorm buffers on the device
+        # without moving their version counters: the next eval forward must
+        # not reuse constants folded from the previous weights
+        invalidate_native_cache(self.model)
         return self.outputs

@@ -301,6 +301,11 @@ class PredictionEngine:
         index_cache = {}
         rank, world = _world()
         presharded = isinstance(getattr(test_loader, "sampler", None), torch.utils.data.DistributedSampler)
+        # a presharded loader interleaves samples over the ranks (and pads with
+        # duplicates): the saved results are put back in dataset order by the
+        # sampler's per-sample indices
+        sample_idx = np.asarray(list(iter(test_loader.sampler))) if presharded and save_path is not None else None
+        seen = 0
         self.model.eval()
         with torch.no_grad():
             for i, (inputs, _, _, all_seqs) in enumerate(test_loader):
@@ -330,7 +335,9 @@ class PredictionEngine:
                 if save_results is not None:
                     pred = self._fill_pred(all_seqs, outputs, used_pos, joint_src, t_out0)[:, input_n:]
                     targ = all_seqs.view(n, seq_len, -1, 3)[:, input_n:]
-                    save_results.append((i, rank, pred.cpu().numpy(), targ.cpu().numpy()))
+                    idx = sample_idx[seen:seen + n] if sample_idx is not None else None
+                    save_results.append((i, rank, pred.cpu().numpy(), targ.cpu().numpy(), idx))
+                seen += n
             if action is None:
                 action = "NA"
             if world > 1:  # per-frame sums and sample counts of every rank
@@ -347,10 +354,12 @@ class PredictionEngine:
     @staticmethod
     def _save_results(save_path, parts, rank, world):
         """np.savez of every batch's (result, target) (:405-409).  With several
-        ranks the per-rank parts are gathered to rank 0, put back in loader
-        order (batch index, then rank: round-robin sharding gives each batch
-        index to one rank) and written by rank 0 alone; a rank without batches
-        contributes nothing."""
+        ranks the per-rank parts are gathered to rank 0 and written by rank 0
+        alone, in the single-process order: the engine's own round-robin batch
+        sharding is undone by (batch index, rank); a presharded loader
+        (DistributedSampler, samples interleaved over the ranks and padded with
+        duplicates) by the sampler's per-sample dataset indices, each index
+        kept once.  A rank without batches contributes nothing."""
         if world > 1:
             gathered = [None] * world
             dist.all_gather_object(gathered, parts)
@@ -359,8 +368,13 @@ class PredictionEngine:
             parts = sorted((p for g in gathered for p in g), key=lambda p: (p[0], p[1]))
         if not parts:
             return
-        np.savez(save_path + ".npz", target=np.concatenate([p[3] for p in parts], 0),
-                 result=np.concatenate([p[2] for p in parts], 0))
+        result = np.concatenate([p[2] for p in parts], 0)
+        target = np.concatenate([p[3] for p in parts], 0)
+        if parts[0][4] is not None:
+            idx = np.concatenate([p[4] for p in parts], 0)
+            _, first = np.unique(idx, return_index=True)  # sorted by dataset index, duplicates dropped
+            result, target = result[first], target[first]
+        np.savez(save_path + ".npz", target=target, result=result)
 
     def _frame_metric(self, all_seqs, outputs, t_out0, used_pos, joint_src, frames, sums):
         """sums[k] += sum over the batch of the MPJPE at frames[k] (:366-404),

@@ -31,6 +31,7 @@ with frozen parameters and input) eval runs the fused inference kernels.
 """
 import itertools
 import operator
+import random
 import math
 import weakref
 from typing import List, Tuple
@@ -144,6 +145,28 @@ def _bump_epoch(*args, **kwargs):
 for _reg in ("register_module_parameter_registration_hook", "register_module_buffer_registration_hook",
              "register_module_module_registration_hook"):
     getattr(torch.nn.modules.module, _reg)(_bump_epoch)
+
+
+def _hook_swap_tensor():
+    """torch.func.functional_call and torch.nn.utils.stateless swap tensors
+    into ``module._parameters`` / ``_buffers`` directly (the accessor's
+    swap_tensor), past the registration hooks: bump the epoch there too, so a
+    cached walk never hands the native kernels the module's own tensors in
+    place of the swapped-in ones."""
+    import torch.nn.utils._named_member_accessor as acc
+    orig = acc.swap_tensor
+    if getattr(orig, "_dstd_epoch", False):
+        return
+
+    def swap_tensor(*args, **kwargs):
+        _STRUCT_EPOCH[0] += 1
+        return orig(*args, **kwargs)
+
+    swap_tensor._dstd_epoch = True
+    acc.swap_tensor = swap_tensor
+
+
+_hook_swap_tensor()
 
 
 class _TensorTree:
@@ -319,10 +342,23 @@ def _model_train_fwd_native(model, x, flags, momentum, drop, seed):
     y = torch.empty_like(x)
     nbytes = L.dstd_model_train_saved_bytes(n, t, v, model.num_feature, model.num_layers)
     saved = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    code = L.dstd_model_train_fwd_ex(model._native_params(), native.ptr(x, "x"), n, momentum, drop, seed,
-                                     native.ptr(y, "y"), saved.data_ptr(), nbytes, native.stream_handle(dev), flags)
-    native.check(code, "dstd_model_train_fwd_ex")
+    args = (model._native_params(), native.ptr(x, "x"), n, momentum, drop, seed, native.ptr(y, "y"),
+            saved.data_ptr(), nbytes, native.stream_handle(dev), flags)
+    sync = _bn_sync(model, flags)
+    if sync is not None:  # cross-rank BatchNorm (dstd_dist.convert_sync_batchnorm)
+        native.check(L.dstd_model_train_fwd_sync(*args, sync), "dstd_model_train_fwd_sync")
+    else:
+        native.check(L.dstd_model_train_fwd_ex(*args), "dstd_model_train_fwd_ex")
     return y, saved
+
+
+def _bn_sync(model, flags):
+    """The model's dstd_bn_sync (dstd_dist.BnSync) when its BatchNorms run on
+    batch statistics; None for per-rank BatchNorm or running statistics."""
+    s = model.__dict__.get("_dstd_bn_sync")
+    if s is None or flags & native.TRAIN_RUNNING_STATS:
+        return None
+    return s.struct_ref()
 
 
 def _model_train_bwd_native(model, x, saved, dy, flags, drop, seed, g, need_dx):
@@ -331,10 +367,14 @@ def _model_train_bwd_native(model, x, saved, dy, flags, drop, seed, g, need_dx):
     dev = x.device
     ws = native.workspace(dev, L.dstd_model_train_workspace_bytes(n, t, v, model.num_feature, model.num_layers))
     dx = torch.empty_like(x) if need_dx else None
-    code = L.dstd_model_train_bwd_ex(model._native_params(), native.ptr(x, "x"), n, drop, seed, saved.data_ptr(),
-                                     saved.numel(), native.ptr(dy, "dy"), g, dx.data_ptr() if dx is not None else None,
-                                     ws.data_ptr(), ws.numel(), native.stream_handle(dev), flags)
-    native.check(code, "dstd_model_train_bwd_ex")
+    args = (model._native_params(), native.ptr(x, "x"), n, drop, seed, saved.data_ptr(), saved.numel(),
+            native.ptr(dy, "dy"), g, dx.data_ptr() if dx is not None else None, ws.data_ptr(), ws.numel(),
+            native.stream_handle(dev), flags)
+    sync = _bn_sync(model, flags)
+    if sync is not None:
+        native.check(L.dstd_model_train_bwd_sync(*args, sync), "dstd_model_train_bwd_sync")
+    else:
+        native.check(L.dstd_model_train_bwd_ex(*args), "dstd_model_train_bwd_ex")
     return dx
 
 
@@ -382,7 +422,8 @@ class _ModelTrain(torch.autograd.Function):
         flags = _bn_flags(model) | (native.TRAIN_PAIRED if paired else 0)
         drop = float(model.do_in.p) if model.do_in.training else 0.0
         seed, ctx.seed_t = 0, None
-        if drop > 0:
+        eager = type(x) is torch.Tensor and not torch.compiler.is_compiling()
+        if drop > 0 and eager:
             # the dropout seed is drawn on the device and read there
             # (DSTD_TRAIN_SEED_DEVICE): no host round trip, and a captured HIP
             # graph (engine.GraphedStep) draws a fresh mask per replay; the
@@ -390,8 +431,15 @@ class _ModelTrain(torch.autograd.Function):
             ctx.seed_t = torch.randint(0, 2 ** 62, (1,), device=x.device, dtype=torch.int64)
             seed = ctx.seed_t.data_ptr()
             flags |= native.TRAIN_SEED_DEVICE
+        elif drop > 0:
+            # the op branch (torch.compile, subclass inputs): the ops' schema
+            # carries the seed as an integer, so it is drawn on the host -- a
+            # device tensor read by pointer would be invisible to the tracer
+            # (and a FakeTensor has no data pointer).  Python's random: dynamo
+            # re-draws it at run time, so every compiled call gets a new mask
+            seed = random.randint(0, 2 ** 62 - 1)
         buffers = model._tree.get(model)[1]
-        if type(x) is torch.Tensor and not torch.compiler.is_compiling():
+        if eager:
             # eager: the op's implementation without the dispatcher's boxing
             # of ~300 tensor arguments (~0.3 ms of host time per step); the
             # running statistics it updates get the version bump the op's

@@ -41,6 +41,7 @@ extern "C" {
 #define DSTD_EINVAL -1      /* bad shape / null pointer */
 #define DSTD_EWORKSPACE -2  /* workspace too small */
 #define DSTD_ELIMIT -3      /* shape outside the supported envelope */
+#define DSTD_ECOLLECTIVE -5 /* a caller-supplied collective returned non-zero (dstd_bn_sync, dstd_gcn_train.h) */
 
 #define DSTD_MODE_SPATIAL 0
 #define DSTD_MODE_TEMPORAL 1

@@ -159,6 +159,46 @@ int dstd_model_train_bwd_ex(const dstd_model_params* p, const float* x, int B, f
                             const dstd_model_grads* g, float* dx, void* workspace, size_t workspace_bytes,
                             void* stream, unsigned flags);
 
+/* ---- cross-rank BatchNorm (SyncBN) for data-parallel training ------------
+ * The reference trains with per-process BatchNorm (DDP's default); SURVEY
+ * §8(e) names SyncBN for an 8-GPU step equal to the single-GPU one.  With a
+ * dstd_bn_sync every train-mode BatchNorm of the model forward normalises with
+ * the statistics of ALL ranks' batches (torch.nn.SyncBatchNorm semantics:
+ * global mean and biased variance, running statistics from the global
+ * unbiased variance), and its backward uses the all-reduced sum(dz) and
+ * sum(dz * xhat) for the input gradient while gamma / beta / PReLU slope
+ * gradients stay the rank's own (the data-parallel gradient average makes
+ * them global).  The library issues no collective itself: at each
+ * BatchNorm it calls `fn` on the stream of the call --
+ *   op DSTD_COLL_ALLGATHER:     buf holds world x count floats, this rank's
+ *                               count at offset rank * count; gather in place;
+ *   op DSTD_COLL_ALLREDUCE_SUM: sum count floats in place over the ranks --
+ * ordered after the kernels already issued on `stream` and before the ones
+ * issued after it returns (RCCL on that stream, or anything synchronous).
+ * `fn` returns 0 on success.  buf: device memory of at least
+ * dstd_bn_sync_buffer_floats(world, num_feature, V) floats.  DSTD_TRAIN_PAIRED
+ * syncs each half's statistics separately.  Pass the same sync to the
+ * backward.  NULL sync: per-rank BatchNorm (the _ex entry points). */
+#define DSTD_COLL_ALLGATHER 0
+#define DSTD_COLL_ALLREDUCE_SUM 1
+typedef int (*dstd_collective_fn)(void* ctx, int op, float* buf, long long count, void* stream);
+typedef struct dstd_bn_sync {
+  int world;
+  int rank;
+  dstd_collective_fn fn;
+  void* ctx;
+  float* buf;
+  long long buf_floats;
+} dstd_bn_sync;
+size_t dstd_bn_sync_buffer_floats(int world, int num_feature, int V);
+int dstd_model_train_fwd_sync(const dstd_model_params* p, const float* x, int B, float momentum, float dropout_p,
+                              unsigned long long seed, float* y, void* saved, size_t saved_bytes, void* stream,
+                              unsigned flags, const dstd_bn_sync* sync);
+int dstd_model_train_bwd_sync(const dstd_model_params* p, const float* x, int B, float dropout_p,
+                              unsigned long long seed, const void* saved, size_t saved_bytes, const float* dy,
+                              const dstd_model_grads* g, float* dx, void* workspace, size_t workspace_bytes,
+                              void* stream, unsigned flags, const dstd_bn_sync* sync);
+
 /* ---- engine: loss and test metric --------------------------------------- */
 size_t dstd_loss_workspace_bytes(void);
 /* loss[0] = mean over n_points of ||pred_k - targ_k||_2 (points are xyz triples). */

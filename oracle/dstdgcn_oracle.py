@@ -294,11 +294,12 @@ def test_metric(all_seqs, outputs, input_n, eval_frame, dim_used, joint_to_ignor
     return np.array([np.linalg.norm(t[:, j] - p[:, j], axis=-1).mean() * n for j in eval_frame])
 
 
-def train_params(sd0, dtype=torch.float64):
+def train_params(sd0, dtype=torch.float64, device="cpu"):
     """Leaf tensors for training: every state-dict parameter except A_s / A_t
     requires grad; BN running statistics are dropped (train-mode BN never
-    reads them)."""
-    P = {k: _t(v, dtype).clone() for k, v in sd0.items()
+    reads them).  ``device`` other than the CPU: the same torch ops on the GPU
+    box's torch-ROCm (tests at training batches, where the CPU takes a minute)."""
+    P = {k: _t(v, dtype, device).clone() for k, v in sd0.items()
          if not k.endswith(("num_batches_tracked", "running_mean", "running_var"))}
     for k in P:
         if not k.endswith((".A_s", ".A_t")):
@@ -310,8 +311,8 @@ def step_loss(P, batch, num_layers, inverse=True):
     """Losses of one PredictionEngine.train step (prediction.py:231-287):
     returns (loss, all_loss) with all_loss = (loss + loss_inv) / 2 when
     ``inverse``.  A_s re-reads R_s's values (the storage alias, :107-109)."""
-    dtype = next(iter(P.values())).dtype
-    inp, inv, seq = (_t(a, dtype) for a in batch)
+    p0 = next(iter(P.values()))
+    inp, inv, seq = (_t(a, p0.dtype, p0.device) for a in batch)
     B, T, VC = inp.shape
     for k in list(P):
         if k.endswith(".A_s"):

@@ -1,0 +1,30 @@
+#!/bin/bash
+# round 4 (r04a): VALU trims of the split GC kernels (one v_max3 per two
+# range-detection values, PReLU as one median, half-empty splits, zero-pad
+# plane reads) -- parity suite of the forward, MFMA shape rates, same-box A/B
+# against the round-3 library and a no-SLP build, phase timeline, kernel trace.
+cd "$(dirname "$0")/.." || exit 2
+R="$PWD"
+O=$R/gpurun_out/r04a
+mkdir -p $O
+timeout -k 10 60 scripts/micro/mfma_rate > $O/mfma_rate.txt 2>&1; st=$?; cat $O/mfma_rate.txt; [ $st -eq 0 ] || exit $st
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py > $O/pytest_parity.log 2>&1
+st=$?; tail -3 $O/pytest_parity.log; [ $st -eq 0 ] || exit $st
+timeout -k 10 400 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread -m gpu tests/test_gpu_train.py -k "training_batch or graphed or step_gradients" > $O/pytest_train.log 2>&1
+st=$?; grep -E "B=|passed|failed" $O/pytest_train.log | tail -5; [ $st -eq 0 ] || exit $st
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_dist.py > $O/pytest_dist.log 2>&1
+st=$?; tail -3 $O/pytest_dist.log; [ $st -eq 0 ] || exit $st
+export DSTD_AB_FOREIGN_LIB=1
+L=dstd-gcn_amd
+for cfg in h36m cmu 3dpw; do
+  echo "# $cfg" >> $O/ab.txt
+  timeout -k 10 300 python -u scripts/ab_kernels.py $L/libdstd_gcn_r03.so $L/libdstd_gcn.so $L/libdstd_gcn_noslp.so --config $cfg --rounds 5 >> $O/ab.txt 2>&1 || exit 1
+done
+grep -v amdgpu.ids $O/ab.txt | cut -c1-400
+timeout -k 10 120 python -u scripts/timeline.py $L/libdstd_gcn_stamps.so --hl > $O/timeline.txt 2>&1; st=$?
+grep -v amdgpu.ids $O/timeline.txt | head -60; [ $st -eq 0 ] || exit $st
+export TMPDIR=/tmp
+unset DSTD_AB_FOREIGN_LIB
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o run -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-variant --no-side > "$O/kt.log" 2>&1)
+st=$?; echo "kt exit $st"; [ $st -eq 0 ] || exit $st
+f=$(find $O/kt -name "*kernel_stats.csv" | head -1); python3 scripts/kstats.py "$f" 13 24

@@ -47,10 +47,23 @@ def test_arithmetic_is_a_per_call_flag():
 def test_library_exports_every_training_header_symbol():
     L = native.lib()
     syms = header_symbols("dstd_gcn_train.h")
-    assert len(syms) == 24, syms
+    assert len(syms) == 27, syms
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(native.TRAIN_EXPORTS)
+
+
+def test_syncbn_buffer_and_error_without_gpu():
+    """dstd_bn_sync (SyncBN): the buffer a caller allocates holds the forward's
+    all-gather (world x 2 groups x C*V x (mean, M2, count)) and the backward's
+    all-reduce; a failed collective has an error string of its own."""
+    L = native.lib()
+    assert L.dstd_bn_sync_buffer_floats(8, 64, 22) == 8 * 2 * 64 * 22 * 3
+    assert L.dstd_bn_sync_buffer_floats(1, 64, 22) == 2 * 64 * 22 * 3
+    assert L.dstd_bn_sync_buffer_floats(2, 64, 25) > L.dstd_bn_sync_buffer_floats(1, 64, 25)
+    s = native.BnSyncStruct(2, 1, native.COLLECTIVE_FN(lambda *a: 0), None, 16, 1 << 20)
+    assert (s.world, s.rank, s.buf_floats) == (2, 1, 1 << 20)
+    assert "SyncBN" in L.dstd_error_string(-5).decode()
 
 
 def test_train_sizes_and_argument_checks_without_gpu():

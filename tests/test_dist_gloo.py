@@ -215,7 +215,15 @@ def _engine_save_body(rank, world):
     return out[2]
 
 
-def _engine_metric_body(rank, world, save_path=None, n_batches=3):
+def _engine_save_presharded_body(rank, world):
+    """The same through a presharded loader: a DistributedSampler interleaves
+    the samples over the ranks and pads the last with a duplicate."""
+    out = _engine_metric_body(rank, world, save_path=os.environ["DSTD_TEST_SAVE"],
+                              presharded=int(os.environ["DSTD_TEST_N"]))
+    return out[2]
+
+
+def _engine_metric_body(rank, world, save_path=None, n_batches=3, presharded=0):
     """PredictionEngine.test under torch.distributed: each rank evaluates its
     round-robin share of the loader's batches and the per-frame sums / counts
     are all-reduced.  No GPU in this leg: the model is the fp64 oracle and the
@@ -257,6 +265,11 @@ def _engine_metric_body(rank, world, save_path=None, n_batches=3):
     # three batches (2, 1, 1): rank 0 takes batches 0 and 2, rank 1 batch 1
     loader = [(inputs[:2], None, None, all_seqs[:2]), (inputs[2:3], None, None, all_seqs[2:3]),
               (inputs[3:], None, None, all_seqs[3:])][:n_batches]
+    if presharded:
+        n = presharded
+        ds = torch.utils.data.TensorDataset(inputs[:n], torch.zeros(n), torch.zeros(n), all_seqs[:n])
+        sampler = torch.utils.data.DistributedSampler(ds, num_replicas=world, rank=rank, shuffle=False)
+        loader = torch.utils.data.DataLoader(ds, batch_size=1, sampler=sampler)
     avg, metric = eng.test(loader, input_n=10, eval_frame=list(d["test/eval_frame"]), dim_used=d["test/dim_used"],
                            joint_to_ignore=d["test/joint_to_ignore"], joint_equal=d["test/joint_equal"],
                            save_path=save_path)
@@ -292,3 +305,23 @@ def test_engine_test_save_path_sharded(tmp_path, n_batches):
     all_seqs = d["test/all_seqs"][:n]
     assert f["target"].shape[0] == n and f["result"].shape == f["target"].shape
     np.testing.assert_array_equal(f["target"], all_seqs.reshape(n, all_seqs.shape[1], -1, 3)[:, 10:])
+
+
+@pytest.mark.parametrize("n", [3, 4])
+def test_engine_test_save_path_presharded(tmp_path, n):
+    """save_path with a DistributedSampler loader (samples interleaved over
+    the ranks; n = 3 pads rank 1 with a duplicate of sample 0): the file holds
+    each sample once, in dataset order."""
+    import numpy as np
+    d = load_npz("engine.npz")
+    prefix = str(tmp_path / "res")
+    os.environ["DSTD_TEST_SAVE"], os.environ["DSTD_TEST_N"] = prefix, str(n)
+    try:
+        seen = run_world("_engine_save_presharded_body")
+    finally:
+        del os.environ["DSTD_TEST_SAVE"], os.environ["DSTD_TEST_N"]
+    assert seen[0] == [1, 1] and seen[1] == [1, 1]
+    f = np.load(prefix + ".npz")
+    all_seqs = d["test/all_seqs"][:n]
+    np.testing.assert_array_equal(f["target"], all_seqs.reshape(n, all_seqs.shape[1], -1, 3)[:, 10:])
+    assert f["result"].shape == f["target"].shape

@@ -138,3 +138,96 @@ def test_dp_training_step_averages_native_arena():
         assert res[r]["arena"], "the engine's gradients were not slices of the native arena"
         assert res[r]["differs"], "the two shards gave the same gradient: the test would prove nothing"
         assert res[r]["equal"], (r, res[r]["maxdiff"])
+
+
+def _syncbn_step(rank, world, sync):
+    """One engine step (forward pair, two losses, native backward, the
+    data-parallel gradient average) on this rank's half of the fixture batch,
+    with cross-rank BatchNorm (dstd_dist.convert_sync_batchnorm) or per-rank;
+    returns the averaged gradients and the buffers after the step."""
+    import dstd_dist as D
+    from engine import PredictionEngine
+
+    class _Log:
+        def info(self, *a, **k):
+            pass
+
+    cfg = dict(learn=dict(opt="adam", lr=3e-3, weight_decay=0, gamma=0.9, step_size=5),
+               loss=dict(joint=["jl2", 1]), n_out=1, transform="tsc", use_weight=False, inverse=True)
+    d = load_npz("engine.npz")
+    batch = tuple(D.shard(torch.from_numpy(d[f"train/{n}0"]), world, rank).contiguous()
+                  for n in ("inp", "inv", "seq", "seq"))
+    m, _ = _model_3dpw()
+    if sync:
+        D.convert_sync_batchnorm(m)
+    eng = PredictionEngine(cfg, m, _Log())
+    seen = {}
+    step = eng.optimizer.step
+
+    def capture():
+        seen.update({n: p.grad.detach().clone().cpu() for n, p in m.named_parameters() if p.grad is not None})
+        return step()
+
+    eng.optimizer.step = capture
+    eng.train([batch], 0, max_iter=1)
+    bufs = {n: b.detach().clone().cpu() for n, b in m.named_buffers()}
+    return seen, bufs, (m._dstd_bn_sync.calls if sync else 0)
+
+
+def _syncbn_body(rank, world):
+    torch.cuda.set_device(0)
+    g_sync, b_sync, calls = _syncbn_step(rank, world, True)
+    g_local, _, _ = _syncbn_step(rank, world, False)
+    return {"g_sync": g_sync, "b_sync": b_sync, "g_local": g_local, "calls": calls}
+
+
+def test_syncbn_dp_step_equals_full_batch_step():
+    """SURVEY §8(e) SyncBN: the two-rank data-parallel step with cross-rank
+    BatchNorm equals ONE process stepping on the whole batch -- gradients
+    within the fp32 summation-order bar of test_forward_pair_equals_two_calls
+    (1e-4 of each tensor's largest entry), running statistics within 1e-5 --
+    while per-rank BatchNorm does not."""
+    import engine.prediction as EP
+    res = run_world("test_gpu_dist:_syncbn_body")
+    # the single-process step on the full batch of 8
+    from engine import PredictionEngine
+
+    class _Log:
+        def info(self, *a, **k):
+            pass
+
+    cfg = dict(learn=dict(opt="adam", lr=3e-3, weight_decay=0, gamma=0.9, step_size=5),
+               loss=dict(joint=["jl2", 1]), n_out=1, transform="tsc", use_weight=False, inverse=True)
+    d = load_npz("engine.npz")
+    batch = tuple(torch.from_numpy(d[f"train/{n}0"]) for n in ("inp", "inv", "seq", "seq"))
+    m, _ = _model_3dpw()
+    eng = PredictionEngine(cfg, m, _Log())
+    ref = {}
+    step = eng.optimizer.step
+    eng.optimizer.step = lambda: (ref.update({n: p.grad.detach().clone().cpu() for n, p in m.named_parameters()
+                                              if p.grad is not None}), step())[1]
+    saved_world = EP._world
+    EP._world = lambda: (0, 1)
+    try:
+        eng.train([batch], 0, max_iter=1)
+    finally:
+        EP._world = saved_world
+    ref_bufs = {n: b.detach().clone().cpu() for n, b in m.named_buffers()}
+    worst_local = 0.0
+    for r in (0, 1):
+        # 15 BatchNorms x (forward all-gather, backward all-reduce) per model call
+        assert res[r]["calls"] > 0
+        for n, g in ref.items():
+            scale = float(g.abs().max())
+            err = float((res[r]["g_sync"][n] - g).abs().max())
+            if n.endswith("residual.0.bias"):  # analytically zero (a train-mode BN follows)
+                assert err < 1e-3, n
+                continue
+            assert err <= 1e-4 * scale + 1e-12, (r, n, err, scale)
+            worst_local = max(worst_local, float((res[r]["g_local"][n] - g).abs().max()) / max(scale, 1e-30))
+        for n, b in ref_bufs.items():
+            if n.endswith("num_batches_tracked"):
+                assert int(res[r]["b_sync"][n]) == int(b), n
+            else:
+                assert float((res[r]["b_sync"][n] - b).abs().max()) <= 1e-5 * max(float(b.abs().max()), 1e-6), n
+    assert worst_local > 1e-3, "per-rank BatchNorm matched the full batch: the test would prove nothing"

@@ -685,6 +685,23 @@ def test_torch_library_ops_opcheck_and_compile():
     y, saved = torch.ops.dstd.dstdgcn_train_forward(*args)
     torch.library.opcheck(torch.ops.dstd.dstdgcn_train_backward.default,
                           (x, saved, torch.randn_like(y), params, m._dstd_uid, 0, 0.0, 0, True), test_utils=ut)
+    # with dropout: the op branch carries a host-drawn integer seed (no device
+    # pointer in the schema); forward and backward regenerate the same mask
+    args = (x, params, buffers, m._dstd_uid, 0, 0.1, 0.3, 12345)
+    torch.library.opcheck(torch.ops.dstd.dstdgcn_train_forward.default, args, test_utils=ut)
+    y, saved = torch.ops.dstd.dstdgcn_train_forward(*args)
+    torch.library.opcheck(torch.ops.dstd.dstdgcn_train_backward.default,
+                          (x, saved, torch.randn_like(y), params, m._dstd_uid, 0, 0.3, 12345, True), test_utils=ut)
+    # a compiled train step with dropout runs the op branch end to end
+    m.do_in.p = 0.3
+    mc = torch.compile(m, backend="aot_eager")
+    xg = x.clone().requires_grad_(True)
+    yc = mc(xg)
+    yc.square().sum().backward()
+    assert torch.isfinite(yc).all() and xg.grad is not None and torch.isfinite(xg.grad).all()
+    assert m.conv_st_out.stgcn[0][0].conv_t[0].conv_f.weight.grad is not None
+    m.do_in.p = 0.0
+    m.zero_grad(set_to_none=True)
     blk = m.encoders[0][0].stgcn[0][0]
     bp, bb = list(blk.parameters()), list(blk.buffers())
     xb = torch.randn(2, 64, 35, 22, device=DEV)

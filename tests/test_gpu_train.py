@@ -298,6 +298,62 @@ def test_model_step_gradients_vs_reference_fp64():
     assert named["conv_st_in.stgcn.0.0.A_s"].grad is None
 
 
+@pytest.mark.parametrize("B", [32, 256])
+def test_model_step_gradients_at_training_batch(B):
+    """One engine step the way PredictionEngine.train runs it (forward_pair
+    over the batch and its time reversal, two mpjpe losses, the native
+    backward into the in-place gradient arena; engine/prediction.py:231-294)
+    at the yaml's train_batch_size, 32 (configs/dstdgcn/dstdgcn_3dpw.yaml:19),
+    and at 256: the reduce GEMMs pick their split-K partition from the sample
+    count, so these batches run other partitions than the fixture's B=8.
+    Reference: the oracle's fp64 step (pinned to the reference's own fp64
+    gradients by tests/test_oracle_golden.py); fp32 noise: the oracle's fp32
+    step as torch ops on the GPU (rocBLAS) and on the CPU -- the same
+    per-tensor criterion as the B=8 fixture step."""
+    from engine import mpjpe_error_3d
+    m, d = _model_3dpw()
+    m._dstd_inplace_grads = True
+    g = torch.Generator().manual_seed(1000 + B)
+    T, VC = 40, 69
+    seq = 0.6 * torch.randn(B, T, VC, generator=g)  # the fixture batches' scale
+    inp = seq.clone()
+    inp[:, 10:] = inp[:, 9:10]  # future frames = the last observed one
+    rev = seq.flip(1)
+    inv = rev.clone()
+    inv[:, 10:] = inv[:, 9:10]
+    batch = (inp.numpy(), inv.numpy(), seq.numpy())
+    # native
+    sq = seq.to(DEV)
+    p1, p2 = m.forward_pair(inp.view(B, T, 23, 3).to(DEV), inv.view(B, T, 23, 3).to(DEV))
+    loss = mpjpe_error_3d(p1.reshape(B, T, VC), sq)
+    all_loss = (loss + mpjpe_error_3d(p2.reshape(B, T, VC), sq.flip(1))) / 2
+    all_loss.backward()
+    # oracle steps
+    sd0 = group(d, "train/sd0/")
+    grads, losses = {}, {}
+    for tag, dt, dev in (("64", torch.float64, DEV), ("32g", torch.float32, DEV), ("32c", torch.float32, "cpu")):
+        P = O.train_params(sd0, dt, dev)
+        l0, lall = O.step_loss(P, batch, 5)
+        lall.backward()
+        losses[tag] = float(l0.detach())
+        grads[tag] = {k: v.grad.double().cpu().numpy() for k, v in P.items() if v.grad is not None}
+    assert abs(float(loss.detach()) - losses["64"]) / losses["64"] < 1e-5
+    named = dict(m.named_parameters())
+    assert set(grads["64"]) == {k for k, p in named.items() if p.requires_grad}
+    ratios = []
+    for k, ref in grads["64"].items():
+        scale = float(np.abs(ref).max())
+        noise = max(float(np.abs(grads["32g"][k] - ref).max()), float(np.abs(grads["32c"][k] - ref).max()),
+                    1e-4 * scale)
+        err = float(np.abs(named[k].grad.double().cpu().numpy() - ref).max())
+        ratios.append((err / noise, k))
+    r = np.array([x[0] for x in sorted(ratios, reverse=True)])
+    print(f"B={B}: err / fp32 noise median {np.median(r):.2f}, p90 {np.quantile(r, 0.9):.2f}, max {r[0]:.2f}")
+    assert np.median(r) <= 1.5, (np.median(r), sorted(ratios, reverse=True)[:8])
+    assert np.quantile(r, 0.9) <= 3.0, (np.quantile(r, 0.9), sorted(ratios, reverse=True)[:8])
+    check_tail(ratios)
+
+
 @pytest.mark.parametrize("inplace", [True, False])
 def test_forward_pair_equals_two_calls(inplace):
     """DSTDGCN.forward_pair (DSTD_TRAIN_PAIRED: one launch sequence over the
@@ -484,6 +540,46 @@ def test_graphed_engine_step_equals_eager():
     lr_g, lr_e = (float(e.optimizer.param_groups[0]["lr"]) for e in (eg, ee))
     assert lr_g == lr_e and abs(lr_g - 1.5e-3) < 1e-9, (lr_g, lr_e)
     assert lg[-1] < lg[0]
+
+
+def test_graphed_engine_test_after_replays():
+    """learn.graph with epochs made only of replays (one full batch): a replay
+    updates parameters and BatchNorm buffers on the device without moving
+    their version counters, so test() after it must not reuse the BatchNorm
+    constants the previous test() folded (engine/graphed.py invalidates the
+    native cache after every replay).  Every epoch's metric equals the eager
+    engine's bit for bit."""
+    from engine import PredictionEngine
+
+    class _Log:
+        def info(self, *a, **k):
+            pass
+
+    d = load_npz("engine.npz")
+    batch = tuple(torch.from_numpy(d[f"train/{n}0"]) for n in ("inp", "inv", "seq", "seq"))
+    g = torch.Generator().manual_seed(7)
+    all_seqs = 0.6 * torch.randn(6, 40, 69, generator=g)
+    inputs = all_seqs.clone()
+    inputs[:, 10:] = inputs[:, 9:10]
+    loader = [(inputs, None, None, all_seqs)]
+    runs = []
+    for graphed in (True, False):
+        m, _ = _model_3dpw()
+        cfg = dict(learn=dict(opt="adam", lr=3e-3, weight_decay=0, gamma=0.5, step_size=2, graph=True),
+                   loss=dict(joint=["jl2", 1]), n_out=1, transform="tsc", use_weight=False, inverse=True)
+        eng = PredictionEngine(cfg, m, _Log())
+        if not graphed:
+            eng._graphed = lambda: False
+        metrics = []
+        for e in range(4):
+            eng.train([batch], e)
+            metrics.append(eng.test(loader, input_n=10, eval_frame=[1, 5, 10, 29])[1])
+        runs.append((eng, metrics))
+    (eg, mg), (ee, me) = runs
+    assert eg._graph_step is not None and ee._graph_step is None
+    for e, (a, b) in enumerate(zip(mg, me)):
+        assert np.array_equal(a, b), (e, a, b)
+    assert not np.array_equal(mg[0], mg[-1])  # the weights did move between the tests
 
 
 def test_dropout_mask_is_regenerated_in_backward():

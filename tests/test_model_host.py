@@ -36,6 +36,32 @@ def test_tensor_tree_matches_torch_walk_and_invalidates():
     assert not any(x is y for x, y in zip(m2._tree.get(m2)[0], m.parameters()))
 
 
+def test_tensor_tree_sees_functional_call_swaps():
+    """torch.func.functional_call swaps tensors into _parameters / _buffers
+    directly (no registration hook): inside the call the cached walk must hand
+    out the swapped-in tensors, after it the module's own again."""
+    m = get_model("dstdgcn", dstdgcn=OPTS)
+    assert same(m)
+    own = m._tree.get(m)[0]
+    new = {k: v.detach().clone() for k, v in m.named_parameters()}
+    seen = {}
+
+    def probe(self, x):
+        seen["params"] = list(self._tree.get(self)[0])
+        seen["same"] = same(self)
+        return x
+
+    orig = type(m).forward
+    type(m).forward = probe
+    try:
+        torch.func.functional_call(m, new, (torch.zeros(1),))
+    finally:
+        type(m).forward = orig
+    assert seen["same"]
+    assert all(a is b for a, b in zip(seen["params"], new.values()))
+    assert same(m) and all(a is b for a, b in zip(m._tree.get(m)[0], own))
+
+
 def test_fast_variant_schema_and_derivation_cpu():
     """model.dstdgcn_fast (reference model/dstdgcn_fast.py): the reference's
     state_dict keys in order, and the dstdgcn.py-schema shadow derived from
