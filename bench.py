@@ -361,7 +361,12 @@ def small_batch_leg(model, x, B, steps, warmup):
             g = model.graphed(xb)
             gms, ghost = timed_calls(lambda: g(xb), steps, warmup)
             out["graph_replay"] = {"value": round(B / gms * 1e3, 2), "ms_per_step": round(gms, 4),
-                                   "host_us_per_call": round(ghost, 2)}
+                                   "host_us_per_call": round(ghost, 2), "note": "refolds the constants per replay"}
+            gz = model.graphed(xb, frozen=True)
+            gms, ghost = timed_calls(lambda: gz(xb), steps, warmup)
+            out["graph_replay_frozen"] = {"value": round(B / gms * 1e3, 2), "ms_per_step": round(gms, 4),
+                                          "host_us_per_call": round(ghost, 2),
+                                          "note": "frozen weights: the GC launches alone after the first replay"}
     return out
 
 

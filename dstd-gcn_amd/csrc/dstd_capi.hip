@@ -917,7 +917,6 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
                       size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof) {
   StreamDeviceGuard dev_guard_(stream, x);
   const bool reuse = (flags & DSTD_FWD_REUSE_CONSTANTS) != 0;
-  const bool exact = (flags & DSTD_FWD_EXACT_FP32) != 0;
   if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32 | DSTD_FWD_SEPARATE_ADJ | DSTD_FWD_FUSED_TEMPORAL))
     return DSTD_EINVAL;
   if (!p || !x || !y || !workspace) return DSTD_EINVAL;

@@ -58,7 +58,6 @@ namespace {
 
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 __device__ __forceinline__ f16x8 as_h8(const uint4& v) { return __builtin_bit_cast(f16x8, v); }
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
@@ -315,6 +314,11 @@ __global__ __launch_bounds__(256) void k_hl_prep(HLPrepArgs a) {
 // so a CU stages one copy of the weight images (A/B against two 4-wave
 // workgroups: forward -2.3%)
 constexpr int spatial_nt() { return 64 * 4 * DSTD_HL_WPE; }
+// identity residual loaded after the aggregations (see spatial_units)
+#ifndef DSTD_SP_LATE_RES
+#define DSTD_SP_LATE_RES (DSTD_HL_WPE > 2)
+#endif
+constexpr bool kSpLateRes = DSTD_SP_LATE_RES;
 
 // 8 consecutive channels k0 .. k0+7 of row `row` of a unit (C channels per
 // row, zero past C; C % 8 == 0 or C == 6 / 3)
@@ -509,16 +513,19 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
     // residual conv -> x rows of the output joints as B fragments
     float4 R[RES ? 1 : 4][RES ? 1 : NWT];
     float4 xw[RES ? NWT : 1][RES ? KSI : 1][2];
+    auto load_res = [&]() {
+#pragma unroll
+      for (int wt = 0; wt < NWT; ++wt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) R[ct][wt] = bld4(rx, (uint32_t)((16 * wt + cl) * 64 + 4 * kl) * 4 + 64 * ct);
+    };
     if constexpr (RES) {
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt)
 #pragma unroll
         for (int ks = 0; ks < KSI; ++ks) row8(rx, rxl, 16 * wt + cl, 32 * ks + 8 * kl, xw[wt][ks][0], xw[wt][ks][1]);
-    } else {
-#pragma unroll
-      for (int wt = 0; wt < NWT; ++wt)
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) R[ct][wt] = bld4(rx, (uint32_t)((16 * wt + cl) * 64 + 4 * kl) * 4 + 64 * ct);
+    } else if constexpr (!kSpLateRes) {
+      load_res();
     }
     // this unit's graph-0 adjacency now, graph 1 after the first conv (a
     // whole-unit-ahead prefetch of both measured 6% slower: registers)
@@ -623,6 +630,14 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
         for (int wt = 0; wt < NWT; ++wt) O[ct][wt] = mfma32(dh[ct], as_h8(ab[g][wt][0]), O[ct][wt]);
     }
 
+    // the identity residual after the aggregations (kSpLateRes: its 32
+    // registers are not live through the convs; the frame was just read, so
+    // the rows come from the cache)
+    if constexpr (!RES && kSpLateRes) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_res();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     // ---- residual conv in output layout: rc[c][w] = sum_k W_r[c][k] x[w][k] ----
     f32x4 rc[RES ? NCT : 1][RES ? NWT : 1];
     if constexpr (RES) {
@@ -917,7 +932,9 @@ __device__ __forceinline__ void stage_temporal(const TemporalHLArgs& a, Temporal
 #ifndef DSTD_TF_LATE_RES
 #define DSTD_TF_LATE_RES 1
 #endif
-template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad>
+// PF: the next unit's h rows are loaded during this one (48 VGPRs); without,
+// each unit loads its own rows first (for more waves per SIMD instead)
+template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad, bool PF = true>
 __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const TemporalStage<T, EPI, C, VB>& st, int u,
                                                int uend, int ustep, AdjLoad load_adj) {
   using SM = SlotMap<T, false>;
@@ -963,8 +980,9 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 #pragma unroll
       for (int ks = 0; ks < KSI; ++ks) load_row8_at<C>(r, xoff[m], 32 * ks + 8 * kl, xr[m][ks][0], xr[m][ks][1]);
   };
-  if (u < uend) load_x(u);
+  if (PF && u < uend) load_x(u);
   while (u < uend) {
+    if constexpr (!PF) load_x(u);
     const int n = u / V, v = u - n * V;
     const int un = u + ustep;
     const int lz = lane + opaque_zero();
@@ -1093,7 +1111,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     // (long sequences: the next unit's rows after the epilogue, so that they,
     // the output accumulators and the residual are not live at once)
     constexpr bool late_x = LAZY && T > 48;
-    if constexpr (!late_x) load_x(un < uend ? un : u);
+    if constexpr (PF && !late_x) load_x(un < uend ? un : u);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- epilogue ----
@@ -1181,7 +1199,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
                          fmaf(acc[ut][3], s, bql[b4 + 3])));
       }
     }
-    if constexpr (late_x) {
+    if constexpr (PF && late_x) {
       __builtin_amdgcn_sched_barrier(0);
       load_x(un < uend ? un : u);
     }
@@ -1616,8 +1634,11 @@ struct TFusedGeom {
   static constexpr int PJ = 2 * T * SL + 8, ZPAD = 2 * T * SL;
   static constexpr int RTG = cdiv(V, 16);  // row tiles of the whole HLJ_RM image
   static constexpr size_t stage_bytes = sizeof(TemporalStage<T, EPI, C, V>);
+  // phase-1 scratch: E / F rows, the chunk's conv_rm rows, the epilogue's
+  // per-column tables (Astat and alpha in plane slot order, ASQ), conv_rm bias
+  static constexpr int ASQ = NCTC * 16;
   static constexpr size_t p1_bytes(int rtc) {
-    return 2 * (size_t)(T + 1) * SE * 4 + (size_t)rtc * (NS * 2 * 64 + TAIL * 64) * 16 + ((size_t)T * T + 1) * 4 +
+    return 2 * (size_t)(T + 1) * SE * 4 + (size_t)rtc * (NS * 2 * 64 + TAIL * 64) * 16 + (size_t)2 * ASQ * 4 +
            (size_t)rtc * 16 * 4;
   }
   static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
@@ -1655,7 +1676,10 @@ struct SAdjGeom {
   static constexpr int WIMG = RT * (FULL + TAIL * 64);  // uint4 of one graph's HLJ_RM image
   static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
   static constexpr size_t EF = al16(2 * (size_t)(V + 1) * SE * 4);  // one graph's E rows then F rows
-  static constexpr size_t AS = al16(((size_t)V * V + 1) * 4);       // one graph's Astat (+ a zero)
+  // one graph's epilogue tables in plane slot order (as phase 1's asq / alq):
+  // 2^-sa Astat[pi][q] then 2^-sa alpha per column, 0 on padding slots
+  static constexpr int ASQ = NCTC * 16;
+  static constexpr size_t AS = al16((size_t)2 * ASQ * 4);
   static constexpr size_t WB = (size_t)WIMG * 16;                   // one graph's image
   static constexpr size_t BB = al16((size_t)16 * RT * 4);           // one graph's conv_rm bias (rows padded)
   static constexpr size_t LDS = 2 * (EF + AS + WB + BB);
@@ -1670,7 +1694,7 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
   constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
   // LDS: [E/F g0][E/F g1][Astat g0][Astat g1][image g0][image g1][bias g0][bias g1]
   auto Elg = [&](int g) { return reinterpret_cast<float*>(dsm + g * Gm::EF); };  // F rows at + (V + 1) * SE
-  auto asg = [&](int g) { return reinterpret_cast<float*>(dsm + 2 * Gm::EF + g * Gm::AS); };
+  auto asg = [&](int g) { return reinterpret_cast<float*>(dsm + 2 * Gm::EF + g * Gm::AS); };  // alq: + ASQ
   uint4* wl = reinterpret_cast<uint4*>(dsm + 2 * (Gm::EF + Gm::AS));  // both images, graph-major
   float* bl = reinterpret_cast<float*>(dsm + 2 * (Gm::EF + Gm::AS + Gm::WB));  // [g][16 RT]
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1679,7 +1703,7 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
   // ---- prologue: both graphs' P/Q -> E/F rows, conv_rm images, Astat, bias;
   // every global load before the first LDS write ----
   const PQLayout L = j.pql;
-  constexpr int NPQ = cdiv(T * V, NT), NWI = cdiv(2 * WIMG, NT), NAS = cdiv(2 * V * V, NT);
+  constexpr int NPQ = cdiv(T * V, NT), NWI = cdiv(2 * WIMG, NT), NAS = cdiv(2 * Gm::ASQ, NT);
   auto pq_at = [&](int g, int i) __attribute__((always_inline)) -> float4 {  // (P_0, P_1, Q_0, Q_1) of element i (joint-major)
     const int t = i % T, v = i / T;
     return ld4(j.pq + (size_t)n * L.sn + j.p_ch[g] + t * L.st + v * L.sv);
@@ -1696,11 +1720,19 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
     const int i = min(tid + it * NT, 2 * WIMG - 1);
     wv[it] = (i >= WIMG ? j.wimg[1] : j.wimg[0])[i >= WIMG ? i - WIMG : i];
   }
+  int aok = 0;  // bit it: the table entry of iteration it is a valid (pi, q)
 #pragma unroll
   for (int it = 0; it < NAS; ++it) {
-    const int i = min(tid + it * NT, 2 * V * V - 1);
-    av[it] = (i >= V * V ? j.astat[1] : j.astat[0])[i >= V * V ? i - V * V : i];
+    const int i = tid + it * NT, g = i >= Gm::ASQ, col = i - g * Gm::ASQ, q = col / SL;
+    const int pi = col < NCOL ? SM::slot_idx(col - q * SL) : V;
+    const bool ok = pi < V && i < 2 * Gm::ASQ;
+    if (ok) aok |= 1 << it;
+    av[it] = (g ? j.astat[1] : j.astat[0])[ok ? pi * V + q : 0];
   }
+  // planes stored as 2^-sa Adj, one sa for both graphs (dstd_hilo.h "range scaling")
+  const float dna = pow2f(-hl_range_shift(
+      fexp_bits(__float_as_uint(fmaxf(j.wscale[0][HLS_BOUND], j.wscale[1][HLS_BOUND])))));
+  const float alpha = *j.alpha * dna;
   const int bg = tid >= 16 * RT, br = tid - bg * 16 * RT;
   const float bv = tid < 2 * 16 * RT && br < T ? (bg ? j.bias[1] : j.bias[0])[br] : 0.f;
 #pragma unroll
@@ -1708,10 +1740,14 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
     if (tid + it * NT < 2 * WIMG) wl[tid + it * NT] = wv[it];
 #pragma unroll
   for (int it = 0; it < NAS; ++it) {
-    const int i = tid + it * NT;
-    if (i < 2 * V * V) asg(i >= V * V)[i >= V * V ? i - V * V : i] = av[it];
+    const int i = tid + it * NT, g = i >= Gm::ASQ;
+    if (i < 2 * Gm::ASQ) {
+      const bool ok = (aok >> it) & 1;
+      float* t = asg(g) + (i - g * Gm::ASQ);
+      t[0] = ok ? av[it] * dna : 0.f;
+      t[Gm::ASQ] = ok ? alpha : 0.f;
+    }
   }
-  if (tid < 2) asg(tid)[V * V] = 0.f;
   if (tid < 2 * 16 * RT) bl[tid] = bv;
   auto ef_pad = [&](int g, float val) __attribute__((always_inline)) {  // padding k and the row p = q = V: tanh 0
     float* El = Elg(g);
@@ -1767,9 +1803,6 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
     }
     __syncthreads();
   }
-  const float dna = pow2f(-hl_range_shift(
-      fexp_bits(__float_as_uint(fmaxf(j.wscale[0][HLS_BOUND], j.wscale[1][HLS_BOUND])))));
-  const float alpha = *j.alpha * dna;
   const float inv0 = *j.wscale[0], inv1 = *j.wscale[1];
   TLH(2, 1)
 
@@ -1815,15 +1848,9 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
       if (g ? sep1 : sep0) tanh_frags<true, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
       else tanh_frags<false, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
       // the accumulator's 4 columns colb .. colb + 3 (one joint q, slots slot0 ..)
-      const int colb = ct * 16 + 4 * kg, q = colb / SL, slot0 = colb - q * SL;
-      float asv[4], al[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int pi = SM::slot_idx(slot0 + r);
-        const bool valid = colb + r < NCOL && pi < V;
-        asv[r] = as[valid ? pi * V + q : V * V] * dna;
-        al[r] = valid ? alpha : 0.f;
-      }
+      const int colb = ct * 16 + 4 * kg;
+      const float4 as4 = ld4(as + colb), al4 = ld4(as + Gm::ASQ + colb);
+      const float asv[4] = {as4.x, as4.y, as4.z, as4.w}, al[4] = {al4.x, al4.y, al4.z, al4.w};
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
         f32x4 acc = zero4();
@@ -1859,13 +1886,23 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
 #endif
 }
 
+// waves per workgroup (one workgroup per CU): 8 = two per SIMD with the
+// next-unit prefetch; 12 = three per SIMD without it (<= 168 VGPRs), which
+// also runs a sample's 22 GC units in two rounds instead of three
+// (H36M; CMU / 3DPW, whose joints run in two chunks, spill at 168 VGPRs and
+// keep 8)
+#ifndef DSTD_TF_NW_H36M
+#define DSTD_TF_NW_H36M 12
+#endif
+template <int T, int V>
+constexpr int tf_waves() { return T == 35 && V == 22 ? DSTD_TF_NW_H36M : 8; }
 template <int T, int V, int EPI, int C>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_temporal_fused(TemporalFusedArgs fa) {
+__global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_waves_per_eu((tf_waves<T, V>() / 4), (tf_waves<T, V>() / 4)))) void k_temporal_fused(TemporalFusedArgs fa) {
   using Gm = TFusedGeom<T, V, EPI, C>;
   using SM = typename Gm::SM;
   constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
-  constexpr int RC = Gm::RC, RTC = Gm::RTC, PJ = Gm::PJ, WIMG = Gm::WIMG, NW = 8, NT = 512;
-  constexpr int NSG = SM::NS, NUT = cdiv(T, 16);  // aggregation K-steps / u tiles of the GC
+  constexpr int RC = Gm::RC, RTC = Gm::RTC, PJ = Gm::PJ, WIMG = Gm::WIMG, NW = tf_waves<T, V>(), NT = 64 * NW;
+  constexpr int NUT = cdiv(T, 16);  // u tiles of the GC
   constexpr float C2 = 2.8853900817779268f;       // 2*log2(e)
   const TemporalHLArgs& a = fa.g;
   const AdjHLArgs& j = fa.j;
@@ -1875,8 +1912,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   float* El = reinterpret_cast<float*>(un);
   float* Fl = El + (T + 1) * SE;
   uint4* wl = reinterpret_cast<uint4*>(Fl + (T + 1) * SE);
-  float* asl = reinterpret_cast<float*>(wl + WIMG);
-  float* bsl = asl + T * T + 1;
+  // plane column col = q * SL + slot (q the output frame, slot <-> input
+  // frame pi = slot_idx(slot)): asq[col] = 2^-sa Astat[pi][q], alq[col] =
+  // 2^-sa alpha -- both 0 on padding slots and past the planes
+  float* asq = reinterpret_cast<float*>(wl + WIMG);
+  float* alq = asq + Gm::ASQ;
+  float* bsl = alq + Gm::ASQ;
   auto& st = *reinterpret_cast<TemporalStage<T, EPI, C, V>*>(un);
 
   // wave index through readfirstlane: wave-uniform to the compiler, so the
@@ -1907,10 +1948,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       // write that needs one (one memory round trip, not one per loop trip)
       constexpr int FULL = NS * 2 * 64;  // uint4 per row tile (full K-steps)
       constexpr int NPQ = cdiv(T * V, NT), NWF = cdiv(RTC * FULL, NT), NWT = TAIL ? cdiv(RTC * 64, NT) : 0;
-      constexpr int NAS = cdiv(T * T, NT);
+      constexpr int NAS = cdiv(Gm::ASQ, NT);
       float4 q4[NPQ];
       uint4 wf[NWF], wt[NWT > 0 ? NWT : 1];
       float av[NAS];
+      int aok = 0;  // bit it: the table entry of iteration it is a valid (pi, q)
       // (the P/Q and Astat loads do not depend on the chunk: an opaque zero
       // in their index keeps hipcc from hoisting them out of the chunk loop,
       // where they would stay live through phase 2 and spill)
@@ -1929,7 +1971,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         for (int it = 0; it < NWT; ++it) wt[it] = wg[Gm::RTG * FULL + rt0 * 64 + min(tid + it * NT, RTC * 64 - 1)];
       }
 #pragma unroll
-      for (int it = 0; it < NAS; ++it) av[it] = j.astat[0][min(tid + it * NT + oz, T * T - 1)];
+      for (int it = 0; it < NAS; ++it) {
+        const int i = tid + it * NT + oz, q = i / SL, pi = i < NCOL ? SM::slot_idx(i - q * SL) : T;
+        if (pi < T) aok |= 1 << it;
+        av[it] = j.astat[0][pi < T ? pi * T + q : 0];
+      }
+      // planes stored as 2^-sa Adj (dstd_hilo.h "range scaling")
+      const float dna = pow2f(-hl_range_shift(fexp_bits(__float_as_uint(j.wscale[0][HLS_BOUND]))));
+      const float alpha = *j.alpha * dna, inv = j.wscale[0][HLS_INV];
       const float bv = tid < 16 * RTC && 16 * rt0 + tid < V ? j.bias[0][16 * rt0 + tid] : 0.f;
       int bad = 0;
 #pragma unroll
@@ -1953,8 +2002,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (tid + it * NT < RTC * 64) wl[RTC * FULL + tid + it * NT] = wt[it];
 #pragma unroll
       for (int it = 0; it < NAS; ++it)
-        if (tid + it * NT < T * T) asl[tid + it * NT] = av[it];
-      if (tid == 0) asl[T * T] = 0.f;
+        if (tid + it * NT < Gm::ASQ) {
+          const bool ok = (aok >> it) & 1;
+          asq[tid + it * NT] = ok ? av[it] * dna : 0.f;
+          alq[tid + it * NT] = ok ? alpha : 0.f;
+        }
       if (tid < 16 * RTC) bsl[tid] = bv;
       if (tid < Gm::jn(RC)) *reinterpret_cast<uint4*>(planes + tid * PJ + Gm::ZPAD) = make_uint4(0u, 0u, 0u, 0u);
       const bool sep = __syncthreads_or(bad) == 0;
@@ -1983,9 +2035,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         __syncthreads();
       }
       // ---- phase 1: the chunk's planes ----
-      // planes stored as 2^-sa Adj (dstd_hilo.h "range scaling")
-      const float dna = pow2f(-hl_range_shift(fexp_bits(__float_as_uint(j.wscale[0][HLS_BOUND]))));
-      const float alpha = *j.alpha * dna, inv = j.wscale[0][HLS_INV];
       // The GEMM runs transposed -- the tanh fragments as the A operand,
       // W_rm as B (the same register layouts) -- so a lane's accumulator holds
       // 4 consecutive slots (columns 16 ct + 4 kg + r) of one joint (16 rt +
@@ -2028,7 +2077,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           // computes padding (its stores are dropped)
           f16x8 bh[TPI][NS], bo[TPI][NS];
           f16x4 th[TPI], to[TPI];
-          float as[TPI][4], al[TPI][4];
+          float4 as[TPI], al[TPI];
           int colb[TPI], q[TPI], slot0[TPI];
 #pragma unroll
           for (int i = 0; i < TPI; ++i) {
@@ -2039,17 +2088,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const bool va = col < NCOL && pa < T;
             tanh_frags<SEP, NS, TAIL, SE>(El, Fl, va ? pa : T, col < NCOL ? qa : T, kg, bh[i], bo[i], th[i], to[i]);
             // columns colb .. colb+3 (one frame q, slots slot0 ..): alpha (acc + b) + Astat,
-            // 0 on padding slots (alpha -> 0, Astat[T*T] = 0)
+            // 0 on padding slots (both tables hold 0 there)
             colb[i] = ct * 16 + 4 * kg;
             q[i] = colb[i] / SL;
             slot0[i] = colb[i] - q[i] * SL;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int pi = SM::slot_idx(slot0[i] + r);
-              const bool valid = colb[i] + r < NCOL && pi < T;
-              as[i][r] = asl[valid ? pi * T + q[i] : T * T] * dna;
-              al[i][r] = valid ? alpha : 0.f;
-            }
+            as[i] = ld4(asq + colb[i]);
+            al[i] = ld4(alq + colb[i]);
           }
 #pragma unroll
           for (int rt = 0; rt < RTC; ++rt) {
@@ -2093,11 +2137,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             const int jv = 16 * rt + cl;
 #pragma unroll
             for (int i = 0; i < TPI; ++i) {
-              float vv[4];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) vv[r] = fmaf(al[i][r], fmaf(acc[i][r], inv, b), as[i][r]);
+              const float4 vv = make_float4(fmaf(al[i].x, fmaf(acc[i][0], inv, b), as[i].x),
+                                            fmaf(al[i].y, fmaf(acc[i][1], inv, b), as[i].y),
+                                            fmaf(al[i].z, fmaf(acc[i][2], inv, b), as[i].z),
+                                            fmaf(al[i].w, fmaf(acc[i][3], inv, b), as[i].w));
               uint2 hi, lo;
-              split4(make_float4(vv[0], vv[1], vv[2], vv[3]), hi, lo);
+              split4(vv, hi, lo);
               if (jv < nv && colb[i] < NCOL) {
                 _Float16* dst = planes + jv * PJ + q[i] * SL + slot0[i];
                 *reinterpret_cast<uint2*>(dst) = hi;
@@ -2164,7 +2209,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
       };
 #ifndef DSTD_TF_SKIP_P2  // (timing experiments: phase 1 alone)
-      temporal_units<T, EPI, C, V, true>(a, st, ub + wave, ub + nv, NW, load_adj);
+      temporal_units<T, EPI, C, V, true, decltype(load_adj), (NW <= 8)>(a, st, ub + wave, ub + nv, NW, load_adj);
 #endif
     }
   }
@@ -2302,7 +2347,7 @@ hipError_t tfused_run(const TemporalFusedArgs& a, hipStream_t s) {
   static const hipError_t attr = hipFuncSetAttribute((const void*)k_temporal_fused<T, V, EPI, C>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::LDS);
   if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_temporal_fused<T, V, EPI, C>), dim3(a.g.B), dim3(512), Gm::LDS, s, a);
+  hipLaunchKernelGGL((k_temporal_fused<T, V, EPI, C>), dim3(a.g.B), dim3(64 * tf_waves<T, V>()), Gm::LDS, s, a);
   return hipGetLastError();
 }
 

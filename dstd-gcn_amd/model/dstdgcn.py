@@ -407,6 +407,15 @@ class _BlockTrain(torch.autograd.Function):
         return (None, dx if need_dx else None, *arena.views())
 
 
+@torch._dynamo.disable
+def _host_seed():
+    """A dropout seed for the op branch of _ModelTrain: an integer drawn on
+    the host at run time (under torch.compile this is a graph break, not a
+    traced random value -- dynamo would turn one into a tensor, which the ops'
+    integer `seed` cannot take)."""
+    return random.randint(0, 2 ** 62 - 1)
+
+
 class _ModelTrain(torch.autograd.Function):
     """DSTDGCN forward + native backward (reference :293-317): train mode, or
     an eval-mode model under autograd (running-statistics BN, no dropout).
@@ -435,9 +444,10 @@ class _ModelTrain(torch.autograd.Function):
             # the op branch (torch.compile, subclass inputs): the ops' schema
             # carries the seed as an integer, so it is drawn on the host -- a
             # device tensor read by pointer would be invisible to the tracer
-            # (and a FakeTensor has no data pointer).  Python's random: dynamo
-            # re-draws it at run time, so every compiled call gets a new mask
-            seed = random.randint(0, 2 ** 62 - 1)
+            # (and a FakeTensor has no data pointer).  Drawn outside the traced
+            # region (_host_seed), so it stays an integer and every compiled call
+            # gets a new mask
+            seed = _host_seed()
         buffers = model._tree.get(model)[1]
         if eager:
             # eager: the op's implementation without the dispatcher's boxing
@@ -937,21 +947,25 @@ class DSTDGCN(_NativeModule):
         y = _ModelTrain.apply(self, True, x, *params)
         return y[:n], y[n:]
 
-    def graphed(self, x):
+    def graphed(self, x, frozen=False):
         """The eval forward for inputs shaped like ``x`` captured once into a
         HIP graph (no per-call launch or Python cost at small
         batch).  Returns ``run(x_new) -> y``: copies ``x_new`` into the graph's
         static input (skipped when it is that tensor, ``run.input``), replays
-        the 21 launches plus the two that fold BatchNorm and prepare the split
-        weight images -- so in-place parameter updates are seen by the next
-        replay -- and returns the graph's static output ``run.output``
-        (overwritten by the next replay).  New parameter storage (e.g.
+        the forward's launches and returns the graph's static output
+        ``run.output`` (overwritten by the next replay).  By default every
+        replay also re-runs the two launches that fold BatchNorm and prepare
+        the split weight images, so in-place parameter updates are seen by the
+        next replay.  ``frozen=True`` (serving fixed weights): the first call
+        folds, later ones replay the GC launches alone; after an in-place
+        parameter update call ``run.refresh()``.  New parameter storage (e.g.
         ``load_state_dict`` into fresh tensors, ``.to()``) needs a new capture."""
         if self.training:
             raise RuntimeError("DSTDGCN.graphed captures the eval forward: call .eval() first")
         dev = x.device
         native.require_device(x, "x")
         x_static = x.detach().clone().contiguous()
+        y_static = torch.empty_like(x_static)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.no_grad(), torch.cuda.stream(side):
@@ -961,18 +975,36 @@ class DSTDGCN(_NativeModule):
         g = torch.cuda.CUDAGraph()
         cap = torch.cuda.Stream(device=dev)  # a stream of its own: its workspace is private to this graph
         with torch.no_grad(), torch.cuda.graph(g, stream=cap):
-            y_static = self(x_static)
+            self._forward_native(x_static, y_static)
+        gf = None
+        if frozen:
+            # the same forward again on the same workspace: the claim finds the
+            # constants graph g folds there (same tag), so this capture holds
+            # only the GC launches
+            gf = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(gf, stream=cap):
+                self._forward_native(x_static, y_static)
         # the capture's workspace lives in the graph's memory pool: keep it
         # with the graph and out of the eager cache
         ws = native._ws_cache.pop((str(dev), cap.cuda_stream), (None, None))[0]
+        state = {"folded": False}
 
         def run(x_new):
             if x_new is not x_static:
                 x_static.copy_(x_new)
-            g.replay()
+            if gf is not None and state["folded"]:
+                gf.replay()
+            else:
+                g.replay()
+                state["folded"] = True
             return y_static
 
-        run.graph, run.input, run.output, run._workspace = g, x_static, y_static, ws
+        def refresh():
+            """(frozen) parameters changed in place: the next call refolds."""
+            state["folded"] = False
+
+        run.graph, run.graph_frozen, run.input, run.output, run._workspace = g, gf, x_static, y_static, ws
+        run.refresh = refresh
         return run
 
     def _forward_native(self, x, y, prof=None, arith=None):

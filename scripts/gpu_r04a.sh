@@ -18,7 +18,7 @@ export DSTD_AB_FOREIGN_LIB=1
 L=dstd-gcn_amd
 for cfg in h36m cmu 3dpw; do
   echo "# $cfg" >> $O/ab.txt
-  timeout -k 10 300 python -u scripts/ab_kernels.py $L/libdstd_gcn_r03.so $L/libdstd_gcn.so $L/libdstd_gcn_noslp.so --config $cfg --rounds 5 >> $O/ab.txt 2>&1 || exit 1
+  timeout -k 10 300 python -u scripts/ab_kernels.py $L/libdstd_gcn_r03.so $L/libdstd_gcn_tf8.so $L/libdstd_gcn.so $L/libdstd_gcn_sp3.so --config $cfg --rounds 5 >> $O/ab.txt 2>&1 || exit 1
 done
 grep -v amdgpu.ids $O/ab.txt | cut -c1-400
 timeout -k 10 120 python -u scripts/timeline.py $L/libdstd_gcn_stamps.so --hl > $O/timeline.txt 2>&1; st=$?

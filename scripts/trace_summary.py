@@ -6,9 +6,18 @@ import csv
 import sys
 
 
-def main(path, steps, top=25):
+def main(path, steps, top=25, marker=None, last=0):
+    """marker / last: only the last `last` complete steps, a step starting at
+    each launch whose name contains `marker` (once per step, e.g. k_prep_nctv
+    of the train forward): steady state, without the first steps' set-up
+    (model init, workspaces, lazy optimizer state)."""
     rows = list(csv.DictReader(open(path)))
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    if marker and last:
+        starts = [i for i, (_, _, k) in enumerate(iv) if marker in k]
+        if len(starts) > last:
+            iv = iv[starts[-last - 1]:starts[-1]]
+            steps = last
     tot = collections.defaultdict(lambda: [0, 0])
     for s, e, k in iv:
         t = tot[k.replace("(anonymous namespace)::", "").split("(")[0][-70:]]
@@ -32,4 +41,12 @@ def main(path, steps, top=25):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]) if len(sys.argv) > 3 else 25)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("steps", type=int)
+    ap.add_argument("top", type=int, nargs="?", default=25)
+    ap.add_argument("--marker", default=None, help="substring of the launch that starts a step (once per step)")
+    ap.add_argument("--last", type=int, default=0, help="summarise only the last N steps")
+    a = ap.parse_args()
+    main(a.trace, a.steps, a.top, a.marker, a.last)

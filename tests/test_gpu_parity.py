@@ -332,6 +332,33 @@ def test_graphed_forward_matches_eager(B):
         assert not torch.equal(y3, y2)
 
 
+@pytest.mark.parametrize("B", [4, 32])
+def test_graphed_frozen_forward(B):
+    """DSTDGCN.graphed(x, frozen=True): the first replay folds the constants,
+    later ones run the GC launches alone -- bit-identical to eager; after an
+    in-place parameter update the frozen graph keeps the old constants until
+    run.refresh(), then matches eager on the new weights."""
+    m, d, sd, opts = load_model("h36m")
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    x1 = synth(B, T, 22, opts["input_time_frame"], 21).to(DEV)
+    x2 = synth(B, T, 22, opts["input_time_frame"], 22).to(DEV)
+    with torch.no_grad():
+        run = m.graphed(x1, frozen=True)
+        assert run.graph_frozen is not None
+        y1 = run(x1).clone()  # folds
+        assert torch.equal(y1, m(x1))
+        y2 = run(x2).clone()  # the frozen graph
+        assert torch.equal(y2, m(x2))
+        assert torch.equal(run(x1), y1)
+        m.encoders[2][1].bn.running_var.mul_(1.5)
+        stale = run(x2).clone()
+        assert torch.equal(stale, y2)  # frozen: the old constants
+        run.refresh()
+        y3 = run(x2).clone()
+        assert torch.equal(y3, m(x2)) and not torch.equal(y3, y2)
+        assert torch.equal(run(x2), y3)
+
+
 def test_deterministic_repeat():
     m, d, _, _ = load_model("cmu")
     x = t(d["x"])
