@@ -938,54 +938,91 @@ __global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
 // ---------------------------------------------------------------------------
 // tanh outer difference
 // ---------------------------------------------------------------------------
+// A workgroup takes KB consecutive (n, r, a) blocks (tanh_kb): their M
+// blocks are one contiguous run of KB*NN*NN floats, moved as 16-byte
+// accesses (one block per workgroup left 529..1600 elements per 256 threads
+// and every workgroup paid a full staging round trip: 8..10 us launches for
+// 2..3 us of traffic at the config-5 batch, profiles/r03y_train_trace_summary.txt)
 constexpr int kTanhMaxNN = 128;  // the frame envelope (T <= 128; V <= 64)
-__global__ void k_tanh_outer_fwd(const float* __restrict__ P, const float* __restrict__ Q, PQView v, int R, int A,
-                                 int NN, float* __restrict__ M) {
-  // one workgroup per (n, r, a); M block [NN][NN]
-  const int blk = blockIdx.x;
+constexpr int kTanhMaxKB = 8;
+__device__ __forceinline__ size_t tanh_pq_base(const PQView& v, int blk, int R, int A) {
   const int n = blk / (R * A), ra = blk - n * R * A, r = ra / A, a = ra - r * A;
-  const float* p = P + n * v.sn + r * v.sr + a * v.sa;
-  const float* q = Q + n * v.sn + r * v.sr + a * v.sa;
-  float* m = M + (size_t)blk * NN * NN;
-  // the block's P and Q rows (strided in the caller's layout) staged once in
-  // LDS instead of two strided loads per output element
-  __shared__ float ps[kTanhMaxNN], qs[kTanhMaxNN];
-  for (int i = threadIdx.x; i < NN; i += blockDim.x) {
-    ps[i] = p[i * v.si];
-    qs[i] = q[i * v.si];
-  }
-  __syncthreads();
-#pragma unroll 4
-  for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
-    const int i = e / NN, j = e - i * NN;
-    m[e] = tanhf(ps[i] - qs[j]);
-  }
+  return n * v.sn + r * v.sr + a * v.sa;
 }
 
-__global__ void k_tanh_outer_bwd(const float* __restrict__ M, const float* __restrict__ dM, PQView v, int R, int A,
-                                 int NN, float* __restrict__ dP, float* __restrict__ dQ) {
-  extern __shared__ float dz[];  // [NN][NN+1]
-  const int blk = blockIdx.x;
-  const int n = blk / (R * A), ra = blk - n * R * A, r = ra / A, a = ra - r * A;
-  const float* m = M + (size_t)blk * NN * NN;
-  const float* dm = dM + (size_t)blk * NN * NN;
-#pragma unroll 4
-  for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
-    const int i = e / NN, j = e - i * NN;
-    const float t = m[e];
-    dz[i * (NN + 1) + j] = dm[e] * (1.f - t * t);
+__global__ __launch_bounds__(256) void k_tanh_outer_fwd(const float* __restrict__ P, const float* __restrict__ Q,
+                                                        PQView v, int R, int A, int NN, int nblk, int kb,
+                                                        float* __restrict__ M) {
+  // M block [NN][NN] per (n, r, a); the blocks' P and Q rows (strided in the
+  // caller's layout) staged once in LDS
+  __shared__ float ps[kTanhMaxKB * kTanhMaxNN], qs[kTanhMaxKB * kTanhMaxNN];
+  const int tid = threadIdx.x;
+  const int b0 = blockIdx.x * kb, nb = min(kb, nblk - b0), NN2 = NN * NN, tot = nb * NN2;
+  for (int e = tid; e < nb * NN; e += 256) {
+    const int k = e / NN, i = e - k * NN;
+    const size_t o = tanh_pq_base(v, b0 + k, R, A) + (size_t)i * v.si;
+    ps[e] = P[o];
+    qs[e] = Q[o];
   }
   __syncthreads();
-  const size_t base = n * v.sn + r * v.sr + a * v.sa;
-  for (int i = threadIdx.x; i < 2 * NN; i += blockDim.x) {
+  const size_t base = (size_t)b0 * NN2;
+  float* m = M + base;
+  auto val = [&](int e) {
+    const int k = e / NN2, rm = e - k * NN2, i = rm / NN, j = rm - i * NN;
+    return tanhf(ps[k * NN + i] - qs[k * NN + j]);
+  };
+  int e0 = 0;
+  if ((base & 3) == 0) {
+    const int t4 = tot >> 2;
+#pragma unroll 2
+    for (int q = tid; q < t4; q += 256)
+      *reinterpret_cast<float4*>(m + 4 * q) = make_float4(val(4 * q), val(4 * q + 1), val(4 * q + 2), val(4 * q + 3));
+    e0 = 4 * t4;
+  }
+  for (int e = e0 + tid; e < tot; e += 256) m[e] = val(e);
+}
+
+__global__ __launch_bounds__(256) void k_tanh_outer_bwd(const float* __restrict__ M, const float* __restrict__ dM,
+                                                        PQView v, int R, int A, int NN, int nblk, int kb,
+                                                        float* __restrict__ dP, float* __restrict__ dQ) {
+  extern __shared__ float dz[];  // [kb][NN][NN+1]
+  const int tid = threadIdx.x;
+  const int b0 = blockIdx.x * kb, nb = min(kb, nblk - b0), NN2 = NN * NN, tot = nb * NN2;
+  const size_t base = (size_t)b0 * NN2;
+  const float* m = M + base;
+  const float* dm = dM + base;
+  auto put = [&](int e, float t, float d) {
+    const int k = e / NN2, rm = e - k * NN2, i = rm / NN, j = rm - i * NN;
+    dz[(k * NN + i) * (NN + 1) + j] = d * (1.f - t * t);
+  };
+  int e0 = 0;
+  if ((base & 3) == 0) {
+    const int t4 = tot >> 2;
+#pragma unroll 4
+    for (int q = tid; q < t4; q += 256) {
+      const float4 t = *reinterpret_cast<const float4*>(m + 4 * q);
+      const float4 d = *reinterpret_cast<const float4*>(dm + 4 * q);
+      put(4 * q, t.x, d.x);
+      put(4 * q + 1, t.y, d.y);
+      put(4 * q + 2, t.z, d.z);
+      put(4 * q + 3, t.w, d.w);
+    }
+    e0 = 4 * t4;
+  }
+  for (int e = e0 + tid; e < tot; e += 256) put(e, m[e], dm[e]);
+  __syncthreads();
+  for (int o = tid; o < nb * 2 * NN; o += 256) {
+    const int k = o / (2 * NN), i = o - k * 2 * NN;
+    const size_t pb = tanh_pq_base(v, b0 + k, R, A);
+    const float* z = dz + k * NN * (NN + 1);
     float s = 0.f;
     if (i < NN) {
-      for (int j = 0; j < NN; ++j) s += dz[i * (NN + 1) + j];
-      dP[base + i * v.si] = s;
+      for (int j = 0; j < NN; ++j) s += z[i * (NN + 1) + j];
+      dP[pb + i * v.si] = s;
     } else {
       const int j = i - NN;
-      for (int k = 0; k < NN; ++k) s += dz[k * (NN + 1) + j];
-      dQ[base + j * v.si] = -s;
+      for (int r = 0; r < NN; ++r) s += z[r * (NN + 1) + j];
+      dQ[pb + j * v.si] = -s;
     }
   }
 }
@@ -1329,8 +1366,10 @@ __device__ __forceinline__ void bn_local_merge(int cv, int ch, int rows, int spl
   m2 = q;
 }
 
-__device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows, int splits, const float* part, int g,
-                                               float& mean, float& rstd, bool store) {
+// part: channel c's split partials [group][split][V][2] (staged in LDS by
+// k_bn_apply_merged), v: the joint of ch = c * V + v
+__device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int v, int V, int rows, int splits,
+                                               const float* part, int g, float& mean, float& rstd, bool store) {
   if (a.use_running) {
     mean = a.running_mean[ch];
     rstd = 1.f / sqrtf(a.running_var[ch] + a.eps);
@@ -1354,7 +1393,7 @@ __device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int rows,
         m2 += q[w * rs + 1] + q[w * rs + 2] * d * d;
       }
     } else {
-      bn_local_merge(a.cv, ch, rows, splits, part, g, m, m2);
+      bn_local_merge(V, v, rows, splits, part, g, m, m2);
     }
     const float var = m2 / n;
     mean = m;
@@ -1388,20 +1427,38 @@ __global__ __launch_bounds__(256) void k_bn_local_stats(int cv, int rows, int sp
 __global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, int T, int V, int splits,
                                                          const float* part, int ns) {
   __shared__ float scl[kBnMaxV], shl[kBnMaxV];
+  // channel c's split partials of the groups this workgroup merges, staged
+  // with every load in flight at once (merging straight from memory chains
+  // 2 x splits dependent loads per group)
+  constexpr int kPl = 2 * kBnMaxSplits * 2 * kBnMaxV, kPlU = kPl / 256;
+  __shared__ float pl[kPl];  // [group][split][V][2]
   const int c = blockIdx.x, n = blockIdx.y * ns, tid = threadIdx.x;
+  const int Bg = B / a.groups, g = n / Bg;
+  if (!a.use_running && !a.gath) {
+    const int per = splits * 2 * V, g0 = n == 0 ? 0 : g, cnt = (n == 0 ? a.groups : 1) * per;
+    float pv[kPlU];
+#pragma unroll
+    for (int u = 0; u < kPlU; ++u) {
+      const int e = min(tid + 256 * u, cnt - 1), gs = e / (2 * V), q = e - gs * 2 * V;  // gs = (group - g0) * splits + sp
+      pv[u] = part[((size_t)(g0 * splits + gs) * a.cv + c * V) * 2 + q];
+    }
+#pragma unroll
+    for (int u = 0; u < kPlU; ++u)
+      if (tid + 256 * u < cnt) pl[g0 * per + tid + 256 * u] = pv[u];
+  }
+  __syncthreads();
   if (tid < V) {
     const int ch = c * V + tid;
-    const int Bg = B / a.groups, g = n / Bg;
     float mean, rstd;
     // workgroup (c, 0) stores every group's mean / rstd and applies the
     // groups' running-statistics updates in group order
     if (n == 0)
       for (int gg = 1; gg < a.groups; ++gg) {
         float m_, r_;
-        bn_merge_stats(a, ch, Bg * T, splits, part, gg - 1, m_, r_, true);
+        bn_merge_stats(a, ch, tid, V, Bg * T, splits, pl, gg - 1, m_, r_, true);
       }
-    bn_merge_stats(a, ch, Bg * T, splits, part, n == 0 ? a.groups - 1 : g, mean, rstd, n == 0);
-    if (n == 0 && a.groups > 1) bn_merge_stats(a, ch, Bg * T, splits, part, 0, mean, rstd, false);
+    bn_merge_stats(a, ch, tid, V, Bg * T, splits, pl, n == 0 ? a.groups - 1 : g, mean, rstd, n == 0);
+    if (n == 0 && a.groups > 1) bn_merge_stats(a, ch, tid, V, Bg * T, splits, pl, 0, mean, rstd, false);
     const float sc = rstd * a.gamma[ch];
     scl[tid] = sc;
     shl[tid] = a.beta[ch] - mean * sc;
@@ -1976,19 +2033,29 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
 
 
 
+// blocks per workgroup: the most of 8 / 4 / 2 that keeps >= 512 workgroups,
+// with the backward's dz tiles within 64 KB of LDS
+int tanh_kb(int nblk, int NN) {
+  for (int kb : {kTanhMaxKB, 4, 2})
+    if (nblk >= 512 * kb && (size_t)kb * NN * (NN + 1) * sizeof(float) <= 64 * 1024) return kb;
+  return 1;
+}
+
 hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int R, int A, int NN, float* M,
                           hipStream_t s) {
   if (NN > kTanhMaxNN) return hipErrorInvalidValue;
-  k_tanh_outer_fwd<<<B * R * A, 256, 0, s>>>(P, Q, v, R, A, NN, M);
+  const int nblk = B * R * A, kb = tanh_kb(nblk, NN);
+  k_tanh_outer_fwd<<<cdiv(nblk, kb), 256, 0, s>>>(P, Q, v, R, A, NN, nblk, kb, M);
   return hipGetLastError();
 }
 
 hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int R, int A, int NN, float* dP,
                           float* dQ, hipStream_t s) {
-  const size_t lds = (size_t)NN * (NN + 1) * sizeof(float);  // 66 KB at the T = 128 envelope top
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (NN > kTanhMaxNN) return hipErrorInvalidValue;
+  const int nblk = B * R * A, kb = tanh_kb(nblk, NN);
+  const size_t lds = (size_t)kb * NN * (NN + 1) * sizeof(float);  // 66 KB at the T = 128 envelope top (kb 1)
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_tanh_outer_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  k_tanh_outer_bwd<<<B * R * A, 256, lds, s>>>(M, dM, v, R, A, NN, dP, dQ);
+  k_tanh_outer_bwd<<<cdiv(nblk, kb), 256, lds, s>>>(M, dM, v, R, A, NN, nblk, kb, dP, dQ);
   return hipGetLastError();
 }
 

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <initializer_list>
+#include <mutex>
 #include <vector>
 
 #include "../../include/dstd_gcn_train.h"
@@ -29,7 +30,7 @@ constexpr int kMaxV = 32;
 constexpr int kMaxC = 64;
 constexpr int kMaxRed = 8;  // red_channels of one DSTDGC (P / Q channels each)
 constexpr unsigned kTrainFlags = DSTD_TRAIN_RUNNING_STATS | DSTD_TRAIN_PAIRED;
-constexpr unsigned kModelTrainFlags = kTrainFlags | DSTD_TRAIN_SEED_DEVICE;
+constexpr unsigned kModelTrainFlags = kTrainFlags | DSTD_TRAIN_SEED_DEVICE | DSTD_TRAIN_ONE_STREAM;
 
 struct Carver {
   char* base;
@@ -139,6 +140,111 @@ bool pack_jobs(CopyJobs& js, const dstd_gc_weights* w, const OpSaved& sv, const 
 struct OpWs {
   float *dG, *dD, *dM, *gW, *gs, *part, *red;
   float* dDp;  // channel-chunk partials of dD (agg_bwd), null when one chunk suffices
+  // the second dG / dD set and the GEMM scratch of the weight-gradient stream
+  // (WgradStream): consecutive ops alternate sets so that an op's weight
+  // gradients can still read its dE / dG while the next op runs
+  float *dG2, *dD2, *gs2;
+};
+
+// ---------------------------------------------------------------------------
+// Weight-gradient stream of the model backward.  An op's two weight-gradient
+// reductions -- dW_rm (reads dE, M) and [dW_f | dW_m1 | dW_m2 | db] (reads
+// dG, x) -- feed nothing later in the backward, so they run on a second HIP
+// stream, forked from the caller's stream by events, while the caller's
+// stream goes on with the input-gradient chain (dM, tanh', dx and the next
+// op).  Their 256..1152-workgroup launches leave most CUs idle at the
+// config-5 batch (one workgroup per CU), which the two chains now share.
+// Everything joins back into the caller's stream before the backward returns
+// (also inside a HIP graph capture: the fork / join events pull the second
+// stream into the capture).  Results are bit-identical to the one-stream
+// order: every reduction keeps its own fixed order and no two concurrent
+// kernels write the same memory.
+// ---------------------------------------------------------------------------
+struct WgradRes {
+  int dev = -1;
+  bool busy = false;  // held by a backward call (host side)
+  hipStream_t st = nullptr;
+  hipEvent_t fork, done[2], join;
+};
+// A free set of the current device's (created on first use -- in practice by
+// an eager warm-up step, not inside a graph capture); concurrent host threads
+// get different sets, consecutive calls share one.
+std::mutex g_wgrad_mu;
+WgradRes* wgrad_acquire() {
+#ifdef DSTD_TRAIN_NO_WGRAD_STREAM
+  return nullptr;
+#else
+  static std::vector<WgradRes*> pool;
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_wgrad_mu);
+  for (WgradRes* r : pool)
+    if (r->dev == dev && !r->busy) {
+      r->busy = true;
+      return r;
+    }
+  WgradRes* r = new WgradRes;
+  r->dev = dev;
+  bool ok = hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&r->fork, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&r->done[0], hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&r->done[1], hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&r->join, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    (void)hipGetLastError();
+    delete r;  // (a partly created set leaks its handles; creation failing means the device is gone)
+    return nullptr;
+  }
+  r->busy = true;
+  pool.push_back(r);
+  return r;
+#endif
+}
+void wgrad_release(WgradRes* r) {
+  if (!r) return;
+  std::lock_guard<std::mutex> lk(g_wgrad_mu);
+  r->busy = false;
+}
+
+// One backward's use of the weight-gradient stream (null res: one stream).
+struct Wgrad {
+  WgradRes* res = nullptr;
+  Wgrad() = default;
+  explicit Wgrad(WgradRes* r) : res(r) {}
+  ~Wgrad() { wgrad_release(res); }
+  Wgrad(const Wgrad&) = delete;
+  Wgrad& operator=(const Wgrad&) = delete;
+  hipStream_t main = nullptr;
+  int next = 0;
+  bool used[2] = {false, false};
+  bool any = false;
+  // the dG / dD set of the next op (waits until the op two back has released it)
+  hipError_t take(const OpWs& w, float*& dG, float*& dD, int& slot) {
+    if (!res) {
+      dG = w.dG, dD = w.dD, slot = 0;
+      return hipSuccess;
+    }
+    slot = next;
+    next ^= 1;
+    dG = slot ? w.dG2 : w.dG;
+    dD = slot ? w.dD2 : w.dD;
+    if (used[slot]) return hipStreamWaitEvent(main, res->done[slot], 0);
+    return hipSuccess;
+  }
+  // the side stream continues after everything enqueued on main so far
+  hipError_t fork() {
+    DSTD_TRYH(hipEventRecord(res->fork, main));
+    return hipStreamWaitEvent(res->st, res->fork, 0);
+  }
+  hipError_t release(int slot) {
+    used[slot] = any = true;
+    return hipEventRecord(res->done[slot], res->st);
+  }
+  hipError_t join() {
+    if (!res || !any) return hipSuccess;
+    DSTD_TRYH(hipEventRecord(res->join, res->st));
+    return hipStreamWaitEvent(main, res->join, 0);
+  }
 };
 // Reduction / BatchNorm / adjacency-backward scratch for a geometry.
 size_t red_floats(const OpGeom& g) {
@@ -167,6 +273,9 @@ void carve_op_ws(Carver& cv, OpWs& w, const std::vector<OpGeom>& gl) {
   w.part = cv.take(std::max(dot_partials(), mpjpe_partials()));
   w.red = cv.take(nred);
   w.dDp = nDp ? cv.take(nDp) : nullptr;
+  w.dG2 = cv.take(nG);
+  w.dD2 = cv.take(nD);
+  w.gs2 = cv.take(gemm_scratch_floats((int)nmn, 1));
 }
 
 // 1x1 conv as GEMMs over NCTV (W [cout][cin]).
@@ -247,9 +356,18 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
 // dx_beta 0: dx (=) instead of (+=); assign_dA: dA likewise (block-internal
 // buffers; the op entry point accumulates both)
 hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* alpha, const OpSaved& sv,
-                  const float* dy, float* dx, const dstd_gc_grads* gr, float* dA, float* dalpha, const OpWs& ws,
-                  hipStream_t s, float dx_beta = 1.f, int assign_dA = 0) {
+                  const float* dy, float* dx, const dstd_gc_grads* gr, float* dA, float* dalpha, const OpWs& ws0,
+                  hipStream_t s, float dx_beta = 1.f, int assign_dA = 0, Wgrad* wg = nullptr) {
   const long long ldG = (long long)g.CG() * g.TV;
+  OpWs ws = ws0;
+  int slot = 0;
+  Wgrad none;
+  if (!wg) wg = &none;
+  wg->main = s;
+  DSTD_TRYH(wg->take(ws0, ws.dG, ws.dD, slot));
+  // the weight-gradient reductions' stream and scratch
+  const hipStream_t ws_s = wg->res ? wg->res->st : s;
+  float* const ws_gs = wg->res ? ws.gs2 : ws.gs;
   // dF -> rows [0, cout) of dG; dD in place or as channel-chunk partials
   int nparts = 0;
   const hipError_t ae = agg_bwd(sv.G, ldG, dy, (long long)g.cout * g.TV, sv.D, ws.dG, ldG, ws.dD, g.B, g.cout, g.T, g.V,
@@ -281,7 +399,8 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   wr.B = sv.M, wr.b_b1 = (long long)g.R * g.A * g.NN2, wr.b_k = 1, wr.b_n = g.NN2;
   wr.C = gr->wrm, wr.c_m = g.R * g.A, wr.c_n = 1;
   wr.beta = 1.f;
-  DSTD_TRYH(gemm(wr, ws.gs, s));
+  if (wg->res) DSTD_TRYH(wg->fork());
+  DSTD_TRYH(gemm(wr, ws_gs, ws_s));
   Gemm dm;  // dM[n][k][ij] = sum_a Wrm[a][k] dE[n][a][ij]
   dm.M = g.R * g.A, dm.N = g.NN2, dm.K = g.A, dm.nb1 = g.B;
   dm.A = w->wrm, dm.a_m = 1, dm.a_k = g.R * g.A;
@@ -291,12 +410,6 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   // dP, dQ -> rows [cout, cout + 2R) of dG
   float* dP = ws.dG + (size_t)g.cout * g.TV;
   DSTD_TRYH(tanh_outer_bwd(sv.M, ws.dM, g.pq(), g.B, g.R, g.A, g.NN, dP, dP + (size_t)g.R * g.TV, s));
-  // the three 1x1 convs at once: dx += Wp^T dG;  [dWp | dbp] = sum dG [x; 1]^T
-  if (dx) {
-    Gemm gx = conv_dx(sv.Wp, ws.dG, dx, g.B, g.cin, g.CG(), g.TV);
-    gx.beta = dx_beta;
-    DSTD_TRYH(gemm(gx, ws.gs, s));
-  }
   // rows [0, cout) / [cout, cout+R) / [cout+R, cout+2R) of [dWp | dbp]
   // accumulate straight into the conv_f / conv_m1 / conv_m2 gradients
   Gemm gw = conv_dw(ws.dG, x, ws.gW, g.B, g.cin + 1, g.CG(), g.TV);
@@ -306,7 +419,18 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   gw.seg[0] = Gemm::Seg{0, g.cout, gr->wf, gr->bf};
   gw.seg[1] = Gemm::Seg{g.cout, g.R, gr->wm1, gr->bm1};
   gw.seg[2] = Gemm::Seg{g.cout + g.R, g.R, gr->wm2, gr->bm2};
-  return gemm(gw, ws.gs, s);
+  if (wg->res) {  // queued before dx, which then runs beside it
+    DSTD_TRYH(wg->fork());
+    DSTD_TRYH(gemm(gw, ws_gs, ws_s));
+    DSTD_TRYH(wg->release(slot));
+  }
+  // the three 1x1 convs at once: dx += Wp^T dG;  [dWp | dbp] = sum dG [x; 1]^T
+  if (dx) {
+    Gemm gx = conv_dx(sv.Wp, ws.dG, dx, g.B, g.cin, g.CG(), g.TV);
+    gx.beta = dx_beta;
+    DSTD_TRYH(gemm(gx, ws.gs, s));
+  }
+  return wg->res ? hipSuccess : gemm(gw, ws.gs, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -424,14 +548,14 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
 hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, int V, const BlockSaved& S,
                      const float* dy, float* dx, const dstd_block_grads* g, const BlockWs& W, hipStream_t s,
                      int run = 0, bool dx_init = false, const float* dx_extra = nullptr,
-                     const dstd_bn_sync* sync = nullptr) {
+                     const dstd_bn_sync* sync = nullptr, Wgrad* wg = nullptr) {
   const int cin = p->cin, cout = p->cout, TV = T * V;
   const bool res = cin != cout;
   const size_t act = (size_t)B * cout * TV;
   const OpGeom gt(DSTD_MODE_TEMPORAL, B, cout, cout, T, V);
   // A_t + R_t: dR_t = dA; dh (=) the temporal op's input gradient
   DSTD_TRYH(op_bwd(gt, S.h, &p->conv_t, p->alpha_tm, S.op[2], dy, W.dh, &g->conv_t, g->R_t, g->alpha_tm, W.op, s,
-                   0.f));
+                   0.f, 0, wg));
   BnBwd bb;
   bb.x = S.ysp;
   bb.zsave = S.z;
@@ -471,7 +595,7 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
   for (int i = 0; i < 2; ++i)  // each graph's dA (=) into its own half of dAs
     DSTD_TRYH(op_bwd(gs, x, &p->conv_s[i], p->alpha_sm, S.op[i], W.dysp, dx, &g->conv_s[i], W.dAs + i * V * V,
-                     g->alpha_sm, W.op, s, 1.f, 1));
+                     g->alpha_sm, W.op, s, 1.f, 1, wg));
   // A_s*W_s + R_s with A_s constant: dR_s = dA, dW_s = dA * A_s (both graphs)
   return adj_param_grads(W.dAs, p->A_s, g->R_s, g->W_s, (size_t)2 * V * V, s);
 }
@@ -810,11 +934,13 @@ int dstd_model_train_bwd_sync(const dstd_model_params* p, const float* x, int B,
   ModelWs W;
   carve_model_ws(cw, W, B, T, V, C);
   const size_t act = (size_t)B * C * T * V;
+  Wgrad wg((flags & DSTD_TRAIN_ONE_STREAM) ? nullptr : wgrad_acquire());
+  wg.main = s;
   DSTD_TRY(out_ntvc_bwd(dy, B, T, V, 3, W.dO, s));
   float* dha = W.dha;
   float* dhb = W.dhb;
   DSTD_TRY(block_bwd(&p->st_out, S.h[L], B, T, V, S.st_out, W.dO, dha, &g->st_out, W.blk, s, run, true, nullptr,
-                     sync));
+                     sync, &wg));
   for (int i = L - 1; i >= 0; --i) {
     BnBwd be;
     be.x = S.yb[i];
@@ -834,7 +960,7 @@ int dstd_model_train_bwd_sync(const dstd_model_params* p, const float* x, int B,
     DSTD_TRY(bn_train_bwd(be, B, C, T, V, W.blk.op.red, g->enc_prelu[i], s));
     // u = block(h) + h: dh = du (identity path) + block backward
     DSTD_TRY(block_bwd(&p->enc[i], S.h[i], B, T, V, S.enc[i], W.du, dhb, &g->enc[i], W.blk, s, run, true, W.du,
-                       sync));
+                       sync, &wg));
     std::swap(dha, dhb);
   }
   if (dropout_p > 0.f) DSTD_TRY(dropout(dha, dha, act, dropout_p, seed, s, (flags & DSTD_TRAIN_SEED_DEVICE) != 0));
@@ -854,8 +980,9 @@ int dstd_model_train_bwd_sync(const dstd_model_params* p, const float* x, int B,
   b0.sync = sync;
   DSTD_TRY(bn_train_bwd(b0, B, C, T, V, W.blk.op.red, g->prelu, s));
   DSTD_TRY(block_bwd(&p->st_in, S.X0, B, T, V, S.st_in, W.du, dx ? W.dX0 : nullptr, &g->st_in, W.blk, s, run, true,
-                     nullptr, sync));
+                     nullptr, sync, &wg));
   if (dx) DSTD_TRY(prep_nctv_bwd(W.dX0, dy, B, T, V, 3, dx, s));  // :298-303, 315
+  DSTD_TRY(wg.join());
   return DSTD_OK;
 }
 

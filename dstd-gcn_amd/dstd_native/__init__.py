@@ -87,6 +87,7 @@ class BnSyncStruct(ctypes.Structure):
 TRAIN_RUNNING_STATS = 1  # include/dstd_gcn_train.h DSTD_TRAIN_RUNNING_STATS
 TRAIN_PAIRED = 2  # DSTD_TRAIN_PAIRED: two BatchNorm batches of B/2 (a forward pair)
 TRAIN_SEED_DEVICE = 4  # DSTD_TRAIN_SEED_DEVICE: the dropout seed is read from device memory
+TRAIN_ONE_STREAM = 8  # DSTD_TRAIN_ONE_STREAM: no weight-gradient stream in the model backward
 FWD_REUSE_CONSTANTS = 1  # include/dstd_gcn.h DSTD_FWD_REUSE_CONSTANTS
 FWD_EXACT_FP32 = 2  # include/dstd_gcn.h DSTD_FWD_EXACT_FP32
 FWD_SEPARATE_ADJ = 4  # include/dstd_gcn.h DSTD_FWD_SEPARATE_ADJ
@@ -203,12 +204,14 @@ def lib():
         L.dstd_model_train_bwd_ex.restype = ci
         L.dstd_model_train_bwd_ex.argtypes = [ctypes.POINTER(ModelParams), vp, ci, f32, u64, vp, sz, vp,
                                               ctypes.POINTER(ModelGrads), vp, vp, sz, vp, uf]
-        L.dstd_bn_sync_buffer_floats.restype = sz
-        L.dstd_bn_sync_buffer_floats.argtypes = [ci, ci, ci]
-        L.dstd_model_train_fwd_sync.restype = ci
-        L.dstd_model_train_fwd_sync.argtypes = L.dstd_model_train_fwd_ex.argtypes + [ctypes.POINTER(BnSyncStruct)]
-        L.dstd_model_train_bwd_sync.restype = ci
-        L.dstd_model_train_bwd_sync.argtypes = L.dstd_model_train_bwd_ex.argtypes + [ctypes.POINTER(BnSyncStruct)]
+        # (absent from a round-3 library loaded for an A/B: only SyncBN calls them)
+        if hasattr(L, "dstd_bn_sync_buffer_floats"):
+            L.dstd_bn_sync_buffer_floats.restype = sz
+            L.dstd_bn_sync_buffer_floats.argtypes = [ci, ci, ci]
+            L.dstd_model_train_fwd_sync.restype = ci
+            L.dstd_model_train_fwd_sync.argtypes = L.dstd_model_train_fwd_ex.argtypes + [ctypes.POINTER(BnSyncStruct)]
+            L.dstd_model_train_bwd_sync.restype = ci
+            L.dstd_model_train_bwd_sync.argtypes = L.dstd_model_train_bwd_ex.argtypes + [ctypes.POINTER(BnSyncStruct)]
         L.dstd_loss_workspace_bytes.restype = sz
         L.dstd_loss_workspace_bytes.argtypes = []
         L.dstd_mpjpe_fwd.restype = ci

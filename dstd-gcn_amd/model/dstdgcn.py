@@ -429,6 +429,8 @@ class _ModelTrain(torch.autograd.Function):
     def forward(ctx, model, paired, x, *params):
         # paired: x is two train-mode batches of B/2 (DSTDGCN.forward_pair)
         flags = _bn_flags(model) | (native.TRAIN_PAIRED if paired else 0)
+        if getattr(model, "_dstd_one_stream", False):  # the backward's launches all on the caller's stream
+            flags |= native.TRAIN_ONE_STREAM
         drop = float(model.do_in.p) if model.do_in.training else 0.0
         seed, ctx.seed_t = 0, None
         eager = type(x) is torch.Tensor and not torch.compiler.is_compiling()

@@ -1,26 +1,34 @@
 #!/bin/bash
-# round 4 (r04a): VALU trims of the split GC kernels (one v_max3 per two
-# range-detection values, PReLU as one median, half-empty splits, zero-pad
-# plane reads) -- parity suite of the forward, MFMA shape rates, same-box A/B
-# against the round-3 library and a no-SLP build, phase timeline, kernel trace.
+# round 4 (r04c): forward -- VALU trims of the split GC kernels, 12-wave fused
+# temporal at H36M, slot-ordered phase-1/3 tables, late spatial residual:
+# parity suite, same-box A/B against the round-3 library (r03), the 8-wave
+# fused kernel (tf8) and 3-wave spatial (sp3), phase timeline.  Training --
+# batched tanh-outer kernels, LDS-staged BN merge, weight-gradient stream:
+# the training suite (incl. the bit-identity test of the two streams) and the
+# training-step A/B main / nows (one stream) / r03.  Kernel trace of the bench.
 cd "$(dirname "$0")/.." || exit 2
 R="$PWD"
-O=$R/gpurun_out/r04a
+O=$R/gpurun_out/r04c
 mkdir -p $O
-timeout -k 10 60 scripts/micro/mfma_rate > $O/mfma_rate.txt 2>&1; st=$?; cat $O/mfma_rate.txt; [ $st -eq 0 ] || exit $st
+L=dstd-gcn_amd
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_parity.py > $O/pytest_parity.log 2>&1
 st=$?; tail -3 $O/pytest_parity.log; [ $st -eq 0 ] || exit $st
-timeout -k 10 400 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread -m gpu tests/test_gpu_train.py -k "training_batch or graphed or step_gradients" > $O/pytest_train.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread -m gpu tests/test_gpu_train.py > $O/pytest_train.log 2>&1
 st=$?; grep -E "B=|passed|failed" $O/pytest_train.log | tail -5; [ $st -eq 0 ] || exit $st
 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_dist.py > $O/pytest_dist.log 2>&1
 st=$?; tail -3 $O/pytest_dist.log; [ $st -eq 0 ] || exit $st
 export DSTD_AB_FOREIGN_LIB=1
-L=dstd-gcn_amd
 for cfg in h36m cmu 3dpw; do
   echo "# $cfg" >> $O/ab.txt
   timeout -k 10 300 python -u scripts/ab_kernels.py $L/libdstd_gcn_r03.so $L/libdstd_gcn_tf8.so $L/libdstd_gcn.so $L/libdstd_gcn_sp3.so --config $cfg --rounds 5 >> $O/ab.txt 2>&1 || exit 1
 done
 grep -v amdgpu.ids $O/ab.txt | cut -c1-400
+for r in 1 2; do
+  for lib in libdstd_gcn libdstd_gcn_nows libdstd_gcn_r03; do
+    DSTD_LIB="$R/$L/$lib.so" timeout -k 10 300 python -u scripts/bench_train.py --batch 32 256 > $O/train_$lib.$r.log 2>&1
+    st=$?; echo "$lib round $r exit $st"; grep metric $O/train_$lib.$r.log | cut -c1-420; [ $st -eq 0 ] || exit $st
+  done
+done
 timeout -k 10 120 python -u scripts/timeline.py $L/libdstd_gcn_stamps.so --hl > $O/timeline.txt 2>&1; st=$?
 grep -v amdgpu.ids $O/timeline.txt | head -60; [ $st -eq 0 ] || exit $st
 export TMPDIR=/tmp

@@ -354,6 +354,40 @@ def test_model_step_gradients_at_training_batch(B):
     check_tail(ratios)
 
 
+def test_wgrad_stream_is_bit_identical():
+    """The model backward's weight-gradient stream (each DSTDGC's dW_rm and
+    packed-conv weight reductions forked onto a second HIP stream, alternating
+    dG / dD buffer sets; dstd_train_capi.hip WgradStream) against every launch
+    on the caller's stream (DSTD_TRAIN_ONE_STREAM): the same step at the
+    training batch gives bit-identical gradients and input gradient, three
+    times over (a missing fork / release / join shows up as a difference)."""
+    from engine import mpjpe_error_3d
+    m, _ = _model_3dpw()
+    g = torch.Generator().manual_seed(77)
+    B, T, VC = 32, 40, 69
+    seq = (0.6 * torch.randn(B, T, VC, generator=g)).to(DEV)
+    inp = seq.clone()
+    inp[:, 10:] = inp[:, 9:10]
+
+    def step(one_stream):
+        m._dstd_one_stream = one_stream
+        m.zero_grad(set_to_none=True)
+        x = inp.view(B, T, 23, 3).clone().requires_grad_(True)
+        loss = mpjpe_error_3d(m(x).reshape(B, T, VC), seq)
+        loss.backward()
+        return [p.grad.clone() for p in m.parameters() if p.grad is not None] + [x.grad.clone()]
+
+    with torch.random.fork_rng(devices=[DEV]):
+        ref = step(True)
+    for _ in range(3):
+        with torch.random.fork_rng(devices=[DEV]):
+            got = step(False)
+        assert len(got) == len(ref)
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b)
+    m._dstd_one_stream = False
+
+
 @pytest.mark.parametrize("inplace", [True, False])
 def test_forward_pair_equals_two_calls(inplace):
     """DSTDGCN.forward_pair (DSTD_TRAIN_PAIRED: one launch sequence over the
