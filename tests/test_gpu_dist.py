@@ -217,14 +217,19 @@ def test_syncbn_dp_step_equals_full_batch_step():
     for r in (0, 1):
         # 15 BatchNorms x (forward all-gather, backward all-reduce) per model call
         assert res[r]["calls"] > 0
+        table = []  # (sync error, per-rank BN error, name) relative to the tensor's largest entry
         for n, g in ref.items():
-            scale = float(g.abs().max())
+            scale = max(float(g.abs().max()), 1e-30)
             err = float((res[r]["g_sync"][n] - g).abs().max())
             if n.endswith("residual.0.bias"):  # analytically zero (a train-mode BN follows)
                 assert err < 1e-3, n
                 continue
-            assert err <= 1e-4 * scale + 1e-12, (r, n, err, scale)
-            worst_local = max(worst_local, float((res[r]["g_local"][n] - g).abs().max()) / max(scale, 1e-30))
+            loc = float((res[r]["g_local"][n] - g).abs().max()) / scale
+            table.append((err / scale, loc, n))
+            worst_local = max(worst_local, loc)
+        table.sort(reverse=True)
+        bad = [t for t in table if t[0] > 1e-4]
+        assert not bad, (r, len(bad), len(table), table[:12])
         for n, b in ref_bufs.items():
             if n.endswith("num_batches_tracked"):
                 assert int(res[r]["b_sync"][n]) == int(b), n
