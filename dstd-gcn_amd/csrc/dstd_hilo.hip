@@ -45,7 +45,7 @@ extern "C" int dstd_debug_w(unsigned* host) {
 // modes: 0 k_adj_hl<0>, 1 k_adj_hl<1>, 2 k_temporal_fused phase 3 (start,
 // E/F ready, tiles issued, stores drained), 3 k_temporal_fused C = 64 (entry,
 // chunk 0 phase 1 done, units done, exit)
-__device__ unsigned long long g_tl_hl[4][2048][4];
+__device__ unsigned long long g_tl_hl[5][2048][4];
 #define TLH(m, i) \
   if (threadIdx.x == 0 && blockIdx.x < 2048) g_tl_hl[m][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();
 #else
@@ -1926,7 +1926,7 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, cl = lane & 15;
   const int n = blockIdx.x;  // one sample per workgroup
-  if constexpr (C == 64) { TLH(3, 0) }
+  if constexpr (C == 64) { TLH(3, 0) TLH(4, 0) }
 
   {
     for (int ch = 0; ch < Gm::NCHUNK; ++ch) {
@@ -2033,6 +2033,9 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
           Fl[T * SE + i] = 0.f;
         }
         __syncthreads();
+      }
+      if constexpr (C == 64) {
+        if (ch == 0) { TLH(4, 1) }
       }
       // ---- phase 1: the chunk's planes ----
       // The GEMM runs transposed -- the tanh fragments as the A operand,
@@ -2176,6 +2179,9 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
         }
       }
 #endif
+      if constexpr (C == 64) {
+        if (ch == 0) { TLH(4, 2) }
+      }
       __syncthreads();  // planes complete; the phase-1 scratch is free
       if constexpr (C == 64) {
         if (ch == 0) { TLH(3, 1) }
@@ -2190,6 +2196,9 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
       // ---- phase 2: the stage, then the chunk's GC units ----
       stage_temporal<T, EPI, C, V, NT>(a, st, tid, Gm::NCHUNK > 1 ? opaque_zero() : 0);
       __syncthreads();
+      if constexpr (C == 64) {
+        if (ch == 0) { TLH(4, 3) }
+      }
       const int ub = n * V + v0;
       // (a lane outside the planes -- frame past T, slot group past ng(s) --
       // reads the joint block's zeroed 16-byte pad instead: no exec-masked
@@ -2401,7 +2410,7 @@ hipError_t launch_temporal_hl(const TemporalHLArgs& a, hipStream_t s) {
 
 #ifdef DSTD_STAMPS
 extern "C" int dstd_debug_timeline_hl(int mode, unsigned long long* host, int n) {
-  if (mode < 0 || mode > 3 || n > 2048 * 4) return 1;
+  if (mode < 0 || mode > 4 || n > 2048 * 4) return 1;
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tl_hl), n * sizeof(unsigned long long),
                                   mode * 2048 * 4 * sizeof(unsigned long long));
 }

@@ -37,8 +37,9 @@ def main():
         torch.cuda.synchronize()
     buf = np.zeros(2048 * 4, dtype=np.uint64)
     names = {0: "k_adj_hl<0>", 1: "k_adj_hl<1>", 2: "k_temporal_fused phase 3 (start, E/F, tiles, drained)",
-             3: "k_temporal_fused C=64 (entry, chunk-0 phase 1, units, exit)"}
-    for mode in ((0, 1, 2, 3) if "--hl" in sys.argv else (0, 1)):
+             3: "k_temporal_fused C=64 (entry, chunk-0 phase 1, units, exit)",
+             4: "k_temporal_fused C=64 chunk 0 (entry, phase-1 prologue, wave 0's tiles, stage)"}
+    for mode in ((0, 1, 2, 3, 4) if "--hl" in sys.argv else (0, 1)):
         fn(mode, buf.ctypes.data, buf.size)
         raw = buf.reshape(2048, 4).copy()
         raw = raw[raw[:, 0] > 0]

@@ -183,13 +183,24 @@ def _syncbn_body(rank, world):
 
 def test_syncbn_dp_step_equals_full_batch_step():
     """SURVEY §8(e) SyncBN: the two-rank data-parallel step with cross-rank
-    BatchNorm equals ONE process stepping on the whole batch -- gradients
-    within the fp32 summation-order bar of test_forward_pair_equals_two_calls
-    (1e-4 of each tensor's largest entry), running statistics within 1e-5 --
-    while per-rank BatchNorm does not."""
+    BatchNorm is the step of ONE process on the whole batch, while per-rank
+    BatchNorm is not.  Gradients: against the CPU oracle's fp64 step on the
+    full batch (tests/test_oracle_golden.py pins it to the reference's own
+    fp64 gradients), with the whole-model criterion of
+    test_gpu_train.test_model_step_gradients_vs_reference_fp64 -- error over
+    the fp32 noise of two other fp32 implementations, median <= 1.5, 90th
+    percentile <= 3, the tail only on global-sum gradients.  (A fixed 1e-4
+    bar does not apply: the 21-op train-mode stack is chaotic in fp32, and the
+    ranks' BatchNorm statistics are Chan merges of per-rank partials, not the
+    full batch's own partition.)  Running statistics within 1e-5 of the
+    single-process native step's."""
+    import numpy as np
+
     import engine.prediction as EP
+    from oracle import dstdgcn_oracle as O
+    from test_gpu_train import check_tail
     res = run_world("test_gpu_dist:_syncbn_body")
-    # the single-process step on the full batch of 8
+    # the single-process native step on the full batch of 8
     from engine import PredictionEngine
 
     class _Log:
@@ -213,26 +224,45 @@ def test_syncbn_dp_step_equals_full_batch_step():
     finally:
         EP._world = saved_world
     ref_bufs = {n: b.detach().clone().cpu() for n, b in m.named_buffers()}
-    worst_local = 0.0
+    # the oracle's step on the full batch: fp64, and fp32 on the GPU and the CPU (the noise)
+    sd0 = group(d, "train/sd0/")
+    batch_np = tuple(d[f"train/{n}0"] for n in ("inp", "inv", "seq"))
+    og = {}
+    for tag, dt, dev in (("64", torch.float64, DEV), ("32g", torch.float32, DEV), ("32c", torch.float32, "cpu")):
+        P = O.train_params(sd0, dt, dev)
+        _, lall = O.step_loss(P, batch_np, 5)
+        lall.backward()
+        og[tag] = {k: v.grad.double().cpu().numpy() for k, v in P.items() if v.grad is not None}
+
+    def ratios(g):
+        out = []
+        for k, r64 in og["64"].items():
+            scale = float(np.abs(r64).max())
+            noise = max(float(np.abs(og["32g"][k] - r64).max()), float(np.abs(og["32c"][k] - r64).max()), 1e-4 * scale)
+            out.append((float(np.abs(g[k].double().numpy() - r64).max()) / noise, k))
+        return out
+
+    def stats(rs):
+        r = np.array(sorted((x[0] for x in rs), reverse=True))
+        return float(np.median(r)), float(np.quantile(r, 0.9)), float(r[0])
+
+    assert set(og["64"]) == set(ref), "the engine step and the oracle step differ in their trainable set"
+    ctrl = ratios(ref)  # control: the single-process native step meets the bar
+    print("single process: median / p90 / max", stats(ctrl))
+    assert stats(ctrl)[0] <= 1.5 and stats(ctrl)[1] <= 3.0, stats(ctrl)
     for r in (0, 1):
         # 15 BatchNorms x (forward all-gather, backward all-reduce) per model call
         assert res[r]["calls"] > 0
-        table = []  # (sync error, per-rank BN error, name) relative to the tensor's largest entry
-        for n, g in ref.items():
-            scale = max(float(g.abs().max()), 1e-30)
-            err = float((res[r]["g_sync"][n] - g).abs().max())
-            if n.endswith("residual.0.bias"):  # analytically zero (a train-mode BN follows)
-                assert err < 1e-3, n
-                continue
-            loc = float((res[r]["g_local"][n] - g).abs().max()) / scale
-            table.append((err / scale, loc, n))
-            worst_local = max(worst_local, loc)
-        table.sort(reverse=True)
-        bad = [t for t in table if t[0] > 1e-4]
-        assert not bad, (r, len(bad), len(table), table[:12])
+        rs = ratios(res[r]["g_sync"])
+        med, p90, mx = stats(rs)
+        print(f"rank {r} SyncBN: median / p90 / max {med:.2f} / {p90:.2f} / {mx:.2f}")
+        assert med <= 1.5 and p90 <= 3.0, (r, med, p90, sorted(rs, reverse=True)[:8])
+        check_tail(rs)
         for n, b in ref_bufs.items():
             if n.endswith("num_batches_tracked"):
                 assert int(res[r]["b_sync"][n]) == int(b), n
             else:
                 assert float((res[r]["b_sync"][n] - b).abs().max()) <= 1e-5 * max(float(b.abs().max()), 1e-6), n
-    assert worst_local > 1e-3, "per-rank BatchNorm matched the full batch: the test would prove nothing"
+    loc = stats(ratios(res[0]["g_local"]))
+    print("per-rank BatchNorm: median / p90 / max", loc)
+    assert loc[0] > 10.0, ("per-rank BatchNorm met the full-batch bar: the test would prove nothing", loc)
