@@ -26,7 +26,7 @@ done
 export TMPDIR=/tmp
 for lib in libdstd_gcn libdstd_gcn_skp1 libdstd_gcn_skp2 libdstd_gcn_noslp; do
   set="SQ_INSTS_VALU,SQ_INSTS_MFMA,SQ_LDS_BANK_CONFLICT,SQ_INSTS_LDS,SQ_WAIT_INST_LDS,SQ_ACTIVE_INST_LDS,SQ_WAVE_CYCLES,SQ_ACTIVE_INST_VALU"
-  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc ${set//,/ } --output-format csv -d "$O/pmc_$lib" -o run -- python3 $R/scripts/ab_kernels.py $R/$L/$lib.so --rounds 1 --steps 2 > "$O/pmc_$lib.log" 2>&1)
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc ${set//,/ } --output-format csv -d "$O/pmc_$lib/pmc1" -o run -- python3 $R/scripts/ab_kernels.py $R/$L/$lib.so --rounds 1 --steps 2 > "$O/pmc_$lib.log" 2>&1)
   st3=$?; echo "pmc $lib exit $st3"; [ $st3 -eq 0 ] || exit $st3
   python3 scripts/pmc_summary.py $O/pmc_$lib > $O/pmc_$lib.txt; grep -A1 "temporal_fused<35, 22, 1\|spatial_hl<22, 64, 64" $O/pmc_$lib.txt | cut -c1-700
 done
