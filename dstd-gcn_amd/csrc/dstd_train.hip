@@ -967,8 +967,10 @@ __global__ __launch_bounds__(256) void k_tanh_outer_fwd(const float* __restrict_
   __syncthreads();
   const size_t base = (size_t)b0 * NN2;
   float* m = M + base;
+  // (multiply-high division: tanh_kb keeps kb * NN * NN < 2^16)
+  const FastDiv dNN2(NN2), dNN(NN);
   auto val = [&](int e) {
-    const int k = e / NN2, rm = e - k * NN2, i = rm / NN, j = rm - i * NN;
+    const int k = dNN2(e), rm = e - k * NN2, i = dNN(rm), j = rm - i * NN;
     return tanhf(ps[k * NN + i] - qs[k * NN + j]);
   };
   int e0 = 0;
@@ -991,8 +993,9 @@ __global__ __launch_bounds__(256) void k_tanh_outer_bwd(const float* __restrict_
   const size_t base = (size_t)b0 * NN2;
   const float* m = M + base;
   const float* dm = dM + base;
+  const FastDiv dNN2(NN2), dNN(NN);  // (tanh_kb keeps kb * NN * NN < 2^16)
   auto put = [&](int e, float t, float d) {
-    const int k = e / NN2, rm = e - k * NN2, i = rm / NN, j = rm - i * NN;
+    const int k = dNN2(e), rm = e - k * NN2, i = dNN(rm), j = rm - i * NN;
     dz[(k * NN + i) * (NN + 1) + j] = d * (1.f - t * t);
   };
   int e0 = 0;
@@ -2037,7 +2040,7 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
 // with the backward's dz tiles within 64 KB of LDS
 int tanh_kb(int nblk, int NN) {
   for (int kb : {kTanhMaxKB, 4, 2})
-    if (nblk >= 512 * kb && (size_t)kb * NN * (NN + 1) * sizeof(float) <= 64 * 1024) return kb;
+    if (nblk >= 512 * kb && (size_t)kb * NN * (NN + 1) * sizeof(float) <= 64 * 1024 && kb * NN * NN < 65536) return kb;
   return 1;
 }
 
