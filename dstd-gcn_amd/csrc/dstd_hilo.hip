@@ -1466,7 +1466,7 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   const float bv = tid < NROW ? a.bias[g][tid] : 0.f;
   // padding: k in [K, KP) and the row p = q = NA: E = F = 1 (tanh 0)
   for (int i = tid; i < (NA + 1) * (KP - K); i += AT) {
-    const int r = i / (KP - K), k = K + i % (KP - K);
+    const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
     El[r * SE + k] = 1.f;
     Fl[r * SE + k] = 1.f;
   }
@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       }
     }
     for (int i = tid; i < (NA + 1) * (KP - K); i += AT) {
-      const int r = i / (KP - K), k = K + i % (KP - K);
+      const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
       El[r * SE + k] = 0.f;
       Fl[r * SE + k] = 0.f;
     }
@@ -1753,7 +1753,7 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
     float* El = Elg(g);
     float* Fl = El + (V + 1) * SE;
     for (int i = tid; i < (V + 1) * (KP - K); i += NT) {
-      const int r = i / (KP - K), k = K + i % (KP - K);
+      const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
       El[r * SE + k] = val;
       Fl[r * SE + k] = val;
     }
@@ -1936,7 +1936,7 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
       const PQLayout L = j.pql;
       const float* pqb = j.pq + (size_t)n * L.sn + j.p_ch[0];
       for (int i = tid; i < (T + 1) * (KP - K); i += NT) {  // padding k and the row t = T: E = F = 1 (tanh 0)
-        const int r = i / (KP - K), k = K + i % (KP - K);
+        const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
         El[r * SE + k] = 1.f;
         Fl[r * SE + k] = 1.f;
       }
@@ -2024,7 +2024,7 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
           Fl[t * SE + V + v] = q4.w;
         }
         for (int i = tid; i < (T + 1) * (KP - K); i += NT) {
-          const int r = i / (KP - K), k = K + i % (KP - K);
+          const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
           El[r * SE + k] = 0.f;
           Fl[r * SE + k] = 0.f;
         }

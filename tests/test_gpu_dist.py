@@ -199,6 +199,7 @@ def test_syncbn_dp_step_equals_full_batch_step():
 
     import engine.prediction as EP
     from oracle import dstdgcn_oracle as O
+    from test_gpu_train import GLOBAL_SUM
     res = run_world("test_gpu_dist:_syncbn_body")
     # the single-process native step on the full batch of 8
     from engine import PredictionEngine
@@ -262,7 +263,10 @@ def test_syncbn_dp_step_equals_full_batch_step():
         med, p90, mx = stats(rs)
         print(f"rank {r} SyncBN: median / p90 / max {med:.2f} / {p90:.2f} / {mx:.2f}")
         assert med <= 1.5 and p90 <= 3.0, (r, med, p90, sorted(rs, reverse=True)[:8])
-        worse = sorted(((v, cref[k], k) for v, k in rs if v > max(3.0, 2.0 * cref[k])), reverse=True)
+        # (global-sum gradients -- scalars, biases, PReLU slopes: GLOBAL_SUM --
+        # keep check_tail's own 12x bar)
+        worse = sorted(((v, cref[k], k) for v, k in rs
+                        if v > max(3.0, 2.0 * cref[k]) and not (GLOBAL_SUM.search(k) and v <= 12.0)), reverse=True)
         assert not worse, (r, worse[:8])
         for n, b in ref_bufs.items():
             if n.endswith("num_batches_tracked"):
