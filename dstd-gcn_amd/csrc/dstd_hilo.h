@@ -322,6 +322,8 @@ struct AdjHLArgs {
   const float* astat[2];    // [NA][NA]
   uint16_t* out;
   long out_sN, out_sG;      // halves
+  int nchunk;               // column chunks per (sample, graph) workgroup set; 0: the launcher picks
+                            // (more below one workgroup per CU: small batches)
 };
 
 hipError_t launch_hl_prep(const HLPrepArgs& a, hipStream_t s);

@@ -165,13 +165,26 @@ __device__ __forceinline__ uint32_t wave_max_bits(float v) {
   const uint32_t r2 = __builtin_amdgcn_readlane(b, 32), r3 = __builtin_amdgcn_readlane(b, 48);
   return max(max(r0, r1), max(r2, r3));
 }
-__device__ __forceinline__ float amax4(float m, const float4& v) { return amax2(amax2(m, v.x, v.y), v.z, v.w); }
-// (f32x4 operands: accumulators after a VALU epilogue; amax4_mfma for ones
-// that may come straight from an MFMA, see amax2)
-__device__ __forceinline__ float amax4(float m, const f32x4& v) { return amax2(amax2(m, v[0], v[1]), v[2], v[3]); }
+// (accumulators that may come straight from an MFMA: plain fmaxf, which the
+// hazard recognizer pads; see amax2)
 __device__ __forceinline__ float amax4_mfma(float m, const f32x4& v) {
   return fmaxf(fmaxf(m, fmaxf(fabsf(v[0]), fabsf(v[1]))), fmaxf(fabsf(v[2]), fabsf(v[3])));
 }
+// max |x| over many values on four independent v_max3 chains: one chain
+// puts an inline-asm max right behind the one it depends on, and hipcc pads
+// every such pair with an s_nop (it cannot see the asm is not a
+// transcendental); four chains leave independent work between them
+struct AmaxAcc {
+  float m[4] = {0.f, 0.f, 0.f, 0.f};
+  int j = 0;  // (compile-time once the caller's loops are unrolled)
+  __device__ __forceinline__ void add(float a, float b) {
+    m[j] = amax2(m[j], a, b);
+    j = (j + 1) & 3;
+  }
+  __device__ __forceinline__ void add(const float4& v) { add(v.x, v.y), add(v.z, v.w); }
+  __device__ __forceinline__ void add(const f32x4& v) { add(v[0], v[1]), add(v[2], v[3]); }
+  __device__ __forceinline__ float get() const { return amax2(amax2(m[0], m[1], m[2]), m[3], m[3]); }
+};
 __device__ __forceinline__ float4 mul4(const float4& v, float s) { return make_float4(v.x * s, v.y * s, v.z * s, v.w * s); }
 // input shift of a GC unit: the smallest sx >= 0 with max|x| * max(1, |W|_inf)
 // < 2^(14 + sx) and max|b| < 2^(14 + sx); efb / eb: fexp of max(1, |W|_inf) / max|b|
@@ -532,11 +545,12 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
     load_adj_g(u, 0, ab[0]);
     __builtin_amdgcn_sched_barrier(0);
     // range shift of the unit's rows (0 unless a half could overflow)
-    float xm = 0.f;
+    AmaxAcc xa;
 #pragma unroll
     for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int ks = 0; ks < KSI; ++ks) xm = amax4(amax4(xm, xr[m][ks][0]), xr[m][ks][1]);
+      for (int ks = 0; ks < KSI; ++ks) xa.add(xr[m][ks][0]), xa.add(xr[m][ks][1]);
+    const float xm = xa.get();
     const int sx = input_shift(wave_max_bits(xm), efb, eb);
     const float dnx = pow2f(-sx);
     if (sx) {
@@ -725,11 +739,12 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
     }
     // ---- P_t/Q_t of h: out[ch][w] = sum_c wq[ch][c] h[c][w] + b ----
     // on h_s = 2^-sh h (range shift of the unit's output)
-    float hm = 0.f;
+    AmaxAcc ha;
 #pragma unroll
     for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-      for (int wt = 0; wt < NWT; ++wt) hm = amax4(hm, O[ct][wt]);
+      for (int wt = 0; wt < NWT; ++wt) ha.add(O[ct][wt]);
+    const float hm = ha.get();
     const int sh = hl_range_shift(fexp_bits(wave_max_bits(hm)));
     if (sh) {
       const float dn = pow2f(-sh);
@@ -994,11 +1009,12 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     if constexpr (!LAZY) load_adj(u, bh, bo);
     __builtin_amdgcn_sched_barrier(0);
     // range shift of the unit's rows (0 unless a half could overflow)
-    float xm = 0.f;
+    AmaxAcc xa;
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int ks = 0; ks < KSI; ++ks) xm = amax4(amax4(xm, xr[m][ks][0]), xr[m][ks][1]);
+      for (int ks = 0; ks < KSI; ++ks) xa.add(xr[m][ks][0]), xa.add(xr[m][ks][1]);
+    const float xm = xa.get();
     const int sx = input_shift(wave_max_bits(xm), efb, eb);
     const float dnx = pow2f(-sx);
     if (sx) {
@@ -1158,10 +1174,19 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     if (has_pq) {
       // on h_s = 2^-sh h (range shift of the unit's output)
       float hm = 0.f;
+      if constexpr (use_bn || use_res) {
+        AmaxAcc ha;
 #pragma unroll
-      for (int ct = 0; ct < NCT; ++ct)
+        for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) hm = use_bn || use_res ? amax4(hm, O[ct][ut]) : amax4_mfma(hm, O[ct][ut]);
+          for (int ut = 0; ut < NUT; ++ut) ha.add(O[ct][ut]);
+        hm = ha.get();
+      } else {
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+          for (int ut = 0; ut < NUT; ++ut) hm = amax4_mfma(hm, O[ct][ut]);
+      }
       const int sh = hl_range_shift(fexp_bits(wave_max_bits(hm)));
       if (sh) {
         const float dn = pow2f(-sh);
@@ -1378,6 +1403,8 @@ struct AdjHLGeom {
   static constexpr int SE = KP + 4;  // LDS row stride of E / F (16-byte aligned, rows spread over banks)
   using SM = SlotMap<NA, MODE == 0>;
   static constexpr int SL = SM::SL, NCOL = NA * SL, NCT = cdiv(NCOL, 16);
+  // column chunks (one workgroup each) per (sample, graph) at full batch;
+  // the launcher raises the count when B * ngroups * NCHUNK leaves CUs idle
   static constexpr int NCHUNK = MODE == 0 ? 1 : 2;
   static constexpr int CPC = cdiv(NCT, NCHUNK);
   static constexpr int OS = 20;  // staging row stride (floats)
@@ -1408,9 +1435,10 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kg = lane >> 4, cl = lane & 15;
-  const int chunk = blockIdx.x % Gm::NCHUNK;
-  const int g = (blockIdx.x / Gm::NCHUNK) % a.ngroups;
-  const int n = blockIdx.x / (Gm::NCHUNK * a.ngroups);
+  const int nch = a.nchunk, cpc = cdiv(Gm::NCT, nch);
+  const int chunk = blockIdx.x % nch;
+  const int g = (blockIdx.x / nch) % a.ngroups;
+  const int n = blockIdx.x / (nch * a.ngroups);
   if (n >= a.B) return;
   TLH(MODE, 0)
 
@@ -1538,10 +1566,10 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   float* so = stg[wave];
   uint16_t* out = a.out + (size_t)n * a.out_sN + (size_t)g * a.out_sG;
   const auto ro = rsrc(out, 2u * NROW * 2 * NCOL);
-  const int ct_end = min(Gm::NCT, (chunk + 1) * Gm::CPC);
+  const int ct_end = min(Gm::NCT, (chunk + 1) * cpc);
   auto tiles = [&](auto sep_c) {
     constexpr bool SEP = decltype(sep_c)::value;
-    for (int ct = chunk * Gm::CPC + wave; ct < ct_end; ct += AW) {
+    for (int ct = chunk * cpc + wave; ct < ct_end; ct += AW) {
       // this lane's column (B operand column j = cl)
       const int col = ct * 16 + cl;
       const int q = col / SL, pi = SM::slot_idx(col - q * SL);
@@ -2307,8 +2335,18 @@ bool spatial_hl_supported(int T, int V) { return hl_shape(T, V); }
 template <int MODE, int NROW, int K, int NA>
 hipError_t adj_hl_run(const AdjHLArgs& a, hipStream_t s) {
   using Gm = AdjHLGeom<MODE, NROW, K, NA>;
-  const int grid = a.B * a.ngroups * Gm::NCHUNK;
-  hipLaunchKernelGGL((k_adj_hl<MODE, NROW, K, NA>), dim3(grid), dim3(Gm::AT), 0, s, a);
+  AdjHLArgs b = a;
+  if (b.nchunk <= 0) {
+    // below one workgroup per CU (small batches) split each (sample, graph)'s
+    // column tiles over more workgroups -- each repeats the prologue, but the
+    // launch is its prologue plus 1/nch of the tiles -- keeping at least half
+    // the waves of a workgroup busy
+    const int sets = a.B * a.ngroups, cus = hl_num_cus();
+    b.nchunk = Gm::NCHUNK;
+    if (sets * Gm::NCHUNK < cus) b.nchunk = max(Gm::NCHUNK, min(cdiv(cus, sets), cdiv(Gm::NCT, cdiv(Gm::AW, 2))));
+  }
+  const int grid = a.B * a.ngroups * b.nchunk;
+  hipLaunchKernelGGL((k_adj_hl<MODE, NROW, K, NA>), dim3(grid), dim3(Gm::AT), 0, s, b);
   return hipGetLastError();
 }
 
