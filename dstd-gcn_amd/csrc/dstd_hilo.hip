@@ -1309,6 +1309,12 @@ __device__ __forceinline__ void tanh_run(const float* ep, const float* fq, float
     ev[h] = e.x, ev[h + 1] = e.y, ev[h + 2] = e.z, ev[h + 3] = e.w;
     fv[h] = f.x, fv[h + 1] = f.y, fv[h + 2] = f.z, fv[h + 3] = f.w;
   }
+#ifdef DSTD_TANH_SCALAR
+  if constexpr (SEP) {
+#pragma unroll
+    for (int e = 0; e < N; ++e) tv[e] = fmaf(__builtin_amdgcn_rcpf(fmaf(ev[e], fv[e], 1.f)), -2.f, 1.f);
+  } else
+#endif
   if constexpr (SEP) {
 #pragma unroll
     for (int e2 = 0; e2 < N; e2 += 2) {  // E F + 1 and 1 - 2 r as packed fp32 (v_pk_fma_f32)

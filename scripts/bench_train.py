@@ -56,7 +56,7 @@ def main():
         torch.manual_seed(0)
         m = get_model("dstdgcn", dstdgcn=opts).to(dev).train()
         m._dstd_inplace_grads = True  # what engine.PredictionEngine.train opts into (prediction.py:161)
-        opt = torch.optim.Adam(m.parameters(), lr=3e-3)
+        opt = torch.optim.Adam(m.parameters(), lr=3e-3, fused=True)  # the engine's optimizer (prediction.py:166)
         if distributed:
             dstd_dist.broadcast_module(m)
         g = torch.Generator().manual_seed(1234 + rank)  # each rank its own shard of sequences
