@@ -1335,14 +1335,13 @@ __device__ __forceinline__ void tanh_run(const float* ep, const float* fq, float
 // Offset of E / F row r (floats): rows r and r + 16 land on the same LDS
 // banks at any 16-byte-aligned stride SE, and the temporal slot order puts
 // such pairs in one quarter-wave read (slots 0-7 of a column are frames
-// 0-3, 16-19); SKEW = 32 more per 16 rows moves each such pair half a bank
-// rotation apart (modelled E/F read conflict degree 1.59 -> 1.10 at
-// T = 35).  The spatial (joint) order reads runs of consecutive rows: no
-// skew there.
+// 0-3, 16-19); SKEW = 32 moves rows 16-31 of every 32 half a bank rotation
+// over (modelled E/F read conflict degree 1.59 -> 1.10 at T = 35).  The
+// spatial (joint) order reads runs of consecutive rows: no skew there.
 template <int SE, int SKEW>
-__host__ __device__ constexpr int efr(int r) { return r * SE + (r >> 4) * SKEW; }
+__host__ __device__ constexpr int efr(int r) { return r * SE + ((r >> 4) & 1) * SKEW; }
 template <int SE, int SKEW>
-__host__ __device__ constexpr int efn(int rows) { return rows * SE + ((rows + 15) >> 4) * SKEW; }  // floats of `rows` rows
+__host__ __device__ constexpr int efn(int rows) { return rows * SE + SKEW; }  // floats of `rows` rows
 
 // B fragments of one 16-column tile: tanh(P[k][p] - Q[k][q]) for
 // k = 32s + 8kg + e (NS full 16x16x32 K-steps) and, with TAIL, k = 32 NS + 4kg
