@@ -1332,35 +1332,22 @@ __device__ __forceinline__ void tanh_run(const float* ep, const float* fq, float
   for (int e = N; e < 8; ++e) tv[e] = 0.f;
 }
 
-// Offset of E / F row r (floats): rows r and r + 16 land on the same LDS
-// banks at any 16-byte-aligned stride SE, and the temporal slot order puts
-// such pairs in one quarter-wave read (slots 0-7 of a column are frames
-// 0-3, 16-19); SKEW = 32 moves rows 16-31 of every 32 half a bank rotation
-// over (modelled E/F read conflict degree 1.59 -> 1.10 at T = 35).  The
-// spatial (joint) order reads runs of consecutive rows: no skew there.
-template <int SE, int SKEW>
-__host__ __device__ constexpr int efr(int r) { return r * SE + ((r >> 4) & 1) * SKEW; }
-template <int SE, int SKEW>
-__host__ __device__ constexpr int efn(int rows) { return rows * SE + SKEW; }  // floats of `rows` rows
-
 // B fragments of one 16-column tile: tanh(P[k][p] - Q[k][q]) for
 // k = 32s + 8kg + e (NS full 16x16x32 K-steps) and, with TAIL, k = 32 NS + 4kg
 // + e (one 16x16x16 step), split into hi / lo.  El / Fl: the [p][k] rows of
 // tanh_run; pr / qr: this lane's rows.
-template <bool SEP, int NS, int TAIL, int SE, int SKEW>
+template <bool SEP, int NS, int TAIL, int SE>
 __device__ __forceinline__ void tanh_frags(const float* El, const float* Fl, int pr, int qr, int kg, f16x8 (&bh)[NS],
                                            f16x8 (&bo)[NS], f16x4& th, f16x4& to) {
-  const float* ep = El + efr<SE, SKEW>(pr);
-  const float* fq = Fl + efr<SE, SKEW>(qr);
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     float tv[8];
-    tanh_run<SEP, 8>(ep + 32 * s + 8 * kg, fq + 32 * s + 8 * kg, tv);
+    tanh_run<SEP, 8>(El + pr * SE + 32 * s + 8 * kg, Fl + qr * SE + 32 * s + 8 * kg, tv);
     split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
   }
   if constexpr (TAIL) {
     float tv[8];
-    tanh_run<SEP, 4>(ep + 32 * NS + 4 * kg, fq + 32 * NS + 4 * kg, tv);
+    tanh_run<SEP, 4>(El + pr * SE + 32 * NS + 4 * kg, Fl + qr * SE + 32 * NS + 4 * kg, tv);
     uint2 hi, lo;
     split4(make_float4(tv[0], tv[1], tv[2], tv[3]), hi, lo);
     th = __builtin_bit_cast(f16x4, hi);
@@ -1420,7 +1407,6 @@ struct AdjHLGeom {
   static constexpr int RT = cdiv(NROW, 16), KH = K / 2;
   static constexpr int WIMG = RT * (NS * 2 * 64 + TAIL * 64);  // uint4 of the HLJ_RM image
   static constexpr int SE = KP + 4;  // LDS row stride of E / F (16-byte aligned, rows spread over banks)
-  static constexpr int SKEW = MODE == 1 ? 32 : 0;  // (efr: temporal slot order)
   using SM = SlotMap<NA, MODE == 0>;
   static constexpr int SL = SM::SL, NCOL = NA * SL, NCT = cdiv(NCOL, 16);
   // column chunks (one workgroup each) per (sample, graph) at full batch;
@@ -1444,10 +1430,10 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   using SM = typename Gm::SM;
   constexpr int RT = Gm::RT, NS = Gm::NS, KP = Gm::KP, KH = Gm::KH, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
   constexpr int AW = Gm::AW, AT = Gm::AT, TAIL = Gm::TAIL, WIMG = Gm::WIMG;
-  constexpr int OS = Gm::OS, T = Gm::T, V = Gm::V, SKEW = Gm::SKEW;
+  constexpr int OS = Gm::OS, T = Gm::T, V = Gm::V;
   constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
-  __shared__ float El[efn<SE, SKEW>(NA + 1)];
-  __shared__ float Fl[efn<SE, SKEW>(NA + 1)];
+  __shared__ float El[(NA + 1) * SE];
+  __shared__ float Fl[(NA + 1) * SE];
   __shared__ uint4 wl[WIMG];
   __shared__ float asl[NA * NA + 1];
   __shared__ float bsl[RT * 16];
@@ -1515,12 +1501,12 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   // padding: k in [K, KP) and the row p = q = NA: E = F = 1 (tanh 0)
   for (int i = tid; i < (NA + 1) * (KP - K); i += AT) {
     const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-    El[efr<SE, SKEW>(r) + k] = 1.f;
-    Fl[efr<SE, SKEW>(r) + k] = 1.f;
+    El[r * SE + k] = 1.f;
+    Fl[r * SE + k] = 1.f;
   }
   for (int i = tid; i < K; i += AT) {
-    El[efr<SE, SKEW>(NA) + i] = 1.f;
-    Fl[efr<SE, SKEW>(NA) + i] = 1.f;
+    El[NA * SE + i] = 1.f;
+    Fl[NA * SE + i] = 1.f;
   }
   int bad = 0;
 #pragma unroll
@@ -1531,10 +1517,10 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       const int pr = MODE == 0 ? v : t, ki = MODE == 0 ? t : v;
       const float ep0 = C2 * q4[it].x, ep1 = C2 * q4[it].y, eq0 = -C2 * q4[it].z, eq1 = -C2 * q4[it].w;
       bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
-      El[efr<SE, SKEW>(pr) + ki] = __builtin_amdgcn_exp2f(ep0);
-      El[efr<SE, SKEW>(pr) + KH + ki] = __builtin_amdgcn_exp2f(ep1);
-      Fl[efr<SE, SKEW>(pr) + ki] = __builtin_amdgcn_exp2f(eq0);
-      Fl[efr<SE, SKEW>(pr) + KH + ki] = __builtin_amdgcn_exp2f(eq1);
+      El[pr * SE + ki] = __builtin_amdgcn_exp2f(ep0);
+      El[pr * SE + KH + ki] = __builtin_amdgcn_exp2f(ep1);
+      Fl[pr * SE + ki] = __builtin_amdgcn_exp2f(eq0);
+      Fl[pr * SE + KH + ki] = __builtin_amdgcn_exp2f(eq1);
     }
   }
 #pragma unroll
@@ -1554,20 +1540,20 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       if (i < T * V) {
         const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;
         const int pr = MODE == 0 ? v : t, ki = MODE == 0 ? t : v;
-        El[efr<SE, SKEW>(pr) + ki] = q4[it].x;
-        El[efr<SE, SKEW>(pr) + KH + ki] = q4[it].y;
-        Fl[efr<SE, SKEW>(pr) + ki] = q4[it].z;
-        Fl[efr<SE, SKEW>(pr) + KH + ki] = q4[it].w;
+        El[pr * SE + ki] = q4[it].x;
+        El[pr * SE + KH + ki] = q4[it].y;
+        Fl[pr * SE + ki] = q4[it].z;
+        Fl[pr * SE + KH + ki] = q4[it].w;
       }
     }
     for (int i = tid; i < (NA + 1) * (KP - K); i += AT) {
       const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-      El[efr<SE, SKEW>(r) + k] = 0.f;
-      Fl[efr<SE, SKEW>(r) + k] = 0.f;
+      El[r * SE + k] = 0.f;
+      Fl[r * SE + k] = 0.f;
     }
     for (int i = tid; i < K; i += AT) {
-      El[efr<SE, SKEW>(NA) + i] = 0.f;
-      Fl[efr<SE, SKEW>(NA) + i] = 0.f;
+      El[NA * SE + i] = 0.f;
+      Fl[NA * SE + i] = 0.f;
     }
     __syncthreads();
   }
@@ -1597,7 +1583,7 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       const int pr = valid ? pi : NA, qr = col < NCOL ? q : NA;
       f16x8 bh[NS], bo[NS];
       f16x4 th, to;
-      tanh_frags<SEP, NS, TAIL, SE, SKEW>(El, Fl, pr, qr, kg, bh, bo, th, to);
+      tanh_frags<SEP, NS, TAIL, SE>(El, Fl, pr, qr, kg, bh, bo, th, to);
       f32x4 acc[RT];
       rm_mfma<RT, NS, TAIL>(wl, lane, bh, bo, th, to, acc);
       // ---- epilogue: alpha * (acc + b) + Astat, 0 on padding slots; staged
@@ -1676,7 +1662,6 @@ template <int T, int V, int EPI, int C>
 struct TFusedGeom {
   using SM = SlotMap<T, false>;
   static constexpr int K = 2 * V, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL, SE = KP + 4;
-  static constexpr int SKEW = 32;  // E / F rows are frames (efr)
   static constexpr int SL = SM::SL, NCOL = T * SL, NCTC = cdiv(NCOL, 16);
   // halves per joint in LDS: two planes + 8 (a joint 4 rows down lands on
   // other banks), the 8 kept zero: the B fragment of a padding slot (ZPAD)
@@ -1687,7 +1672,7 @@ struct TFusedGeom {
   // per-column tables (Astat and alpha in plane slot order, ASQ), conv_rm bias
   static constexpr int ASQ = NCTC * 16;
   static constexpr size_t p1_bytes(int rtc) {
-    return 2 * (size_t)efn<SE, SKEW>(T + 1) * 4 + (size_t)rtc * (NS * 2 * 64 + TAIL * 64) * 16 + (size_t)2 * ASQ * 4 +
+    return 2 * (size_t)(T + 1) * SE * 4 + (size_t)rtc * (NS * 2 * 64 + TAIL * 64) * 16 + (size_t)2 * ASQ * 4 +
            (size_t)rtc * 16 * 4;
   }
   static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
@@ -1894,8 +1879,8 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
       const bool va = col < NCOL && pa < V;
       f16x8 bh[NS], bo[NS];
       f16x4 th, to;
-      if (g ? sep1 : sep0) tanh_frags<true, NS, TAIL, SE, 0>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
-      else tanh_frags<false, NS, TAIL, SE, 0>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
+      if (g ? sep1 : sep0) tanh_frags<true, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
+      else tanh_frags<false, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
       // the accumulator's 4 columns colb .. colb + 3 (one joint q, slots slot0 ..)
       const int colb = ct * 16 + 4 * kg;
       const float4 as4 = ld4(as + colb), al4 = ld4(as + Gm::ASQ + colb);
@@ -1951,7 +1936,6 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   using SM = typename Gm::SM;
   constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
   constexpr int RC = Gm::RC, RTC = Gm::RTC, PJ = Gm::PJ, WIMG = Gm::WIMG, NW = tf_waves<T, V>(), NT = 64 * NW;
-  constexpr int SKEW = Gm::SKEW;
   constexpr int NUT = cdiv(T, 16);  // u tiles of the GC
   constexpr float C2 = 2.8853900817779268f;       // 2*log2(e)
   const TemporalHLArgs& a = fa.g;
@@ -1960,8 +1944,8 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   _Float16* planes = reinterpret_cast<_Float16*>(dsm);
   unsigned char* un = dsm + Gm::PLANES;  // phase-1 scratch / phase-2 stage (union)
   float* El = reinterpret_cast<float*>(un);
-  float* Fl = El + efn<SE, SKEW>(T + 1);
-  uint4* wl = reinterpret_cast<uint4*>(Fl + efn<SE, SKEW>(T + 1));
+  float* Fl = El + (T + 1) * SE;
+  uint4* wl = reinterpret_cast<uint4*>(Fl + (T + 1) * SE);
   // plane column col = q * SL + slot (q the output frame, slot <-> input
   // frame pi = slot_idx(slot)): asq[col] = 2^-sa Astat[pi][q], alq[col] =
   // 2^-sa alpha -- both 0 on padding slots and past the planes
@@ -1987,12 +1971,12 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
       const float* pqb = j.pq + (size_t)n * L.sn + j.p_ch[0];
       for (int i = tid; i < (T + 1) * (KP - K); i += NT) {  // padding k and the row t = T: E = F = 1 (tanh 0)
         const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-        El[efr<SE, SKEW>(r) + k] = 1.f;
-        Fl[efr<SE, SKEW>(r) + k] = 1.f;
+        El[r * SE + k] = 1.f;
+        Fl[r * SE + k] = 1.f;
       }
       for (int i = tid; i < K; i += NT) {
-        El[efr<SE, SKEW>(T) + i] = 1.f;
-        Fl[efr<SE, SKEW>(T) + i] = 1.f;
+        El[T * SE + i] = 1.f;
+        Fl[T * SE + i] = 1.f;
       }
       // every global load of the prologue is issued before the first LDS
       // write that needs one (one memory round trip, not one per loop trip)
@@ -2038,10 +2022,10 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
           const int t = i / V, v = i - t * V;
           const float ep0 = C2 * q4[it].x, ep1 = C2 * q4[it].y, eq0 = -C2 * q4[it].z, eq1 = -C2 * q4[it].w;
           bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
-          El[efr<SE, SKEW>(t) + v] = __builtin_amdgcn_exp2f(ep0);
-          El[efr<SE, SKEW>(t) + V + v] = __builtin_amdgcn_exp2f(ep1);
-          Fl[efr<SE, SKEW>(t) + v] = __builtin_amdgcn_exp2f(eq0);
-          Fl[efr<SE, SKEW>(t) + V + v] = __builtin_amdgcn_exp2f(eq1);
+          El[t * SE + v] = __builtin_amdgcn_exp2f(ep0);
+          El[t * SE + V + v] = __builtin_amdgcn_exp2f(ep1);
+          Fl[t * SE + v] = __builtin_amdgcn_exp2f(eq0);
+          Fl[t * SE + V + v] = __builtin_amdgcn_exp2f(eq1);
         }
       }
 #pragma unroll
@@ -2068,19 +2052,19 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
         for (int i = tid; i < T * V; i += NT) {
           const int t = i / V, v = i % V;
           const float4 q4 = ld4(pqb + t * L.st + v * L.sv);
-          El[efr<SE, SKEW>(t) + v] = q4.x;
-          El[efr<SE, SKEW>(t) + V + v] = q4.y;
-          Fl[efr<SE, SKEW>(t) + v] = q4.z;
-          Fl[efr<SE, SKEW>(t) + V + v] = q4.w;
+          El[t * SE + v] = q4.x;
+          El[t * SE + V + v] = q4.y;
+          Fl[t * SE + v] = q4.z;
+          Fl[t * SE + V + v] = q4.w;
         }
         for (int i = tid; i < (T + 1) * (KP - K); i += NT) {
           const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-          El[efr<SE, SKEW>(r) + k] = 0.f;
-          Fl[efr<SE, SKEW>(r) + k] = 0.f;
+          El[r * SE + k] = 0.f;
+          Fl[r * SE + k] = 0.f;
         }
         for (int i = tid; i < K; i += NT) {
-          El[efr<SE, SKEW>(T) + i] = 0.f;
-          Fl[efr<SE, SKEW>(T) + i] = 0.f;
+          El[T * SE + i] = 0.f;
+          Fl[T * SE + i] = 0.f;
         }
         __syncthreads();
       }
@@ -2139,7 +2123,7 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
             const int col = ct * 16 + cl;
             const int qa = col / SL, pa = SM::slot_idx(col - qa * SL);
             const bool va = col < NCOL && pa < T;
-            tanh_frags<SEP, NS, TAIL, SE, SKEW>(El, Fl, va ? pa : T, col < NCOL ? qa : T, kg, bh[i], bo[i], th[i], to[i]);
+            tanh_frags<SEP, NS, TAIL, SE>(El, Fl, va ? pa : T, col < NCOL ? qa : T, kg, bh[i], bo[i], th[i], to[i]);
             // columns colb .. colb+3 (one frame q, slots slot0 ..): alpha (acc + b) + Astat,
             // 0 on padding slots (both tables hold 0 there)
             colb[i] = ct * 16 + 4 * kg;
