@@ -1719,54 +1719,10 @@ struct SAdjGeom {
   static constexpr size_t LDS = 2 * (EF + AS + WB + BB);
 };
 
-// Phase 3's constants -- both conv_rm images, the Astat table entries, the
-// bias, the range scale -- loaded into registers BEFORE the barrier that
-// waits for the sample's last GC unit (nothing in them depends on the units),
-// so their round trip overlaps the wait; the P/Q loads follow the barrier.
 template <int T, int V, int NT>
-struct SAdjPre {
-  using Gm = SAdjGeom<T, V>;
-  static constexpr int NWI = cdiv(2 * Gm::WIMG, NT), NAS = cdiv(2 * Gm::ASQ, NT);
-  uint4 wv[NWI];
-  float av[NAS];
-  int aok;  // bit it: the table entry of iteration it is a valid (pi, q)
-  float bv, dna, alpha;
-};
-
-template <int T, int V, int NT>
-__device__ __forceinline__ void sadj_prefetch(const AdjHLArgs& j, SAdjPre<T, V, NT>& p) {
+__device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, unsigned char* dsm) {
   using Gm = SAdjGeom<T, V>;
   using SM = typename Gm::SM;
-  using P = SAdjPre<T, V, NT>;
-  constexpr int SL = Gm::SL, NCOL = Gm::NCOL, RT = Gm::RT, WIMG = Gm::WIMG;
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int it = 0; it < P::NWI; ++it) {
-    const int i = min(tid + it * NT, 2 * WIMG - 1);
-    p.wv[it] = (i >= WIMG ? j.wimg[1] : j.wimg[0])[i >= WIMG ? i - WIMG : i];
-  }
-  p.aok = 0;
-#pragma unroll
-  for (int it = 0; it < P::NAS; ++it) {
-    const int i = tid + it * NT, g = i >= Gm::ASQ, col = i - g * Gm::ASQ, q = col / SL;
-    const int pi = col < NCOL ? SM::slot_idx(col - q * SL) : V;
-    const bool ok = pi < V && i < 2 * Gm::ASQ;
-    if (ok) p.aok |= 1 << it;
-    p.av[it] = (g ? j.astat[1] : j.astat[0])[ok ? pi * V + q : 0];
-  }
-  // planes stored as 2^-sa Adj, one sa for both graphs (dstd_hilo.h "range scaling")
-  p.dna = pow2f(-hl_range_shift(fexp_bits(__float_as_uint(fmaxf(j.wscale[0][HLS_BOUND], j.wscale[1][HLS_BOUND])))));
-  p.alpha = *j.alpha * p.dna;
-  const int bg = tid >= 16 * RT, br = tid - bg * 16 * RT;
-  p.bv = tid < 2 * 16 * RT && br < T ? (bg ? j.bias[1] : j.bias[0])[br] : 0.f;
-}
-
-template <int T, int V, int NT>
-__device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, unsigned char* dsm,
-                                                   const SAdjPre<T, V, NT>& pre) {
-  using Gm = SAdjGeom<T, V>;
-  using SM = typename Gm::SM;
-  using P = SAdjPre<T, V, NT>;
   constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
   constexpr int RT = Gm::RT, FULL = Gm::FULL, WIMG = Gm::WIMG, NW = NT / 64, NCTC = Gm::NCTC;
   constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
@@ -1778,9 +1734,10 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, cl = lane & 15;
 
-  // ---- prologue: both graphs' P/Q -> E/F rows; the constants (pre) -> LDS ----
+  // ---- prologue: both graphs' P/Q -> E/F rows, conv_rm images, Astat, bias;
+  // every global load before the first LDS write ----
   const PQLayout L = j.pql;
-  constexpr int NPQ = cdiv(T * V, NT);
+  constexpr int NPQ = cdiv(T * V, NT), NWI = cdiv(2 * WIMG, NT), NAS = cdiv(2 * Gm::ASQ, NT);
   auto pq_at = [&](int g, int i) __attribute__((always_inline)) -> float4 {  // (P_0, P_1, Q_0, Q_1) of element i (joint-major)
     const int t = i % T, v = i / T;
     return ld4(j.pq + (size_t)n * L.sn + j.p_ch[g] + t * L.st + v * L.sv);
@@ -1790,17 +1747,38 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
   for (int g = 0; g < 2; ++g)
 #pragma unroll
     for (int it = 0; it < NPQ; ++it) q4[g][it] = pq_at(g, min(tid + it * NT, T * V - 1));
-  const float dna = pre.dna, alpha = pre.alpha, bv = pre.bv;
+  uint4 wv[NWI];
+  float av[NAS];
 #pragma unroll
-  for (int it = 0; it < P::NWI; ++it)
-    if (tid + it * NT < 2 * WIMG) wl[tid + it * NT] = pre.wv[it];
+  for (int it = 0; it < NWI; ++it) {
+    const int i = min(tid + it * NT, 2 * WIMG - 1);
+    wv[it] = (i >= WIMG ? j.wimg[1] : j.wimg[0])[i >= WIMG ? i - WIMG : i];
+  }
+  int aok = 0;  // bit it: the table entry of iteration it is a valid (pi, q)
 #pragma unroll
-  for (int it = 0; it < P::NAS; ++it) {
+  for (int it = 0; it < NAS; ++it) {
+    const int i = tid + it * NT, g = i >= Gm::ASQ, col = i - g * Gm::ASQ, q = col / SL;
+    const int pi = col < NCOL ? SM::slot_idx(col - q * SL) : V;
+    const bool ok = pi < V && i < 2 * Gm::ASQ;
+    if (ok) aok |= 1 << it;
+    av[it] = (g ? j.astat[1] : j.astat[0])[ok ? pi * V + q : 0];
+  }
+  // planes stored as 2^-sa Adj, one sa for both graphs (dstd_hilo.h "range scaling")
+  const float dna = pow2f(-hl_range_shift(
+      fexp_bits(__float_as_uint(fmaxf(j.wscale[0][HLS_BOUND], j.wscale[1][HLS_BOUND])))));
+  const float alpha = *j.alpha * dna;
+  const int bg = tid >= 16 * RT, br = tid - bg * 16 * RT;
+  const float bv = tid < 2 * 16 * RT && br < T ? (bg ? j.bias[1] : j.bias[0])[br] : 0.f;
+#pragma unroll
+  for (int it = 0; it < NWI; ++it)
+    if (tid + it * NT < 2 * WIMG) wl[tid + it * NT] = wv[it];
+#pragma unroll
+  for (int it = 0; it < NAS; ++it) {
     const int i = tid + it * NT, g = i >= Gm::ASQ;
     if (i < 2 * Gm::ASQ) {
-      const bool ok = (pre.aok >> it) & 1;
+      const bool ok = (aok >> it) & 1;
       float* t = asg(g) + (i - g * Gm::ASQ);
-      t[0] = ok ? pre.av[it] * dna : 0.f;
+      t[0] = ok ? av[it] * dna : 0.f;
       t[Gm::ASQ] = ok ? alpha : 0.f;
     }
   }
@@ -2283,11 +2261,9 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
     static_assert(SAdjGeom<T, V>::LDS <= Gm::LDS, "phase 3 reuses the launch's LDS");
     TLH(3, 2)
     if (fa.sn.out) {
-      SAdjPre<T, V, NT> pre;
-      sadj_prefetch<T, V, NT>(fa.sn, pre);  // in flight across the barrier
       __syncthreads();  // every unit's P/Q written (one CU: the workgroup-scope fences of the barrier suffice)
       TLH(2, 0)
-      spatial_adj_sample<T, V, NT>(fa.sn, n, dsm, pre);
+      spatial_adj_sample<T, V, NT>(fa.sn, n, dsm);
     }
     TLH(3, 3)
   }
