@@ -938,94 +938,54 @@ __global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
 // ---------------------------------------------------------------------------
 // tanh outer difference
 // ---------------------------------------------------------------------------
-// A workgroup takes KB consecutive (n, r, a) blocks (tanh_kb): their M
-// blocks are one contiguous run of KB*NN*NN floats, moved as 16-byte
-// accesses (one block per workgroup left 529..1600 elements per 256 threads
-// and every workgroup paid a full staging round trip: 8..10 us launches for
-// 2..3 us of traffic at the config-5 batch, profiles/r03y_train_trace_summary.txt)
 constexpr int kTanhMaxNN = 128;  // the frame envelope (T <= 128; V <= 64)
-constexpr int kTanhMaxKB = 8;
-__device__ __forceinline__ size_t tanh_pq_base(const PQView& v, int blk, int R, int A) {
+__global__ void k_tanh_outer_fwd(const float* __restrict__ P, const float* __restrict__ Q, PQView v, int R, int A,
+                                 int NN, float* __restrict__ M) {
+  // one workgroup per (n, r, a); M block [NN][NN]
+  const int blk = blockIdx.x;
   const int n = blk / (R * A), ra = blk - n * R * A, r = ra / A, a = ra - r * A;
-  return n * v.sn + r * v.sr + a * v.sa;
-}
-
-__global__ __launch_bounds__(256) void k_tanh_outer_fwd(const float* __restrict__ P, const float* __restrict__ Q,
-                                                        PQView v, int R, int A, int NN, int nblk, int kb,
-                                                        float* __restrict__ M) {
-  // M block [NN][NN] per (n, r, a); the blocks' P and Q rows (strided in the
-  // caller's layout) staged once in LDS
-  __shared__ float ps[kTanhMaxKB * kTanhMaxNN], qs[kTanhMaxKB * kTanhMaxNN];
-  const int tid = threadIdx.x;
-  const int b0 = blockIdx.x * kb, nb = min(kb, nblk - b0), NN2 = NN * NN, tot = nb * NN2;
-  for (int e = tid; e < nb * NN; e += 256) {
-    const int k = e / NN, i = e - k * NN;
-    const size_t o = tanh_pq_base(v, b0 + k, R, A) + (size_t)i * v.si;
-    ps[e] = P[o];
-    qs[e] = Q[o];
+  const float* p = P + n * v.sn + r * v.sr + a * v.sa;
+  const float* q = Q + n * v.sn + r * v.sr + a * v.sa;
+  float* m = M + (size_t)blk * NN * NN;
+  // the block's P and Q rows (strided in the caller's layout) staged once in
+  // LDS instead of two strided loads per output element
+  __shared__ float ps[kTanhMaxNN], qs[kTanhMaxNN];
+  for (int i = threadIdx.x; i < NN; i += blockDim.x) {
+    ps[i] = p[i * v.si];
+    qs[i] = q[i * v.si];
   }
   __syncthreads();
-  const size_t base = (size_t)b0 * NN2;
-  float* m = M + base;
-  // (multiply-high division: tanh_kb keeps kb * NN * NN < 2^16)
-  const FastDiv dNN2(NN2), dNN(NN);
-  auto val = [&](int e) {
-    const int k = dNN2(e), rm = e - k * NN2, i = dNN(rm), j = rm - i * NN;
-    return tanhf(ps[k * NN + i] - qs[k * NN + j]);
-  };
-  int e0 = 0;
-  if ((base & 3) == 0) {
-    const int t4 = tot >> 2;
-#pragma unroll 2
-    for (int q = tid; q < t4; q += 256)
-      *reinterpret_cast<float4*>(m + 4 * q) = make_float4(val(4 * q), val(4 * q + 1), val(4 * q + 2), val(4 * q + 3));
-    e0 = 4 * t4;
-  }
-  for (int e = e0 + tid; e < tot; e += 256) m[e] = val(e);
-}
-
-__global__ __launch_bounds__(256) void k_tanh_outer_bwd(const float* __restrict__ M, const float* __restrict__ dM,
-                                                        PQView v, int R, int A, int NN, int nblk, int kb,
-                                                        float* __restrict__ dP, float* __restrict__ dQ) {
-  extern __shared__ float dz[];  // [kb][NN][NN+1]
-  const int tid = threadIdx.x;
-  const int b0 = blockIdx.x * kb, nb = min(kb, nblk - b0), NN2 = NN * NN, tot = nb * NN2;
-  const size_t base = (size_t)b0 * NN2;
-  const float* m = M + base;
-  const float* dm = dM + base;
-  const FastDiv dNN2(NN2), dNN(NN);  // (tanh_kb keeps kb * NN * NN < 2^16)
-  auto put = [&](int e, float t, float d) {
-    const int k = dNN2(e), rm = e - k * NN2, i = dNN(rm), j = rm - i * NN;
-    dz[(k * NN + i) * (NN + 1) + j] = d * (1.f - t * t);
-  };
-  int e0 = 0;
-  if ((base & 3) == 0) {
-    const int t4 = tot >> 2;
 #pragma unroll 4
-    for (int q = tid; q < t4; q += 256) {
-      const float4 t = *reinterpret_cast<const float4*>(m + 4 * q);
-      const float4 d = *reinterpret_cast<const float4*>(dm + 4 * q);
-      put(4 * q, t.x, d.x);
-      put(4 * q + 1, t.y, d.y);
-      put(4 * q + 2, t.z, d.z);
-      put(4 * q + 3, t.w, d.w);
-    }
-    e0 = 4 * t4;
+  for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
+    const int i = e / NN, j = e - i * NN;
+    m[e] = tanhf(ps[i] - qs[j]);
   }
-  for (int e = e0 + tid; e < tot; e += 256) put(e, m[e], dm[e]);
+}
+
+__global__ void k_tanh_outer_bwd(const float* __restrict__ M, const float* __restrict__ dM, PQView v, int R, int A,
+                                 int NN, float* __restrict__ dP, float* __restrict__ dQ) {
+  extern __shared__ float dz[];  // [NN][NN+1]
+  const int blk = blockIdx.x;
+  const int n = blk / (R * A), ra = blk - n * R * A, r = ra / A, a = ra - r * A;
+  const float* m = M + (size_t)blk * NN * NN;
+  const float* dm = dM + (size_t)blk * NN * NN;
+#pragma unroll 4
+  for (int e = threadIdx.x; e < NN * NN; e += blockDim.x) {
+    const int i = e / NN, j = e - i * NN;
+    const float t = m[e];
+    dz[i * (NN + 1) + j] = dm[e] * (1.f - t * t);
+  }
   __syncthreads();
-  for (int o = tid; o < nb * 2 * NN; o += 256) {
-    const int k = o / (2 * NN), i = o - k * 2 * NN;
-    const size_t pb = tanh_pq_base(v, b0 + k, R, A);
-    const float* z = dz + k * NN * (NN + 1);
+  const size_t base = n * v.sn + r * v.sr + a * v.sa;
+  for (int i = threadIdx.x; i < 2 * NN; i += blockDim.x) {
     float s = 0.f;
     if (i < NN) {
-      for (int j = 0; j < NN; ++j) s += z[i * (NN + 1) + j];
-      dP[pb + i * v.si] = s;
+      for (int j = 0; j < NN; ++j) s += dz[i * (NN + 1) + j];
+      dP[base + i * v.si] = s;
     } else {
       const int j = i - NN;
-      for (int r = 0; r < NN; ++r) s += z[r * (NN + 1) + j];
-      dQ[pb + j * v.si] = -s;
+      for (int k = 0; k < NN; ++k) s += dz[k * (NN + 1) + j];
+      dQ[base + j * v.si] = -s;
     }
   }
 }
@@ -2036,29 +1996,19 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
 
 
 
-// blocks per workgroup: the most of 8 / 4 / 2 that keeps >= 512 workgroups,
-// with the backward's dz tiles within 64 KB of LDS
-int tanh_kb(int nblk, int NN) {
-  for (int kb : {kTanhMaxKB, 4, 2})
-    if (nblk >= 512 * kb && (size_t)kb * NN * (NN + 1) * sizeof(float) <= 64 * 1024 && kb * NN * NN < 65536) return kb;
-  return 1;
-}
-
 hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int R, int A, int NN, float* M,
                           hipStream_t s) {
   if (NN > kTanhMaxNN) return hipErrorInvalidValue;
-  const int nblk = B * R * A, kb = tanh_kb(nblk, NN);
-  k_tanh_outer_fwd<<<cdiv(nblk, kb), 256, 0, s>>>(P, Q, v, R, A, NN, nblk, kb, M);
+  k_tanh_outer_fwd<<<B * R * A, 256, 0, s>>>(P, Q, v, R, A, NN, M);
   return hipGetLastError();
 }
 
 hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int R, int A, int NN, float* dP,
                           float* dQ, hipStream_t s) {
-  if (NN > kTanhMaxNN) return hipErrorInvalidValue;
-  const int nblk = B * R * A, kb = tanh_kb(nblk, NN);
-  const size_t lds = (size_t)kb * NN * (NN + 1) * sizeof(float);  // 66 KB at the T = 128 envelope top (kb 1)
+  const size_t lds = (size_t)NN * (NN + 1) * sizeof(float);  // 66 KB at the T = 128 envelope top
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_tanh_outer_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  k_tanh_outer_bwd<<<cdiv(nblk, kb), 256, lds, s>>>(M, dM, v, R, A, NN, nblk, kb, dP, dQ);
+  k_tanh_outer_bwd<<<B * R * A, 256, lds, s>>>(M, dM, v, R, A, NN, dP, dQ);
   return hipGetLastError();
 }
 
