@@ -201,6 +201,42 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
     return;
   }
   float* Db = g.d_out ? g.d_out + b1 * g.c_b1 + b2 * g.c_b2 : nullptr;
+  if (Db && !g.nseg) {
+    // C and the adjacency D = d_alpha * C + (d_A (* d_W) (+ d_R)) per column:
+    // a lane's columns are the same for all its 4 * FM rows, so the combine
+    // is loaded once per column, not per element (gemm_store's order of
+    // operations otherwise)
+    const float ad = *g.d_alpha;
+    float ac[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int gn = min(n0 + wn + j * 16 + (lane & 15), g.N - 1);
+      ac[j] = g.d_A[gn];
+      if (g.d_W) ac[j] *= g.d_W[gn];
+      if (g.d_R) ac[j] += g.d_R[gn];
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+        if (gm >= g.M) continue;
+        const float bm = g.bias_m ? g.bias_m[gm] : 0.f;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int gn = n0 + wn + j * 16 + (lane & 15);
+          if (gn < g.N) {
+            float v = g.alpha * acc[i][j][r];
+            if (g.bias_m) v += bm;
+            Db[gm * g.c_m + gn * g.c_n] = fmaf(ad, v, ac[j]);
+            float* c = Cb + gm * g.c_m + gn * g.c_n;
+            if (g.beta != 0.f) v += g.beta * *c;
+            *c = v;
+          }
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
