@@ -947,6 +947,9 @@ __device__ __forceinline__ void stage_temporal(const TemporalHLArgs& a, Temporal
 #ifndef DSTD_TF_LATE_RES
 #define DSTD_TF_LATE_RES 1
 #endif
+#ifndef DSTD_TF_RES_ACC
+#define DSTD_TF_RES_ACC 1
+#endif
 // PF: the next unit's h rows are loaded during this one (48 VGPRs); without,
 // each unit loads its own rows first (for more waves per SIMD instead)
 template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad, bool PF = true>
@@ -1076,8 +1079,17 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
         for (int ct = 0; ct < NCT; ++ct) R[ct][ut] = bld4(rr, uoff[ut] + 64 * ct);
     };
     constexpr bool late_res = LAZY && DSTD_TF_LATE_RES;
+    // RES_ACC: the ENC residual is the aggregation accumulator's initial
+    // value (scaled like the sum, 2^-(sx+sa)) -- the MFMAs add it, the
+    // epilogue does not (48 VALU adds per unit), and it needs no registers of
+    // its own across the aggregation.  Per frame count T (k_temporal_hl's
+    // instantiations are per T, and the fused and unfused schedules of one
+    // shape stay bit-identical): T = 40 (3DPW, whose 8-wave fused kernel then
+    // fits 256 VGPRs without its 4 spills); not T = 35 (H36M's 12-wave fused
+    // kernel would spill at 168) nor T = 75 (k_temporal_hl would spill)
+    constexpr bool res_acc = EPI == TEPI_ENC && DSTD_TF_RES_ACC && T == 40;
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (EPI == TEPI_ENC && !late_res) {
+    if constexpr (EPI == TEPI_ENC && !late_res && !res_acc) {
       load_res_enc();
     } else if constexpr (EPI == TEPI_ENC) {
     } else if constexpr (EPI == TEPI_OUT) {
@@ -1093,10 +1105,28 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     __builtin_amdgcn_sched_barrier(0);
     // ---- aggregation: O[c][u] = sum_t D[t][c] Adj[v][t][u] ----
     f32x4 O[NCT][NUT];
+    if constexpr (res_acc) {
+      const auto rr = rsrc(a.xres + cbase, col_bytes);
 #pragma unroll
-    for (int ct = 0; ct < NCT; ++ct)
+      for (int ut = 0; ut < NUT; ++ut)
 #pragma unroll
-      for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = zero4();
+        for (int ct = 0; ct < NCT; ++ct) {
+          const float4 r4 = bld4(rr, uoff[ut] + 64 * ct);
+          O[ct][ut] = f32x4{r4.x, r4.y, r4.z, r4.w};
+        }
+      if (const int su0 = min(sx + sa, 127)) {
+        const float dn = pow2f(-su0);
+#pragma unroll
+        for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+          for (int ut = 0; ut < NUT; ++ut) O[ct][ut] *= dn;
+      }
+    } else {
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = zero4();
+    }
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int sb = LAZY ? 0 : s;
@@ -1123,7 +1153,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     // next unit's h rows (unconditional -- the last unit reloads itself -- so
     // that no branch hides the loads from hipcc's vmcnt bookkeeping)
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (EPI == TEPI_ENC && late_res) load_res_enc();
+    if constexpr (EPI == TEPI_ENC && late_res && !res_acc) load_res_enc();
     // (long sequences: the next unit's rows after the epilogue, so that they,
     // the output accumulators and the residual are not live at once)
     constexpr bool late_x = LAZY && T > 48;
@@ -1145,7 +1175,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
         f32x4& o = O[ct][ut];
-        if constexpr (use_res) {
+        if constexpr (use_res && !res_acc) {
           o[0] += R[ct][ut].x;
           o[1] += R[ct][ut].y;
           o[2] += R[ct][ut].z;
