@@ -950,6 +950,9 @@ __device__ __forceinline__ void stage_temporal(const TemporalHLArgs& a, Temporal
 #ifndef DSTD_TF_RES_ACC
 #define DSTD_TF_RES_ACC 1
 #endif
+#ifndef DSTD_TF_RES_ACC35  // (A/B: the same at T = 35, where the 12-wave fused kernel spills 3 VGPRs)
+#define DSTD_TF_RES_ACC35 0
+#endif
 // PF: the next unit's h rows are loaded during this one (48 VGPRs); without,
 // each unit loads its own rows first (for more waves per SIMD instead)
 template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad, bool PF = true>
@@ -1087,7 +1090,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     // shape stay bit-identical): T = 40 (3DPW, whose 8-wave fused kernel then
     // fits 256 VGPRs without its 4 spills); not T = 35 (H36M's 12-wave fused
     // kernel would spill at 168) nor T = 75 (k_temporal_hl would spill)
-    constexpr bool res_acc = EPI == TEPI_ENC && DSTD_TF_RES_ACC && T == 40;
+    constexpr bool res_acc = EPI == TEPI_ENC && DSTD_TF_RES_ACC && (T == 40 || (T == 35 && DSTD_TF_RES_ACC35));
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (EPI == TEPI_ENC && !late_res && !res_acc) {
       load_res_enc();
