@@ -950,12 +950,15 @@ __device__ __forceinline__ void stage_temporal(const TemporalHLArgs& a, Temporal
 #ifndef DSTD_TF_RES_ACC
 #define DSTD_TF_RES_ACC 1
 #endif
-#ifndef DSTD_TF_RES_ACC35  // (A/B: the same at T = 35, where the 12-wave fused kernel spills 3 VGPRs)
-#define DSTD_TF_RES_ACC35 0
-#endif
+// shapes whose ENC units take the residual as the accumulator's initial
+// value: CMU (T 35, V 25; -2.8% per forward) and 3DPW (T 40, V 23; -2.3%, and
+// its 8-wave fused kernel fits 256 VGPRs without its 4 spills); not H36M
+// (the 12-wave fused kernel spills 3 VGPRs at 168: +1.1%) nor T = 75
+// (k_temporal_hl would spill 40); profiles/r04m_res_acc_ab.txt, r04n_res_acc35_ab.txt
+__host__ __device__ constexpr bool tf_res_acc(int T, int V) { return (T == 35 && V == 25) || (T == 40 && V == 23); }
 // PF: the next unit's h rows are loaded during this one (48 VGPRs); without,
 // each unit loads its own rows first (for more waves per SIMD instead)
-template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad, bool PF = true>
+template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad, bool PF = true, bool RA = false>
 __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const TemporalStage<T, EPI, C, VB>& st, int u,
                                                int uend, int ustep, AdjLoad load_adj) {
   using SM = SlotMap<T, false>;
@@ -1085,12 +1088,10 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     // RES_ACC: the ENC residual is the aggregation accumulator's initial
     // value (scaled like the sum, 2^-(sx+sa)) -- the MFMAs add it, the
     // epilogue does not (48 VALU adds per unit), and it needs no registers of
-    // its own across the aggregation.  Per frame count T (k_temporal_hl's
-    // instantiations are per T, and the fused and unfused schedules of one
-    // shape stay bit-identical): T = 40 (3DPW, whose 8-wave fused kernel then
-    // fits 256 VGPRs without its 4 spills); not T = 35 (H36M's 12-wave fused
-    // kernel would spill at 168) nor T = 75 (k_temporal_hl would spill)
-    constexpr bool res_acc = EPI == TEPI_ENC && DSTD_TF_RES_ACC && (T == 40 || (T == 35 && DSTD_TF_RES_ACC35));
+    // its own across the aggregation.  Chosen per shape by the kernels
+    // (tf_res_acc, the same for the fused and unfused schedules of a shape so
+    // they stay bit-identical)
+    constexpr bool res_acc = EPI == TEPI_ENC && DSTD_TF_RES_ACC && RA;
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (EPI == TEPI_ENC && !late_res && !res_acc) {
       load_res_enc();
@@ -1266,7 +1267,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 }
 
 
-template <int T, int EPI, int C>
+template <int T, int EPI, int C, bool RA = false>
 __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_per_eu(temporal_hl_wpe<T, C>(), temporal_hl_wpe<T, C>()))) void k_temporal_hl(
     TemporalHLArgs a) {
   static_assert(C == 64 || (C == 3 && (EPI == TEPI_OUT || EPI == TEPI_RAW)), "shapes of the forward");
@@ -1309,9 +1310,9 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
         bo[ut] = bldu4(rl, off);
       }
     };
-    temporal_units<T, EPI, C, 32, true>(a, st, u0, uend, 1, load_adj_s);
+    temporal_units<T, EPI, C, 32, true, decltype(load_adj_s), true, RA>(a, st, u0, uend, 1, load_adj_s);
   } else {
-    temporal_units<T, EPI, C, 32, false>(a, st, u0, uend, 1, load_adj);
+    temporal_units<T, EPI, C, 32, false, decltype(load_adj), true, RA>(a, st, u0, uend, 1, load_adj);
   }
 }
 
@@ -2285,7 +2286,8 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
         }
       };
 #ifndef DSTD_TF_SKIP_P2  // (timing experiments: phase 1 alone)
-      temporal_units<T, EPI, C, V, true, decltype(load_adj), (NW <= 8)>(a, st, ub + wave, ub + nv, NW, load_adj);
+      temporal_units<T, EPI, C, V, true, decltype(load_adj), (NW <= 8), tf_res_acc(T, V)>(a, st, ub + wave, ub + nv, NW,
+                                                                                             load_adj);
 #endif
     }
   }
@@ -2347,7 +2349,14 @@ hipError_t temporal_hl_t(const TemporalHLArgs& a, hipStream_t s) {
   }
   if (a.C != 64) return hipErrorNotSupported;
   switch (a.epi) {
-    case TEPI_ENC: return launch_units<k_temporal_hl<T, TEPI_ENC, 64>, temporal_nt<T, 64>()>(a.B * a.V, a, s);
+    case TEPI_ENC:
+      if constexpr (tf_res_acc(T, 25)) {
+        if (a.V == 25) return launch_units<k_temporal_hl<T, TEPI_ENC, 64, true>, temporal_nt<T, 64>()>(a.B * a.V, a, s);
+      }
+      if constexpr (tf_res_acc(T, 23)) {
+        if (a.V == 23) return launch_units<k_temporal_hl<T, TEPI_ENC, 64, true>, temporal_nt<T, 64>()>(a.B * a.V, a, s);
+      }
+      return launch_units<k_temporal_hl<T, TEPI_ENC, 64>, temporal_nt<T, 64>()>(a.B * a.V, a, s);
     case TEPI_IN: return launch_units<k_temporal_hl<T, TEPI_IN, 64>, temporal_nt<T, 64>()>(a.B * a.V, a, s);
     case TEPI_RAW: return launch_units<k_temporal_hl<T, TEPI_RAW, 64>, temporal_nt<T, 64>()>(a.B * a.V, a, s);
     default: return hipErrorNotSupported;
