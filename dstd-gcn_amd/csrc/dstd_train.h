@@ -95,9 +95,11 @@ hipError_t tanh_outer_bwd(const float* M, const float* dM, PQView v, int B, int 
 size_t adj_bwd_scratch_floats(int B, int A, int NN2);
 // assign_dA: dA (=) instead of (+=).  nparts > 1: dD is the fixed-order sum
 // of the partials dDpart[p][B][A][NN2] (agg_bwd), dE written to dD.
+// dW2 / Amul (optional): also dW2 += dA * Amul element-wise (the spatial
+// adjacency's dW_s = dA * A_s, with dA itself accumulated into dR_s)
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
                    float* dalpha, float* scratch, hipStream_t s, int assign_dA = 0, const float* dDpart = nullptr,
-                   int nparts = 1);
+                   int nparts = 1, float* dW2 = nullptr, const float* Amul = nullptr);
 
 // Batched strided 2-D copies in one launch: dst[r*dst_ld + c] (+)= src[r*src_ld + c].
 struct CopyJob {

@@ -1084,10 +1084,13 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
 
 // stage 2: blocks [0, cdiv(NN2,16)) finish dA (16 outputs x 16 slices over the
 // A*nch partial rows); the last block finishes dbrm and dalpha.
+// dW2 (optional): also dW2[ij] += dA-contribution * Amul[ij] (the spatial
+// adjacency A_s * W_s + R_s: dR_s = dA as dA itself, dW_s = dA * A_s)
 __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict__ pdA, const float* __restrict__ pbr,
                                                         const float* __restrict__ pal, int A, int NN2, int nch,
                                                         float* __restrict__ dA, float* __restrict__ dbrm,
-                                                        float* __restrict__ dalpha, int assign_dA) {
+                                                        float* __restrict__ dalpha, int assign_dA, float* __restrict__ dW2,
+                                                        const float* __restrict__ Amul) {
   __shared__ float lds[16][17];
   __shared__ float red[4];
   const int nblk = (NN2 + 15) / 16;
@@ -1104,6 +1107,7 @@ __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict_
       float t = 0.f;
       for (int k = 0; k < 16; ++k) t += lds[k][el];
       dA[ij] = assign_dA ? t : dA[ij] + t;
+      if (dW2) dW2[ij] += t * Amul[ij];
     }
     return;
   }
@@ -2057,14 +2061,17 @@ size_t adj_bwd_scratch_floats(int B, int A, int NN2) {
 }
 
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
-                   float* dalpha, float* scratch, hipStream_t s, int assign_dA, const float* dDpart, int nparts) {
+                   float* dalpha, float* scratch, hipStream_t s, int assign_dA, const float* dDpart, int nparts,
+                   float* dW2, const float* Amul) {
+  if (dW2 && !Amul) return hipErrorInvalidValue;
   if (nparts > 1 && !dDpart) return hipErrorInvalidValue;
   const int nch = adj_bwd_chunks(B, A);
   float* pdA = scratch;
   float* pbr = pdA + (size_t)nch * A * NN2;
   float* pal = pbr + (size_t)nch * A;
   k_adj_bwd_part<<<dim3(A, nch), 256, 0, s>>>(dD, E, alpha, B, A, NN2, nch, pdA, pbr, pal, dDpart, nparts);
-  k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(pdA, pbr, pal, A, NN2, nch, dA, dbrm, dalpha, assign_dA);
+  k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(pdA, pbr, pal, A, NN2, nch, dA, dbrm, dalpha, assign_dA, dW2,
+                                                      Amul);
   return hipGetLastError();
 }
 

@@ -357,7 +357,8 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
 // buffers; the op entry point accumulates both)
 hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* alpha, const OpSaved& sv,
                   const float* dy, float* dx, const dstd_gc_grads* gr, float* dA, float* dalpha, const OpWs& ws0,
-                  hipStream_t s, float dx_beta = 1.f, int assign_dA = 0, Wgrad* wg = nullptr) {
+                  hipStream_t s, float dx_beta = 1.f, int assign_dA = 0, Wgrad* wg = nullptr,
+                  float* dW2 = nullptr, const float* Amul = nullptr) {
   const long long ldG = (long long)g.CG() * g.TV;
   OpWs ws = ws0;
   int slot = 0;
@@ -391,7 +392,8 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
     nparts = 1;
   }
   // Adj = alpha * (conv_rm(M)) + A:  dalpha, dA, d b_rm, and dE = alpha dD in place
-  DSTD_TRYH(adj_bwd(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, dA, gr->brm, dalpha, ws.red, s, assign_dA, ws.dDp, nparts));
+  DSTD_TRYH(adj_bwd(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, dA, gr->brm, dalpha, ws.red, s, assign_dA, ws.dDp, nparts,
+                    dW2, Amul));
   const float* dE = ws.dD;
   Gemm wr;  // dWrm[a][k] = sum_{n,ij} dE[n][a][ij] M[n][k][ij]
   wr.M = g.A, wr.N = g.R * g.A, wr.K = g.NN2, wr.nb1 = g.B, wr.reduce = 1;
@@ -461,7 +463,7 @@ void carve_block_saved(Carver& cv, BlockSaved& s, int B, int cin, int cout, int 
 
 struct BlockWs {
   OpWs op;
-  float *dh, *dysp, *dr, *drc, *dAs, *pp;
+  float *dh, *dysp, *dr, *drc, *pp;
 };
 struct Chans {
   int cin, cout;
@@ -483,21 +485,33 @@ void carve_block_ws(Carver& cv, BlockWs& w, int B, int T, int V, std::initialize
   w.dysp = cv.take(act);
   w.dr = cv.take(act);
   w.drc = res ? cv.take(act) : nullptr;
-  w.dAs = cv.take(2 * V * V);
   w.pp = cv.take(cmax);
 }
 
+// conv weights of the block's three ops -> packed [W_f; W_m1; W_m2] (18 jobs)
+constexpr int kBlockPackJobs = 18;
+void pack_block(CopyJobs& js, const dstd_block_params* p, const BlockSaved& S, int B, int T, int V) {
+  const OpGeom gs(DSTD_MODE_SPATIAL, B, p->cin, p->cout, T, V);
+  const OpGeom gt(DSTD_MODE_TEMPORAL, B, p->cout, p->cout, T, V);
+  pack_jobs(js, &p->conv_s[0], S.op[0], gs);
+  pack_jobs(js, &p->conv_s[1], S.op[1], gs);
+  pack_jobs(js, &p->conv_t, S.op[2], gt);
+}
+
+// packed: the caller already packed the block's weights (the model forward
+// packs all blocks in two launches)
 hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum, float* y,
-                     const BlockSaved& S, hipStream_t s, int run = 0, const dstd_bn_sync* sync = nullptr) {
+                     const BlockSaved& S, hipStream_t s, int run = 0, const dstd_bn_sync* sync = nullptr,
+                     bool packed = false) {
   const int cin = p->cin, cout = p->cout, TV = T * V;
   const bool res = cin != cout;
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
   const OpGeom gt(DSTD_MODE_TEMPORAL, B, cout, cout, T, V);
-  CopyJobs js;  // conv weights of the block's three ops -> packed [W_f; W_m1; W_m2]
-  pack_jobs(js, &p->conv_s[0], S.op[0], gs);
-  pack_jobs(js, &p->conv_s[1], S.op[1], gs);
-  pack_jobs(js, &p->conv_t, S.op[2], gt);
-  DSTD_TRYH(copy_jobs(js, s));
+  if (!packed) {
+    CopyJobs js;
+    pack_block(js, p, S, B, T, V);
+    DSTD_TRYH(copy_jobs(js, s));
+  }
   for (int i = 0; i < 2; ++i)  // :145-150, A_s*W_s + R_s (:146-149)
     DSTD_TRYH(op_fwd(gs, x, &p->conv_s[i], p->A_s + i * V * V, p->W_s + i * V * V, p->R_s + i * V * V, p->alpha_sm,
                      S.ysp, i ? 1.f : 0.f, S.op[i], s));
@@ -593,11 +607,12 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
     DSTD_TRYH(acc_mul(W.dr, nullptr, dx, act, s, dx_extra, dx_init ? 1 : 0));
   }
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
-  for (int i = 0; i < 2; ++i)  // each graph's dA (=) into its own half of dAs
-    DSTD_TRYH(op_bwd(gs, x, &p->conv_s[i], p->alpha_sm, S.op[i], W.dysp, dx, &g->conv_s[i], W.dAs + i * V * V,
-                     g->alpha_sm, W.op, s, 1.f, 1, wg));
-  // A_s*W_s + R_s with A_s constant: dR_s = dA, dW_s = dA * A_s (both graphs)
-  return adj_param_grads(W.dAs, p->A_s, g->R_s, g->W_s, (size_t)2 * V * V, s);
+  // A_s*W_s + R_s with A_s constant: each graph's dA accumulates straight into
+  // its dR_s, and dW_s += dA * A_s, in the adjacency-backward finish
+  for (int i = 0; i < 2; ++i)
+    DSTD_TRYH(op_bwd(gs, x, &p->conv_s[i], p->alpha_sm, S.op[i], W.dysp, dx, &g->conv_s[i], g->R_s + i * V * V,
+                     g->alpha_sm, W.op, s, 1.f, 0, wg, g->W_s + i * V * V, p->A_s + i * V * V));
+  return hipSuccess;
 }
 
 // ---------------------------------------------------------------------------
@@ -846,7 +861,22 @@ int dstd_model_train_fwd_sync(const dstd_model_params* p, const float* x, int B,
   carve_model_saved(cv, S, B, T, V, C, L);
   const size_t act = (size_t)B * C * T * V;
   DSTD_TRY(prep_nctv(x, B, T, V, 3, S.X0, s));                                   // :298-303
-  DSTD_TRY(block_fwd(&p->st_in, S.X0, B, T, V, momentum, S.y0, S.st_in, s, run, sync));  // :305
+  {  // every block's packed conv weights, kMaxCopyJobs per launch
+    CopyJobs js;
+    auto add = [&](const dstd_block_params* bp, const BlockSaved& bs) -> hipError_t {
+      if (js.n + kBlockPackJobs > kMaxCopyJobs) {
+        DSTD_TRYH(copy_jobs(js, s));
+        js.n = 0;
+      }
+      pack_block(js, bp, bs, B, T, V);
+      return hipSuccess;
+    };
+    DSTD_TRY(add(&p->st_in, S.st_in));
+    for (int i = 0; i < L; ++i) DSTD_TRY(add(&p->enc[i], S.enc[i]));
+    DSTD_TRY(add(&p->st_out, S.st_out));
+    DSTD_TRY(copy_jobs(js, s));
+  }
+  DSTD_TRY(block_fwd(&p->st_in, S.X0, B, T, V, momentum, S.y0, S.st_in, s, run, sync, true));  // :305
   BnFwd b0;                                                                      // :306-308
   b0.x = S.y0;
   b0.gamma = p->bn_in.weight;
@@ -866,7 +896,7 @@ int dstd_model_train_fwd_sync(const dstd_model_params* p, const float* x, int B,
   DSTD_TRY(bn_train_fwd(b0, B, C, T, V, S.red, s));
   if (dropout_p > 0.f) DSTD_TRY(dropout(S.hp0, S.h[0], act, dropout_p, seed, s, (flags & DSTD_TRAIN_SEED_DEVICE) != 0));  // do_in
   for (int i = 0; i < L; ++i) {                                                  // :310-311
-    DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s, run, sync));
+    DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s, run, sync, true));
     BnFwd be;  // BN(block(h) + h) -> PReLU  (:278-285, Identity residual :247-248)
     be.x = S.yb[i];
     be.x2 = S.h[i];
@@ -886,7 +916,7 @@ int dstd_model_train_fwd_sync(const dstd_model_params* p, const float* x, int B,
     be.sync = sync;
     DSTD_TRY(bn_train_fwd(be, B, C, T, V, S.red, s));
   }
-  DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s, run, sync));  // :313
+  DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s, run, sync, true));  // :313
   DSTD_TRY(out_ntvc(S.o, x, B, T, V, 3, y, s));                                       // :314-315
   return DSTD_OK;
 }
