@@ -201,6 +201,7 @@ struct BnBwd {
   const float* gamma;
   float* du;
   float* dz_out = nullptr;
+  const float* dz_add = nullptr;  // dz_out = dz + dz_add (an identity path's gradient joined in the same pass)
   float* dgamma;
   float* dbeta;
   int use_running = 0;  // mean / rstd are constants (eval-mode BN): du = gamma * rstd * dz

@@ -1644,7 +1644,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int
       const float mean = mnl[v], rstd = rsl[v];
       const float xh = (uv[j] - mean) * rstd;
       a.du[i] = a.use_running ? gml[v] * rstd * dz : gml[v] * rstd * (dz - sdl[v] * inv - xh * sxl[v] * inv);
-      if (a.dz_out) a.dz_out[i] = dz;
+      if (a.dz_out) a.dz_out[i] = a.dz_add ? dz + a.dz_add[i] : dz;
     }
   }
 }

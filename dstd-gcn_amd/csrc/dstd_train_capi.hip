@@ -580,6 +580,13 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
   bb.gamma = p->bn.weight;
   bb.du = W.dysp;
   bb.dz_out = W.dr;
+  // identity residual, first contribution to dx: the BN backward writes
+  // dx = dz (+ dx_extra) itself (no separate accumulate pass)
+  const bool dz_to_dx = !res && dx && dx_init;
+  if (dz_to_dx) {
+    bb.dz_out = dx;
+    bb.dz_add = dx_extra;
+  }
   bb.dgamma = g->bn.weight;
   bb.dbeta = g->bn.bias;
   bb.use_running = (run & DSTD_TRAIN_RUNNING_STATS) != 0;
@@ -603,7 +610,7 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
     if (dx_extra) return hipErrorInvalidValue;
     DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, W.op.red, s,
                        dx_init ? 0.f : 1.f));
-  } else if (dx) {
+  } else if (dx && !dz_to_dx) {
     DSTD_TRYH(acc_mul(W.dr, nullptr, dx, act, s, dx_extra, dx_init ? 1 : 0));
   }
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
