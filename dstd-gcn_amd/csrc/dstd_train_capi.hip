@@ -307,14 +307,20 @@ Gemm conv_dw(const float* dY, const float* X, float* dW, int B, int cin, int cou
   return g;
 }
 hipError_t conv_bwd(const float* W, const float* X, const float* dY, float* dX, float* dW, float* db, int B, int cin,
-                    int cout, int TV, float* gs, float* red, hipStream_t s, float dx_beta = 1.f) {
+                    int cout, int TV, float* gs, hipStream_t s, float dx_beta = 1.f) {
   if (dX) {
     Gemm gx = conv_dx(W, dY, dX, B, cin, cout, TV);
     gx.beta = dx_beta;
     DSTD_TRYH(gemm(gx, gs, s));
   }
-  DSTD_TRYH(gemm(conv_dw(dY, X, dW, B, cin, cout, TV), gs, s));
-  return reduce_rows(dY, cout, B, TV, (long long)cout * TV, TV, 1, db, 1.f, red, s);
+  // [dW | db] = sum dY [X; 1]^T in one reduce GEMM (the bias as the ones
+  // column), accumulated into the parameters' gradients
+  Gemm gw = conv_dw(dY, X, dW, B, cin + 1, cout, TV);
+  gw.b_ones_last = 1;
+  gw.b_b1 = (long long)cin * TV;
+  gw.nseg = 1;
+  gw.seg[0] = Gemm::Seg{0, cout, dW, db};
+  return gemm(gw, gs, s);
 }
 
 // y (beta_y: 0 '=' / 1 '+=') = DSTDGC(x, Acomb, alpha); fills sv.  The packed
@@ -608,7 +614,7 @@ hipError_t block_bwd(const dstd_block_params* p, const float* x, int B, int T, i
     rb.sync = sync;
     DSTD_TRYH(bn_train_bwd(rb, B, cout, T, V, W.op.red, nullptr, s));
     if (dx_extra) return hipErrorInvalidValue;
-    DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, W.op.red, s,
+    DSTD_TRYH(conv_bwd(p->res_w, x, W.drc, dx, g->res_w, g->res_b, B, cin, cout, TV, W.op.gs, s,
                        dx_init ? 0.f : 1.f));
   } else if (dx && !dz_to_dx) {
     DSTD_TRYH(acc_mul(W.dr, nullptr, dx, act, s, dx_extra, dx_init ? 1 : 0));

@@ -2,7 +2,9 @@
 # round 4 (r04p): forward parity suite (the residual accumulator now per
 # shape: CMU and 3DPW), training suite, then the B=32 / B=256 training step
 # A/B of HEAD against the previous commit (prev): spatial dR_s / dW_s in the
-# adjacency-backward finish, all blocks' conv weights packed in two launches
+# adjacency-backward finish, all blocks' conv weights packed in two launches,
+# the BN backward writing dz + identity gradient, the residual conv bias
+# gradient folded into its weight-gradient GEMM
 cd "$(dirname "$0")/.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04p
