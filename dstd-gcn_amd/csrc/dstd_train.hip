@@ -290,6 +290,161 @@ struct FastDiv {
 };
 
 // ---------------------------------------------------------------------------
+// Streaming GEMM of the training step's 1x1 convolutions and conv_rm products:
+// C[b][m][p] = alpha * sum_k A[m][k] B[b][k][p] + bias_m[m] (+ beta C) (+ the
+// d_out adjacency), M, K <= 80, B and C rows contiguous.  The weight matrix
+// stays in registers as MFMA A fragments for the whole launch (staged once
+// per workgroup through LDS); each wave then streams 16-column items
+// (b, column tile) with the next item's B fragments in flight during the
+// current item's MFMAs -- no LDS round trip and no barrier per tile.  The
+// panel kernels below staged both operands per workgroup and ran load,
+// compute and store in lockstep (conv forward 20.4 us, conv dx 23.8 us at
+// the config-5 batch against a 4 us copy of the panel, profiles/r03v).
+// ---------------------------------------------------------------------------
+constexpr int kCsMax = 80;  // M, K
+constexpr uint32_t kCsOOB = 0x80000000u;
+// a zero hipcc cannot see through: keeps the loop-invariant A-fragment LDS
+// reads inside the item loop instead of hoisted into ~100 live registers
+__device__ __forceinline__ int cs_opaque_zero() {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}  // buffer offset past any range: loads 0, stores dropped
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t cs_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ float cs_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ void cs_st(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
+}
+// Launch constants of k_conv_stream (byte strides of one batch's panels)
+struct CsArgs {
+  int ntile, nb2;
+  uint32_t b_bytes, c_bytes;  // one batch's B / C extent (buffer ranges)
+};
+template <int MF, int KS>
+__global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
+  // A in LDS in fragment order, four k-steps per lane per 16-byte read:
+  // As[((x KS4 + s4) 64 + lane) 4 + j] = A[16x + lr][4 (4 s4 + j) + lk]
+  constexpr int KS4 = (KS + 3) / 4;
+  __shared__ float4 As[MF * KS4 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
+  float* Af = reinterpret_cast<float*>(As);
+  for (int e = tid; e < MF * KS4 * 256; e += 256) {
+    const int j = e & 3, l = (e >> 2) & 63, f = e >> 8, x = f / KS4, s4 = f - x * KS4;
+    const int m = x * 16 + (l & 15), k = 4 * (4 * s4 + j) + (l >> 4);
+    const bool in = m < g.M && k < g.K;
+    const float v = g.A[in ? m * g.a_m + k * g.a_k : 0];
+    Af[e] = in ? v : 0.f;
+  }
+  __syncthreads();
+
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntile = ca.ntile, nw = gridDim.x * 4, items = g.nb1 * ca.nb2 * ntile;
+  const int K = g.K, M = g.M, N = g.N;
+  const int bk = (int)g.b_k, cm = (int)g.c_m;
+  // the item's batch panels (wave-uniform) and this lane's column
+  auto panel = [&](int it, const float*& Bb, float*& Cb, float*& Db, int& p) {
+    const int b = it / ntile, t = it - b * ntile;
+    const int b1 = b / ca.nb2, b2 = b - b1 * ca.nb2;
+    Bb = g.B + b1 * g.b_b1 + b2 * g.b_b2;
+    Cb = g.C + b1 * g.c_b1 + b2 * g.c_b2;
+    Db = g.d_out ? g.d_out + b1 * g.c_b1 + b2 * g.c_b2 : nullptr;
+    p = t * 16 + lr;
+  };
+  auto load = [&](int it, float (&v)[KS]) {
+    const float* Bb;
+    float* Cb;
+    float* Db;
+    int p;
+    panel(it, Bb, Cb, Db, p);
+    const auto rb = cs_rsrc(Bb, ca.b_bytes);
+#pragma unroll
+    for (int sk = 0; sk < KS; ++sk) {
+      const int k = 4 * sk + lk;
+      v[sk] = cs_ld(rb, k < K && p < N ? (uint32_t)(k * bk + p) * 4u : kCsOOB);
+    }
+  };
+  int it = blockIdx.x * 4 + wave;
+  float bf[KS];
+  if (it < items) load(it, bf);
+  for (; it < items; it += nw) {
+    float bn[KS];
+    const int nx = it + nw;
+    load(nx < items ? nx : it, bn);  // the next item's fragments (the last reloads its own)
+    const float* Bb;
+    float* Cb;
+    float* Db;
+    int p;
+    panel(it, Bb, Cb, Db, p);
+    const auto rc = cs_rsrc(Cb, ca.c_bytes);
+    const bool pin = p < N;
+    // beta: this item's C values, loaded before the MFMAs so they arrive under them
+    float cv[MF][4];
+    if (g.beta != 0.f) {
+#pragma unroll
+      for (int x = 0; x < MF; ++x)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = x * 16 + lk * 4 + r;
+          cv[x][r] = cs_ld(rc, pin && m < M ? (uint32_t)(m * cm + p) * 4u : kCsOOB);
+        }
+    }
+    f32x4 acc[MF];
+#pragma unroll
+    for (int x = 0; x < MF; ++x) acc[x] = zero4();
+    const int lz = lane + cs_opaque_zero();
+#pragma unroll
+    for (int s4 = 0; s4 < KS4; ++s4) {
+      float4 a[MF];
+#pragma unroll
+      for (int x = 0; x < MF; ++x) a[x] = As[(x * KS4 + s4) * 64 + lz];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (4 * s4 + j >= KS) break;
+#pragma unroll
+        for (int x = 0; x < MF; ++x)
+          acc[x] = mfma16x16x4(j == 0 ? a[x].x : j == 1 ? a[x].y : j == 2 ? a[x].z : a[x].w, bf[4 * s4 + j], acc[x]);
+      }
+    }
+    if (Db) {  // C and D = d_alpha * C + (d_A (* d_W) (+ d_R)) of this column (k_gemm's order)
+      const auto rd = cs_rsrc(Db, ca.c_bytes);
+      const float ad = *g.d_alpha;
+      const int pc = pin ? p : 0;
+      float ac = g.d_A[pc];
+      if (g.d_W) ac *= g.d_W[pc];
+      if (g.d_R) ac += g.d_R[pc];
+#pragma unroll
+      for (int x = 0; x < MF; ++x)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = x * 16 + lk * 4 + r;
+          const uint32_t off = pin && m < M ? (uint32_t)(m * cm + p) * 4u : kCsOOB;
+          float v = g.alpha * acc[x][r];
+          if (g.bias_m) v += g.bias_m[m < M ? m : 0];
+          cs_st(rd, off, fmaf(ad, v, ac));
+          if (g.beta != 0.f) v += g.beta * cv[x][r];
+          cs_st(rc, off, v);
+        }
+    } else {
+#pragma unroll
+      for (int x = 0; x < MF; ++x)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = x * 16 + lk * 4 + r;
+          float v = fmaf(g.alpha, acc[x][r], g.bias_m ? g.bias_m[m < M ? m : 0] : 0.f);
+          if (g.beta != 0.f) v = fmaf(g.beta, cv[x][r], v);
+          cs_st(rc, pin && m < M ? (uint32_t)(m * cm + p) * 4u : kCsOOB, v);
+        }
+    }
+#pragma unroll
+    for (int sk = 0; sk < KS; ++sk) bf[sk] = bn[sk];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Skinny GEMM of the training step's 1x1 convolutions: a small weight matrix
 // (M, K <= 80) times a wide panel of contiguous rows.  gemm() routes the
 // matching shapes here; the whole K extent of both operands sits in LDS.
@@ -1806,6 +1961,68 @@ void sk_go(K kern, int grid, size_t lds, hipStream_t s, Args... args) {
   }
   kern<<<grid, 256, lds, s>>>(args...);
 }
+#ifndef DSTD_GEMM_STREAM
+#define DSTD_GEMM_STREAM 1
+#endif
+template <int MF, int KS>
+hipError_t cs_go(const Gemm& g, int ntile, hipStream_t s) {
+  static const int occ = [] {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k_conv_stream<MF, KS>, 256, 0) != hipSuccess ||
+        nb < 1)
+      nb = 1;
+    (void)hipGetLastError();
+    return nb;
+  }();
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  const long items = (long)g.nb1 * g.nb2 * ntile;
+  const int grid = (int)std::max(1L, std::min((long)cus * occ, (items + 3) / 4));
+  CsArgs ca;
+  ca.ntile = ntile;
+  ca.nb2 = g.nb2;
+  ca.b_bytes = (uint32_t)(((long long)(g.K - 1) * g.b_k + g.N) * 4);
+  ca.c_bytes = (uint32_t)(((long long)(g.M - 1) * g.c_m + g.N) * 4);
+  k_conv_stream<MF, KS><<<grid, 256, 0, s>>>(g, ca);
+  return hipGetLastError();
+}
+template <int MF>
+hipError_t cs_ks(const Gemm& g, int ntile, hipStream_t s) {
+  const int ks = cdiv(g.K, 4);
+  if (ks <= 4) return cs_go<MF, 4>(g, ntile, s);
+  if (ks <= 8) return cs_go<MF, 8>(g, ntile, s);
+  if (ks <= 16) return cs_go<MF, 16>(g, ntile, s);
+  if (ks <= 17) return cs_go<MF, 17>(g, ntile, s);
+  return cs_go<MF, 20>(g, ntile, s);
+}
+// hipErrorNotSupported: not a streaming shape (nothing launched)
+hipError_t gemm_stream(const Gemm& g, hipStream_t s) {
+  if (!DSTD_GEMM_STREAM || g.reduce || g.b_n != 1 || g.c_n != 1 || g.b_ones_last || g.nseg || g.M > kCsMax ||
+      g.K > kCsMax || g.K < 1 || g.N < 16)
+    return hipErrorNotSupported;
+  const long long nbat = (long long)g.nb1 * g.nb2;
+  const int ntile = cdiv(g.N, 16);
+  // 32-bit buffer offsets over one batch's panels
+  if (nbat * ntile >= (1LL << 31) || g.b_k < g.N || g.c_m < g.N || ((long long)(g.K - 1) * g.b_k + g.N) * 4 >= (1LL << 31) ||
+      ((long long)(g.M - 1) * g.c_m + g.N) * 4 >= (1LL << 31))
+    return hipErrorNotSupported;
+#ifdef DSTD_GEMM_LOG
+  fprintf(stderr, "gemm stream M %d N %d K %d nb %lld beta %g bias %d d_out %d stream %p\n", g.M, g.N, g.K, nbat, g.beta,
+          g.bias_m != nullptr, g.d_out != nullptr, (void*)s);
+#endif
+  switch (cdiv(g.M, 16)) {
+    case 1: return cs_ks<1>(g, ntile, s);
+    case 2: return cs_ks<2>(g, ntile, s);
+    case 3: return cs_ks<3>(g, ntile, s);
+    case 4: return cs_ks<4>(g, ntile, s);
+    default: return cs_ks<5>(g, ntile, s);
+  }
+}
 // hipErrorNotSupported: not a skinny shape (nothing launched)
 hipError_t gemm_skinny(const Gemm& g, float* scratch, hipStream_t s) {
   const int nbat = g.nb1 * g.nb2;
@@ -1818,6 +2035,10 @@ hipError_t gemm_skinny(const Gemm& g, float* scratch, hipStream_t s) {
     const int MF = cdiv(g.M, 16), K4 = rup(g.K, 4), KP = sk_pitch(K4, 4), BP = sk_pitch(kSkPT, 16);
     const size_t lds = sizeof(float) * ((size_t)MF * 16 * KP + (size_t)K4 * BP);
     const int grid = nbat * cdiv(g.N, kSkPT);
+#ifdef DSTD_GEMM_LOG
+    fprintf(stderr, "gemm skinny MF %d M %d N %d K %d nb %d beta %g bias %d stream %p\n", MF, g.M, g.N, g.K, nbat, g.beta,
+            g.bias_m != nullptr, (void*)s);
+#endif
     const int vec = g.N % 4 == 0 && g.b_k % 4 == 0 && g.b_b1 % 4 == 0 && g.b_b2 % 4 == 0 &&
                     ((uintptr_t)g.B & 15) == 0;
     switch (MF) {
@@ -1836,6 +2057,10 @@ hipError_t gemm_skinny(const Gemm& g, float* scratch, hipStream_t s) {
 hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.d_out && (g.reduce || !g.d_A || !g.d_alpha)) return hipErrorInvalidValue;
+  {
+    const hipError_t e = gemm_stream(g, s);
+    if (e != hipErrorNotSupported) return e;
+  }
   {
     const hipError_t e = gemm_skinny(g, scratch, s);
     if (e != hipErrorNotSupported) return e;
@@ -1863,9 +2088,9 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
   dim3 grid(cdiv(g.N, TN), cdiv(g.M, TM), g.reduce ? nsplit : nbat);
   float* part = nsplit > 1 ? scratch : nullptr;
 #ifdef DSTD_GEMM_LOG  // (debug builds: the shape mix of a training step)
-  fprintf(stderr, "gemm M %d N %d K %d nb %d reduce %d nsplit %d a_m %lld a_k %lld b_k %lld b_n %lld c_m %lld c_n %lld "
-          "d_out %d nseg %d bias %d beta %g\n", g.M, g.N, g.K, nbat, g.reduce, nsplit, g.a_m, g.a_k, g.b_k, g.b_n, g.c_m,
-          g.c_n, g.d_out != nullptr, g.nseg, g.bias_m != nullptr, g.beta);
+  fprintf(stderr, "gemm tile %dx%d M %d N %d K %d nb %d reduce %d nsplit %d a_m %lld a_k %lld b_k %lld b_n %lld c_m %lld "
+          "c_n %lld d_out %d nseg %d bias %d beta %g stream %p\n", TM, TN, g.M, g.N, g.K, nbat, g.reduce, nsplit, g.a_m,
+          g.a_k, g.b_k, g.b_n, g.c_m, g.c_n, g.d_out != nullptr, g.nseg, g.bias_m != nullptr, g.beta, (void*)s);
 #endif
 #define DSTD_GEMM_GO(tm, tn) \
   if (TM == tm && TN == tn) k_gemm<tm, tn><<<grid, 256, 0, s>>>(g, nsplit, kch, kc_len, part)

@@ -5,3 +5,8 @@ cd "$(dirname "$0")" || exit 2
   -L../../dstd-gcn_amd -ldstd_gcn -Wl,-rpath,'$ORIGIN/../../dstd-gcn_amd'
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 skinny_micro.cpp -o skinny_micro \
   -L../../dstd-gcn_amd -ldstd_gcn -Wl,-rpath,'$ORIGIN/../../dstd-gcn_amd'
+# the same benchmark against a variant library (e.g. libdstd_gcn_nostream.so)
+if [ -f ../../dstd-gcn_amd/libdstd_gcn_nostream.so ]; then
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 skinny_micro.cpp -o skinny_micro_nostream \
+    -L../../dstd-gcn_amd -l:libdstd_gcn_nostream.so -Wl,-rpath,'$ORIGIN/../../dstd-gcn_amd'
+fi

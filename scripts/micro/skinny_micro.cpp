@@ -3,6 +3,7 @@
 // (DSTD_GEMM_GENERIC=1 for k_gemm), plus a D2D copy of the panel for scale.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
+#include <math.h>
 #include <stdlib.h>
 #include <vector>
 
@@ -89,6 +90,41 @@ int main() {
   e.A = W, e.a_m = 80, e.a_k = 1;
   e.B = Mt, e.b_b1 = 80 * 529, e.b_k = 529, e.b_n = 1;
   e.C = Et, e.c_b1 = 40 * 529, e.c_m = 529, e.c_n = 1;
+  // correctness of the dispatched kernels against a double host reference
+  // (batches 0, 17, 63; C restored before each check run)
+  auto check = [&](const char* name, const Gemm& g, int nbat) {
+    const size_t na = (size_t)(g.M - 1) * g.a_m + (size_t)(g.K - 1) * g.a_k + 1;
+    const size_t nbb = (size_t)(nbat - 1) * g.b_b1 + (size_t)(g.K - 1) * g.b_k + (size_t)(g.N - 1) * g.b_n + 1;
+    const size_t nc = (size_t)(nbat - 1) * g.c_b1 + (size_t)(g.M - 1) * g.c_m + (size_t)(g.N - 1) * g.c_n + 1;
+    std::vector<float> ha(na), hb(nbb), hc0(nc), hc(nc), hbias(g.M, 0.f);
+    CK(hipMemcpy(ha.data(), g.A, na * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hb.data(), g.B, nbb * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hc0.data(), g.C, nc * 4, hipMemcpyDeviceToHost));
+    if (g.bias_m) CK(hipMemcpy(hbias.data(), g.bias_m, g.M * 4, hipMemcpyDeviceToHost));
+    CK(gemm(g, nullptr, 0));
+    CK(hipMemcpy(hc.data(), g.C, nc * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(g.C, hc0.data(), nc * 4, hipMemcpyHostToDevice));
+    double worst = 0;
+    const int bs[3] = {0, 17, nbat - 1};
+    for (int bi = 0; bi < 3; ++bi)
+      for (int m = 0; m < g.M; ++m)
+        for (int n = 0; n < g.N; ++n) {
+          double acc = 0, mag = 0;
+          for (int k = 0; k < g.K; ++k) {
+            const double t = (double)ha[m * g.a_m + k * g.a_k] * hb[bs[bi] * g.b_b1 + k * g.b_k + n * g.b_n];
+            acc += t;
+            mag += fabs(t);
+          }
+          const size_t ci = bs[bi] * g.c_b1 + m * g.c_m + n * g.c_n;
+          double ref = g.alpha * acc + hbias[m];
+          if (g.beta != 0.f) ref += g.beta * (double)hc0[ci];
+          const double err = fabs(hc[ci] - ref) / (mag + fabs(hbias[m]) + fabs(g.beta * hc0[ci]) + 1e-30);
+          if (err > worst) worst = err;
+        }
+    printf("%s: max |err| / sum|terms| = %.3g%s\n", name, worst, worst < 1e-6 ? "" : "  <-- FAIL");
+    return worst < 1e-6;
+  };
+  bool ok = check("conv fwd", f, B) & check("conv dx", x, B) & check("E", e, B);
   const double tf = time_us([&] { return gemm(f, nullptr, 0); });
   const double tx = time_us([&] { return gemm(x, nullptr, 0); });
   const double tw = time_us([&] { return gemm(w, scratch, 0); });
@@ -98,5 +134,5 @@ int main() {
   const double tc = time_us([&] { return hipMemcpyAsync(Y, X, xb, hipMemcpyDeviceToDevice, 0); });
   printf("conv fwd %.1f us  conv dx %.1f us  conv dw %.1f us  wr %.1f us  E %.1f us | D2D copy of x (%.1f MB) %.1f us\n", tf,
          tx, tw, tr, te, xb / 1e6, tc);
-  return 0;
+  return ok ? 0 : 1;
 }
