@@ -317,6 +317,9 @@ __device__ __forceinline__ float cs_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 __device__ __forceinline__ void cs_st(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+#if defined(DSTD_CS_ABL) && (DSTD_CS_ABL & 2)  // (ablation builds: stores dropped)
+  if (v != 12345.f) off = kCsOOB;
+#endif
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off, 0, 0);
 }
 // Launch constants of k_conv_stream (byte strides of one batch's panels)
@@ -396,6 +399,11 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
 #pragma unroll
     for (int x = 0; x < MF; ++x) acc[x] = zero4();
     const int lz = lane + cs_opaque_zero();
+#if defined(DSTD_CS_ABL) && (DSTD_CS_ABL & 1)  // (ablation builds: no MFMAs)
+#pragma unroll
+    for (int sk = 0; sk < KS; ++sk) acc[sk % MF][sk & 3] += bf[sk];
+    if (lz < 0) 
+#endif
 #pragma unroll
     for (int s4 = 0; s4 < KS4; ++s4) {
       float4 a[MF];
@@ -1982,7 +1990,10 @@ hipError_t cs_go(const Gemm& g, int ntile, hipStream_t s) {
     return v;
   }();
   const long items = (long)g.nb1 * g.nb2 * ntile;
-  const int grid = (int)std::max(1L, std::min((long)cus * occ, (items + 3) / 4));
+#ifndef DSTD_CS_GRID_DIV  // (experiments: fewer resident workgroups, more items per wave)
+#define DSTD_CS_GRID_DIV 1
+#endif
+  const int grid = (int)std::max(1L, std::min((long)cus * occ / DSTD_CS_GRID_DIV, (items + 3) / 4));
   CsArgs ca;
   ca.ntile = ntile;
   ca.nb2 = g.nb2;
@@ -2002,7 +2013,8 @@ hipError_t cs_ks(const Gemm& g, int ntile, hipStream_t s) {
 }
 // hipErrorNotSupported: not a streaming shape (nothing launched)
 hipError_t gemm_stream(const Gemm& g, hipStream_t s) {
-  if (!DSTD_GEMM_STREAM || g.reduce || g.b_n != 1 || g.c_n != 1 || g.b_ones_last || g.nseg || g.M > kCsMax ||
+  // (one A shared by every batch: it is staged once per workgroup)
+  if (!DSTD_GEMM_STREAM || g.reduce || g.a_b1 || g.a_b2 || g.b_n != 1 || g.c_n != 1 || g.b_ones_last || g.nseg || g.M > kCsMax ||
       g.K > kCsMax || g.K < 1 || g.N < 16)
     return hipErrorNotSupported;
   const long long nbat = (long long)g.nb1 * g.nb2;
@@ -2030,7 +2042,7 @@ hipError_t gemm_skinny(const Gemm& g, float* scratch, hipStream_t s) {
   // forward, K = Cin = 64: 20.5 vs 25.5 us at the config-5 batch,
   // profiles/r03v_skinny_micro.txt); conv dx (K = 68, beta 1), conv_rm (d_out)
   // and its transposed product (K = A) stay on k_gemm.
-  if (!g.reduce && g.b_n == 1 && g.c_n == 1 && !g.b_ones_last && !g.d_out && !g.nseg && g.beta == 0.f &&
+  if (!g.reduce && !g.a_b1 && !g.a_b2 && g.b_n == 1 && g.c_n == 1 && !g.b_ones_last && !g.d_out && !g.nseg && g.beta == 0.f &&
       g.M <= kSkMax && g.K <= kSkMax && g.K >= 48 && g.N >= 64) {
     const int MF = cdiv(g.M, 16), K4 = rup(g.K, 4), KP = sk_pitch(K4, 4), BP = sk_pitch(kSkPT, 16);
     const size_t lds = sizeof(float) * ((size_t)MF * 16 * KP + (size_t)K4 * BP);

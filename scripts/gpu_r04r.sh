@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 4 (r04r): streaming 1x1-conv GEMM diagnostics -- microbenchmark of the
+# default build against the panel / tile kernels (nostream), fewer resident
+# workgroups (csg2 / csg4: more items per wave), no MFMAs (csnomfma), no
+# stores (csnost); then the training suites with HEAD (shared-A routing fix)
+cd "$(dirname "$0")/.." || exit 2
+R="$PWD"
+O=$R/gpurun_out/r04r
+mkdir -p $O
+for v in nostream "" csg2 csg4 csnomfma csnost; do
+  b=scripts/micro/skinny_micro${v:+_$v}
+  timeout -k 10 60 $b > $O/micro_${v:-stream}.txt 2>&1; st=$?
+  echo "== ${v:-stream} (exit $st)"; cat $O/micro_${v:-stream}.txt | grep -v FAIL | tail -1
+  [ $st -eq 0 ] || [ $st -eq 1 ] || exit $st
+done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_train.py tests/test_gpu_fast.py > $O/pytest_train.log 2>&1
+st=$?; tail -2 $O/pytest_train.log; [ $st -eq 0 ] || exit $st

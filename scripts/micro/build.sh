@@ -5,8 +5,9 @@ cd "$(dirname "$0")" || exit 2
   -L../../dstd-gcn_amd -ldstd_gcn -Wl,-rpath,'$ORIGIN/../../dstd-gcn_amd'
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 skinny_micro.cpp -o skinny_micro \
   -L../../dstd-gcn_amd -ldstd_gcn -Wl,-rpath,'$ORIGIN/../../dstd-gcn_amd'
-# the same benchmark against a variant library (e.g. libdstd_gcn_nostream.so)
-if [ -f ../../dstd-gcn_amd/libdstd_gcn_nostream.so ]; then
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 skinny_micro.cpp -o skinny_micro_nostream \
-    -L../../dstd-gcn_amd -l:libdstd_gcn_nostream.so -Wl,-rpath,'$ORIGIN/../../dstd-gcn_amd'
-fi
+# the same benchmark against variant libraries: MICRO_VARIANTS="nostream csg2 ..."
+# builds skinny_micro_<name> linked with libdstd_gcn_<name>.so
+for v in ${MICRO_VARIANTS:-}; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 skinny_micro.cpp -o skinny_micro_$v \
+    -L../../dstd-gcn_amd -l:libdstd_gcn_$v.so -Wl,-rpath,'$ORIGIN/../../dstd-gcn_amd' || exit 1
+done
