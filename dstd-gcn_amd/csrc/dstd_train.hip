@@ -327,8 +327,15 @@ struct CsArgs {
   int ntile, nb2;
   uint32_t b_bytes, c_bytes;  // one batch's B / C extent (buffer ranges)
 };
+#ifndef DSTD_CS_NT  // 16-column tiles per item (experiments: 1, 2, 4)
+#define DSTD_CS_NT 1
+#endif
+#ifndef DSTD_CS_PF  // next item's B fragments loaded during this item's MFMAs
+#define DSTD_CS_PF 1
+#endif
 template <int MF, int KS>
 __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
+  constexpr int NT = DSTD_CS_NT, PF = DSTD_CS_PF;
   // A in LDS in fragment order, four k-steps per lane per 16-byte read:
   // As[((x KS4 + s4) 64 + lane) 4 + j] = A[16x + lr][4 (4 s4 + j) + lk]
   constexpr int KS4 = (KS + 3) / 4;
@@ -345,19 +352,19 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
   __syncthreads();
 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ntile = ca.ntile, nw = gridDim.x * 4, items = g.nb1 * ca.nb2 * ntile;
+  const int ntile = ca.ntile, nw = gridDim.x * 4, items = g.nb1 * ca.nb2 * ntile;  // ntile: items per batch
   const int K = g.K, M = g.M, N = g.N;
   const int bk = (int)g.b_k, cm = (int)g.c_m;
-  // the item's batch panels (wave-uniform) and this lane's column
+  // the item's batch panels (wave-uniform) and this lane's first column
   auto panel = [&](int it, const float*& Bb, float*& Cb, float*& Db, int& p) {
     const int b = it / ntile, t = it - b * ntile;
     const int b1 = b / ca.nb2, b2 = b - b1 * ca.nb2;
     Bb = g.B + b1 * g.b_b1 + b2 * g.b_b2;
     Cb = g.C + b1 * g.c_b1 + b2 * g.c_b2;
     Db = g.d_out ? g.d_out + b1 * g.c_b1 + b2 * g.c_b2 : nullptr;
-    p = t * 16 + lr;
+    p = t * 16 * NT + lr;
   };
-  auto load = [&](int it, float (&v)[KS]) {
+  auto load = [&](int it, float (&v)[NT][KS]) {
     const float* Bb;
     float* Cb;
     float* Db;
@@ -365,44 +372,53 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
     panel(it, Bb, Cb, Db, p);
     const auto rb = cs_rsrc(Bb, ca.b_bytes);
 #pragma unroll
-    for (int sk = 0; sk < KS; ++sk) {
-      const int k = 4 * sk + lk;
-      v[sk] = cs_ld(rb, k < K && p < N ? (uint32_t)(k * bk + p) * 4u : kCsOOB);
-    }
+    for (int sk = 0; sk < KS; ++sk)
+#pragma unroll
+      for (int q = 0; q < NT; ++q) {
+        const int k = 4 * sk + lk, pq = p + 16 * q;
+        v[q][sk] = cs_ld(rb, k < K && pq < N ? (uint32_t)(k * bk + pq) * 4u : kCsOOB);
+      }
   };
   int it = blockIdx.x * 4 + wave;
-  float bf[KS];
-  if (it < items) load(it, bf);
+  float bf[NT][KS];
+  if (PF && it < items) load(it, bf);
   for (; it < items; it += nw) {
-    float bn[KS];
-    const int nx = it + nw;
-    load(nx < items ? nx : it, bn);  // the next item's fragments (the last reloads its own)
+    float bn[NT][KS];
+    if constexpr (PF) {
+      const int nx = it + nw;
+      load(nx < items ? nx : it, bn);  // the next item's fragments (the last reloads its own)
+    } else {
+      load(it, bf);
+    }
     const float* Bb;
     float* Cb;
     float* Db;
     int p;
     panel(it, Bb, Cb, Db, p);
     const auto rc = cs_rsrc(Cb, ca.c_bytes);
-    const bool pin = p < N;
     // beta: this item's C values, loaded before the MFMAs so they arrive under them
-    float cv[MF][4];
+    float cv[NT][MF][4];
     if (g.beta != 0.f) {
 #pragma unroll
-      for (int x = 0; x < MF; ++x)
+      for (int q = 0; q < NT; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = x * 16 + lk * 4 + r;
-          cv[x][r] = cs_ld(rc, pin && m < M ? (uint32_t)(m * cm + p) * 4u : kCsOOB);
-        }
+        for (int x = 0; x < MF; ++x)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = x * 16 + lk * 4 + r, pq = p + 16 * q;
+            cv[q][x][r] = cs_ld(rc, pq < N && m < M ? (uint32_t)(m * cm + pq) * 4u : kCsOOB);
+          }
     }
-    f32x4 acc[MF];
+    f32x4 acc[NT][MF];
 #pragma unroll
-    for (int x = 0; x < MF; ++x) acc[x] = zero4();
+    for (int q = 0; q < NT; ++q)
+#pragma unroll
+      for (int x = 0; x < MF; ++x) acc[q][x] = zero4();
     const int lz = lane + cs_opaque_zero();
 #if defined(DSTD_CS_ABL) && (DSTD_CS_ABL & 1)  // (ablation builds: no MFMAs)
 #pragma unroll
-    for (int sk = 0; sk < KS; ++sk) acc[sk % MF][sk & 3] += bf[sk];
-    if (lz < 0) 
+    for (int sk = 0; sk < KS; ++sk) acc[0][sk % MF][sk & 3] += bf[0][sk];
+    if (lz < 0)
 #endif
 #pragma unroll
     for (int s4 = 0; s4 < KS4; ++s4) {
@@ -413,42 +429,54 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
       for (int j = 0; j < 4; ++j) {
         if (4 * s4 + j >= KS) break;
 #pragma unroll
-        for (int x = 0; x < MF; ++x)
-          acc[x] = mfma16x16x4(j == 0 ? a[x].x : j == 1 ? a[x].y : j == 2 ? a[x].z : a[x].w, bf[4 * s4 + j], acc[x]);
+        for (int q = 0; q < NT; ++q)
+#pragma unroll
+          for (int x = 0; x < MF; ++x)
+            acc[q][x] = mfma16x16x4(j == 0 ? a[x].x : j == 1 ? a[x].y : j == 2 ? a[x].z : a[x].w, bf[q][4 * s4 + j],
+                                    acc[q][x]);
       }
     }
-    if (Db) {  // C and D = d_alpha * C + (d_A (* d_W) (+ d_R)) of this column (k_gemm's order)
-      const auto rd = cs_rsrc(Db, ca.c_bytes);
-      const float ad = *g.d_alpha;
-      const int pc = pin ? p : 0;
-      float ac = g.d_A[pc];
-      if (g.d_W) ac *= g.d_W[pc];
-      if (g.d_R) ac += g.d_R[pc];
 #pragma unroll
-      for (int x = 0; x < MF; ++x)
+    for (int q = 0; q < NT; ++q) {
+      const int pq = p + 16 * q;
+      const bool pin = pq < N;
+      if (Db) {  // C and D = d_alpha * C + (d_A (* d_W) (+ d_R)) of this column (k_gemm's order)
+        const auto rd = cs_rsrc(Db, ca.c_bytes);
+        const float ad = *g.d_alpha;
+        const int pc = pin ? pq : 0;
+        float ac = g.d_A[pc];
+        if (g.d_W) ac *= g.d_W[pc];
+        if (g.d_R) ac += g.d_R[pc];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = x * 16 + lk * 4 + r;
-          const uint32_t off = pin && m < M ? (uint32_t)(m * cm + p) * 4u : kCsOOB;
-          float v = g.alpha * acc[x][r];
-          if (g.bias_m) v += g.bias_m[m < M ? m : 0];
-          cs_st(rd, off, fmaf(ad, v, ac));
-          if (g.beta != 0.f) v += g.beta * cv[x][r];
-          cs_st(rc, off, v);
-        }
-    } else {
+        for (int x = 0; x < MF; ++x)
 #pragma unroll
-      for (int x = 0; x < MF; ++x)
+          for (int r = 0; r < 4; ++r) {
+            const int m = x * 16 + lk * 4 + r;
+            const uint32_t off = pin && m < M ? (uint32_t)(m * cm + pq) * 4u : kCsOOB;
+            float v = g.alpha * acc[q][x][r];
+            if (g.bias_m) v += g.bias_m[m < M ? m : 0];
+            cs_st(rd, off, fmaf(ad, v, ac));
+            if (g.beta != 0.f) v += g.beta * cv[q][x][r];
+            cs_st(rc, off, v);
+          }
+      } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = x * 16 + lk * 4 + r;
-          float v = fmaf(g.alpha, acc[x][r], g.bias_m ? g.bias_m[m < M ? m : 0] : 0.f);
-          if (g.beta != 0.f) v = fmaf(g.beta, cv[x][r], v);
-          cs_st(rc, pin && m < M ? (uint32_t)(m * cm + p) * 4u : kCsOOB, v);
-        }
+        for (int x = 0; x < MF; ++x)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = x * 16 + lk * 4 + r;
+            float v = fmaf(g.alpha, acc[q][x][r], g.bias_m ? g.bias_m[m < M ? m : 0] : 0.f);
+            if (g.beta != 0.f) v = fmaf(g.beta, cv[q][x][r], v);
+            cs_st(rc, pin && m < M ? (uint32_t)(m * cm + pq) * 4u : kCsOOB, v);
+          }
+      }
     }
+    if constexpr (PF) {
 #pragma unroll
-    for (int sk = 0; sk < KS; ++sk) bf[sk] = bn[sk];
+      for (int q = 0; q < NT; ++q)
+#pragma unroll
+        for (int sk = 0; sk < KS; ++sk) bf[q][sk] = bn[q][sk];
+    }
   }
 }
 
@@ -2018,7 +2046,7 @@ hipError_t gemm_stream(const Gemm& g, hipStream_t s) {
       g.K > kCsMax || g.K < 1 || g.N < 16)
     return hipErrorNotSupported;
   const long long nbat = (long long)g.nb1 * g.nb2;
-  const int ntile = cdiv(g.N, 16);
+  const int ntile = cdiv(g.N, 16 * DSTD_CS_NT);  // items per batch
   // 32-bit buffer offsets over one batch's panels
   if (nbat * ntile >= (1LL << 31) || g.b_k < g.N || g.c_m < g.N || ((long long)(g.K - 1) * g.b_k + g.N) * 4 >= (1LL << 31) ||
       ((long long)(g.M - 1) * g.c_m + g.N) * 4 >= (1LL << 31))

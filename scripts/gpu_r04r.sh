@@ -2,12 +2,12 @@
 # round 4 (r04r): streaming 1x1-conv GEMM diagnostics -- microbenchmark of the
 # default build against the panel / tile kernels (nostream), fewer resident
 # workgroups (csg2 / csg4: more items per wave), no MFMAs (csnomfma), no
-# stores (csnost); then the training suites with HEAD (shared-A routing fix)
+# stores (csnost), 32 / 64-column items (nt2, nt2n, nt4n: n = no prefetch); then the training suites with HEAD (shared-A routing fix)
 cd "$(dirname "$0")/.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04r
 mkdir -p $O
-for v in nostream "" csg2 csg4 csnomfma csnost; do
+for v in nostream "" csg2 csg4 csnomfma csnost nt2 nt2n nt4n; do
   b=scripts/micro/skinny_micro${v:+_$v}
   timeout -k 10 60 $b > $O/micro_${v:-stream}.txt 2>&1; st=$?
   echo "== ${v:-stream} (exit $st)"; cat $O/micro_${v:-stream}.txt | grep -v FAIL | tail -1
