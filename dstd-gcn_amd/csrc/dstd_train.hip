@@ -1659,24 +1659,28 @@ __global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, 
   }
   __syncthreads();
   const float w = a.prelu ? *a.prelu : 0.f;
-  constexpr int EB = 4;  // elements per thread per batch, loads issued first
-  for (int k = 0; k < ns; ++k)
-  for (int e0 = tid; e0 < T * V; e0 += EB * 256) {
-    const size_t base = ((size_t)(n + k) * C + c) * T * V;
+#ifndef DSTD_BN_APPLY_EB
+#define DSTD_BN_APPLY_EB 4
+#endif
+  constexpr int EB = DSTD_BN_APPLY_EB;  // elements per thread per batch, loads issued first
+  // (batches run over the ns samples' planes as one range of ns * T * V elements)
+  const int TV = T * V;
+  const size_t base = ((size_t)n * C + c) * TV;
+  for (int e0 = tid; e0 < ns * TV; e0 += EB * 256) {
     float u[EB], r[EB];
 #pragma unroll
     for (int j = 0; j < EB; ++j) {
-      const int e = e0 + j * 256;
-      const size_t i = base + e;
-      u[j] = e < T * V ? (a.x2 ? a.x[i] + a.x2[i] : a.x[i]) : 0.f;
-      r[j] = (e < T * V && a.res) ? a.res[i] : 0.f;
+      const int e = e0 + j * 256, k = e / TV;
+      const size_t i = base + (size_t)k * C * TV + (e - k * TV);
+      u[j] = e < ns * TV ? (a.x2 ? a.x[i] + a.x2[i] : a.x[i]) : 0.f;
+      r[j] = (e < ns * TV && a.res) ? a.res[i] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < EB; ++j) {
-      const int e = e0 + j * 256;
-      if (e >= T * V) break;
-      const size_t i = base + e;
-      const int v = e % V;
+      const int e = e0 + j * 256, k = e / TV;
+      if (e >= ns * TV) break;
+      const size_t i = base + (size_t)k * C * TV + (e - k * TV);
+      const int v = (e - k * TV) % V;
       float z = fmaf(u[j], scl[v], shl[v]);
       if (a.res) z += r[j];
       if (a.prelu) {
@@ -2401,6 +2405,9 @@ hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStre
 // samples per apply workgroup: more than one only while >= 4096 workgroups
 // remain (measured: 4 per workgroup -2.7% at B=256, +1% at B=32 paired)
 int bn_apply_samples(int Bg, int B, int C) {
+#ifdef DSTD_BN_NS  // (experiments: samples per apply workgroup)
+  if (Bg % DSTD_BN_NS == 0) return DSTD_BN_NS;
+#endif
   for (int ns : {4, 2})
     if (Bg % ns == 0 && (size_t)C * (B / ns) >= 4096) return ns;
   return 1;
