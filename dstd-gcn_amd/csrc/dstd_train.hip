@@ -1562,7 +1562,8 @@ __device__ __forceinline__ void bn_local_merge(int cv, int ch, int rows, int spl
 
 // part: channel c's split partials [group][split][V][2] (staged in LDS by
 // k_bn_apply_merged), v: the joint of ch = c * V + v
-__device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int v, int V, int rows, int splits,
+// (pcv, pch): the partials' channel count and this channel's index in them
+__device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int pch, int pcv, int rows, int splits,
                                                const float* part, int g, float& mean, float& rstd, bool store) {
   if (a.use_running) {
     mean = a.running_mean[ch];
@@ -1587,7 +1588,7 @@ __device__ __forceinline__ void bn_merge_stats(const BnFwd& a, int ch, int v, in
         m2 += q[w * rs + 1] + q[w * rs + 2] * d * d;
       }
     } else {
-      bn_local_merge(V, v, rows, splits, part, g, m, m2);
+      bn_local_merge(pcv, pch, rows, splits, part, g, m, m2);
     }
     const float var = m2 / n;
     mean = m;
@@ -1616,6 +1617,54 @@ __global__ __launch_bounds__(256) void k_bn_local_stats(int cv, int rows, int sp
   d[1] = m2;
   d[2] = (float)rows;
 }
+
+// DSTD_BN_SEP: the merge as a launch of its own (one thread per channel (c,
+// v): every group's mean / rstd, the running statistics in group order, the
+// apply's scale / shift in ss[group][C*V][2]), then a flat element-wise apply
+#ifdef DSTD_BN_SEP
+__global__ __launch_bounds__(256) void k_bn_merge(BnFwd a, int rows, int splits, const float* part, float* ss, int C,
+                                                  int V) {
+  const int ch = blockIdx.x * 256 + threadIdx.x;
+  if (ch >= a.cv) return;
+  for (int g = 0; g < a.groups; ++g) {
+    float mean, rstd;
+    bn_merge_stats(a, ch, ch, a.cv, rows, splits, part, g, mean, rstd, true);
+    const float sc = rstd * a.gamma[ch];
+    ss[((size_t)g * a.cv + ch) * 2] = sc;
+    ss[((size_t)g * a.cv + ch) * 2 + 1] = a.beta[ch] - mean * sc;
+  }
+}
+__global__ __launch_bounds__(256) void k_bn_apply_flat(BnFwd a, int Bg, int C, int TV, int V, long long total,
+                                                       const float* ss) {
+  const float w = a.prelu ? *a.prelu : 0.f;
+  const long long stride = (long long)gridDim.x * 256 * 4;
+  for (long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i0 < total; i0 += stride) {
+    // TV % 4 == 0: the 4 elements share (n, c)
+    const long long nc = i0 / TV;
+    const int e0 = (int)(i0 - nc * TV), n = (int)(nc / C), c = (int)(nc - (long long)n * C), g = n / Bg;
+    float4 u = *reinterpret_cast<const float4*>(a.x + i0);
+    if (a.x2) {
+      const float4 u2 = *reinterpret_cast<const float4*>(a.x2 + i0);
+      u.x += u2.x, u.y += u2.y, u.z += u2.z, u.w += u2.w;
+    }
+    const float4 r = a.res ? *reinterpret_cast<const float4*>(a.res + i0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float uu[4] = {u.x, u.y, u.z, u.w}, rr[4] = {r.x, r.y, r.z, r.w};
+    float zz[4], oo[4];
+    int v = e0 % V;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float* q = ss + ((size_t)g * a.cv + c * V + v) * 2;
+      float z = fmaf(uu[j], q[0], q[1]);
+      if (a.res) z += rr[j];
+      zz[j] = z;
+      oo[j] = a.prelu ? prelu_f(z, w) : z;
+      v = v + 1 == V ? 0 : v + 1;
+    }
+    if (a.prelu) *reinterpret_cast<float4*>(a.zsave + i0) = make_float4(zz[0], zz[1], zz[2], zz[3]);
+    *reinterpret_cast<float4*>(a.out + i0) = make_float4(oo[0], oo[1], oo[2], oo[3]);
+  }
+}
+#endif
 
 // workgroup (c, y) covers samples [ns*y, ns*y + ns) (one group: ns divides B/groups)
 __global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, int T, int V, int splits,
@@ -2415,8 +2464,8 @@ int bn_apply_samples(int Bg, int B, int C) {
 
 int bn_splits(int B, int T) { return std::max(1, std::min(kBnMaxSplits, cdiv(B * T, 64))); }
 
-size_t bn_scratch_floats(int B, int C, int T, int V) {  // sized for up to 2 groups
-  return 2 * ((size_t)bn_splits(B, T) * C * V * 2 + (size_t)bn_splits(B, T) * C) + (size_t)2 * C * V;
+size_t bn_scratch_floats(int B, int C, int T, int V) {  // sized for up to 2 groups (+ DSTD_BN_SEP's scale / shift)
+  return 2 * ((size_t)bn_splits(B, T) * C * V * 2 + (size_t)bn_splits(B, T) * C) + (size_t)2 * C * V + (size_t)4 * C * V;
 }
 
 hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scratch, hipStream_t s) {
@@ -2439,6 +2488,20 @@ hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scrat
     b.gath = y.buf;
     b.world = y.world;
   }
+#ifdef DSTD_BN_SEP
+  const long long total = (long long)B * C * T * V;
+  const bool al = ((uintptr_t)a.x | (uintptr_t)a.x2 | (uintptr_t)a.res | (uintptr_t)a.out | (uintptr_t)a.zsave) % 16 == 0;
+  if ((T * V) % 4 == 0 && al) {
+    float* ss = scratch + (size_t)a.groups * splits * b.cv * 2;
+    k_bn_merge<<<cdiv(b.cv, 256), 256, 0, s>>>(b, (B / a.groups) * T, splits, scratch, ss, C, V);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const long long q = total / 4;
+    const int grid = (int)std::min<long long>(cdiv(q, 256), 8192);
+    k_bn_apply_flat<<<grid, 256, 0, s>>>(b, B / a.groups, C, T * V, V, total, ss);
+    return hipGetLastError();
+  }
+#endif
   const int ns = bn_apply_samples(B / a.groups, B, C);
   k_bn_apply_merged<<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, scratch, ns);
   return hipGetLastError();

@@ -16,11 +16,15 @@ done
 timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_train.py tests/test_gpu_fast.py > $O/pytest_train.log 2>&1
 st=$?; tail -2 $O/pytest_train.log; [ $st -eq 0 ] || exit $st
 # training step A/B at B=32: panel / tile GEMMs (nostream) vs HEAD (streaming
-# GEMM), and HEAD with 4 samples per BN-apply workgroup (bnns4, bnns4eb8)
+# GEMM), and HEAD with 4 samples per BN-apply workgroup (bnns4, bnns4eb8) or
+# the BN merge as its own launch + a flat float4 apply (bnsep)
 export DSTD_AB_FOREIGN_LIB=1
 for r in 1 2; do
-  for lib in libdstd_gcn_nostream libdstd_gcn libdstd_gcn_bnns4 libdstd_gcn_bnns4eb8; do
+  for lib in libdstd_gcn_nostream libdstd_gcn libdstd_gcn_bnns4 libdstd_gcn_bnns4eb8 libdstd_gcn_bnsep; do
     DSTD_LIB="$R/dstd-gcn_amd/$lib.so" timeout -k 10 200 python -u scripts/bench_train.py --batch 32 > $O/train_$lib.$r.log 2>&1
     st=$?; echo "$lib round $r exit $st $(grep metric $O/train_$lib.$r.log | cut -c1-110)"; [ $st -eq 0 ] || exit $st
   done
 done
+# the bnsep variant against the block / model-step parity tests
+DSTD_LIB="$R/dstd-gcn_amd/libdstd_gcn_bnsep.so" timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_train.py -k "dstdgcb or model_step or forward_pair" > $O/pytest_bnsep.log 2>&1
+st=$?; echo "bnsep parity: $(tail -1 $O/pytest_bnsep.log)"; [ $st -eq 0 ] || exit $st
