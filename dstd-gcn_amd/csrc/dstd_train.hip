@@ -1808,6 +1808,78 @@ __global__ __launch_bounds__(256) void k_bn_bwd_local_sums(int cv, int groups, i
   dst[((size_t)g * cv + ch) * 2 + 1] = sdx;
 }
 
+#ifdef DSTD_BN_SEP
+// DSTD_BN_SEP backward: the merge as a launch of its own (one thread per
+// channel: the group sums in split order into sx[group][C*V][2] -- SyncBN's
+// all-reduced ones for the input gradient -- dgamma / dbeta, and workgroup 0
+// the PReLU slope), then a flat float4 apply.  Same arithmetic as
+// k_bn_bwd_apply_merged.
+__global__ __launch_bounds__(256) void k_bn_bwd_merge(BnBwd a, int splits, int C, const float* part,
+                                                      const float* wpart, float* dprelu, float* sx, int CV) {
+  __shared__ float red[kRedThreads / 64];
+  if (a.prelu && blockIdx.x == 0) {  // uniform per workgroup
+    float t = 0.f;
+    for (int e = threadIdx.x; e < splits * a.groups * C; e += blockDim.x) t += wpart[e];
+    t = block_sum(t, red);
+    if (threadIdx.x == 0) dprelu[0] += t;
+  }
+  const int ch = blockIdx.x * 256 + threadIdx.x;
+  if (ch >= CV) return;
+  float tb = 0.f, tg = 0.f;
+  for (int gg = 0; gg < a.groups; ++gg) {
+    float sd = 0.f, sdx = 0.f;
+    for (int sp = 0; sp < splits; ++sp) {
+      const float2 pv = *reinterpret_cast<const float2*>(part + ((size_t)(gg * splits + sp) * CV + ch) * 2);
+      sd += pv.x;
+      sdx += pv.y;
+    }
+    sx[((size_t)gg * CV + ch) * 2] = a.gsum ? a.gsum[((size_t)gg * CV + ch) * 2] : sd;
+    sx[((size_t)gg * CV + ch) * 2 + 1] = a.gsum ? a.gsum[((size_t)gg * CV + ch) * 2 + 1] : sdx;
+    tb += sd;
+    tg += sdx;
+  }
+  a.dbeta[ch] += tb;
+  a.dgamma[ch] += tg;
+}
+__global__ __launch_bounds__(256) void k_bn_bwd_apply_flat(BnBwd a, int Bg, int C, int TV, int V, int T,
+                                                           long long total, const float* sx) {
+  const float w = a.prelu ? *a.prelu : 0.f;
+  const int CV = C * V;
+  const long long stride = (long long)gridDim.x * 256 * 4;
+  for (long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i0 < total; i0 += stride) {
+    const long long nc = i0 / TV;
+    const int e0 = (int)(i0 - nc * TV), n = (int)(nc / C), c = (int)(nc - (long long)n * C), g = n / Bg;
+    const float inv = 1.f / (a.gsum ? a.gsum[(size_t)a.groups * CV * 2 + g] : (float)(Bg * T));
+    const float4 d4 = *reinterpret_cast<const float4*>(a.dout + i0);
+    const float4 z4 = a.prelu ? *reinterpret_cast<const float4*>(a.zsave + i0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 u4 = *reinterpret_cast<const float4*>(a.x + i0);
+    if (a.x2) {
+      const float4 u2 = *reinterpret_cast<const float4*>(a.x2 + i0);
+      u4.x += u2.x, u4.y += u2.y, u4.z += u2.z, u4.w += u2.w;
+    }
+    const float4 ad4 = a.dz_add ? *reinterpret_cast<const float4*>(a.dz_add + i0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float dv[4] = {d4.x, d4.y, d4.z, d4.w}, zv[4] = {z4.x, z4.y, z4.z, z4.w}, uv[4] = {u4.x, u4.y, u4.z, u4.w};
+    const float av[4] = {ad4.x, ad4.y, ad4.z, ad4.w};
+    float du[4], dzo[4];
+    int v = e0 % V;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ch = c * V + v;
+      const float d = dv[j];
+      const float dz = (a.prelu && !(zv[j] > 0.f)) ? w * d : d;
+      const float mean = a.mean[g * CV + ch], rstd = a.rstd[g * CV + ch], gm = a.gamma[ch];
+      const float xh = (uv[j] - mean) * rstd;
+      const float sdl = sx[((size_t)g * CV + ch) * 2], sxl = sx[((size_t)g * CV + ch) * 2 + 1];
+      du[j] = a.use_running ? gm * rstd * dz : gm * rstd * (dz - sdl * inv - xh * sxl * inv);
+      dzo[j] = a.dz_add ? dz + av[j] : dz;
+      v = v + 1 == V ? 0 : v + 1;
+    }
+    *reinterpret_cast<float4*>(a.du + i0) = make_float4(du[0], du[1], du[2], du[3]);
+    if (a.dz_out) *reinterpret_cast<float4*>(a.dz_out + i0) = make_float4(dzo[0], dzo[1], dzo[2], dzo[3]);
+  }
+}
+#endif
+
 // Merge + apply of the backward in one launch: workgroup (c, n) sums the
 // split partials of its V channels (split order), the n == 0 one accumulates
 // dgamma / dbeta (and workgroup (0, 0) the PReLU slope: the partials in the
@@ -2526,6 +2598,23 @@ hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scrat
       return collective_failed();
     b.gsum = y.buf;
   }
+#ifdef DSTD_BN_SEP
+  {
+    const long long total = (long long)B * C * T * V;
+    const bool al = ((uintptr_t)a.x | (uintptr_t)a.x2 | (uintptr_t)a.zsave | (uintptr_t)a.dout | (uintptr_t)a.du |
+                     (uintptr_t)a.dz_out | (uintptr_t)a.dz_add) % 16 == 0;
+    if ((T * V) % 4 == 0 && al) {
+      const int cv = C * V;
+      float* sx = wpart + (size_t)splits * a.groups * C;
+      k_bn_bwd_merge<<<cdiv(cv, 256), 256, 0, s>>>(b, splits, C, part, wpart, dprelu, sx, cv);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      const int grid = (int)std::min<long long>(cdiv(total / 4, 256), 8192);
+      k_bn_bwd_apply_flat<<<grid, 256, 0, s>>>(b, B / a.groups, C, T * V, V, T, total, sx);
+      return hipGetLastError();
+    }
+  }
+#endif
   const int ns = bn_apply_samples(B / a.groups, B, C);
   k_bn_bwd_apply_merged<<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, part, wpart, dprelu, ns);
   return hipGetLastError();

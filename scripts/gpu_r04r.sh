@@ -17,7 +17,8 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 st=$?; tail -2 $O/pytest_train.log; [ $st -eq 0 ] || exit $st
 # training step A/B at B=32: panel / tile GEMMs (nostream) vs HEAD (streaming
 # GEMM), and HEAD with 4 samples per BN-apply workgroup (bnns4, bnns4eb8) or
-# the BN merge as its own launch + a flat float4 apply (bnsep)
+# the BN merges as launches of their own + flat float4 applies, both
+# directions (bnsep)
 export DSTD_AB_FOREIGN_LIB=1
 for r in 1 2; do
   for lib in libdstd_gcn_nostream libdstd_gcn libdstd_gcn_bnns4 libdstd_gcn_bnns4eb8 libdstd_gcn_bnsep; do
