@@ -340,8 +340,10 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
   // As[((x KS4 + s4) 64 + lane) 4 + j] = A[16x + lr][4 (4 s4 + j) + lk]
   constexpr int KS4 = (KS + 3) / 4;
   __shared__ float4 As[MF * KS4 * 64];
+  __shared__ float bsl[MF * 16];  // bias_m (0 past M or without one)
   const int tid = threadIdx.x, lane = tid & 63, lr = lane & 15, lk = lane >> 4;
   float* Af = reinterpret_cast<float*>(As);
+  if (tid < MF * 16) bsl[tid] = g.bias_m && tid < g.M ? g.bias_m[tid] : 0.f;
   for (int e = tid; e < MF * KS4 * 256; e += 256) {
     const int j = e & 3, l = (e >> 2) & 63, f = e >> 8, x = f / KS4, s4 = f - x * KS4;
     const int m = x * 16 + (l & 15), k = 4 * (4 * s4 + j) + (l >> 4);
@@ -454,7 +456,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
             const int m = x * 16 + lk * 4 + r;
             const uint32_t off = pin && m < M ? (uint32_t)(m * cm + pq) * 4u : kCsOOB;
             float v = g.alpha * acc[q][x][r];
-            if (g.bias_m) v += g.bias_m[m < M ? m : 0];
+            if (g.bias_m) v += bsl[m];
             cs_st(rd, off, fmaf(ad, v, ac));
             if (g.beta != 0.f) v += g.beta * cv[q][x][r];
             cs_st(rc, off, v);
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int m = x * 16 + lk * 4 + r;
-            float v = fmaf(g.alpha, acc[q][x][r], g.bias_m ? g.bias_m[m < M ? m : 0] : 0.f);
+            float v = fmaf(g.alpha, acc[q][x][r], bsl[m]);
             if (g.beta != 0.f) v = fmaf(g.beta, cv[q][x][r], v);
             cs_st(rc, pin && m < M ? (uint32_t)(m * cm + pq) * 4u : kCsOOB, v);
           }
