@@ -12,19 +12,20 @@ def main(path, steps, top=25, marker=None, last=0):
     of the train forward): steady state, without the first steps' set-up
     (model init, workspaces, lazy optimizer state)."""
     rows = list(csv.DictReader(open(path)))
-    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r.get("Queue_Id", "0"))
+                for r in rows)
     if marker and last:
-        starts = [i for i, (_, _, k) in enumerate(iv) if marker in k]
+        starts = [i for i, (_, _, k, _) in enumerate(iv) if marker in k]
         if len(starts) > last:
             iv = iv[starts[-last - 1]:starts[-1]]
             steps = last
     tot = collections.defaultdict(lambda: [0, 0])
-    for s, e, k in iv:
+    for s, e, k, _ in iv:
         t = tot[k.replace("(anonymous namespace)::", "").split("(")[0][-70:]]
         t[0] += e - s
         t[1] += 1
     busy, cur_s, cur_e = 0, None, None
-    for s, e, _ in iv:
+    for s, e, _, _ in iv:
         if cur_e is None or s > cur_e:
             if cur_e is not None:
                 busy += cur_e - cur_s
@@ -38,6 +39,14 @@ def main(path, steps, top=25, marker=None, last=0):
           f"busy/step {busy / steps / 1e3:.1f} us  span/step {span / steps / 1e3:.1f} us")
     for k, (t, c) in sorted(tot.items(), key=lambda kv: -kv[1][0])[:top]:
         print(f"{t / steps / 1e3:9.1f} us/step {c / steps:6.1f}/step {t / c / 1e3:8.2f} us  {k}")
+    # per hardware queue (the training backward's weight-gradient stream runs on its own)
+    byq = collections.defaultdict(lambda: [0, 0])
+    for s, e, _, q in iv:
+        byq[q][0] += e - s
+        byq[q][1] += 1
+    if len(byq) > 1:
+        for q, (t, c) in sorted(byq.items(), key=lambda kv: -kv[1][1]):
+            print(f"queue {q}: {c / steps:.0f} launches/step, kernel-sum {t / steps / 1e3:.1f} us/step")
 
 
 if __name__ == "__main__":
