@@ -1222,26 +1222,30 @@ __global__ void k_tanh_outer_bwd(const float* __restrict__ M, const float* __res
 
 // Fused adjacency backward, stage 1: workgroup (row a, sample chunk); each
 // thread owns entries ij and walks the chunk's samples (no atomics).
+// stage 1: workgroup (a, sample chunk, 256-column block): one (i, j) per
+// thread, the chunk's samples 8 at a time with every load in flight
 __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, const float* __restrict__ E,
                                                       const float* __restrict__ alpha, int B, int A, int NN2, int nch,
                                                       float* __restrict__ pdA, float* __restrict__ pbr,
                                                       float* __restrict__ pal, const float* __restrict__ dDp,
                                                       int np) {
   __shared__ float red[4];
-  const int a = blockIdx.x, ch = blockIdx.y;
+  constexpr int SG = 8;
+  const int a = blockIdx.x, ch = blockIdx.y, nij = gridDim.z;
   const int per = (B + nch - 1) / nch, n0 = ch * per, n1 = min(B, n0 + per);
   const float al = *alpha;
   // dD, or the sum of its np <= 4 channel-chunk partials in chunk order
   const float* src = np > 1 ? dDp : dD;
   const int nq = np > 1 ? np : 1;
   const size_t qs = np > 1 ? (size_t)B * A * NN2 : 0;
+  const int ij = blockIdx.z * 256 + threadIdx.x;
   float sbr = 0.f, sal = 0.f;
-  for (int ij = threadIdx.x; ij < NN2; ij += blockDim.x) {
+  if (ij < NN2) {
     float sa = 0.f;
-    for (int nb = n0; nb < n1; nb += 4) {  // 4 samples' loads in flight, then use in order
-      float dv[4], ev[4];
+    for (int nb = n0; nb < n1; nb += SG) {  // SG samples' loads in flight, then use in order
+      float dv[SG], ev[SG];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {  // (clamped sample: loads without branches)
+      for (int u = 0; u < SG; ++u) {  // (clamped sample: loads without branches)
         const size_t i = ((size_t)min(nb + u, n1 - 1) * A + a) * NN2 + ij;
         if (nq > 1) {
           float pv[4];
@@ -1257,7 +1261,7 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
         ev[u] = E[i];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < SG; ++u) {
         if (nb + u >= n1) break;
         sa += dv[u];
         sal = fmaf(dv[u], ev[u], sal);
@@ -1265,13 +1269,13 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
       }
     }
     pdA[((size_t)ch * A + a) * NN2 + ij] = sa;
-    sbr += sa;
+    sbr = sa;
   }
   sbr = block_sum(sbr, red);
   sal = block_sum(sal, red);
   if (threadIdx.x == 0) {
-    pbr[ch * A + a] = al * sbr;
-    pal[ch * A + a] = sal;
+    pbr[((size_t)ch * A + a) * nij + blockIdx.z] = al * sbr;
+    pal[((size_t)ch * A + a) * nij + blockIdx.z] = sal;
   }
 }
 
@@ -1283,7 +1287,7 @@ __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict_
                                                         const float* __restrict__ pal, int A, int NN2, int nch,
                                                         float* __restrict__ dA, float* __restrict__ dbrm,
                                                         float* __restrict__ dalpha, int assign_dA, float* __restrict__ dW2,
-                                                        const float* __restrict__ Amul) {
+                                                        const float* __restrict__ Amul, int nij) {
   __shared__ float lds[16][17];
   __shared__ float red[4];
   const int nblk = (NN2 + 15) / 16;
@@ -1306,11 +1310,12 @@ __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict_
   }
   for (int a = threadIdx.x; a < A; a += blockDim.x) {
     float t = 0.f;
-    for (int c = 0; c < nch; ++c) t += pbr[c * A + a];
+    for (int c = 0; c < nch; ++c)
+      for (int z = 0; z < nij; ++z) t += pbr[((size_t)c * A + a) * nij + z];
     dbrm[a] += t;
   }
   float t = 0.f;
-  for (int i = threadIdx.x; i < A * nch; i += blockDim.x) t += pal[i];
+  for (int i = threadIdx.x; i < A * nch * nij; i += blockDim.x) t += pal[i];
   t = block_sum(t, red);
   if (threadIdx.x == 0) dalpha[0] += t;
 }
@@ -2449,7 +2454,7 @@ int adj_bwd_chunks(int B, int A) { return std::max(1, std::min(std::min(B, 16), 
 
 size_t adj_bwd_scratch_floats(int B, int A, int NN2) {
   const int nch = adj_bwd_chunks(B, A);
-  return (size_t)nch * A * NN2 + 2 * (size_t)nch * A + 64;
+  return (size_t)nch * A * NN2 + 2 * (size_t)nch * A * cdiv(NN2, 256) + 64;
 }
 
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
@@ -2457,13 +2462,13 @@ hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, 
                    float* dW2, const float* Amul) {
   if (dW2 && !Amul) return hipErrorInvalidValue;
   if (nparts > 1 && !dDpart) return hipErrorInvalidValue;
-  const int nch = adj_bwd_chunks(B, A);
+  const int nch = adj_bwd_chunks(B, A), nij = cdiv(NN2, 256);
   float* pdA = scratch;
   float* pbr = pdA + (size_t)nch * A * NN2;
-  float* pal = pbr + (size_t)nch * A;
-  k_adj_bwd_part<<<dim3(A, nch), 256, 0, s>>>(dD, E, alpha, B, A, NN2, nch, pdA, pbr, pal, dDpart, nparts);
+  float* pal = pbr + (size_t)nch * A * nij;
+  k_adj_bwd_part<<<dim3(A, nch, nij), 256, 0, s>>>(dD, E, alpha, B, A, NN2, nch, pdA, pbr, pal, dDpart, nparts);
   k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(pdA, pbr, pal, A, NN2, nch, dA, dbrm, dalpha, assign_dA, dW2,
-                                                      Amul);
+                                                      Amul, nij);
   return hipGetLastError();
 }
 
