@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4 (r04b): the whole GPU suite on the default library, smoke, the bench
 # line, kernel traces at B=256 and B=32, HBM traffic (PMC) of the forward
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04b
 mkdir -p $O

@@ -7,7 +7,7 @@
 # batched tanh-outer kernels, LDS-staged BN merge, weight-gradient stream:
 # the training suite (incl. the bit-identity test of the two streams) and the
 # training-step A/B main / nows (one stream) / r03.  Kernel trace of the bench.
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04d
 mkdir -p $O

@@ -2,7 +2,7 @@
 # round 4 (r04e): SyncBN test against the fp64 oracle; fused-kernel phase-1
 # breakdown (stamps mode 4); VALU / MFMA / LDS counters of the forward, r03
 # and HEAD in separate processes; kernel trace of the B=32 training step.
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04e
 mkdir -p $O

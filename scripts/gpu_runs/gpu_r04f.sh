@@ -4,7 +4,7 @@
 # compiler's packed-f32 v_pk_* pairs, an issue-cost anti-lever beside MFMAs
 # per the MI355X guide); LDS / VALU counters per fused-kernel phase through
 # builds that skip phase 1 (skp1) or phase 2 (skp2).
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04f
 mkdir -p $O

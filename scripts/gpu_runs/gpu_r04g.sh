@@ -3,7 +3,7 @@
 # previous commit (prev): four-chain range maxima (fewer hazard s_nops) and
 # the adjacency kernel's column chunks spread over more workgroups below one
 # (sample, graph) set per CU -- B=256 at H36M / CMU / 3DPW and B=32 at H36M.
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04g
 mkdir -p $O

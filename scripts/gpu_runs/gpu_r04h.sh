@@ -3,7 +3,7 @@
 # tanh's two FMAs as scalar v_fma_f32 instead of one v_pk_fma_f32 pair:
 # packed f32 beside MFMAs is an issue-cost anti-lever per the MI355X guide),
 # B=256 H36M / CMU / 3DPW; B=32 training step with the fused Adam.
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04h
 mkdir -p $O

@@ -2,7 +2,7 @@
 # round 4 (r04l): training suite; B=32 / B=256 training step A/B of HEAD
 # against the previous commit (prev): the strided GEMM's adjacency epilogue
 # (conv_rm -> E and D = alpha E + A_comb) loads the combine once per column
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04l
 mkdir -p $O

@@ -2,7 +2,7 @@
 # round 4 (r04m): forward parity suite; same-box A/B of HEAD against the
 # previous commit (prev): the encoder residual as the aggregation
 # accumulator's initial value at T = 40 (3DPW; its fused kernel's spills gone)
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04m
 mkdir -p $O

@@ -2,7 +2,7 @@
 # round 4 (r04n): same-box A/B of HEAD against ra35 (the encoder residual as
 # the accumulator's initial value at T = 35 too: 48 VALU adds per unit fewer,
 # but 3 VGPRs spilled in the 12-wave H36M fused kernel), H36M and CMU
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04n
 mkdir -p $O

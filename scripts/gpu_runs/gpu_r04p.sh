@@ -5,7 +5,7 @@
 # adjacency-backward finish, all blocks' conv weights packed in two launches,
 # the BN backward writing dz + identity gradient, the residual conv bias
 # gradient folded into its weight-gradient GEMM
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04p
 mkdir -p $O

@@ -3,7 +3,7 @@
 # and host-reference check against the panel / tile kernels (nostream build),
 # the GEMM shape log of one B=32 training step, the training suites, then the
 # B=32 / B=256 training step A/B nostream vs HEAD
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04q
 mkdir -p $O

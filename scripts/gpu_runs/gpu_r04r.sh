@@ -3,7 +3,7 @@
 # default build against the panel / tile kernels (nostream), fewer resident
 # workgroups (csg2 / csg4: more items per wave), no MFMAs (csnomfma), no
 # stores (csnost), 32 / 64-column items (nt2, nt2n, nt4n: n = no prefetch); then the training suites with HEAD (shared-A routing fix)
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04r
 mkdir -p $O

@@ -2,7 +2,7 @@
 # round 4 (r04s): the state at the end of the round -- whole
 # GPU suite, smoke, the bench line, kernel traces at B=256 / B=32 and of the
 # B=32 training step (steady state, last 3 steps)
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04s
 mkdir -p $O

@@ -8,7 +8,7 @@
 #  3. training step A/B, B=32 / 256: prev (HEAD before the adjacency change),
 #     nostream and bnsep (prev + that one switch), HEAD
 #  4. the bnsep variant against the block / model-step parity tests
-cd "$(dirname "$0")/.." || exit 2
+cd "$(dirname "$0")/../.." || exit 2
 R="$PWD"
 O=$R/gpurun_out/r04t
 mkdir -p $O
