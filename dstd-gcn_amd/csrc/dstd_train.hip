@@ -1222,8 +1222,10 @@ __global__ void k_tanh_outer_bwd(const float* __restrict__ M, const float* __res
 
 // Fused adjacency backward, stage 1: workgroup (row a, sample chunk); each
 // thread owns entries ij and walks the chunk's samples (no atomics).
-// stage 1: workgroup (a, sample chunk, 256-column block): one (i, j) per
-// thread, the chunk's samples 8 at a time with every load in flight
+// stage 1: workgroup (a, sample chunk, column block): the chunk's samples 8
+// at a time with every load in flight.  DSTD_ADJ_SPLIT: 256-column blocks,
+// one (i, j) per thread (off by default until measured on the GPU; the
+// default, one block per (a, chunk), is the former kernel's arithmetic)
 __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, const float* __restrict__ E,
                                                       const float* __restrict__ alpha, int B, int A, int NN2, int nch,
                                                       float* __restrict__ pdA, float* __restrict__ pbr,
@@ -1238,9 +1240,8 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
   const float* src = np > 1 ? dDp : dD;
   const int nq = np > 1 ? np : 1;
   const size_t qs = np > 1 ? (size_t)B * A * NN2 : 0;
-  const int ij = blockIdx.z * 256 + threadIdx.x;
   float sbr = 0.f, sal = 0.f;
-  if (ij < NN2) {
+  for (int ij = blockIdx.z * 256 + threadIdx.x; ij < NN2; ij += 256 * nij) {
     float sa = 0.f;
     for (int nb = n0; nb < n1; nb += SG) {  // SG samples' loads in flight, then use in order
       float dv[SG], ev[SG];
@@ -1269,7 +1270,7 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
       }
     }
     pdA[((size_t)ch * A + a) * NN2 + ij] = sa;
-    sbr = sa;
+    sbr += sa;
   }
   sbr = block_sum(sbr, red);
   sal = block_sum(sal, red);
@@ -1719,24 +1720,23 @@ __global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, 
 #define DSTD_BN_APPLY_EB 4
 #endif
   constexpr int EB = DSTD_BN_APPLY_EB;  // elements per thread per batch, loads issued first
-  // (batches run over the ns samples' planes as one range of ns * T * V elements)
-  const int TV = T * V;
-  const size_t base = ((size_t)n * C + c) * TV;
-  for (int e0 = tid; e0 < ns * TV; e0 += EB * 256) {
+  for (int k = 0; k < ns; ++k)
+  for (int e0 = tid; e0 < T * V; e0 += EB * 256) {
+    const size_t base = ((size_t)(n + k) * C + c) * T * V;
     float u[EB], r[EB];
 #pragma unroll
     for (int j = 0; j < EB; ++j) {
-      const int e = e0 + j * 256, k = e / TV;
-      const size_t i = base + (size_t)k * C * TV + (e - k * TV);
-      u[j] = e < ns * TV ? (a.x2 ? a.x[i] + a.x2[i] : a.x[i]) : 0.f;
-      r[j] = (e < ns * TV && a.res) ? a.res[i] : 0.f;
+      const int e = e0 + j * 256;
+      const size_t i = base + e;
+      u[j] = e < T * V ? (a.x2 ? a.x[i] + a.x2[i] : a.x[i]) : 0.f;
+      r[j] = (e < T * V && a.res) ? a.res[i] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < EB; ++j) {
-      const int e = e0 + j * 256, k = e / TV;
-      if (e >= ns * TV) break;
-      const size_t i = base + (size_t)k * C * TV + (e - k * TV);
-      const int v = (e - k * TV) % V;
+      const int e = e0 + j * 256;
+      if (e >= T * V) break;
+      const size_t i = base + e;
+      const int v = e % V;
       float z = fmaf(u[j], scl[v], shl[v]);
       if (a.res) z += r[j];
       if (a.prelu) {
@@ -2129,8 +2129,8 @@ void sk_go(K kern, int grid, size_t lds, hipStream_t s, Args... args) {
   }
   kern<<<grid, 256, lds, s>>>(args...);
 }
-#ifndef DSTD_GEMM_STREAM
-#define DSTD_GEMM_STREAM 1
+#ifndef DSTD_GEMM_STREAM  // (off by default until its A/B and the training suites have run on the GPU)
+#define DSTD_GEMM_STREAM 0
 #endif
 template <int MF, int KS>
 hipError_t cs_go(const Gemm& g, int ntile, hipStream_t s) {
@@ -2462,7 +2462,11 @@ hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, 
                    float* dW2, const float* Amul) {
   if (dW2 && !Amul) return hipErrorInvalidValue;
   if (nparts > 1 && !dDpart) return hipErrorInvalidValue;
+#ifdef DSTD_ADJ_SPLIT
   const int nch = adj_bwd_chunks(B, A), nij = cdiv(NN2, 256);
+#else
+  const int nch = adj_bwd_chunks(B, A), nij = 1;
+#endif
   float* pdA = scratch;
   float* pbr = pdA + (size_t)nch * A * NN2;
   float* pal = pbr + (size_t)nch * A * nij;
