@@ -1223,9 +1223,9 @@ __global__ void k_tanh_outer_bwd(const float* __restrict__ M, const float* __res
 // Fused adjacency backward, stage 1: workgroup (row a, sample chunk); each
 // thread owns entries ij and walks the chunk's samples (no atomics).
 // stage 1: workgroup (a, sample chunk, column block): the chunk's samples 8
-// at a time with every load in flight.  DSTD_ADJ_SPLIT: 256-column blocks,
-// one (i, j) per thread (off by default until measured on the GPU; the
-// default, one block per (a, chunk), is the former kernel's arithmetic)
+// at a time with every load in flight.  DSTD_ADJ_SPLIT (default): 256-column
+// blocks, one (i, j) per thread; 0: one block per (a, chunk), a 3-trip
+// column loop (profiles/r04u_train_switches_ab.txt)
 __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, const float* __restrict__ E,
                                                       const float* __restrict__ alpha, int B, int A, int NN2, int nch,
                                                       float* __restrict__ pdA, float* __restrict__ pbr,
@@ -2129,8 +2129,8 @@ void sk_go(K kern, int grid, size_t lds, hipStream_t s, Args... args) {
   }
   kern<<<grid, 256, lds, s>>>(args...);
 }
-#ifndef DSTD_GEMM_STREAM  // (off by default until its A/B and the training suites have run on the GPU)
-#define DSTD_GEMM_STREAM 0
+#ifndef DSTD_GEMM_STREAM  // (r04u: B=256 step 27.9 -> 25.2 ms, B=32 -0.5%; 0 = the panel / tile kernels)
+#define DSTD_GEMM_STREAM 1
 #endif
 template <int MF, int KS>
 hipError_t cs_go(const Gemm& g, int ntile, hipStream_t s) {
@@ -2462,11 +2462,10 @@ hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, 
                    float* dW2, const float* Amul) {
   if (dW2 && !Amul) return hipErrorInvalidValue;
   if (nparts > 1 && !dDpart) return hipErrorInvalidValue;
-#ifdef DSTD_ADJ_SPLIT
-  const int nch = adj_bwd_chunks(B, A), nij = cdiv(NN2, 256);
-#else
-  const int nch = adj_bwd_chunks(B, A), nij = 1;
+#ifndef DSTD_ADJ_SPLIT  // (r04u: B=256 step 27.9 -> 27.0 ms, B=32 neutral; 0 = one column block)
+#define DSTD_ADJ_SPLIT 1
 #endif
+  const int nch = adj_bwd_chunks(B, A), nij = DSTD_ADJ_SPLIT ? cdiv(NN2, 256) : 1;
   float* pdA = scratch;
   float* pbr = pdA + (size_t)nch * A * NN2;
   float* pal = pbr + (size_t)nch * A * nij;

@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 4 (r04v): streaming GEMM and adjacency column blocks now on by
+# default -- the whole GPU suite on HEAD, then the streaming GEMM's item width
+# (nt2: 32-column items, nt2n: without the next-item prefetch, nt4n: 64-column
+# items without it) in the microbenchmark and the training step, against HEAD
+# and the former defaults (off)
+cd "$(dirname "$0")/../.." || exit 2
+R="$PWD"
+O=$R/gpurun_out/r04v
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ > $O/pytest_gpu.log 2>&1
+st=$?; echo "suite: $(tail -1 $O/pytest_gpu.log)"; [ $st -eq 0 ] || exit $st
+for v in off "" nt2 nt2n nt4n; do
+  b=scripts/micro/skinny_micro${v:+_$v}
+  timeout -k 10 60 $b > $O/micro_${v:-head}.txt 2>&1; st=$?
+  echo "== ${v:-head} (exit $st): $(tail -1 $O/micro_${v:-head}.txt)"; [ $st -eq 0 ] || exit $st
+done
+export DSTD_AB_FOREIGN_LIB=1
+for r in 1 2; do
+  for lib in libdstd_gcn_off libdstd_gcn libdstd_gcn_nt2 libdstd_gcn_nt2n libdstd_gcn_nt4n; do
+    DSTD_LIB="$R/dstd-gcn_amd/$lib.so" timeout -k 10 300 python -u scripts/bench_train.py --batch 32 256 > $O/train_$lib.$r.log 2>&1
+    st=$?; echo "$lib round $r exit $st"; grep metric $O/train_$lib.$r.log | cut -c1-110; [ $st -eq 0 ] || exit $st
+  done
+done
