@@ -22,3 +22,10 @@ for r in 1 2; do
     st=$?; echo "$lib round $r exit $st"; grep metric $O/train_$lib.$r.log | cut -c1-110; [ $st -eq 0 ] || exit $st
   done
 done
+# kernel trace of the B=32 step on HEAD (per-queue busy time: is the main
+# stream waiting on the weight-gradient stream?)
+unset DSTD_AB_FOREIGN_LIB
+export TMPDIR=/tmp
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/tt" -o run -- python3 "$R/scripts/bench_train.py" --batch 32 --steps 6 --warmup 3 > "$O/tt.log" 2>&1)
+st=$?; echo "train trace exit $st"; [ $st -eq 0 ] || exit $st
+python3 scripts/trace_summary.py $O/tt/run_kernel_trace.csv 3 30 --marker k_prep_nctv --last 3 > $O/train_trace_summary.txt; tail -3 $O/train_trace_summary.txt

@@ -46,7 +46,18 @@ def main(path, steps, top=25, marker=None, last=0):
         byq[q][1] += 1
     if len(byq) > 1:
         for q, (t, c) in sorted(byq.items(), key=lambda kv: -kv[1][1]):
-            print(f"queue {q}: {c / steps:.0f} launches/step, kernel-sum {t / steps / 1e3:.1f} us/step")
+            qiv = sorted((s, e) for s, e, _, qq in iv if qq == q)
+            busy_q, cs, ce = 0, None, None
+            for s, e in qiv:
+                if ce is None or s > ce:
+                    if ce is not None:
+                        busy_q += ce - cs
+                    cs, ce = s, e
+                else:
+                    ce = max(ce, e)
+            busy_q += ce - cs
+            print(f"queue {q}: {c / steps:.0f} launches/step, kernel-sum {t / steps / 1e3:.1f} us/step, "
+                  f"busy {busy_q / steps / 1e3:.1f} us/step, idle in span {(span - busy_q) / steps / 1e3:.1f} us/step")
 
 
 if __name__ == "__main__":
