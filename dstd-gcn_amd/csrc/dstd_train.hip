@@ -1310,9 +1310,20 @@ __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict_
     return;
   }
   for (int a = threadIdx.x; a < A; a += blockDim.x) {
+    // (chunk, column block) partials in that order, 8 loads in flight at a time
+    const int n = nch * nij;
     float t = 0.f;
-    for (int c = 0; c < nch; ++c)
-      for (int z = 0; z < nij; ++z) t += pbr[((size_t)c * A + a) * nij + z];
+    for (int i0 = 0; i0 < n; i0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = min(i0 + u, n - 1), c = i / nij, z = i - c * nij;
+        v[u] = pbr[((size_t)c * A + a) * nij + z];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (i0 + u < n) t += v[u];
+    }
     dbrm[a] += t;
   }
   float t = 0.f;
