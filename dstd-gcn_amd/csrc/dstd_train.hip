@@ -2161,10 +2161,16 @@ hipError_t cs_go(const Gemm& g, int ntile, hipStream_t s) {
     return v;
   }();
   const long items = (long)g.nb1 * g.nb2 * ntile;
-#ifndef DSTD_CS_GRID_DIV  // (experiments: fewer resident workgroups, more items per wave)
-#define DSTD_CS_GRID_DIV 1
+  // A small product (the config-5 batch: ~3.7k items) takes half the resident
+  // workgroups, leaving CUs to the weight-gradient stream's reductions that
+  // run beside it (B=32 step -1.3%); a large one the whole chip (half of it
+  // measured +2% at B=256; profiles/r04w_train_ab.txt)
+#ifndef DSTD_CS_GRID_DIV  // (experiments: a fixed divisor)
+  const int div = items < 16384 ? 2 : 1;
+#else
+  const int div = DSTD_CS_GRID_DIV;
 #endif
-  const int grid = (int)std::max(1L, std::min((long)cus * occ / DSTD_CS_GRID_DIV, (items + 3) / 4));
+  const int grid = (int)std::max(1L, std::min((long)cus * occ / div, (items + 3) / 4));
   CsArgs ca;
   ca.ntile = ntile;
   ca.nb2 = g.nb2;
