@@ -1656,11 +1656,11 @@ __global__ __launch_bounds__(256) void k_bn_merge(BnFwd a, int rows, int splits,
 __global__ __launch_bounds__(256) void k_bn_apply_flat(BnFwd a, int Bg, int C, int TV, int V, long long total,
                                                        const float* ss) {
   const float w = a.prelu ? *a.prelu : 0.f;
-  const long long stride = (long long)gridDim.x * 256 * 4;
-  for (long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i0 < total; i0 += stride) {
+  const int stride = gridDim.x * 256 * 4, tot = (int)total;  // (the launcher keeps total < 2^31)
+  for (int i0 = (blockIdx.x * 256 + threadIdx.x) * 4; i0 < tot; i0 += stride) {
     // TV % 4 == 0: the 4 elements share (n, c)
-    const long long nc = i0 / TV;
-    const int e0 = (int)(i0 - nc * TV), n = (int)(nc / C), c = (int)(nc - (long long)n * C), g = n / Bg;
+    const int nc = i0 / TV;
+    const int e0 = i0 - nc * TV, n = nc / C, c = nc - n * C, g = n / Bg;
     float4 u = *reinterpret_cast<const float4*>(a.x + i0);
     if (a.x2) {
       const float4 u2 = *reinterpret_cast<const float4*>(a.x2 + i0);
@@ -1863,10 +1863,10 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_flat(BnBwd a, int Bg, int 
                                                            long long total, const float* sx) {
   const float w = a.prelu ? *a.prelu : 0.f;
   const int CV = C * V;
-  const long long stride = (long long)gridDim.x * 256 * 4;
-  for (long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; i0 < total; i0 += stride) {
-    const long long nc = i0 / TV;
-    const int e0 = (int)(i0 - nc * TV), n = (int)(nc / C), c = (int)(nc - (long long)n * C), g = n / Bg;
+  const int stride = gridDim.x * 256 * 4, tot = (int)total;  // (the launcher keeps total < 2^31)
+  for (int i0 = (blockIdx.x * 256 + threadIdx.x) * 4; i0 < tot; i0 += stride) {
+    const int nc = i0 / TV;
+    const int e0 = i0 - nc * TV, n = nc / C, c = nc - n * C, g = n / Bg;
     const float inv = 1.f / (a.gsum ? a.gsum[(size_t)a.groups * CV * 2 + g] : (float)(Bg * T));
     const float4 d4 = *reinterpret_cast<const float4*>(a.dout + i0);
     const float4 z4 = a.prelu ? *reinterpret_cast<const float4*>(a.zsave + i0) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2590,7 +2590,7 @@ hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scrat
 #ifdef DSTD_BN_SEP
   const long long total = (long long)B * C * T * V;
   const bool al = ((uintptr_t)a.x | (uintptr_t)a.x2 | (uintptr_t)a.res | (uintptr_t)a.out | (uintptr_t)a.zsave) % 16 == 0;
-  if ((T * V) % 4 == 0 && al) {
+  if ((T * V) % 4 == 0 && al && total < (1LL << 31)) {
     float* ss = scratch + (size_t)a.groups * splits * b.cv * 2;
     k_bn_merge<<<cdiv(b.cv, 256), 256, 0, s>>>(b, (B / a.groups) * T, splits, scratch, ss, C, V);
     const hipError_t e = hipGetLastError();
@@ -2630,7 +2630,7 @@ hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scrat
     const long long total = (long long)B * C * T * V;
     const bool al = ((uintptr_t)a.x | (uintptr_t)a.x2 | (uintptr_t)a.zsave | (uintptr_t)a.dout | (uintptr_t)a.du |
                      (uintptr_t)a.dz_out | (uintptr_t)a.dz_add) % 16 == 0;
-    if ((T * V) % 4 == 0 && al) {
+    if ((T * V) % 4 == 0 && al && total < (1LL << 31)) {
       const int cv = C * V;
       float* sx = wpart + (size_t)splits * a.groups * C;
       k_bn_bwd_merge<<<cdiv(cv, 256), 256, 0, s>>>(b, splits, C, part, wpart, dprelu, sx, cv);
