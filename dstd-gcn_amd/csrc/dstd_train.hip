@@ -1637,10 +1637,9 @@ __global__ __launch_bounds__(256) void k_bn_local_stats(int cv, int rows, int sp
   d[2] = (float)rows;
 }
 
-// DSTD_BN_SEP: the merge as a launch of its own (one thread per channel (c,
+// Separate merge (bn_sep): the merge as a launch of its own (one thread per channel (c,
 // v): every group's mean / rstd, the running statistics in group order, the
 // apply's scale / shift in ss[group][C*V][2]), then a flat element-wise apply
-#ifdef DSTD_BN_SEP
 __global__ __launch_bounds__(256) void k_bn_merge(BnFwd a, int rows, int splits, const float* part, float* ss, int C,
                                                   int V) {
   const int ch = blockIdx.x * 256 + threadIdx.x;
@@ -1683,7 +1682,6 @@ __global__ __launch_bounds__(256) void k_bn_apply_flat(BnFwd a, int Bg, int C, i
     *reinterpret_cast<float4*>(a.out + i0) = make_float4(oo[0], oo[1], oo[2], oo[3]);
   }
 }
-#endif
 
 // workgroup (c, y) covers samples [ns*y, ns*y + ns) (one group: ns divides B/groups)
 __global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, int T, int V, int splits,
@@ -1826,7 +1824,6 @@ __global__ __launch_bounds__(256) void k_bn_bwd_local_sums(int cv, int groups, i
   dst[((size_t)g * cv + ch) * 2 + 1] = sdx;
 }
 
-#ifdef DSTD_BN_SEP
 // DSTD_BN_SEP backward: the merge as a launch of its own (one thread per
 // channel: the group sums in split order into sx[group][C*V][2] -- SyncBN's
 // all-reduced ones for the input gradient -- dgamma / dbeta, and workgroup 0
@@ -1896,7 +1893,6 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_flat(BnBwd a, int Bg, int 
     if (a.dz_out) *reinterpret_cast<float4*>(a.dz_out + i0) = make_float4(dzo[0], dzo[1], dzo[2], dzo[3]);
   }
 }
-#endif
 
 // Merge + apply of the backward in one launch: workgroup (c, n) sums the
 // split partials of its V channels (split order), the n == 0 one accumulates
@@ -2552,6 +2548,18 @@ hipError_t acc_mul(const float* a, const float* b, float* out, size_t n, hipStre
 
 // samples per apply workgroup: more than one only while >= 4096 workgroups
 // remain (measured: 4 per workgroup -2.7% at B=256, +1% at B=32 paired)
+// Separate merge + flat apply for large batches only: at the config-5 batch
+// (3.8M elements per BN) the 30 merge launches cost more than the re-merges
+// they save (+4%), at B=256 they save 2% (profiles/r04y_bn_sep_ab.txt).
+// DSTD_BN_SEP=0 / 1 forces it.
+bool bn_sep(long long total) {
+#ifdef DSTD_BN_SEP
+  (void)total;
+  return DSTD_BN_SEP;
+#else
+  return total >= (1LL << 24);
+#endif
+}
 int bn_apply_samples(int Bg, int B, int C) {
 #ifdef DSTD_BN_NS  // (experiments: samples per apply workgroup)
   if (Bg % DSTD_BN_NS == 0) return DSTD_BN_NS;
@@ -2587,10 +2595,9 @@ hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scrat
     b.gath = y.buf;
     b.world = y.world;
   }
-#ifdef DSTD_BN_SEP
   const long long total = (long long)B * C * T * V;
   const bool al = ((uintptr_t)a.x | (uintptr_t)a.x2 | (uintptr_t)a.res | (uintptr_t)a.out | (uintptr_t)a.zsave) % 16 == 0;
-  if ((T * V) % 4 == 0 && al && total < (1LL << 31)) {
+  if (bn_sep(total) && (T * V) % 4 == 0 && al && total < (1LL << 31)) {
     float* ss = scratch + (size_t)a.groups * splits * b.cv * 2;
     k_bn_merge<<<cdiv(b.cv, 256), 256, 0, s>>>(b, (B / a.groups) * T, splits, scratch, ss, C, V);
     const hipError_t e = hipGetLastError();
@@ -2600,7 +2607,6 @@ hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scrat
     k_bn_apply_flat<<<grid, 256, 0, s>>>(b, B / a.groups, C, T * V, V, total, ss);
     return hipGetLastError();
   }
-#endif
   const int ns = bn_apply_samples(B / a.groups, B, C);
   k_bn_apply_merged<<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, scratch, ns);
   return hipGetLastError();
@@ -2625,12 +2631,11 @@ hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scrat
       return collective_failed();
     b.gsum = y.buf;
   }
-#ifdef DSTD_BN_SEP
   {
     const long long total = (long long)B * C * T * V;
     const bool al = ((uintptr_t)a.x | (uintptr_t)a.x2 | (uintptr_t)a.zsave | (uintptr_t)a.dout | (uintptr_t)a.du |
                      (uintptr_t)a.dz_out | (uintptr_t)a.dz_add) % 16 == 0;
-    if ((T * V) % 4 == 0 && al && total < (1LL << 31)) {
+    if (bn_sep(total) && (T * V) % 4 == 0 && al && total < (1LL << 31)) {
       const int cv = C * V;
       float* sx = wpart + (size_t)splits * a.groups * C;
       k_bn_bwd_merge<<<cdiv(cv, 256), 256, 0, s>>>(b, splits, C, part, wpart, dprelu, sx, cv);
@@ -2641,7 +2646,6 @@ hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scrat
       return hipGetLastError();
     }
   }
-#endif
   const int ns = bn_apply_samples(B / a.groups, B, C);
   k_bn_bwd_apply_merged<<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, part, wpart, dprelu, ns);
   return hipGetLastError();
