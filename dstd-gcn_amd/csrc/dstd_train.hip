@@ -1309,24 +1309,28 @@ __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict_
     }
     return;
   }
-  for (int a = threadIdx.x; a < A; a += blockDim.x) {
-    // (chunk, column block) partials in that order, 8 loads in flight at a time
-    const int n = nch * nij;
-    float t = 0.f;
-    for (int i0 = 0; i0 < n; i0 += 8) {
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = min(i0 + u, n - 1), c = i / nij, z = i - c * nij;
-        v[u] = pbr[((size_t)c * A + a) * nij + z];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (i0 + u < n) t += v[u];
+  // dbrm: S threads per row a, each summing every S-th (chunk, column block)
+  // partial, combined in slice order (A <= 128: A * S <= 256)
+  __shared__ float sp[256];
+  const int n = nch * nij, S = max(1, (int)blockDim.x / A);
+  const int ar = threadIdx.x / S, sl = threadIdx.x - ar * S;
+  float tb = 0.f;
+  if (ar < A) {
+#pragma unroll 4
+    for (int i = sl; i < n; i += S) {
+      const int c = i / nij, z = i - c * nij;
+      tb += pbr[((size_t)c * A + ar) * nij + z];
     }
-    dbrm[a] += t;
+  }
+  sp[threadIdx.x] = tb;
+  __syncthreads();
+  if (ar < A && sl == 0) {
+    float u = 0.f;
+    for (int k = 0; k < S; ++k) u += sp[ar * S + k];
+    dbrm[ar] += u;
   }
   float t = 0.f;
+#pragma unroll 4
   for (int i = threadIdx.x; i < A * nch * nij; i += blockDim.x) t += pal[i];
   t = block_sum(t, red);
   if (threadIdx.x == 0) dalpha[0] += t;
@@ -2475,6 +2479,7 @@ hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, 
                    float* dW2, const float* Amul) {
   if (dW2 && !Amul) return hipErrorInvalidValue;
   if (nparts > 1 && !dDpart) return hipErrorInvalidValue;
+  if (A > 256) return hipErrorInvalidValue;  // (k_adj_bwd_finish: S threads per row, A * S <= 256)
 #ifndef DSTD_ADJ_SPLIT  // (r04u: B=256 step 27.9 -> 27.0 ms, B=32 neutral; 0 = one column block)
 #define DSTD_ADJ_SPLIT 1
 #endif
