@@ -2184,6 +2184,8 @@ hipError_t cs_ks(const Gemm& g, int ntile, hipStream_t s) {
   const int ks = cdiv(g.K, 4);
   if (ks <= 4) return cs_go<MF, 4>(g, ntile, s);
   if (ks <= 8) return cs_go<MF, 8>(g, ntile, s);
+  if (ks <= 10) return cs_go<MF, 10>(g, ntile, s);  // (K = 40: conv_rm's transposed product, spatial)
+  if (ks <= 12) return cs_go<MF, 12>(g, ntile, s);  // (K = 44 / 46: temporal conv_rm)
   if (ks <= 16) return cs_go<MF, 16>(g, ntile, s);
   if (ks <= 17) return cs_go<MF, 17>(g, ntile, s);
   return cs_go<MF, 20>(g, ntile, s);
