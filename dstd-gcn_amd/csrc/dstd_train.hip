@@ -2183,6 +2183,7 @@ template <int MF>
 hipError_t cs_ks(const Gemm& g, int ntile, hipStream_t s) {
   const int ks = cdiv(g.K, 4);
   if (ks <= 4) return cs_go<MF, 4>(g, ntile, s);
+  if (ks <= 6) return cs_go<MF, 6>(g, ntile, s);  // (K = 23: temporal dM at V = 23)
   if (ks <= 8) return cs_go<MF, 8>(g, ntile, s);
   if (ks <= 10) return cs_go<MF, 10>(g, ntile, s);  // (K = 40: conv_rm's transposed product, spatial)
   if (ks <= 12) return cs_go<MF, 12>(g, ntile, s);  // (K = 44 / 46: temporal conv_rm)
