@@ -2572,8 +2572,10 @@ int bn_apply_samples(int Bg, int B, int C) {
 #ifdef DSTD_BN_NS  // (experiments: samples per apply workgroup)
   if (Bg % DSTD_BN_NS == 0) return DSTD_BN_NS;
 #endif
+  // (>= 1024 workgroups: 4 samples each at the config-5 batch, a quarter of
+  // the per-workgroup merges; B=32 step -1.4%, profiles/r04ad_bn_ns_ab.txt)
   for (int ns : {4, 2})
-    if (Bg % ns == 0 && (size_t)C * (B / ns) >= 4096) return ns;
+    if (Bg % ns == 0 && (size_t)C * (B / ns) >= 1024) return ns;
   return 1;
 }
 
