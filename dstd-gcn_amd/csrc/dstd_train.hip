@@ -357,6 +357,8 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
   const int ntile = ca.ntile, nw = gridDim.x * 4, items = g.nb1 * ca.nb2 * ntile;  // ntile: items per batch
   const int K = g.K, M = g.M, N = g.N;
   const int bk = (int)g.b_k, cm = (int)g.c_m;
+  const uint32_t kstep = 16u * (uint32_t)bk;  // bytes between k-steps (4 rows)
+  (void)K, (void)M;
   // the item's batch panels (wave-uniform) and this lane's first column
   auto panel = [&](int it, const float*& Bb, float*& Cb, float*& Db, int& p) {
     const int b = it / ntile, t = it - b * ntile;
@@ -373,13 +375,16 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
     int p;
     panel(it, Bb, Cb, Db, p);
     const auto rb = cs_rsrc(Bb, ca.b_bytes);
+    // one lane base per column tile; rows k >= K fall past the buffer range by
+    // themselves (b_k >= N: row K starts at or after the range's end), columns
+    // past N take an out-of-range base
 #pragma unroll
-    for (int sk = 0; sk < KS; ++sk)
+    for (int q = 0; q < NT; ++q) {
+      const int pq = p + 16 * q;
+      const uint32_t base = pq < N ? (uint32_t)(lk * bk + pq) * 4u : kCsOOB;
 #pragma unroll
-      for (int q = 0; q < NT; ++q) {
-        const int k = 4 * sk + lk, pq = p + 16 * q;
-        v[q][sk] = cs_ld(rb, k < K && pq < N ? (uint32_t)(k * bk + pq) * 4u : kCsOOB);
-      }
+      for (int sk = 0; sk < KS; ++sk) v[q][sk] = cs_ld(rb, base + (uint32_t)sk * kstep);
+    }
   };
   int it = blockIdx.x * 4 + wave;
   float bf[NT][KS];
@@ -407,8 +412,10 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
         for (int x = 0; x < MF; ++x)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int m = x * 16 + lk * 4 + r, pq = p + 16 * q;
-            cv[q][x][r] = cs_ld(rc, pq < N && m < M ? (uint32_t)(m * cm + pq) * 4u : kCsOOB);
+            // (rows m >= M lie past the range: c_m >= N)
+            const int pq = p + 16 * q;
+            const uint32_t cb = pq < N ? (uint32_t)(lk * 4 * cm + pq) * 4u : kCsOOB;
+            cv[q][x][r] = cs_ld(rc, cb + (uint32_t)((x * 16 + r) * cm) * 4u);
           }
     }
     f32x4 acc[NT][MF];
@@ -442,6 +449,8 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
     for (int q = 0; q < NT; ++q) {
       const int pq = p + 16 * q;
       const bool pin = pq < N;
+      // this lane's column base (rows m >= M lie past the range: c_m >= N)
+      const uint32_t cbq = pin ? (uint32_t)(lk * 4 * cm + pq) * 4u : kCsOOB;
       if (Db) {  // C and D = d_alpha * C + (d_A (* d_W) (+ d_R)) of this column (k_gemm's order)
         const auto rd = cs_rsrc(Db, ca.c_bytes);
         const float ad = *g.d_alpha;
@@ -454,7 +463,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int m = x * 16 + lk * 4 + r;
-            const uint32_t off = pin && m < M ? (uint32_t)(m * cm + pq) * 4u : kCsOOB;
+            const uint32_t off = cbq + (uint32_t)((x * 16 + r) * cm) * 4u;
             float v = g.alpha * acc[q][x][r];
             if (g.bias_m) v += bsl[m];
             cs_st(rd, off, fmaf(ad, v, ac));
@@ -469,7 +478,7 @@ __global__ __launch_bounds__(256) void k_conv_stream(Gemm g, CsArgs ca) {
             const int m = x * 16 + lk * 4 + r;
             float v = fmaf(g.alpha, acc[q][x][r], bsl[m]);
             if (g.beta != 0.f) v = fmaf(g.beta, cv[q][x][r], v);
-            cs_st(rc, pin && m < M ? (uint32_t)(m * cm + pq) * 4u : kCsOOB, v);
+            cs_st(rc, cbq + (uint32_t)((x * 16 + r) * cm) * 4u, v);
           }
       }
     }
@@ -2200,8 +2209,10 @@ hipError_t gemm_stream(const Gemm& g, hipStream_t s) {
   const long long nbat = (long long)g.nb1 * g.nb2;
   const int ntile = cdiv(g.N, 16 * DSTD_CS_NT);  // items per batch
   // 32-bit buffer offsets over one batch's panels
-  if (nbat * ntile >= (1LL << 31) || g.b_k < g.N || g.c_m < g.N || ((long long)(g.K - 1) * g.b_k + g.N) * 4 >= (1LL << 31) ||
-      ((long long)(g.M - 1) * g.c_m + g.N) * 4 >= (1LL << 31))
+  // (rows past K / M are read / written at offsets past the buffer range: the
+  // padded k-steps and row tiles must stay below 2^31 bytes too)
+  if (nbat * ntile >= (1LL << 31) || g.b_k < g.N || g.c_m < g.N || ((long long)g.K + 84) * g.b_k * 4 >= (1LL << 31) ||
+      ((long long)g.M + 16) * g.c_m * 4 >= (1LL << 31))
     return hipErrorNotSupported;
 #ifdef DSTD_GEMM_LOG
   fprintf(stderr, "gemm stream M %d N %d K %d nb %lld beta %g bias %d d_out %d stream %p\n", g.M, g.N, g.K, nbat, g.beta,
