@@ -211,7 +211,14 @@ struct Wgrad {
   WgradRes* res = nullptr;
   Wgrad() = default;
   explicit Wgrad(WgradRes* r) : res(r) {}
-  ~Wgrad() { wgrad_release(res); }
+  // an error return between a fork and the success-path join() must not
+  // leave side-stream work unordered before the caller's stream (it still
+  // reads the workspace / saved state and writes the gradient arena), nor a
+  // graph capture unjoined: the destructor joins whatever was forked
+  ~Wgrad() {
+    if (res && any) (void)join();
+    wgrad_release(res);
+  }
   Wgrad(const Wgrad&) = delete;
   Wgrad& operator=(const Wgrad&) = delete;
   hipStream_t main = nullptr;
@@ -233,6 +240,7 @@ struct Wgrad {
   }
   // the side stream continues after everything enqueued on main so far
   hipError_t fork() {
+    any = true;  // from here on the side stream may hold work to join
     DSTD_TRYH(hipEventRecord(res->fork, main));
     return hipStreamWaitEvent(res->st, res->fork, 0);
   }
@@ -242,6 +250,7 @@ struct Wgrad {
   }
   hipError_t join() {
     if (!res || !any) return hipSuccess;
+    any = false;
     DSTD_TRYH(hipEventRecord(res->join, res->st));
     return hipStreamWaitEvent(main, res->join, 0);
   }

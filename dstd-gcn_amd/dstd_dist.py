@@ -151,38 +151,61 @@ class BnSync:
         self._fn = native.COLLECTIVE_FN(self._collective)  # kept alive with the struct
         self._s = native.BnSyncStruct(self.world, self.rank, self._fn, None, self.buf.data_ptr(), n)
         self.calls = 0
+        self._ext = {}  # ExternalStream per foreign stream handle
 
     def struct_ref(self):
         return ctypes.byref(self._s)
 
+    def _stream_ctx(self, stream):
+        """torch's stream context for the library's call stream (the header's
+        contract: the collective is ordered on ``stream``), a no-op when it
+        already is torch's current stream (every native call site today)."""
+        import contextlib
+        if not self.buf.is_cuda:
+            return contextlib.nullcontext()
+        dev = self.buf.device
+        handle = stream or 0
+        if handle == torch.cuda.current_stream(dev).cuda_stream:
+            return contextlib.nullcontext()
+        if handle == 0:
+            return torch.cuda.stream(torch.cuda.default_stream(dev))
+        ext = self._ext.get(handle)
+        if ext is None:
+            ext = self._ext[handle] = torch.cuda.ExternalStream(handle, device=dev)
+        return torch.cuda.stream(ext)
+
     def _collective(self, ctx, op, buf, count, stream):
         try:
-            if buf != self.buf.data_ptr():
-                raise RuntimeError("dstd_bn_sync: foreign buffer")
-            self.calls += 1
-            if op == native.COLL_ALLGATHER:
-                out = self.buf[:count * self.world]
-                mine = out[self.rank * count:(self.rank + 1) * count].clone()
-                if self.host:
-                    o = torch.empty(out.shape, dtype=out.dtype)
-                    dist.all_gather_into_tensor(o, mine.cpu(), group=self.group)
-                    out.copy_(o)
-                else:
-                    dist.all_gather_into_tensor(out, mine, group=self.group)
-            elif op == native.COLL_ALLREDUCE_SUM:
-                t = self.buf[:count]
-                if self.host:
-                    c = t.cpu()
-                    dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group)
-                    t.copy_(c)
-                else:
-                    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-            else:
-                raise ValueError(f"dstd_bn_sync: unknown collective {op}")
-            return 0
+            with self._stream_ctx(stream):
+                return self._collective_on_stream(op, buf, count)
         except Exception as e:  # the library returns DSTD_ECOLLECTIVE
             print(f"dstd_bn_sync collective failed: {e!r}", file=sys.stderr)
             return 1
+
+    def _collective_on_stream(self, op, buf, count):
+        if buf != self.buf.data_ptr():
+            raise RuntimeError("dstd_bn_sync: foreign buffer")
+        self.calls += 1
+        if op == native.COLL_ALLGATHER:
+            out = self.buf[:count * self.world]
+            mine = out[self.rank * count:(self.rank + 1) * count].clone()
+            if self.host:
+                o = torch.empty(out.shape, dtype=out.dtype)
+                dist.all_gather_into_tensor(o, mine.cpu(), group=self.group)
+                out.copy_(o)
+            else:
+                dist.all_gather_into_tensor(out, mine, group=self.group)
+        elif op == native.COLL_ALLREDUCE_SUM:
+            t = self.buf[:count]
+            if self.host:
+                c = t.cpu()
+                dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group)
+                t.copy_(c)
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        else:
+            raise ValueError(f"dstd_bn_sync: unknown collective {op}")
+        return 0
 
 
 def convert_sync_batchnorm(model, group=None):

@@ -305,6 +305,10 @@ class PredictionEngine:
         # duplicates): the saved results are put back in dataset order by the
         # sampler's per-sample indices
         sample_idx = np.asarray(list(iter(test_loader.sampler))) if presharded and save_path is not None else None
+        # ... and its padding duplicates are the last of each rank's samples
+        # (positions >= len(dataset) of the padded, interleaved index list):
+        # the metric counts every dataset sample once, as a single process does
+        n_real = self._presharded_real(test_loader.sampler) if presharded else None
         seen = 0
         self.model.eval()
         with torch.no_grad():
@@ -330,8 +334,13 @@ class PredictionEngine:
                     index_cache[key] = self._metric_indices(D, outputs.shape[2], seq_len, input_n, eval_frame,
                                                             dim_used, joint_to_ignore, joint_equal)
                 used_pos, joint_src, frames = index_cache[key]
-                self._frame_metric(all_seqs, outputs, t_out0, used_pos, joint_src, frames, sums)
-                N += n
+                k = n if n_real is None else min(n, max(0, n_real - seen))
+                if k == n:
+                    self._frame_metric(all_seqs, outputs, t_out0, used_pos, joint_src, frames, sums)
+                elif k > 0:
+                    self._frame_metric(all_seqs[:k].contiguous(), outputs[:k].contiguous(), t_out0, used_pos,
+                                       joint_src, frames, sums)
+                N += k
                 if save_results is not None:
                     pred = self._fill_pred(all_seqs, outputs, used_pos, joint_src, t_out0)[:, input_n:]
                     targ = all_seqs.view(n, seq_len, -1, 3)[:, input_n:]
@@ -350,6 +359,18 @@ class PredictionEngine:
                 self._save_results(save_path, save_results, rank, world)
         # t_l.avg of the reference = sum over (batch, frame) of metric_k / (N * frames)
         return float(t_metric.mean()), t_metric
+
+    @staticmethod
+    def _presharded_real(sampler):
+        """How many of this rank's samples from a DistributedSampler are
+        dataset samples rather than padding: the rank reads positions
+        rank, rank + world, ... of the index list padded to total_size, and
+        the positions past len(dataset) are the duplicates."""
+        n_data = len(sampler.dataset)
+        if getattr(sampler, "drop_last", False) or sampler.total_size <= n_data:
+            return sampler.num_samples
+        r, w = sampler.rank, sampler.num_replicas
+        return max(0, -(-(n_data - r) // w))
 
     @staticmethod
     def _save_results(save_path, parts, rank, world):

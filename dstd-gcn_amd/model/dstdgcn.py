@@ -31,7 +31,6 @@ with frozen parameters and input) eval runs the fused inference kernels.
 """
 import itertools
 import operator
-import random
 import math
 import weakref
 from typing import List, Tuple
@@ -412,8 +411,10 @@ def _host_seed():
     """A dropout seed for the op branch of _ModelTrain: an integer drawn on
     the host at run time (under torch.compile this is a graph break, not a
     traced random value -- dynamo would turn one into a tensor, which the ops'
-    integer `seed` cannot take)."""
-    return random.randint(0, 2 ** 62 - 1)
+    integer `seed` cannot take).  Drawn from torch's CPU generator, so
+    torch.manual_seed makes compiled training with dropout reproducible like
+    the eager path."""
+    return int(torch.randint(0, 2 ** 62, (1,)).item())
 
 
 class _ModelTrain(torch.autograd.Function):

@@ -220,7 +220,7 @@ def _engine_save_presharded_body(rank, world):
     the samples over the ranks and pads the last with a duplicate."""
     out = _engine_metric_body(rank, world, save_path=os.environ["DSTD_TEST_SAVE"],
                               presharded=int(os.environ["DSTD_TEST_N"]))
-    return out[2]
+    return out[2], out[1]
 
 
 def _engine_metric_body(rank, world, save_path=None, n_batches=3, presharded=0):
@@ -311,16 +311,23 @@ def test_engine_test_save_path_sharded(tmp_path, n_batches):
 def test_engine_test_save_path_presharded(tmp_path, n):
     """save_path with a DistributedSampler loader (samples interleaved over
     the ranks; n = 3 pads rank 1 with a duplicate of sample 0): the file holds
-    each sample once, in dataset order."""
+    each sample once, in dataset order, and the metric counts each sample
+    once too -- the padding duplicate stays out of the per-frame sums and the
+    sample count, so both ranks report the single-process metric."""
     import numpy as np
     d = load_npz("engine.npz")
     prefix = str(tmp_path / "res")
     os.environ["DSTD_TEST_SAVE"], os.environ["DSTD_TEST_N"] = prefix, str(n)
     try:
-        seen = run_world("_engine_save_presharded_body")
+        res = run_world("_engine_save_presharded_body")
     finally:
         del os.environ["DSTD_TEST_SAVE"], os.environ["DSTD_TEST_N"]
-    assert seen[0] == [1, 1] and seen[1] == [1, 1]
+    seen = {r: v[0] for r, v in res.items()}
+    # the batches each rank put into the metric (rank 1's padding batch: none)
+    assert seen[0] == [1, 1] and seen[1] == ([1] if n == 3 else [1, 1])
+    _, single, _ = _engine_metric_body(0, 1, presharded=n)  # one process, same sampler
+    for r in (0, 1):
+        np.testing.assert_allclose(np.asarray(res[r][1]), np.asarray(single), rtol=1e-6)  # fp32 sums, other order
     f = np.load(prefix + ".npz")
     all_seqs = d["test/all_seqs"][:n]
     np.testing.assert_array_equal(f["target"], all_seqs.reshape(n, all_seqs.shape[1], -1, 3)[:, 10:])

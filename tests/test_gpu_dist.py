@@ -279,3 +279,65 @@ def test_syncbn_dp_step_equals_full_batch_step():
     loc = stats(ratios(res[0]["g_local"]))
     print("per-rank BatchNorm: median / p90 / max", loc)
     assert loc[0] > 10.0, ("per-rank BatchNorm met the full-batch bar: the test would prove nothing", loc)
+
+
+class _FailingSync:
+    """A one-rank dstd_bn_sync whose collective fails at the n-th backward
+    all-reduce (the forward all-gathers succeed: with one rank they move
+    nothing) -- DSTD_ECOLLECTIVE in the middle of the model backward, after
+    the weight-gradient stream has been forked."""
+
+    def __init__(self, model, fail_at):
+        import dstd_native as native
+        n = native.lib().dstd_bn_sync_buffer_floats(1, model.num_feature, model.joints_to_consider)
+        self.buf = torch.zeros(n, dtype=torch.float32, device=DEV)
+        self.fail_at, self.reduces = fail_at, 0
+        self._fn = native.COLLECTIVE_FN(self._collective)
+        self._s = native.BnSyncStruct(1, 0, self._fn, None, self.buf.data_ptr(), n)
+        self.calls = 0
+
+    def struct_ref(self):
+        import ctypes
+        return ctypes.byref(self._s)
+
+    def _collective(self, ctx, op, buf, count, stream):
+        import dstd_native as native
+        self.calls += 1
+        if op == native.COLL_ALLREDUCE_SUM:
+            self.reduces += 1
+            if self.reduces == self.fail_at:
+                return 1
+        return 0
+
+
+def test_backward_error_after_fork_joins_the_side_stream():
+    """an error return from the model backward after the weight-
+    gradient stream was forked (a SyncBN collective failing mid-backward)
+    must still order the side stream's work before the caller's stream
+    (Wgrad's destructor joins it).  The failing call raises naming the entry
+    point; afterwards the device is healthy and a plain step on a fresh model
+    reproduces the reference step bit for bit."""
+    from engine import mpjpe_error_3d
+
+    def step(m):
+        g = torch.Generator().manual_seed(5)
+        seq = (0.6 * torch.randn(32, 40, 69, generator=g)).to(DEV)
+        inp = seq.clone()
+        inp[:, 10:] = inp[:, 9:10]
+        y = m(inp.view(32, 40, 23, 3)).view(32, 40, 69)
+        mpjpe_error_3d(y, seq).backward()
+        return {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+
+    m0, _ = _model_3dpw()
+    want = step(m0)
+    for fail_at in (3, 15):  # an early and a late BatchNorm of the backward
+        m, _ = _model_3dpw()
+        m._dstd_bn_sync = _FailingSync(m, fail_at)
+        with pytest.raises(RuntimeError, match="dstd_model_train_bwd_sync"):
+            step(m)
+        assert m._dstd_bn_sync.reduces == fail_at
+        torch.cuda.synchronize()
+    m1, _ = _model_3dpw()
+    got = step(m1)
+    for n in want:
+        assert torch.equal(got[n], want[n]), n
