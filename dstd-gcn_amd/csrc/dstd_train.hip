@@ -16,15 +16,16 @@ namespace {
 
 constexpr int kRedThreads = 256;
 
-__device__ __forceinline__ float block_sum(float v, float* red) {
-  // wave64 butterfly, then one float per wave through LDS
+template <typename F>
+__device__ __forceinline__ F block_sum(F v, F* red) {
+  // wave64 butterfly, then one value per wave through LDS
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   __syncthreads();
   if (lane == 0) red[w] = v;
   __syncthreads();
-  float t = 0.f;
+  F t = 0;
   for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
   return t;
 }
@@ -1238,9 +1239,10 @@ __global__ void k_tanh_outer_bwd(const float* __restrict__ M, const float* __res
 __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, const float* __restrict__ E,
                                                       const float* __restrict__ alpha, int B, int A, int NN2, int nch,
                                                       float* __restrict__ pdA, float* __restrict__ pbr,
-                                                      float* __restrict__ pal, const float* __restrict__ dDp,
+                                                      double* __restrict__ pal, const float* __restrict__ dDp,
                                                       int np) {
   __shared__ float red[4];
+  __shared__ double redd[4];
   constexpr int SG = 8;
   const int a = blockIdx.x, ch = blockIdx.y, nij = gridDim.z;
   const int per = (B + nch - 1) / nch, n0 = ch * per, n1 = min(B, n0 + per);
@@ -1249,7 +1251,12 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
   const float* src = np > 1 ? dDp : dD;
   const int nq = np > 1 ? np : 1;
   const size_t qs = np > 1 ? (size_t)B * A * NN2 : 0;
-  float sbr = 0.f, sal = 0.f;
+  // d alpha = sum over every (n, a, i, j) of dD E: a global sum whose terms
+  // cancel to ~1% of their magnitude on trained blocks, so its products and
+  // partial sums are carried in fp64 (fp32 accumulation put it at ~3x the
+  // fp32 torch error: scripts/grad_tail_bisect.py)
+  float sbr = 0.f;
+  double sal = 0.0;
   for (int ij = blockIdx.z * 256 + threadIdx.x; ij < NN2; ij += 256 * nij) {
     float sa = 0.f;
     for (int nb = n0; nb < n1; nb += SG) {  // SG samples' loads in flight, then use in order
@@ -1274,7 +1281,7 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
       for (int u = 0; u < SG; ++u) {
         if (nb + u >= n1) break;
         sa += dv[u];
-        sal = fmaf(dv[u], ev[u], sal);
+        sal = fma((double)dv[u], (double)ev[u], sal);
         dD[((size_t)(nb + u) * A + a) * NN2 + ij] = al * dv[u];
       }
     }
@@ -1282,7 +1289,7 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
     sbr += sa;
   }
   sbr = block_sum(sbr, red);
-  sal = block_sum(sal, red);
+  sal = block_sum(sal, redd);
   if (threadIdx.x == 0) {
     pbr[((size_t)ch * A + a) * nij + blockIdx.z] = al * sbr;
     pal[((size_t)ch * A + a) * nij + blockIdx.z] = sal;
@@ -1294,12 +1301,12 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
 // dW2 (optional): also dW2[ij] += dA-contribution * Amul[ij] (the spatial
 // adjacency A_s * W_s + R_s: dR_s = dA as dA itself, dW_s = dA * A_s)
 __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict__ pdA, const float* __restrict__ pbr,
-                                                        const float* __restrict__ pal, int A, int NN2, int nch,
+                                                        const double* __restrict__ pal, int A, int NN2, int nch,
                                                         float* __restrict__ dA, float* __restrict__ dbrm,
                                                         float* __restrict__ dalpha, int assign_dA, float* __restrict__ dW2,
                                                         const float* __restrict__ Amul, int nij) {
   __shared__ float lds[16][17];
-  __shared__ float red[4];
+  __shared__ double redd[4];
   const int nblk = (NN2 + 15) / 16;
   if ((int)blockIdx.x < nblk) {
     const int el = threadIdx.x & 15, sl = threadIdx.x >> 4;
@@ -1338,11 +1345,11 @@ __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict_
     for (int k = 0; k < S; ++k) u += sp[ar * S + k];
     dbrm[ar] += u;
   }
-  float t = 0.f;
+  double t = 0.0;
 #pragma unroll 4
   for (int i = threadIdx.x; i < A * nch * nij; i += blockDim.x) t += pal[i];
-  t = block_sum(t, red);
-  if (threadIdx.x == 0) dalpha[0] += t;
+  t = block_sum(t, redd);
+  if (threadIdx.x == 0) dalpha[0] += (float)t;
 }
 
 __global__ void k_copy_jobs(CopyJobs js) {
@@ -2485,7 +2492,7 @@ int adj_bwd_chunks(int B, int A) { return std::max(1, std::min(std::min(B, 16), 
 
 size_t adj_bwd_scratch_floats(int B, int A, int NN2) {
   const int nch = adj_bwd_chunks(B, A);
-  return (size_t)nch * A * NN2 + 2 * (size_t)nch * A * cdiv(NN2, 256) + 64;
+  return (size_t)nch * A * NN2 + 3 * (size_t)nch * A * cdiv(NN2, 256) + 64;  // pal: doubles
 }
 
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
@@ -2498,9 +2505,9 @@ hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, 
 #define DSTD_ADJ_SPLIT 1
 #endif
   const int nch = adj_bwd_chunks(B, A), nij = DSTD_ADJ_SPLIT ? cdiv(NN2, 256) : 1;
-  float* pdA = scratch;
+  double* pal = reinterpret_cast<double*>(scratch);  // (scratch: 256-byte aligned workspace carve)
+  float* pdA = scratch + 2 * (size_t)nch * A * nij;
   float* pbr = pdA + (size_t)nch * A * NN2;
-  float* pal = pbr + (size_t)nch * A * nij;
   k_adj_bwd_part<<<dim3(A, nch, nij), 256, 0, s>>>(dD, E, alpha, B, A, NN2, nch, pdA, pbr, pal, dDpart, nparts);
   k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(pdA, pbr, pal, A, NN2, nch, dA, dbrm, dalpha, assign_dA, dW2,
                                                       Amul, nij);

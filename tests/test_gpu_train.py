@@ -219,27 +219,81 @@ def _bn_of(module, key):
 
 
 # ---- whole model: one engine step vs the reference's fp64 gradients ---------
-# Gradients that are one sum over every position of the batch: the scalars
-# (alpha_sm / alpha_tm, the PReLU slopes) and the conv biases (conv_f /
-# conv_m1 / conv_m2 / conv_rm / residual conv, each summed over all (n, t, v)
-# or (n, t, v, w)).  Their fp32 round-off is the heavy tail of the 21-op
-# stack's chaos: the reference's own fp32 run and the fp32
-# oracle land several times apart on them.  Every other tensor (conv weights,
-# W_s, R_s, R_t, BatchNorm weights and biases) must stay within 3x the fp32
-# noise of two other implementations; a global-sum tensor within 12x.
+# The 21-op train-mode stack is ill-conditioned in fp32: a
+# gradient's fp32 error is a draw from a wide distribution whose spread
+# depends on the tensor (global sums such as alpha_sm are one sum over every
+# position of both passes, cancelling ~5x10^4-fold on trained blocks:
+# scripts/grad_tail_bisect.py, DESIGN.md section 8 "Gradient accuracy").  So
+# the noise floor of each tensor is MEASURED as the largest fp32 error among
+# several fp32 implementations / summation orders of the same step -- the
+# fp32 oracle on the CPU, on the GPU (torch-ROCm ops), and on the GPU over
+# N_ORDERS sample orders of the batch (the loss and train-mode BatchNorm are
+# order-invariant, so each order is only another rounding sequence), plus the
+# reference's own fp32 run where the fixture holds it -- and every tensor of
+# the native step must be within 4x that floor (median <= 1.5, 90th
+# percentile <= 2).  Before round 5 the floor was the max of two samples,
+# and a tail exemption (12x for global sums) covered its undershoot.  (The
+# native step is one more draw from the same heavy-tailed distribution: at
+# B=32 its largest ratio was 3.16, on a PReLU slope -- a sum over 3.8M
+# positions -- against 8 samples, r05f.)
+N_ORDERS = 8
+
+
+def fp32_noise(sd0, batch, g64, extra=None, n_orders=N_ORDERS):
+    """Per tensor: the largest |g32 - g64| over the fp32 oracle step on the
+    CPU, on the GPU and on the GPU over n_orders sample orders of ``batch``
+    (numpy (inp, inv, seq)); ``extra``: more per-tensor fp32 errors (the
+    reference's own, train_grads.npz g32err)."""
+    B = batch[0].shape[0]
+    runs = [("cpu", None), (DEV, None)] + [(DEV, np.random.default_rng(s).permutation(B))
+                                           for s in range(1, n_orders + 1)]
+    noise = {k: float(extra[k]) if extra is not None else 0.0 for k in g64}
+    for dev, perm in runs:
+        P = O.train_params(sd0, torch.float32, dev)
+        _, lall = O.step_loss(P, batch if perm is None else tuple(x[perm] for x in batch), 5)
+        lall.backward()
+        for k, v in P.items():
+            if v.grad is not None:
+                noise[k] = max(noise[k], float(np.abs(v.grad.double().cpu().numpy() - g64[k]).max()))
+    return noise
+
+
+def noise_ratios(grads, g64, noise):
+    """(|g - g64|_max / max(noise, 1e-4 |g64|_max), tensor) for every tensor of g64."""
+    out = []
+    for k, r64 in g64.items():
+        g = grads[k].double().cpu().numpy() if torch.is_tensor(grads[k]) else grads[k]
+        scale = float(np.abs(r64).max())
+        out.append((float(np.abs(g - r64).max()) / max(noise[k], 1e-4 * scale), k))
+    return out
+
+
+def check_ratios(ratios, what=""):
+    r = np.array(sorted((v for v, _ in ratios), reverse=True))
+    top = sorted(ratios, reverse=True)[:6]
+    print(f"{what} err / fp32 noise floor: median {np.median(r):.2f}, p90 {np.quantile(r, 0.9):.2f}, "
+          f"max {r[0]:.2f}", [(round(v, 2), k) for v, k in top[:3]])
+    assert np.median(r) <= 1.5, (what, np.median(r), top)
+    assert np.quantile(r, 0.9) <= 2.0, (what, np.quantile(r, 0.9), top)
+    assert r[0] <= 4.0, (what, top)
+
+
+# The eval-mode backward tests (tests/test_gpu_parity.py, test_gpu_fast.py;
+# running-statistics BatchNorm, a random upstream gradient) keep the former
+# two-sample criterion: every tensor above 3x must be a global sum
+# (GLOBAL_SUM: the scalars and conv biases), those within 12x.
 GLOBAL_SUM = re.compile(r"(alpha_sm|alpha_tm|prelu\.weight|encoders\.\d+\.2\.weight|"
                         r"conv_(f|m1|m2|rm)\.bias|residual\.0\.bias)$")
 
 
 def check_tail(ratios, bar=3.0, global_bar=12.0):
-    """ratios: (error / fp32 noise, tensor name).  Prints every tensor above
-    `bar`; those must all be global-sum gradients (GLOBAL_SUM), within
-    `global_bar`."""
     above = sorted(((v, k) for v, k in ratios if v > bar), reverse=True)
     print(f"gradient error / fp32 noise above {bar}x ({len(above)} of {len(ratios)}):",
           [(round(v, 2), k) for v, k in above])
     assert all(GLOBAL_SUM.search(k) for _, k in above), [(v, k) for v, k in above if not GLOBAL_SUM.search(k)]
     assert all(v <= global_bar for v, _ in above), above[:4]
+
+
 def _realias(model):
     """Module.to() converts each parameter separately and so splits the
     A_s/R_s storage alias (the reference's runner does the same with
@@ -276,25 +330,10 @@ def test_model_step_gradients_vs_reference_fp64():
     named = dict(m.named_parameters())
     keys = [k[4:] for k in g.files if k.startswith("g64/")]
     assert set(keys) == {k for k, p in named.items() if p.requires_grad}
-    # a second, independent fp32 implementation (the oracle on the CPU) shows
-    # how far fp32 round-off alone moves each gradient of this chaotic stack
-    P = O.train_params(group(d, "train/sd0/"), torch.float32)
-    _, l32 = O.step_loss(P, tuple(d[f"train/{n}0"] for n in ("inp", "inv", "seq")), 5)
-    l32.backward()
-    ratios = []
-    for k in keys:
-        ref = g["g64/" + k]
-        scale = float(np.abs(ref).max())
-        noise = max(float(g["g32err/" + k]), float(np.abs(P[k].grad.double().numpy() - ref).max()), 1e-4 * scale)
-        err = float(np.abs(named[k].grad.double().cpu().numpy() - ref).max())
-        ratios.append((err / noise, k, err, noise, scale))
-    ratios.sort(reverse=True)
-    r = np.array([x[0] for x in ratios])
-    # as accurate as a typical fp32 implementation (the CPU oracle's own fp32
-    # error reaches ~9x the reference's on global-sum gradients)
-    assert np.median(r) <= 1.5, (np.median(r), ratios[:8])
-    assert np.quantile(r, 0.9) <= 3.0, (np.quantile(r, 0.9), ratios[:8])
-    check_tail([(x[0], x[1]) for x in ratios])
+    g64 = {k: g["g64/" + k] for k in keys}
+    noise = fp32_noise(group(d, "train/sd0/"), tuple(d[f"train/{n}0"] for n in ("inp", "inv", "seq")), g64,
+                       extra={k: g["g32err/" + k] for k in keys})
+    check_ratios(noise_ratios({k: named[k].grad for k in keys}, g64, noise), "fixture step (two calls)")
     assert named["conv_st_in.stgcn.0.0.A_s"].grad is None
 
 
@@ -328,30 +367,17 @@ def test_model_step_gradients_at_training_batch(B):
     loss = mpjpe_error_3d(p1.reshape(B, T, VC), sq)
     all_loss = (loss + mpjpe_error_3d(p2.reshape(B, T, VC), sq.flip(1))) / 2
     all_loss.backward()
-    # oracle steps
+    # the oracle's fp64 step and the fp32 noise floor
     sd0 = group(d, "train/sd0/")
-    grads, losses = {}, {}
-    for tag, dt, dev in (("64", torch.float64, DEV), ("32g", torch.float32, DEV), ("32c", torch.float32, "cpu")):
-        P = O.train_params(sd0, dt, dev)
-        l0, lall = O.step_loss(P, batch, 5)
-        lall.backward()
-        losses[tag] = float(l0.detach())
-        grads[tag] = {k: v.grad.double().cpu().numpy() for k, v in P.items() if v.grad is not None}
-    assert abs(float(loss.detach()) - losses["64"]) / losses["64"] < 1e-5
+    P = O.train_params(sd0, torch.float64, DEV)
+    l0, lall = O.step_loss(P, batch, 5)
+    lall.backward()
+    g64 = {k: v.grad.double().cpu().numpy() for k, v in P.items() if v.grad is not None}
+    assert abs(float(loss.detach()) - float(l0)) / float(l0) < 1e-5
     named = dict(m.named_parameters())
-    assert set(grads["64"]) == {k for k, p in named.items() if p.requires_grad}
-    ratios = []
-    for k, ref in grads["64"].items():
-        scale = float(np.abs(ref).max())
-        noise = max(float(np.abs(grads["32g"][k] - ref).max()), float(np.abs(grads["32c"][k] - ref).max()),
-                    1e-4 * scale)
-        err = float(np.abs(named[k].grad.double().cpu().numpy() - ref).max())
-        ratios.append((err / noise, k))
-    r = np.array([x[0] for x in sorted(ratios, reverse=True)])
-    print(f"B={B}: err / fp32 noise median {np.median(r):.2f}, p90 {np.quantile(r, 0.9):.2f}, max {r[0]:.2f}")
-    assert np.median(r) <= 1.5, (np.median(r), sorted(ratios, reverse=True)[:8])
-    assert np.quantile(r, 0.9) <= 3.0, (np.quantile(r, 0.9), sorted(ratios, reverse=True)[:8])
-    check_tail(ratios)
+    assert set(g64) == {k for k, p in named.items() if p.requires_grad}
+    noise = fp32_noise(sd0, batch, g64)
+    check_ratios(noise_ratios({k: named[k].grad for k in g64}, g64, noise), f"B={B} step")
 
 
 def test_wgrad_stream_is_bit_identical():
@@ -742,3 +768,36 @@ def test_native_conv2d_strided_padded():
     assert rel(xg.grad, x64.grad) < 1e-5
     assert rel(conv.weight.grad, W64.grad) < 1e-5
     assert rel(conv.bias.grad, b64.grad) < 1e-5
+
+
+def test_model_step_gradient_tail_is_propagation():
+    """where the whole-model gradient tail comes from.  Every
+    DSTDGCB of the fixture step (the engine's paired step) gets the fp64
+    oracle step's own block input and upstream gradient (both halves), and
+    its native train-mode forward + backward is compared per tensor with fp64
+    autograd of the oracle block (scripts/grad_tail_bisect.py prints the
+    tables): every parameter and input gradient within the block bar (2e-4,
+    test_dstdgcb_train_forward_backward) or within 3x the fp32 oracle's own
+    error on the same block over 10 implementations / sample orders -- the
+    block's own arithmetic is an fp32 implementation's, so the model-level
+    tail is propagation through the ill-conditioned stack, not a kernel's
+    summation.  The spatial DSTDGCs of the worst block alone: each op's
+    d alpha (a sum cancelling 10^2-10^3-fold) within 2x the fp32 oracle's
+    error."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    import grad_tail_bisect as GT
+    d, batch = GT.batch_np()
+    sd0 = group(d, "train/sd0/")
+    _, rec = GT.oracle_step(sd0, batch, torch.float64, DEV, record=True)
+    worst_b, worst_v = 0, 0.0
+    for b in range(len(GT.PREFIXES)):
+        pre, rows = GT.block_detail(sd0, rec, b)
+        for e, k, sc, tol, ec, eg in rows:
+            assert e <= max(1.0, 3.0 * max(ec, eg)), (pre, k, e, ec, eg)
+        print(pre, "native err / tol max", round(rows[0][0], 3), rows[0][1])
+        if rows[0][0] > worst_v:
+            worst_b, worst_v = b, rows[0][0]
+    pre, orows = GT.op_detail(sd0, batch, worst_b)
+    for i, g64, en, ec, eg, canc in orows:
+        assert abs(en) <= 2.0 * max(abs(ec), abs(eg), 1e-6 * abs(g64)), (pre, i, g64, en, ec, eg)
