@@ -400,9 +400,19 @@ def train_leg(device, B, steps, warmup):
         opt.step()
 
     ms, host = timed_calls(step, steps, warmup)
+    # host_us_per_step above is the host's time per step in a back-to-back run,
+    # which includes waiting for a full launch queue when the device is behind;
+    # the cost of issuing one step is its host time from an idle queue
+    issue = []
+    for _ in range(7):
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        step()
+        issue.append((time.perf_counter() - h0) * 1e6)
+    torch.cuda.synchronize()
     out = {"workload": f"3DPW-shape synthetic T=40 V=23, B={B}: forward pair + 2 mpjpe + backward + Adam (fp32)",
            "value": round(B / ms * 1e3, 2), "unit": "train seq/s", "ms_per_step": round(ms, 4),
-           "host_us_per_step": round(host, 2)}
+           "host_us_per_step": round(host, 2), "host_issue_us_per_step": round(sorted(issue)[3], 2)}
     # the same step captured as one HIP graph (engine/graphed.py; what
     # PredictionEngine runs with learn.graph): capturable Adam, tensor lr
     from engine.graphed import GraphedStep

@@ -233,6 +233,42 @@ __host__ __device__ constexpr inline int hl_range_shift(int e) { return e - 14 <
 //   (i = lane&15, kg = lane>>4, zero outside).
 __host__ __device__ constexpr inline int hl_rm_nsf(int K) { return K % 32 > 16 ? K / 32 + 1 : K / 32; }
 __host__ __device__ constexpr inline int hl_rm_tail(int K) { return K % 32 != 0 && K % 32 <= 16 ? 1 : 0; }
+__host__ __device__ constexpr inline int hl_rm_kp(int K) { return 32 * hl_rm_nsf(K) + 16 * hl_rm_tail(K); }
+
+// Row placement of the E / F arrays of the tanh GEMMs (k_adj_hl, phases 1 and
+// 3 of k_temporal_fused): row r starts at float r * SE + 4 * (((r >> SH) & MSK)
+// * MUL).  A lane of the tanh fragments reads 16 bytes of row pr (E) and qr
+// (F) at k = 32 s + 8 kg (+ 4); in the slot order of the planes the 16 lanes
+// of one ds_read_b128 bank group read rows whose plain-stride starts collide
+// on the 64 banks (2-3 extra LDS cycles per read).  The offsets, chosen per
+// shape by a bank model of the access (the guide's ds_read_b128 lane groups),
+// spread them; rows stay disjoint (SE >= KP + 4 MSK MUL) and 16-byte aligned.
+template <int SE_, int SH = 0, int MSK = 0, int MUL = 0>
+struct EfRows {
+  static constexpr int SE = SE_;
+  __host__ __device__ static constexpr int row(int r) { return r * SE + 4 * (((r >> SH) & MSK) * MUL); }
+  __host__ __device__ static constexpr int floats(int nrows) { return row(nrows - 1) + SE; }
+};
+// TEMPORAL: rows = frames (NA = T slots, K = 2V); spatial: rows = joints (NA =
+// V, K = 2T).  Modelled extra LDS cycles per tile set (E and F reads) in the
+// comments: plain KP + 4 stride -> this placement.
+#ifndef DSTD_EF_PLAIN
+template <bool TEMPORAL, int NA, int K>
+struct EfPick {
+  using type = EfRows<hl_rm_kp(K) + 4>;
+};
+template <> struct EfPick<true, 35, 44> { using type = EfRows<72, 0, 1, 5>; };    // H36M temporal: 1044 -> 484
+template <> struct EfPick<false, 22, 70> { using type = EfRows<88, 0, 1, 1>; };   // H36M spatial: 660 -> 132
+template <> struct EfPick<true, 40, 46> { using type = EfRows<56, 0, 1, 1>; };    // 3DPW temporal: 1200 -> 800
+template <> struct EfPick<false, 23, 80> { using type = EfRows<88, 0, 1, 1>; };   // 3DPW spatial: 692 -> 140
+template <> struct EfPick<true, 35, 50> { using type = EfRows<72, 0, 1, 1>; };    // CMU temporal: 1808 -> 272
+template <> struct EfPick<false, 25, 70> { using type = EfRows<112, 3, 1, 1>; };  // CMU spatial: 800 -> 200
+#else  // (A/B build: the round-4 stride everywhere)
+template <bool TEMPORAL, int NA, int K>
+struct EfPick {
+  using type = EfRows<hl_rm_kp(K) + 4>;
+};
+#endif
 enum HLJobKind { HLJ_CONV = 0, HLJ_PQ = 1, HLJ_RM = 2 };
 struct HLJob {
   int kind;

@@ -1370,18 +1370,19 @@ __device__ __forceinline__ void tanh_run(const float* ep, const float* fq, float
 // k = 32s + 8kg + e (NS full 16x16x32 K-steps) and, with TAIL, k = 32 NS + 4kg
 // + e (one 16x16x16 step), split into hi / lo.  El / Fl: the [p][k] rows of
 // tanh_run; pr / qr: this lane's rows.
-template <bool SEP, int NS, int TAIL, int SE>
-__device__ __forceinline__ void tanh_frags(const float* El, const float* Fl, int pr, int qr, int kg, f16x8 (&bh)[NS],
+template <bool SEP, int NS, int TAIL>
+__device__ __forceinline__ void tanh_frags(const float* El, const float* Fl, int pb, int qb, int kg, f16x8 (&bh)[NS],
                                            f16x8 (&bo)[NS], f16x4& th, f16x4& to) {
+  // pb / qb: the lane's E / F row starts (EfRows::row of its rows)
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     float tv[8];
-    tanh_run<SEP, 8>(El + pr * SE + 32 * s + 8 * kg, Fl + qr * SE + 32 * s + 8 * kg, tv);
+    tanh_run<SEP, 8>(El + pb + 32 * s + 8 * kg, Fl + qb + 32 * s + 8 * kg, tv);
     split8(make_float4(tv[0], tv[1], tv[2], tv[3]), make_float4(tv[4], tv[5], tv[6], tv[7]), bh[s], bo[s]);
   }
   if constexpr (TAIL) {
     float tv[8];
-    tanh_run<SEP, 4>(El + pr * SE + 32 * NS + 4 * kg, Fl + qr * SE + 32 * NS + 4 * kg, tv);
+    tanh_run<SEP, 4>(El + pb + 32 * NS + 4 * kg, Fl + qb + 32 * NS + 4 * kg, tv);
     uint2 hi, lo;
     split4(make_float4(tv[0], tv[1], tv[2], tv[3]), hi, lo);
     th = __builtin_bit_cast(f16x4, hi);
@@ -1440,7 +1441,8 @@ struct AdjHLGeom {
   static constexpr int NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL;
   static constexpr int RT = cdiv(NROW, 16), KH = K / 2;
   static constexpr int WIMG = RT * (NS * 2 * 64 + TAIL * 64);  // uint4 of the HLJ_RM image
-  static constexpr int SE = KP + 4;  // LDS row stride of E / F (16-byte aligned, rows spread over banks)
+  using EF = typename EfPick<MODE == 1, NA, K>::type;  // E / F row placement
+  static constexpr int SE = EF::SE;
   using SM = SlotMap<NA, MODE == 0>;
   static constexpr int SL = SM::SL, NCOL = NA * SL, NCT = cdiv(NCOL, 16);
   // column chunks (one workgroup each) per (sample, graph) at full batch;
@@ -1462,12 +1464,13 @@ template <int MODE, int NROW, int K, int NA>
 __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(AdjHLArgs a) {
   using Gm = AdjHLGeom<MODE, NROW, K, NA>;
   using SM = typename Gm::SM;
-  constexpr int RT = Gm::RT, NS = Gm::NS, KP = Gm::KP, KH = Gm::KH, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
+  constexpr int RT = Gm::RT, NS = Gm::NS, KP = Gm::KP, KH = Gm::KH, SL = Gm::SL, NCOL = Gm::NCOL;
   constexpr int AW = Gm::AW, AT = Gm::AT, TAIL = Gm::TAIL, WIMG = Gm::WIMG;
   constexpr int OS = Gm::OS, T = Gm::T, V = Gm::V;
   constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
-  __shared__ float El[(NA + 1) * SE];
-  __shared__ float Fl[(NA + 1) * SE];
+  using EF = typename Gm::EF;
+  __shared__ float El[EF::floats(NA + 1)];
+  __shared__ float Fl[EF::floats(NA + 1)];
   __shared__ uint4 wl[WIMG];
   __shared__ float asl[NA * NA + 1];
   __shared__ float bsl[RT * 16];
@@ -1535,12 +1538,12 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   // padding: k in [K, KP) and the row p = q = NA: E = F = 1 (tanh 0)
   for (int i = tid; i < (NA + 1) * (KP - K); i += AT) {
     const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-    El[r * SE + k] = 1.f;
-    Fl[r * SE + k] = 1.f;
+    El[EF::row(r) + k] = 1.f;
+    Fl[EF::row(r) + k] = 1.f;
   }
   for (int i = tid; i < K; i += AT) {
-    El[NA * SE + i] = 1.f;
-    Fl[NA * SE + i] = 1.f;
+    El[EF::row(NA) + i] = 1.f;
+    Fl[EF::row(NA) + i] = 1.f;
   }
   int bad = 0;
 #pragma unroll
@@ -1551,10 +1554,10 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       const int pr = MODE == 0 ? v : t, ki = MODE == 0 ? t : v;
       const float ep0 = C2 * q4[it].x, ep1 = C2 * q4[it].y, eq0 = -C2 * q4[it].z, eq1 = -C2 * q4[it].w;
       bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
-      El[pr * SE + ki] = __builtin_amdgcn_exp2f(ep0);
-      El[pr * SE + KH + ki] = __builtin_amdgcn_exp2f(ep1);
-      Fl[pr * SE + ki] = __builtin_amdgcn_exp2f(eq0);
-      Fl[pr * SE + KH + ki] = __builtin_amdgcn_exp2f(eq1);
+      El[EF::row(pr) + ki] = __builtin_amdgcn_exp2f(ep0);
+      El[EF::row(pr) + KH + ki] = __builtin_amdgcn_exp2f(ep1);
+      Fl[EF::row(pr) + ki] = __builtin_amdgcn_exp2f(eq0);
+      Fl[EF::row(pr) + KH + ki] = __builtin_amdgcn_exp2f(eq1);
     }
   }
 #pragma unroll
@@ -1574,20 +1577,20 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       if (i < T * V) {
         const int t = MODE == 0 ? i % T : i / V, v = MODE == 0 ? i / T : i % V;
         const int pr = MODE == 0 ? v : t, ki = MODE == 0 ? t : v;
-        El[pr * SE + ki] = q4[it].x;
-        El[pr * SE + KH + ki] = q4[it].y;
-        Fl[pr * SE + ki] = q4[it].z;
-        Fl[pr * SE + KH + ki] = q4[it].w;
+        El[EF::row(pr) + ki] = q4[it].x;
+        El[EF::row(pr) + KH + ki] = q4[it].y;
+        Fl[EF::row(pr) + ki] = q4[it].z;
+        Fl[EF::row(pr) + KH + ki] = q4[it].w;
       }
     }
     for (int i = tid; i < (NA + 1) * (KP - K); i += AT) {
       const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-      El[r * SE + k] = 0.f;
-      Fl[r * SE + k] = 0.f;
+      El[EF::row(r) + k] = 0.f;
+      Fl[EF::row(r) + k] = 0.f;
     }
     for (int i = tid; i < K; i += AT) {
-      El[NA * SE + i] = 0.f;
-      Fl[NA * SE + i] = 0.f;
+      El[EF::row(NA) + i] = 0.f;
+      Fl[EF::row(NA) + i] = 0.f;
     }
     __syncthreads();
   }
@@ -1617,7 +1620,7 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
       const int pr = valid ? pi : NA, qr = col < NCOL ? q : NA;
       f16x8 bh[NS], bo[NS];
       f16x4 th, to;
-      tanh_frags<SEP, NS, TAIL, SE>(El, Fl, pr, qr, kg, bh, bo, th, to);
+      tanh_frags<SEP, NS, TAIL>(El, Fl, EF::row(pr), EF::row(qr), kg, bh, bo, th, to);
       f32x4 acc[RT];
       rm_mfma<RT, NS, TAIL>(wl, lane, bh, bo, th, to, acc);
       // ---- epilogue: alpha * (acc + b) + Astat, 0 on padding slots; staged
@@ -1695,7 +1698,9 @@ constexpr int kLdsBudget = 160 * 1024;
 template <int T, int V, int EPI, int C>
 struct TFusedGeom {
   using SM = SlotMap<T, false>;
-  static constexpr int K = 2 * V, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL, SE = KP + 4;
+  static constexpr int K = 2 * V, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL;
+  using EF = typename EfPick<true, T, K>::type;  // E / F row placement
+  static constexpr int SE = EF::SE, EFN = EF::floats(T + 1);  // floats per E (F) array
   static constexpr int SL = SM::SL, NCOL = T * SL, NCTC = cdiv(NCOL, 16);
   // halves per joint in LDS: two planes + 8 (a joint 4 rows down lands on
   // other banks), the 8 kept zero: the B fragment of a padding slot (ZPAD)
@@ -1706,7 +1711,7 @@ struct TFusedGeom {
   // per-column tables (Astat and alpha in plane slot order, ASQ), conv_rm bias
   static constexpr int ASQ = NCTC * 16;
   static constexpr size_t p1_bytes(int rtc) {
-    return 2 * (size_t)(T + 1) * SE * 4 + (size_t)rtc * (NS * 2 * 64 + TAIL * 64) * 16 + (size_t)2 * ASQ * 4 +
+    return 2 * (size_t)EFN * 4 + (size_t)rtc * (NS * 2 * 64 + TAIL * 64) * 16 + (size_t)2 * ASQ * 4 +
            (size_t)rtc * 16 * 4;
   }
   static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
@@ -1739,32 +1744,35 @@ struct TemporalFusedArgs {
 template <int T, int V>
 struct SAdjGeom {
   using SM = SlotMap<V, true>;
-  static constexpr int K = 2 * T, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL, SE = KP + 4;
+  static constexpr int K = 2 * T, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL;
+  using EF = typename EfPick<false, V, K>::type;  // E / F row placement
+  static constexpr int SE = EF::SE, EFN = EF::floats(V + 1);  // floats per E (F) array
   static constexpr int SL = SM::SL, NCOL = V * SL, NCTC = cdiv(NCOL, 16), RT = cdiv(T, 16), FULL = NS * 2 * 64;
   static constexpr int WIMG = RT * (FULL + TAIL * 64);  // uint4 of one graph's HLJ_RM image
   static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
-  static constexpr size_t EF = al16(2 * (size_t)(V + 1) * SE * 4);  // one graph's E rows then F rows
+  static constexpr size_t EFB = al16(2 * (size_t)EFN * 4);  // one graph's E rows then F rows
   // one graph's epilogue tables in plane slot order (as phase 1's asq / alq):
   // 2^-sa Astat[pi][q] then 2^-sa alpha per column, 0 on padding slots
   static constexpr int ASQ = NCTC * 16;
   static constexpr size_t AS = al16((size_t)2 * ASQ * 4);
   static constexpr size_t WB = (size_t)WIMG * 16;                   // one graph's image
   static constexpr size_t BB = al16((size_t)16 * RT * 4);           // one graph's conv_rm bias (rows padded)
-  static constexpr size_t LDS = 2 * (EF + AS + WB + BB);
+  static constexpr size_t LDS = 2 * (EFB + AS + WB + BB);
 };
 
 template <int T, int V, int NT>
 __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, unsigned char* dsm) {
   using Gm = SAdjGeom<T, V>;
   using SM = typename Gm::SM;
-  constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
+  using EF = typename Gm::EF;
+  constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, EFN = Gm::EFN, SL = Gm::SL, NCOL = Gm::NCOL;
   constexpr int RT = Gm::RT, FULL = Gm::FULL, WIMG = Gm::WIMG, NW = NT / 64, NCTC = Gm::NCTC;
   constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
   // LDS: [E/F g0][E/F g1][Astat g0][Astat g1][image g0][image g1][bias g0][bias g1]
-  auto Elg = [&](int g) { return reinterpret_cast<float*>(dsm + g * Gm::EF); };  // F rows at + (V + 1) * SE
-  auto asg = [&](int g) { return reinterpret_cast<float*>(dsm + 2 * Gm::EF + g * Gm::AS); };  // alq: + ASQ
-  uint4* wl = reinterpret_cast<uint4*>(dsm + 2 * (Gm::EF + Gm::AS));  // both images, graph-major
-  float* bl = reinterpret_cast<float*>(dsm + 2 * (Gm::EF + Gm::AS + Gm::WB));  // [g][16 RT]
+  auto Elg = [&](int g) { return reinterpret_cast<float*>(dsm + g * Gm::EFB); };  // F rows at + EFN
+  auto asg = [&](int g) { return reinterpret_cast<float*>(dsm + 2 * Gm::EFB + g * Gm::AS); };  // alq: + ASQ
+  uint4* wl = reinterpret_cast<uint4*>(dsm + 2 * (Gm::EFB + Gm::AS));  // both images, graph-major
+  float* bl = reinterpret_cast<float*>(dsm + 2 * (Gm::EFB + Gm::AS + Gm::WB));  // [g][16 RT]
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, cl = lane & 15;
 
@@ -1819,15 +1827,15 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
   if (tid < 2 * 16 * RT) bl[tid] = bv;
   auto ef_pad = [&](int g, float val) __attribute__((always_inline)) {  // padding k and the row p = q = V: tanh 0
     float* El = Elg(g);
-    float* Fl = El + (V + 1) * SE;
+    float* Fl = El + EFN;
     for (int i = tid; i < (V + 1) * (KP - K); i += NT) {
       const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-      El[r * SE + k] = val;
-      Fl[r * SE + k] = val;
+      El[EF::row(r) + k] = val;
+      Fl[EF::row(r) + k] = val;
     }
     for (int i = tid; i < K; i += NT) {
-      El[V * SE + i] = val;
-      Fl[V * SE + i] = val;
+      El[EF::row(V) + i] = val;
+      Fl[EF::row(V) + i] = val;
     }
   };
   ef_pad(0, 1.f);
@@ -1836,7 +1844,7 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     float* El = Elg(g);
-    float* Fl = El + (V + 1) * SE;
+    float* Fl = El + EFN;
 #pragma unroll
     for (int it = 0; it < NPQ; ++it) {
       const int i = tid + it * NT;
@@ -1844,10 +1852,10 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
         const int t = i % T, v = i / T;
         const float ep0 = C2 * q4[g][it].x, ep1 = C2 * q4[g][it].y, eq0 = -C2 * q4[g][it].z, eq1 = -C2 * q4[g][it].w;
         bad[g] |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
-        El[v * SE + t] = __builtin_amdgcn_exp2f(ep0);
-        El[v * SE + T + t] = __builtin_amdgcn_exp2f(ep1);
-        Fl[v * SE + t] = __builtin_amdgcn_exp2f(eq0);
-        Fl[v * SE + T + t] = __builtin_amdgcn_exp2f(eq1);
+        El[EF::row(v) + t] = __builtin_amdgcn_exp2f(ep0);
+        El[EF::row(v) + T + t] = __builtin_amdgcn_exp2f(ep1);
+        Fl[EF::row(v) + t] = __builtin_amdgcn_exp2f(eq0);
+        Fl[EF::row(v) + T + t] = __builtin_amdgcn_exp2f(eq1);
       }
     }
   }
@@ -1859,14 +1867,14 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
       if (g ? sep1 : sep0) continue;
       ef_pad(g, 0.f);
       float* El = Elg(g);
-      float* Fl = El + (V + 1) * SE;
+      float* Fl = El + EFN;
       for (int i = tid; i < T * V; i += NT) {
         const int t = i % T, v = i / T;
         const float4 p4 = pq_at(g, i);
-        El[v * SE + t] = p4.x;
-        El[v * SE + T + t] = p4.y;
-        Fl[v * SE + t] = p4.z;
-        Fl[v * SE + T + t] = p4.w;
+        El[EF::row(v) + t] = p4.x;
+        El[EF::row(v) + T + t] = p4.y;
+        Fl[EF::row(v) + t] = p4.z;
+        Fl[EF::row(v) + T + t] = p4.w;
       }
     }
     __syncthreads();
@@ -1904,7 +1912,7 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
       }
       const float inv = g ? inv1 : inv0;
       const float* El = Elg(g);
-      const float* Fl = El + (V + 1) * SE;
+      const float* Fl = El + EFN;
       const float* as = asg(g);
       const auto ro = rsrc(j.out + (size_t)n * j.out_sN + (size_t)g * j.out_sG, 2u * T * 2 * NCOL);
       // this lane's A-operand row = column ct * 16 + cl of the planes
@@ -1913,8 +1921,9 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
       const bool va = col < NCOL && pa < V;
       f16x8 bh[NS], bo[NS];
       f16x4 th, to;
-      if (g ? sep1 : sep0) tanh_frags<true, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
-      else tanh_frags<false, NS, TAIL, SE>(El, Fl, va ? pa : V, col < NCOL ? qa : V, kg, bh, bo, th, to);
+      const int pb = EF::row(va ? pa : V), qb = EF::row(col < NCOL ? qa : V);
+      if (g ? sep1 : sep0) tanh_frags<true, NS, TAIL>(El, Fl, pb, qb, kg, bh, bo, th, to);
+      else tanh_frags<false, NS, TAIL>(El, Fl, pb, qb, kg, bh, bo, th, to);
       // the accumulator's 4 columns colb .. colb + 3 (one joint q, slots slot0 ..)
       const int colb = ct * 16 + 4 * kg;
       const float4 as4 = ld4(as + colb), al4 = ld4(as + Gm::ASQ + colb);
@@ -1968,7 +1977,8 @@ template <int T, int V, int EPI, int C>
 __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_waves_per_eu((tf_waves<T, V>() / 4), (tf_waves<T, V>() / 4)))) void k_temporal_fused(TemporalFusedArgs fa) {
   using Gm = TFusedGeom<T, V, EPI, C>;
   using SM = typename Gm::SM;
-  constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SE = Gm::SE, SL = Gm::SL, NCOL = Gm::NCOL;
+  using EF = typename Gm::EF;
+  constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SL = Gm::SL, NCOL = Gm::NCOL;
   constexpr int RC = Gm::RC, RTC = Gm::RTC, PJ = Gm::PJ, WIMG = Gm::WIMG, NW = tf_waves<T, V>(), NT = 64 * NW;
   constexpr int NUT = cdiv(T, 16);  // u tiles of the GC
   constexpr float C2 = 2.8853900817779268f;       // 2*log2(e)
@@ -1978,8 +1988,8 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   _Float16* planes = reinterpret_cast<_Float16*>(dsm);
   unsigned char* un = dsm + Gm::PLANES;  // phase-1 scratch / phase-2 stage (union)
   float* El = reinterpret_cast<float*>(un);
-  float* Fl = El + (T + 1) * SE;
-  uint4* wl = reinterpret_cast<uint4*>(Fl + (T + 1) * SE);
+  float* Fl = El + Gm::EFN;
+  uint4* wl = reinterpret_cast<uint4*>(Fl + Gm::EFN);
   // plane column col = q * SL + slot (q the output frame, slot <-> input
   // frame pi = slot_idx(slot)): asq[col] = 2^-sa Astat[pi][q], alq[col] =
   // 2^-sa alpha -- both 0 on padding slots and past the planes
@@ -2005,12 +2015,12 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
       const float* pqb = j.pq + (size_t)n * L.sn + j.p_ch[0];
       for (int i = tid; i < (T + 1) * (KP - K); i += NT) {  // padding k and the row t = T: E = F = 1 (tanh 0)
         const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-        El[r * SE + k] = 1.f;
-        Fl[r * SE + k] = 1.f;
+        El[EF::row(r) + k] = 1.f;
+        Fl[EF::row(r) + k] = 1.f;
       }
       for (int i = tid; i < K; i += NT) {
-        El[T * SE + i] = 1.f;
-        Fl[T * SE + i] = 1.f;
+        El[EF::row(T) + i] = 1.f;
+        Fl[EF::row(T) + i] = 1.f;
       }
       // every global load of the prologue is issued before the first LDS
       // write that needs one (one memory round trip, not one per loop trip)
@@ -2056,10 +2066,10 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
           const int t = i / V, v = i - t * V;
           const float ep0 = C2 * q4[it].x, ep1 = C2 * q4[it].y, eq0 = -C2 * q4[it].z, eq1 = -C2 * q4[it].w;
           bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
-          El[t * SE + v] = __builtin_amdgcn_exp2f(ep0);
-          El[t * SE + V + v] = __builtin_amdgcn_exp2f(ep1);
-          Fl[t * SE + v] = __builtin_amdgcn_exp2f(eq0);
-          Fl[t * SE + V + v] = __builtin_amdgcn_exp2f(eq1);
+          El[EF::row(t) + v] = __builtin_amdgcn_exp2f(ep0);
+          El[EF::row(t) + V + v] = __builtin_amdgcn_exp2f(ep1);
+          Fl[EF::row(t) + v] = __builtin_amdgcn_exp2f(eq0);
+          Fl[EF::row(t) + V + v] = __builtin_amdgcn_exp2f(eq1);
         }
       }
 #pragma unroll
@@ -2086,19 +2096,19 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
         for (int i = tid; i < T * V; i += NT) {
           const int t = i / V, v = i % V;
           const float4 q4 = ld4(pqb + t * L.st + v * L.sv);
-          El[t * SE + v] = q4.x;
-          El[t * SE + V + v] = q4.y;
-          Fl[t * SE + v] = q4.z;
-          Fl[t * SE + V + v] = q4.w;
+          El[EF::row(t) + v] = q4.x;
+          El[EF::row(t) + V + v] = q4.y;
+          Fl[EF::row(t) + v] = q4.z;
+          Fl[EF::row(t) + V + v] = q4.w;
         }
         for (int i = tid; i < (T + 1) * (KP - K); i += NT) {
           const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-          El[r * SE + k] = 0.f;
-          Fl[r * SE + k] = 0.f;
+          El[EF::row(r) + k] = 0.f;
+          Fl[EF::row(r) + k] = 0.f;
         }
         for (int i = tid; i < K; i += NT) {
-          El[T * SE + i] = 0.f;
-          Fl[T * SE + i] = 0.f;
+          El[EF::row(T) + i] = 0.f;
+          Fl[EF::row(T) + i] = 0.f;
         }
         __syncthreads();
       }
@@ -2157,7 +2167,8 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
             const int col = ct * 16 + cl;
             const int qa = col / SL, pa = SM::slot_idx(col - qa * SL);
             const bool va = col < NCOL && pa < T;
-            tanh_frags<SEP, NS, TAIL, SE>(El, Fl, va ? pa : T, col < NCOL ? qa : T, kg, bh[i], bo[i], th[i], to[i]);
+            tanh_frags<SEP, NS, TAIL>(El, Fl, EF::row(va ? pa : T), EF::row(col < NCOL ? qa : T), kg, bh[i], bo[i], th[i],
+                                      to[i]);
             // columns colb .. colb+3 (one frame q, slots slot0 ..): alpha (acc + b) + Astat,
             // 0 on padding slots (both tables hold 0 there)
             colb[i] = ct * 16 + 4 * kg;
@@ -2214,11 +2225,30 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
                                             fmaf(al[i].w, fmaf(acc[i][3], inv, b), as[i].w));
               uint2 hi, lo;
               split4(vv, hi, lo);
+#ifndef DSTD_TF_ST64
+              // lanes kg and kg ^ 1 hold the 8 consecutive slots 8 (kg >> 1) ..
+              // + 7 of one joint: v_permlane16_swap trades the even row's lo
+              // quad for the odd row's hi quad, so the even lane stores the hi
+              // plane's 16 bytes and the odd lane the lo plane's -- one
+              // ds_write_b128 per lane (8-lane groups over 32 banks: the joint
+              // stride PJ puts 8 joints on 8 distinct bank quads) instead of two
+              // ds_write_b64 whose 16-lane groups can reach only 16 of the 32
+              // banks from 16-byte-aligned rows (2-way)
+              const auto sx = __builtin_amdgcn_permlane16_swap(hi.x, lo.x, false, false);
+              const auto sy = __builtin_amdgcn_permlane16_swap(hi.y, lo.y, false, false);
+              const bool odd = kg & 1;
+              const uint4 w4 = odd ? make_uint4(sx[0], sy[0], lo.x, lo.y) : make_uint4(hi.x, hi.y, sx[1], sy[1]);
+              if (jv < nv && colb[i] < NCOL) {
+                _Float16* dst = planes + jv * PJ + q[i] * SL + slot0[i] - (odd ? 4 : 0) + (odd ? T * SL : 0);
+                *reinterpret_cast<uint4*>(dst) = w4;
+              }
+#else  // (A/B build: two 8-byte stores per lane)
               if (jv < nv && colb[i] < NCOL) {
                 _Float16* dst = planes + jv * PJ + q[i] * SL + slot0[i];
                 *reinterpret_cast<uint2*>(dst) = hi;
                 *reinterpret_cast<uint2*>(dst + T * SL) = lo;
               }
+#endif
             }
           }
         }

@@ -1500,6 +1500,8 @@ __device__ __forceinline__ float slice_sum(float v, float* lds, int V, int S) {
   return t;
 }
 
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
 // Rows are visited RB at a time with all RB loads issued before the first
 // use (a row-at-a-time loop pays one memory latency per row, ~8 per chunk at
 // the config-5 batch); the accumulation order is unchanged.
@@ -1704,6 +1706,9 @@ __global__ __launch_bounds__(256) void k_bn_apply_flat(BnFwd a, int Bg, int C, i
 }
 
 // workgroup (c, y) covers samples [ns*y, ns*y + ns) (one group: ns divides B/groups)
+// VEC: T V % 4 == 0 and 16-byte aligned tensors -- the ns planes of channel c
+// as one run of float4 items (the same arithmetic per element)
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, int T, int V, int splits,
                                                          const float* part, int ns) {
   __shared__ float scl[kBnMaxV], shl[kBnMaxV];
@@ -1745,6 +1750,47 @@ __global__ __launch_bounds__(256) void k_bn_apply_merged(BnFwd a, int B, int C, 
   }
   __syncthreads();
   const float w = a.prelu ? *a.prelu : 0.f;
+  if constexpr (VEC) {
+    constexpr int EB = 2;  // float4 items per thread per batch, loads issued first
+    const int tv4 = T * V / 4, tot = ns * tv4;
+    const FastDiv divV(V);
+    for (int i0 = tid; i0 < tot; i0 += EB * 256) {
+      float4 u[EB], r[EB];
+      size_t at[EB];
+      int vv[EB];
+#pragma unroll
+      for (int j = 0; j < EB; ++j) {
+        const int i = min(i0 + j * 256, tot - 1);  // (clamped: loads without branches)
+        const int k = (i >= tv4) + (i >= 2 * tv4) + (i >= 3 * tv4), e = 4 * (i - k * tv4);
+        at[j] = ((size_t)(n + k) * C + c) * T * V + e;
+        vv[j] = e - divV(e) * V;
+        u[j] = ld4(a.x + at[j]);
+        if (a.x2) {
+          const float4 u2 = ld4(a.x2 + at[j]);
+          u[j].x += u2.x, u[j].y += u2.y, u[j].z += u2.z, u[j].w += u2.w;
+        }
+        r[j] = a.res ? ld4(a.res + at[j]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < EB; ++j) {
+        if (i0 + j * 256 >= tot) break;
+        const float uu[4] = {u[j].x, u[j].y, u[j].z, u[j].w}, rr[4] = {r[j].x, r[j].y, r[j].z, r[j].w};
+        float zz[4], oo[4];
+        int v = vv[j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float z = fmaf(uu[q], scl[v], shl[v]);
+          if (a.res) z += rr[q];
+          zz[q] = z;
+          oo[q] = a.prelu ? prelu_f(z, w) : z;
+          v = v + 1 == V ? 0 : v + 1;
+        }
+        if (a.prelu) *reinterpret_cast<float4*>(a.zsave + at[j]) = make_float4(zz[0], zz[1], zz[2], zz[3]);
+        *reinterpret_cast<float4*>(a.out + at[j]) = make_float4(oo[0], oo[1], oo[2], oo[3]);
+      }
+    }
+    return;
+  }
 #ifndef DSTD_BN_APPLY_EB
 #define DSTD_BN_APPLY_EB 4
 #endif
@@ -1918,6 +1964,7 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_flat(BnBwd a, int Bg, int 
 // split partials of its V channels (split order), the n == 0 one accumulates
 // dgamma / dbeta (and workgroup (0, 0) the PReLU slope: the partials in the
 // order of the former sum_into pass), then writes du over the sample's plane.
+template <bool VEC>
 __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int C, int T, int V, int splits,
                                                              const float* part, const float* wpart, float* dprelu,
                                                              int ns) {
@@ -1969,6 +2016,52 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply_merged(BnBwd a, int B, int
   __syncthreads();
   const float w = a.prelu ? *a.prelu : 0.f;
   const float inv = 1.f / (a.gsum ? a.gsum[(size_t)a.groups * CV * 2 + grp] : (float)(Bg * T));
+  if constexpr (VEC) {  // (k_bn_apply_merged VEC: float4 items over the ns planes)
+    constexpr int EB = 2;
+    const int tv4 = T * V / 4, tot = ns * tv4;
+    const FastDiv divV(V);
+    for (int i0 = tid; i0 < tot; i0 += EB * 256) {
+      float4 d4[EB], z4[EB], u4[EB], a4[EB];
+      size_t at[EB];
+      int vv[EB];
+#pragma unroll
+      for (int j = 0; j < EB; ++j) {
+        const int i = min(i0 + j * 256, tot - 1);
+        const int k = (i >= tv4) + (i >= 2 * tv4) + (i >= 3 * tv4), e = 4 * (i - k * tv4);
+        at[j] = ((size_t)(n + k) * C + c) * T * V + e;
+        vv[j] = e - divV(e) * V;
+        d4[j] = ld4(a.dout + at[j]);
+        z4[j] = a.prelu ? ld4(a.zsave + at[j]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        u4[j] = ld4(a.x + at[j]);
+        if (a.x2) {
+          const float4 u2 = ld4(a.x2 + at[j]);
+          u4[j].x += u2.x, u4[j].y += u2.y, u4[j].z += u2.z, u4[j].w += u2.w;
+        }
+        a4[j] = a.dz_add ? ld4(a.dz_add + at[j]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int j = 0; j < EB; ++j) {
+        if (i0 + j * 256 >= tot) break;
+        const float dv[4] = {d4[j].x, d4[j].y, d4[j].z, d4[j].w}, zv[4] = {z4[j].x, z4[j].y, z4[j].z, z4[j].w};
+        const float uv[4] = {u4[j].x, u4[j].y, u4[j].z, u4[j].w}, av[4] = {a4[j].x, a4[j].y, a4[j].z, a4[j].w};
+        float du[4], dzo[4];
+        int v = vv[j];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float d = dv[q];
+          const float dz = (a.prelu && !(zv[q] > 0.f)) ? w * d : d;
+          const float mean = mnl[v], rstd = rsl[v];
+          const float xh = (uv[q] - mean) * rstd;
+          du[q] = a.use_running ? gml[v] * rstd * dz : gml[v] * rstd * (dz - sdl[v] * inv - xh * sxl[v] * inv);
+          dzo[q] = a.dz_add ? dz + av[q] : dz;
+          v = v + 1 == V ? 0 : v + 1;
+        }
+        *reinterpret_cast<float4*>(a.du + at[j]) = make_float4(du[0], du[1], du[2], du[3]);
+        if (a.dz_out) *reinterpret_cast<float4*>(a.dz_out + at[j]) = make_float4(dzo[0], dzo[1], dzo[2], dzo[3]);
+      }
+    }
+    return;
+  }
   constexpr int EB = 4;  // elements per thread per batch, loads issued first
   for (int k = 0; k < ns; ++k)
   for (int e0 = tid; e0 < T * V; e0 += EB * 256) {
@@ -2586,6 +2679,11 @@ bool bn_sep(long long total) {
   return total >= (1LL << 24);
 #endif
 }
+#ifndef DSTD_BN_NOVEC  // (A/B builds: the scalar element loops)
+constexpr bool kBnVec = true;
+#else
+constexpr bool kBnVec = false;
+#endif
 int bn_apply_samples(int Bg, int B, int C) {
 #ifdef DSTD_BN_NS  // (experiments: samples per apply workgroup)
   if (Bg % DSTD_BN_NS == 0) return DSTD_BN_NS;
@@ -2636,7 +2734,10 @@ hipError_t bn_train_fwd(const BnFwd& a, int B, int C, int T, int V, float* scrat
     return hipGetLastError();
   }
   const int ns = bn_apply_samples(B / a.groups, B, C);
-  k_bn_apply_merged<<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, scratch, ns);
+  if (kBnVec && (T * V) % 4 == 0 && al && ns <= 4)
+    k_bn_apply_merged<true><<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, scratch, ns);
+  else
+    k_bn_apply_merged<false><<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, scratch, ns);
   return hipGetLastError();
 }
 
@@ -2659,10 +2760,10 @@ hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scrat
       return collective_failed();
     b.gsum = y.buf;
   }
+  const bool al = ((uintptr_t)a.x | (uintptr_t)a.x2 | (uintptr_t)a.zsave | (uintptr_t)a.dout | (uintptr_t)a.du |
+                   (uintptr_t)a.dz_out | (uintptr_t)a.dz_add) % 16 == 0;
   {
     const long long total = (long long)B * C * T * V;
-    const bool al = ((uintptr_t)a.x | (uintptr_t)a.x2 | (uintptr_t)a.zsave | (uintptr_t)a.dout | (uintptr_t)a.du |
-                     (uintptr_t)a.dz_out | (uintptr_t)a.dz_add) % 16 == 0;
     if (bn_sep(total) && (T * V) % 4 == 0 && al && total < (1LL << 31)) {
       const int cv = C * V;
       float* sx = wpart + (size_t)splits * a.groups * C;
@@ -2675,7 +2776,10 @@ hipError_t bn_train_bwd(const BnBwd& a, int B, int C, int T, int V, float* scrat
     }
   }
   const int ns = bn_apply_samples(B / a.groups, B, C);
-  k_bn_bwd_apply_merged<<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, part, wpart, dprelu, ns);
+  if (kBnVec && (T * V) % 4 == 0 && al && ns <= 4)
+    k_bn_bwd_apply_merged<true><<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, part, wpart, dprelu, ns);
+  else
+    k_bn_bwd_apply_merged<false><<<dim3(C, B / ns), 256, 0, s>>>(b, B, C, T, V, splits, part, wpart, dprelu, ns);
   return hipGetLastError();
 }
 
