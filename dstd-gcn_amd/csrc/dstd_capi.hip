@@ -287,7 +287,8 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int B, int T
   // one workgroup per sample: below one sample per CU the fused kernel leaves
   // CUs idle and the unit-parallel pair (k_adj_hl<1> + k_temporal_hl) wins
   // (B = 16..128: 25-30% faster forward; B = 256: 8% slower, profiles/r03m_small_batch_ab.txt)
-  r.tf = r.t && temporal_fused_supported(T, V) && (B >= hl_device_cus() || (flags & DSTD_FWD_FUSED_TEMPORAL));
+  r.tf = r.t && temporal_fused_supported(T, V) &&
+         ((B >= hl_device_cus() && temporal_fused_default(T, V)) || (flags & DSTD_FWD_FUSED_TEMPORAL));
 #endif
   return r;
 }
@@ -1003,7 +1004,7 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
   // a block's spatial adjacency from the previous block's fused temporal
   // launch (phase 3), which writes the P/Q it is built from
   for (int b = 1; b < NB && !(flags & DSTD_FWD_SEPARATE_ADJ); ++b)
-    if (hls[b].s && hls[b - 1].tf && blk[b - 1]->cout == 64) {
+    if (hls[b].s && hls[b - 1].tf && blk[b - 1]->cout == 64 && temporal_fused_phase3(T, V)) {
       hls[b].s_pre = true;
       tails[b - 1].next_f = fold[b];
       tails[b - 1].next_adj = true;

@@ -240,9 +240,13 @@ __host__ __device__ constexpr inline int hl_rm_kp(int K) { return 32 * hl_rm_nsf
 // * MUL).  A lane of the tanh fragments reads 16 bytes of row pr (E) and qr
 // (F) at k = 32 s + 8 kg (+ 4); in the slot order of the planes the 16 lanes
 // of one ds_read_b128 bank group read rows whose plain-stride starts collide
-// on the 64 banks (2-3 extra LDS cycles per read).  The offsets, chosen per
-// shape by a bank model of the access (the guide's ds_read_b128 lane groups),
-// spread them; rows stay disjoint (SE >= KP + 4 MSK MUL) and 16-byte aligned.
+// on the 64 banks (2-3 extra LDS cycles per read).  -DDSTD_EF_SWIZZLE places
+// the rows by offsets chosen per shape with a bank model of the access (the
+// guide's ds_read_b128 lane groups; rows disjoint and 16-byte aligned): the
+// fused temporal kernel's bank-conflict cycles fell 1.041e6 -> 6.37e5 per
+// launch, bit-identical, but the forward got 0.7% slower at H36M (the row
+// offsets cost VALU in a kernel that is issue-bound, not LDS-bound:
+// profiles/r05h_lds_layout_ab.txt), so the plain stride stays the default.
 template <int SE_, int SH = 0, int MSK = 0, int MUL = 0>
 struct EfRows {
   static constexpr int SE = SE_;
@@ -252,7 +256,7 @@ struct EfRows {
 // TEMPORAL: rows = frames (NA = T slots, K = 2V); spatial: rows = joints (NA =
 // V, K = 2T).  Modelled extra LDS cycles per tile set (E and F reads) in the
 // comments: plain KP + 4 stride -> this placement.
-#ifndef DSTD_EF_PLAIN
+#ifdef DSTD_EF_SWIZZLE  // (off: measured slower, DESIGN.md section 4 "LDS bank conflicts")
 template <bool TEMPORAL, int NA, int K>
 struct EfPick {
   using type = EfRows<hl_rm_kp(K) + 4>;
@@ -263,7 +267,7 @@ template <> struct EfPick<true, 40, 46> { using type = EfRows<56, 0, 1, 1>; };  
 template <> struct EfPick<false, 23, 80> { using type = EfRows<88, 0, 1, 1>; };   // 3DPW spatial: 692 -> 140
 template <> struct EfPick<true, 35, 50> { using type = EfRows<72, 0, 1, 1>; };    // CMU temporal: 1808 -> 272
 template <> struct EfPick<false, 25, 70> { using type = EfRows<112, 3, 1, 1>; };  // CMU spatial: 800 -> 200
-#else  // (A/B build: the round-4 stride everywhere)
+#else  // the plain KP + 4 stride
 template <bool TEMPORAL, int NA, int K>
 struct EfPick {
   using type = EfRows<hl_rm_kp(K) + 4>;
@@ -379,5 +383,7 @@ bool temporal_hl_supported(int T, int V);
 // hipErrorNotSupported off its shapes
 hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn, hipStream_t s);
 bool temporal_fused_supported(int T, int V);
+bool temporal_fused_phase3(int T, int V);  // the next block's spatial adjacency in the same launch
+bool temporal_fused_default(int T, int V);  // fused at full batch without DSTD_FWD_FUSED_TEMPORAL
 
 }  // namespace dstd

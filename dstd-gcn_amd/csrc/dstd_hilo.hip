@@ -958,12 +958,16 @@ __device__ __forceinline__ void stage_temporal(const TemporalHLArgs& a, Temporal
 __host__ __device__ constexpr bool tf_res_acc(int T, int V) { return (T == 35 && V == 25) || (T == 40 && V == 23); }
 // PF: the next unit's h rows are loaded during this one (48 VGPRs); without,
 // each unit loads its own rows first (for more waves per SIMD instead)
-template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad, bool PF = true, bool RA = false>
+template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad, bool PF = true, bool RA = false,
+          int NUTC = cdiv(T, 16)>
 __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const TemporalStage<T, EPI, C, VB>& st, int u,
-                                               int uend, int ustep, AdjLoad load_adj) {
+                                               int uend, int ustep, AdjLoad load_adj, int ut0 = 0) {
+  // NUTC / ut0: the u tiles ut0 .. ut0 + NUTC - 1 of each unit (a u chunk of
+  // k_temporal_fused at T = 75; every tile otherwise); load_adj fills
+  // [NUTC] fragments for them
   using SM = SlotMap<T, false>;
   using S = TemporalStage<T, EPI, C, VB>;
-  constexpr int MT = SM::MT, NS = SM::NS, NUT = cdiv(T, 16);
+  constexpr int MT = SM::MT, NS = SM::NS;
   constexpr int KSI = S::KSI, NCT = S::NCT, KSO = S::KSO;
   constexpr bool use_bn = S::use_bn;
   constexpr bool use_res = EPI == TEPI_ENC || EPI == TEPI_OUT;
@@ -987,10 +991,10 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
   for (int m = 0; m < MT; ++m) xoff[m] = 16 * m + cl < T ? (uint32_t)(16 * m + cl) * frame_bytes : OOB;
   // output frame uo = 16ut + cl (OOB past T), channels 4kl .. (C = 64) or the
   // 3 channels on lanes kl == 0 (C = 3)
-  uint32_t uoff[NUT], upq[NUT];
+  uint32_t uoff[NUTC], upq[NUTC];
 #pragma unroll
-  for (int ut = 0; ut < NUT; ++ut) {
-    const int uo = 16 * ut + cl;
+  for (int ut = 0; ut < NUTC; ++ut) {
+    const int uo = 16 * (ut0 + ut) + cl;
     uoff[ut] = uo < T && (C % 4 == 0 || kl == 0) ? (uint32_t)uo * frame_bytes + (C % 4 == 0 ? 16 * kl : 0) : OOB;
     upq[ut] = uo < T && kl < 2 ? (uint32_t)(uo * 8 + 4 * kl) * 4 : OOB;
   }
@@ -1014,7 +1018,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     // Issue order matters: vmcnt retires in order, so every load this unit
     // waits for (adjacency, residual) is issued before the next unit's h-row
     // prefetch, which lands behind them.
-    uint4 bh[LAZY ? 1 : NS][NUT], bo[LAZY ? 1 : NS][NUT];  // adjacency B fragments [K-step][u tile]
+    uint4 bh[LAZY ? 1 : NS][NUTC], bo[LAZY ? 1 : NS][NUTC];  // adjacency B fragments [K-step][u tile]
     if constexpr (!LAZY) load_adj(u, bh, bo);
     __builtin_amdgcn_sched_barrier(0);
     // range shift of the unit's rows (0 unless a half could overflow)
@@ -1042,7 +1046,12 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
       for (int ks = 0; ks < KSI; ++ks) split8(xr[m][ks][0], xr[m][ks][1], xh[m][ks], xo[m][ks]);
 
     // ---- conv (transposed): D[t][c] = sum_k h[t][k] W'[c][k] ----
-    f32x4 D[MT][NCT];
+    // CTO (a u chunk of one tile at T = 75): conv and aggregation run per
+    // output channel tile (below), so only that tile's MT accumulators are
+    // live -- the same MFMA sequence on every accumulator, bit-identical
+    constexpr bool CTO = LAZY && NUTC < cdiv(T, 16);
+    f32x4 D[CTO ? 1 : MT][NCT];
+    if constexpr (!CTO) {
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
@@ -1072,15 +1081,16 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
           for (int r = 0; r < 4; ++r) D[m][ct][r] = fmaf(D[m][ct][r], s, b);
       }
     }
+    }  // !CTO
     // residual of the epilogue: the encoder input (ENC) or the model input's
     // last observed frame (OUT); LAZY (LDS adjacency, no HBM loads to wait
     // for in the aggregation) defers the ENC residual past the aggregation
     // so its 48 registers are not live across it
-    float4 R[use_res ? NCT : 1][use_res ? NUT : 1];
+    float4 R[use_res ? NCT : 1][use_res ? NUTC : 1];
     auto load_res_enc = [&]() {
       const auto rr = rsrc(a.xres + cbase, col_bytes);
 #pragma unroll
-      for (int ut = 0; ut < NUT; ++ut)
+      for (int ut = 0; ut < NUTC; ++ut)
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) R[ct][ut] = bld4(rr, uoff[ut] + 64 * ct);
     };
@@ -1104,15 +1114,15 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
       for (int i = 0; i < C && i < 4; ++i)
         e[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, kl == 0 ? 4 * i : OOB, 0, 0));
 #pragma unroll
-      for (int ut = 0; ut < NUT; ++ut) R[0][ut] = make_float4(e[0], e[1], e[2], e[3]);
+      for (int ut = 0; ut < NUTC; ++ut) R[0][ut] = make_float4(e[0], e[1], e[2], e[3]);
     }
     __builtin_amdgcn_sched_barrier(0);
     // ---- aggregation: O[c][u] = sum_t D[t][c] Adj[v][t][u] ----
-    f32x4 O[NCT][NUT];
+    f32x4 O[NCT][NUTC];
     if constexpr (res_acc) {
       const auto rr = rsrc(a.xres + cbase, col_bytes);
 #pragma unroll
-      for (int ut = 0; ut < NUT; ++ut)
+      for (int ut = 0; ut < NUTC; ++ut)
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) {
           const float4 r4 = bld4(rr, uoff[ut] + 64 * ct);
@@ -1123,16 +1133,56 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-          for (int ut = 0; ut < NUT; ++ut) O[ct][ut] *= dn;
+          for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] *= dn;
       }
     } else {
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = zero4();
+        for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] = zero4();
+    }
+    if constexpr (CTO) {
+      uint4 bhs[NS][NUTC], bos[NS][NUTC];  // every K-step's fragments (one u tile)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) load_adj(u, s, bhs[s], bos[s]);
+      const float sc0 = scl[0];
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) {
+        f32x4 Dc[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) Dc[m] = zero4();
+#pragma unroll
+        for (int ks = 0; ks < KSI; ++ks) {
+          const f16x8 wh = as_h8(wl[((ct * KSI + ks) * 2 + 0) * 64 + lz]);
+          const f16x8 wo = as_h8(wl[((ct * KSI + ks) * 2 + 1) * 64 + lz]);
+#pragma unroll
+          for (int m = 0; m < MT; ++m) Dc[m] = mfma32(xo[m][ks], wh, Dc[m]);
+#pragma unroll
+          for (int m = 0; m < MT; ++m) Dc[m] = mfma32(xh[m][ks], wo, Dc[m]);
+#pragma unroll
+          for (int m = 0; m < MT; ++m) Dc[m] = mfma32(xh[m][ks], wh, Dc[m]);
+        }
+        const float b = bfl[16 * ct + cl] * dnx;
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Dc[m][r] = fmaf(Dc[m][r], sc0, b);
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          f16x8 dh, dl;
+          if (2 * s + 1 < MT) split_acc(Dc[2 * s], Dc[2 * s + 1 < MT ? 2 * s + 1 : 0], dh, dl);
+          else split_acc(Dc[2 * s], dh, dl);
+#pragma unroll
+          for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] = mfma32(dl, as_h8(bhs[s][ut]), O[ct][ut]);
+#pragma unroll
+          for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] = mfma32(dh, as_h8(bos[s][ut]), O[ct][ut]);
+#pragma unroll
+          for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] = mfma32(dh, as_h8(bhs[s][ut]), O[ct][ut]);
+        }
+      }
     }
 #pragma unroll
-    for (int s = 0; s < NS; ++s) {
+    for (int s = 0; s < (CTO ? 0 : NS); ++s) {
       const int sb = LAZY ? 0 : s;
       if constexpr (LAZY) load_adj(u, s, bh[0], bo[0]);
       f16x8 dh[NCT], dl[NCT];
@@ -1144,15 +1194,15 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dl[ct], as_h8(bh[sb][ut]), O[ct][ut]);
+        for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] = mfma32(dl[ct], as_h8(bh[sb][ut]), O[ct][ut]);
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bo[sb][ut]), O[ct][ut]);
+        for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bo[sb][ut]), O[ct][ut]);
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bh[sb][ut]), O[ct][ut]);
+        for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] = mfma32(dh[ct], as_h8(bh[sb][ut]), O[ct][ut]);
     }
     // next unit's h rows (unconditional -- the last unit reloads itself -- so
     // that no branch hides the loads from hipcc's vmcnt bookkeeping)
@@ -1171,11 +1221,11 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) O[ct][ut] *= up;
+        for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] *= up;
     }
     const auto ry = rsrc(a.y + cbase, col_bytes);
 #pragma unroll
-    for (int ut = 0; ut < NUT; ++ut) {
+    for (int ut = 0; ut < NUTC; ++ut) {
 #pragma unroll
       for (int ct = 0; ct < NCT; ++ct) {
         f32x4& o = O[ct][ut];
@@ -1207,51 +1257,62 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     // ---- next block's P_s/Q_s (8 channels) of the output ----
     if (has_pq) {
       // on h_s = 2^-sh h (range shift of the unit's output)
-      float hm = 0.f;
-      if constexpr (use_bn || use_res) {
-        AmaxAcc ha;
+      // (long sequences: one shift per u tile, so that a u chunk of the fused
+      // kernel, which holds one tile, shifts exactly as the whole unit does)
+      constexpr bool PTS = T > 48;
+      constexpr int NSH = PTS ? NUTC : 1;
+      int sh[NSH];
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct)
+      for (int k = 0; k < NSH; ++k) {
+        float hm = 0.f;
+        if constexpr (use_bn || use_res) {
+          AmaxAcc ha;
 #pragma unroll
-          for (int ut = 0; ut < NUT; ++ut) ha.add(O[ct][ut]);
-        hm = ha.get();
-      } else {
+          for (int ct = 0; ct < NCT; ++ct)
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct)
+            for (int ut = 0; ut < NUTC; ++ut)
+              if (!PTS || ut == k) ha.add(O[ct][ut]);
+          hm = ha.get();
+        } else {
 #pragma unroll
-          for (int ut = 0; ut < NUT; ++ut) hm = amax4_mfma(hm, O[ct][ut]);
+          for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+            for (int ut = 0; ut < NUTC; ++ut)
+              if (!PTS || ut == k) hm = amax4_mfma(hm, O[ct][ut]);
+        }
+        sh[k] = hl_range_shift(fexp_bits(wave_max_bits(hm)));
+        if (sh[k]) {
+          const float dn = pow2f(-sh[k]);
+#pragma unroll
+          for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+            for (int ut = 0; ut < NUTC; ++ut)
+              if (!PTS || ut == k) O[ct][ut] *= dn;
+        }
       }
-      const int sh = hl_range_shift(fexp_bits(wave_max_bits(hm)));
-      if (sh) {
-        const float dn = pow2f(-sh);
+      f32x4 acc[NUTC];
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct)
-#pragma unroll
-          for (int ut = 0; ut < NUT; ++ut) O[ct][ut] *= dn;
-      }
-      f32x4 acc[NUT];
-#pragma unroll
-      for (int ut = 0; ut < NUT; ++ut) acc[ut] = zero4();
+      for (int ut = 0; ut < NUTC; ++ut) acc[ut] = zero4();
 #pragma unroll
       for (int ks = 0; ks < KSO; ++ks) {
         const f16x8 qh = as_h8(pql[(ks * 2 + 0) * 64 + lz]), qo = as_h8(pql[(ks * 2 + 1) * 64 + lz]);
-        f16x8 hh[NUT], hl[NUT];
+        f16x8 hh[NUTC], hl[NUTC];
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) {
+        for (int ut = 0; ut < NUTC; ++ut) {
           if (2 * ks + 1 < NCT) split_acc(O[2 * ks][ut], O[2 * ks + 1 < NCT ? 2 * ks + 1 : 0][ut], hh[ut], hl[ut]);
           else split_acc(O[2 * ks][ut], hh[ut], hl[ut]);
         }
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma32(qo, hh[ut], acc[ut]);
+        for (int ut = 0; ut < NUTC; ++ut) acc[ut] = mfma32(qo, hh[ut], acc[ut]);
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma32(qh, hl[ut], acc[ut]);
+        for (int ut = 0; ut < NUTC; ++ut) acc[ut] = mfma32(qh, hl[ut], acc[ut]);
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) acc[ut] = mfma32(qh, hh[ut], acc[ut]);
+        for (int ut = 0; ut < NUTC; ++ut) acc[ut] = mfma32(qh, hh[ut], acc[ut]);
       }
-      const float s = scl[1] * pow2f(sh);
       const auto rp = rsrc(a.pq + (size_t)u * T * 8, T * 32);
 #pragma unroll
-      for (int ut = 0; ut < NUT; ++ut) {
+      for (int ut = 0; ut < NUTC; ++ut) {
+        const float s = scl[1] * pow2f(sh[PTS ? ut : 0]);
         const int b4 = 4 * (kl & 1);
         bst4(rp, upq[ut],
              make_float4(fmaf(acc[ut][0], s, bql[b4]), fmaf(acc[ut][1], s, bql[b4 + 1]), fmaf(acc[ut][2], s, bql[b4 + 2]),
@@ -1700,31 +1761,47 @@ struct TFusedGeom {
   using SM = SlotMap<T, false>;
   static constexpr int K = 2 * V, NS = hl_rm_nsf(K), TAIL = hl_rm_tail(K), KP = 32 * NS + 16 * TAIL;
   using EF = typename EfPick<true, T, K>::type;  // E / F row placement
-  static constexpr int SE = EF::SE, EFN = EF::floats(T + 1);  // floats per E (F) array
-  static constexpr int SL = SM::SL, NCOL = T * SL, NCTC = cdiv(NCOL, 16);
-  // halves per joint in LDS: two planes + 8 (a joint 4 rows down lands on
-  // other banks), the 8 kept zero: the B fragment of a padding slot (ZPAD)
-  static constexpr int PJ = 2 * T * SL + 8, ZPAD = 2 * T * SL;
+  static constexpr int SE = EF::SE, EFE = EF::floats(T + 1);  // floats of the E array (every input frame + pad row)
+  static constexpr int SL = SM::SL, NUT = cdiv(T, 16);
   static constexpr int RTG = cdiv(V, 16);  // row tiles of the whole HLJ_RM image
   static constexpr size_t stage_bytes = sizeof(TemporalStage<T, EPI, C, V>);
-  // phase-1 scratch: E / F rows, the chunk's conv_rm rows, the epilogue's
-  // per-column tables (Astat and alpha in plane slot order, ASQ), conv_rm bias
-  static constexpr int ASQ = NCTC * 16;
-  static constexpr size_t p1_bytes(int rtc) {
-    return 2 * (size_t)EFN * 4 + (size_t)rtc * (NS * 2 * 64 + TAIL * 64) * 16 + (size_t)2 * ASQ * 4 +
-           (size_t)rtc * 16 * 4;
-  }
   static constexpr size_t al16(size_t b) { return (b + 15) & ~size_t(15); }
   static constexpr int jn(int rc) { return rc < V ? rc : V; }  // joints stored per chunk
-  static constexpr size_t total(int rc) {
-    return al16((size_t)jn(rc) * PJ * 2) + al16(p1_bytes(rc / 16) > stage_bytes ? p1_bytes(rc / 16) : stage_bytes);
+  // a chunk's planes hold uf output frames (T: all of them; 16: one u tile)
+  // halves per joint: two planes + 8 (a joint 4 rows down lands on other
+  // banks), the 8 kept zero: the B fragment of a padding slot
+  static constexpr int pj(int uf) { return 2 * uf * SL + 8; }
+  // F rows: the chunk's output frames + the pad row
+  static constexpr int eff(int uf) { return EF::floats((uf == T ? T : uf) + 1); }
+  static constexpr int asq(int uf) { return cdiv(uf * SL, 16) * 16; }
+  // phase-1 scratch: E / F rows, the chunk's conv_rm rows, the epilogue's
+  // per-column tables (Astat and alpha in plane slot order), conv_rm bias
+  static constexpr size_t p1_bytes(int rtc, int uf) {
+    return (size_t)(EFE + eff(uf)) * 4 + (size_t)rtc * (NS * 2 * 64 + TAIL * 64) * 16 + (size_t)2 * asq(uf) * 4 +
+           (size_t)rtc * 16 * 4;
   }
-  // joints per chunk: all of them when the planes fit, else one row tile
-  static constexpr int RC = total(16 * RTG) <= kLdsBudget ? 16 * RTG : 16;
-  static constexpr int RTC = RC / 16, NCHUNK = cdiv(V, RC);
+  static constexpr size_t total(int rc, int uf) {
+    return al16((size_t)jn(rc) * pj(uf) * 2) +
+           al16(p1_bytes(rc / 16, uf) > stage_bytes ? p1_bytes(rc / 16, uf) : stage_bytes);
+  }
+  // chunking: none when every joint's planes fit (H36M); else chunks of one
+  // row tile of joints (CMU, 3DPW: each chunk regenerates the tanh operand,
+  // shared by every joint row); else (T = 75: 528 KB of planes per sample)
+  // every joint but one u tile of 16 output frames per chunk -- the tanh
+  // operand's columns split with no regeneration, each chunk re-running the
+  // units' conv (their K is every input frame) for its u tile's aggregation
+  static constexpr bool FIT = total(16 * RTG, T) <= kLdsBudget;
+  static constexpr bool JCH = !FIT && total(16, T) <= kLdsBudget;
+  static constexpr bool UCH = !FIT && !JCH;
+  static constexpr int UF = UCH ? 16 : T, NUTC = UCH ? 1 : NUT;  // output frames / u tiles per chunk
+  static constexpr int RC = JCH ? 16 : 16 * RTG;
+  static constexpr int RTC = RC / 16, NJCH = cdiv(V, RC), NUCH = UCH ? NUT : 1, NCHUNK = NJCH * NUCH;
+  static constexpr int EFF = eff(UF), NFR = (UCH ? UF : T) + 1;  // F array floats / rows (pad row NFR - 1)
+  static constexpr int NCOL = UF * SL, NCTC = cdiv(NCOL, 16), ASQ = asq(UF);
+  static constexpr int PJ = pj(UF), ZPAD = 2 * UF * SL;
   static constexpr int WIMG = RTC * (NS * 2 * 64 + TAIL * 64);  // uint4 of the chunk's HLJ_RM rows
-  static constexpr size_t PLANES = al16((size_t)jn(RC) * PJ * 2), LDS = total(RC);
-  static_assert(LDS <= kLdsBudget, "planes of one row tile must fit");
+  static constexpr size_t PLANES = al16((size_t)jn(RC) * PJ * 2), LDS = total(RC, UF);
+  static_assert(LDS <= kLdsBudget, "planes of one chunk must fit");
 };
 
 struct TemporalFusedArgs {
@@ -1963,6 +2040,14 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
 #endif
 }
 
+// phase 3 of k_temporal_fused reuses the launch's LDS for the next block's
+// spatial adjacency scratch: only where that fits
+template <int T, int V>
+constexpr bool tf_phase3() {
+  return SAdjGeom<T, V>::LDS <= TFusedGeom<T, V, TEPI_ENC, 64>::LDS && SAdjGeom<T, V>::LDS <= TFusedGeom<T, V, TEPI_IN, 64>::LDS &&
+         SAdjGeom<T, V>::LDS <= TFusedGeom<T, V, TEPI_RAW, 64>::LDS;
+}
+
 // waves per workgroup (one workgroup per CU): 8 = two per SIMD with the
 // next-unit prefetch; 12 = three per SIMD without it (<= 168 VGPRs), which
 // also runs a sample's 22 GC units in two rounds instead of three
@@ -1980,7 +2065,7 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   using EF = typename Gm::EF;
   constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SL = Gm::SL, NCOL = Gm::NCOL;
   constexpr int RC = Gm::RC, RTC = Gm::RTC, PJ = Gm::PJ, WIMG = Gm::WIMG, NW = tf_waves<T, V>(), NT = 64 * NW;
-  constexpr int NUT = cdiv(T, 16);  // u tiles of the GC
+  constexpr int UF = Gm::UF, NUTC = Gm::NUTC, NFR = Gm::NFR;  // frames / u tiles per chunk, F rows
   constexpr float C2 = 2.8853900817779268f;       // 2*log2(e)
   const TemporalHLArgs& a = fa.g;
   const AdjHLArgs& j = fa.j;
@@ -1988,8 +2073,8 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   _Float16* planes = reinterpret_cast<_Float16*>(dsm);
   unsigned char* un = dsm + Gm::PLANES;  // phase-1 scratch / phase-2 stage (union)
   float* El = reinterpret_cast<float*>(un);
-  float* Fl = El + Gm::EFN;
-  uint4* wl = reinterpret_cast<uint4*>(Fl + Gm::EFN);
+  float* Fl = El + Gm::EFE;
+  uint4* wl = reinterpret_cast<uint4*>(Fl + Gm::EFF);
   // plane column col = q * SL + slot (q the output frame, slot <-> input
   // frame pi = slot_idx(slot)): asq[col] = 2^-sa Astat[pi][q], alq[col] =
   // 2^-sa alpha -- both 0 on padding slots and past the planes
@@ -2008,20 +2093,26 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
 
   {
     for (int ch = 0; ch < Gm::NCHUNK; ++ch) {
-      const int v0 = ch * RC, nv = min(RC, V - v0), rt0 = ch * RTC;
+      // joint chunk jc (v0 .. v0 + nv - 1), u chunk uc (output frames u0 .. u0 + UF - 1)
+      const int jc = ch % Gm::NJCH, uc = ch / Gm::NJCH;
+      const int v0 = jc * RC, nv = min(RC, V - v0), rt0 = jc * RTC, u0 = uc * UF;
       if (ch) __syncthreads();  // the previous chunk's phase 2 is done with the planes and the stage
       // ---- phase 1 prologue: P/Q -> E/F rows, the chunk's conv_rm rows, Astat, bias ----
       const PQLayout L = j.pql;
       const float* pqb = j.pq + (size_t)n * L.sn + j.p_ch[0];
-      for (int i = tid; i < (T + 1) * (KP - K); i += NT) {  // padding k and the row t = T: E = F = 1 (tanh 0)
-        const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-        El[EF::row(r) + k] = 1.f;
-        Fl[EF::row(r) + k] = 1.f;
-      }
-      for (int i = tid; i < K; i += NT) {
-        El[EF::row(T) + i] = 1.f;
-        Fl[EF::row(T) + i] = 1.f;
-      }
+      // padding k and the pad rows (E: t = T, F: NFR - 1): E = F = 1 (tanh 0)
+      auto ef_pad = [&](float val) __attribute__((always_inline)) {
+        for (int i = tid; i < (T + 1) * (KP - K); i += NT) {
+          const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
+          El[EF::row(r) + k] = val;
+          if (r < NFR) Fl[EF::row(r) + k] = val;
+        }
+        for (int i = tid; i < K; i += NT) {
+          El[EF::row(T) + i] = val;
+          Fl[EF::row(NFR - 1) + i] = val;
+        }
+      };
+      ef_pad(1.f);
       // every global load of the prologue is issued before the first LDS
       // write that needs one (one memory round trip, not one per loop trip)
       constexpr int FULL = NS * 2 * 64;  // uint4 per row tile (full K-steps)
@@ -2050,9 +2141,11 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
       }
 #pragma unroll
       for (int it = 0; it < NAS; ++it) {
+        // column i of the chunk: output frame u0 + q, slot <-> input frame pi
         const int i = tid + it * NT + oz, q = i / SL, pi = i < NCOL ? SM::slot_idx(i - q * SL) : T;
-        if (pi < T) aok |= 1 << it;
-        av[it] = j.astat[0][pi < T ? pi * T + q : 0];
+        const bool ok = pi < T && u0 + q < T;
+        if (ok) aok |= 1 << it;
+        av[it] = j.astat[0][ok ? pi * T + u0 + q : 0];
       }
       // planes stored as 2^-sa Adj (dstd_hilo.h "range scaling")
       const float dna = pow2f(-hl_range_shift(fexp_bits(__float_as_uint(j.wscale[0][HLS_BOUND]))));
@@ -2068,8 +2161,13 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
           bad |= !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
           El[EF::row(t) + v] = __builtin_amdgcn_exp2f(ep0);
           El[EF::row(t) + V + v] = __builtin_amdgcn_exp2f(ep1);
-          Fl[EF::row(t) + v] = __builtin_amdgcn_exp2f(eq0);
-          Fl[EF::row(t) + V + v] = __builtin_amdgcn_exp2f(eq1);
+          // (F rows: the chunk's output frames; the separable / direct choice
+          // above still looks at every frame, as k_adj_hl<1> does)
+          const int tq = t - u0;
+          if (tq >= 0 && tq < UF) {
+            Fl[EF::row(tq) + v] = __builtin_amdgcn_exp2f(eq0);
+            Fl[EF::row(tq) + V + v] = __builtin_amdgcn_exp2f(eq1);
+          }
         }
       }
 #pragma unroll
@@ -2098,18 +2196,13 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
           const float4 q4 = ld4(pqb + t * L.st + v * L.sv);
           El[EF::row(t) + v] = q4.x;
           El[EF::row(t) + V + v] = q4.y;
-          Fl[EF::row(t) + v] = q4.z;
-          Fl[EF::row(t) + V + v] = q4.w;
+          const int tq = t - u0;
+          if (tq >= 0 && tq < UF) {
+            Fl[EF::row(tq) + v] = q4.z;
+            Fl[EF::row(tq) + V + v] = q4.w;
+          }
         }
-        for (int i = tid; i < (T + 1) * (KP - K); i += NT) {
-          const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
-          El[EF::row(r) + k] = 0.f;
-          Fl[EF::row(r) + k] = 0.f;
-        }
-        for (int i = tid; i < K; i += NT) {
-          El[EF::row(T) + i] = 0.f;
-          Fl[EF::row(T) + i] = 0.f;
-        }
+        ef_pad(0.f);
         __syncthreads();
       }
       if constexpr (C == 64) {
@@ -2132,9 +2225,12 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
 #define DSTD_TF_HOISTW 1  // (A/B r03a: -1..2% per launch at H36M / 3DPW, tie at CMU)
 #endif
       constexpr int TPI = DSTD_TF_TPI;  // column tiles per iteration (independent chains)
+      // (u chunks: the W fragments re-read per tile -- hoisted, their 24
+      // registers are live through the whole chunk loop and phase 2 spills)
+      constexpr bool HW = DSTD_TF_HOISTW && !Gm::UCH;
       // W_rm fragments of the chunk's row tiles (HOISTW: read once, held across tiles)
-      f16x8 wfh[DSTD_TF_HOISTW ? RTC : 1][NS], wfo[DSTD_TF_HOISTW ? RTC : 1][NS];
-      f16x4 wth[DSTD_TF_HOISTW ? RTC : 1], wto[DSTD_TF_HOISTW ? RTC : 1];
+      f16x8 wfh[HW ? RTC : 1][NS], wfo[HW ? RTC : 1][NS];
+      f16x4 wth[HW ? RTC : 1], wto[HW ? RTC : 1];
       auto load_w = [&](int rt, f16x8 (&h)[NS], f16x8 (&o)[NS], f16x4& th4, f16x4& to4) {
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
@@ -2147,7 +2243,7 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
           to4 = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
         }
       };
-      if constexpr (DSTD_TF_HOISTW) {
+      if constexpr (HW) {
 #pragma unroll
         for (int rt = 0; rt < RTC; ++rt) load_w(rt, wfh[rt], wfo[rt], wth[rt], wto[rt]);
       }
@@ -2167,7 +2263,8 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
             const int col = ct * 16 + cl;
             const int qa = col / SL, pa = SM::slot_idx(col - qa * SL);
             const bool va = col < NCOL && pa < T;
-            tanh_frags<SEP, NS, TAIL>(El, Fl, EF::row(va ? pa : T), EF::row(col < NCOL ? qa : T), kg, bh[i], bo[i], th[i],
+            const bool vq = col < NCOL && u0 + qa < T;  // (F rows are chunk-local)
+            tanh_frags<SEP, NS, TAIL>(El, Fl, EF::row(va ? pa : T), EF::row(vq ? qa : NFR - 1), kg, bh[i], bo[i], th[i],
                                       to[i]);
             // columns colb .. colb+3 (one frame q, slots slot0 ..): alpha (acc + b) + Astat,
             // 0 on padding slots (both tables hold 0 there)
@@ -2181,7 +2278,7 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
           for (int rt = 0; rt < RTC; ++rt) {
             f16x8 wh_[NS], wo_[NS];
             f16x4 wth_, wto_;
-            if constexpr (DSTD_TF_HOISTW) {
+            if constexpr (HW) {
 #pragma unroll
               for (int s = 0; s < NS; ++s) {
                 wh_[s] = wfh[rt][s];
@@ -2225,7 +2322,7 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
                                             fmaf(al[i].w, fmaf(acc[i][3], inv, b), as[i].w));
               uint2 hi, lo;
               split4(vv, hi, lo);
-#ifndef DSTD_TF_ST64
+#ifdef DSTD_TF_ST128  // (off: 0.7-1.1% slower forward, profiles/r05h_lds_layout_ab.txt)
               // lanes kg and kg ^ 1 hold the 8 consecutive slots 8 (kg >> 1) ..
               // + 7 of one joint: v_permlane16_swap trades the even row's lo
               // quad for the odd row's hi quad, so the even lane stores the hi
@@ -2239,14 +2336,14 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
               const bool odd = kg & 1;
               const uint4 w4 = odd ? make_uint4(sx[0], sy[0], lo.x, lo.y) : make_uint4(hi.x, hi.y, sx[1], sy[1]);
               if (jv < nv && colb[i] < NCOL) {
-                _Float16* dst = planes + jv * PJ + q[i] * SL + slot0[i] - (odd ? 4 : 0) + (odd ? T * SL : 0);
+                _Float16* dst = planes + jv * PJ + q[i] * SL + slot0[i] - (odd ? 4 : 0) + (odd ? UF * SL : 0);
                 *reinterpret_cast<uint4*>(dst) = w4;
               }
-#else  // (A/B build: two 8-byte stores per lane)
+#else  // two 8-byte stores per lane (2-way bank conflicted, cheaper in VALU)
               if (jv < nv && colb[i] < NCOL) {
                 _Float16* dst = planes + jv * PJ + q[i] * SL + slot0[i];
                 *reinterpret_cast<uint2*>(dst) = hi;
-                *reinterpret_cast<uint2*>(dst + T * SL) = lo;
+                *reinterpret_cast<uint2*>(dst + UF * SL) = lo;
               }
 #endif
             }
@@ -2301,29 +2398,29 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
       // (a lane outside the planes -- frame past T, slot group past ng(s) --
       // reads the joint block's zeroed 16-byte pad instead: no exec-masked
       // read, no select)
-      auto load_adj = [&](int u, int s, uint4 (&bh)[NUT], uint4 (&bo)[NUT]) {
+      auto load_adj = [&](int u, int s, uint4 (&bh)[NUTC], uint4 (&bo)[NUTC]) {
         const _Float16* base = planes + (u - ub) * PJ;
         // (the offsets are lane constants: recomputed per call from an opaque
         // lane index instead of 12 registers held through the unit loop)
         const int clz = cl + opaque_zero();
 #pragma unroll
-        for (int ut = 0; ut < NUT; ++ut) {
-          const int uo = 16 * ut + clz;
-          const bool ok = uo < T && kg < SM::ng(s);
+        for (int ut = 0; ut < NUTC; ++ut) {
+          const int uo = 16 * ut + clz;  // chunk-local output frame
+          const bool ok = u0 + uo < T && uo < UF && kg < SM::ng(s);
           const int off = uo * SL + 8 * (SM::goff(s) + kg);
           bh[ut] = *reinterpret_cast<const uint4*>(base + (ok ? off : Gm::ZPAD));
-          bo[ut] = *reinterpret_cast<const uint4*>(base + (ok ? T * SL + off : Gm::ZPAD));
+          bo[ut] = *reinterpret_cast<const uint4*>(base + (ok ? UF * SL + off : Gm::ZPAD));
         }
       };
 #ifndef DSTD_TF_SKIP_P2  // (timing experiments: phase 1 alone)
-      temporal_units<T, EPI, C, V, true, decltype(load_adj), (NW <= 8), tf_res_acc(T, V)>(a, st, ub + wave, ub + nv, NW,
-                                                                                             load_adj);
+      temporal_units<T, EPI, C, V, true, decltype(load_adj), (NW <= 8 && !Gm::UCH), tf_res_acc(T, V), NUTC>(
+          a, st, ub + wave, ub + nv, NW, load_adj, u0 / 16);
 #endif
     }
   }
-  // ---- phase 3: the next block's spatial adjacency planes of this sample ----
-  if constexpr (C == 64) {
-    static_assert(SAdjGeom<T, V>::LDS <= Gm::LDS, "phase 3 reuses the launch's LDS");
+  // ---- phase 3: the next block's spatial adjacency planes of this sample
+  // (where its scratch fits the launch's LDS: not at T = 75) ----
+  if constexpr (C == 64 && tf_phase3<T, V>()) {
     TLH(3, 2)
     if (fa.sn.out) {
       __syncthreads();  // every unit's P/Q written (one CU: the workgroup-scope fences of the barrier suffice)
@@ -2495,13 +2592,32 @@ hipError_t tfused_tv(const TemporalFusedArgs& a, hipStream_t s) {
   }
 }
 
-bool temporal_fused_supported(int T, int V) { return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23); }
+bool temporal_fused_supported(int T, int V) {
+  return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23) || (T == 75 && V == 22);
+}
+// the schedule's default at full batch: T = 75 runs its u chunks only when
+// asked (DSTD_FWD_FUSED_TEMPORAL) -- measured 8.8% slower per forward than the
+// unfused pair (profiles/r05h_t75_fused_ab.txt)
+bool temporal_fused_default(int T, int V) {
+#ifdef DSTD_TF75_DEFAULT
+  return temporal_fused_supported(T, V);
+#else
+  return temporal_fused_supported(T, V) && T != 75;
+#endif
+}
+bool temporal_fused_phase3(int T, int V) {
+  if (T == 35 && V == 22) return tf_phase3<35, 22>();
+  if (T == 35 && V == 25) return tf_phase3<35, 25>();
+  if (T == 40 && V == 23) return tf_phase3<40, 23>();
+  if (T == 75 && V == 22) return tf_phase3<75, 22>();
+  return false;
+}
 
 hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn, hipStream_t s) {
   if (!temporal_fused_supported(g.T, g.V) || g.V != (int)(j.pql.st / 4) || j.pql.sch != 1 || j.pql.sv != 4 ||
       ((uintptr_t)j.pq & 15))
     return hipErrorNotSupported;
-  if (sn && (g.C != 64 || !g.pq || sn->pq != g.pq || sn->ngroups != 2 || sn->xin || sn->pql.sch != 1 ||
+  if (sn && (!temporal_fused_phase3(g.T, g.V) || g.C != 64 || !g.pq || sn->pq != g.pq || sn->ngroups != 2 || sn->xin || sn->pql.sch != 1 ||
              (sn->pql.st & 3) || (sn->pql.sv & 3) || (sn->pql.sn & 3) || (sn->p_ch[0] & 3) || (sn->p_ch[1] & 3) ||
              !sn->out))
     return hipErrorNotSupported;
@@ -2509,6 +2625,7 @@ hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, co
   if (g.T == 35 && g.V == 22) return tfused_tv<35, 22>(a, s);
   if (g.T == 35 && g.V == 25) return tfused_tv<35, 25>(a, s);
   if (g.T == 40 && g.V == 23) return tfused_tv<40, 23>(a, s);
+  if (g.T == 75 && g.V == 22) return tfused_tv<75, 22>(a, s);
   return hipErrorNotSupported;
 }
 

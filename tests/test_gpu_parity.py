@@ -263,14 +263,16 @@ def test_phase3_spatial_adjacency_bit_identical(tag):
         assert torch.equal(y0, y1), (scale, float((y0 - y1).abs().max()))
 
 
-@pytest.mark.parametrize("tag", ["h36m", "cmu", "3dpw"])
+@pytest.mark.parametrize("tag", ["h36m", "cmu", "3dpw", "h36m75"])
 def test_fused_temporal_schedule_bit_identical(tag):
     """Below one sample per CU the forward runs the unit-parallel temporal pair
     (k_adj_hl<1> + k_temporal_hl); DSTD_FWD_FUSED_TEMPORAL forces the fused
     kernel (and phase 3) at any batch.  Both schedules are the same arithmetic:
     bit-identical at small batches, ragged B, the fixture input and inputs
     x1000 (range-scaled planes) -- so every oracle test of the default
-    schedule covers the fused kernels too."""
+    schedule covers the fused kernels too.  At T=75 the fused kernel runs in
+    u chunks (one u tile of output frames per chunk, the units' conv re-run
+    per chunk) without phase 3."""
     import dstd_native as native
     m, d, _, opts = load_model(tag)
     T = opts["input_time_frame"] + opts["output_time_frame"]
