@@ -500,6 +500,30 @@ class _ModelTrain(torch.autograd.Function):
         return (None, None, dx if need_dx else None, *arena.views())
 
 
+class _ModelTrainPair(torch.autograd.Function):
+    """DSTDGCN.forward_pair's Function: _ModelTrain over the concatenated
+    pair (DSTD_TRAIN_PAIRED) with the two halves as two outputs.  The backward
+    joins their gradients with one copy; slicing one output instead left it to
+    autograd's slice backward -- a zero-filled pair-sized buffer and a copy per
+    half, then their sum (five launches and their host time per step)."""
+
+    @staticmethod
+    def forward(ctx, model, n, x, *params):
+        y = _ModelTrain.forward(ctx, model, True, x, *params)
+        return y[:n], y[n:]
+
+    @staticmethod
+    def backward(ctx, d1, d2):
+        (x,) = ctx.saved_tensors
+        n = x.shape[0] // 2
+        if d1 is None:
+            d1 = x.new_zeros((n,) + tuple(x.shape[1:]))
+        if d2 is None:
+            d2 = x.new_zeros((x.shape[0] - n,) + tuple(x.shape[1:]))
+        # (argument positions: model, n, x, params -- as _ModelTrain's model, paired, x, params)
+        return _ModelTrain.backward(ctx, torch.cat([d1, d2]))
+
+
 class BatchNorm(nn.Module):
     """BN1d over C*V channels of an NCTV tensor (reference :35-50).  Glue only:
     on the hot path every BatchNorm is folded into a kernel epilogue."""
@@ -947,8 +971,7 @@ class DSTDGCN(_NativeModule):
         x = torch.cat([x1, x2]).contiguous()
         native.require_device(x, "x")
         params = self._tree.get(self)[0]
-        y = _ModelTrain.apply(self, True, x, *params)
-        return y[:n], y[n:]
+        return _ModelTrainPair.apply(self, n, x, *params)
 
     def graphed(self, x, frozen=False):
         """The eval forward for inputs shaped like ``x`` captured once into a
