@@ -683,6 +683,10 @@ struct AggArgs {
   int C, A, NN, V, TV, AC, QP, RK, P;
   int vec;  // k_aggc: 16-byte loads / stores (T*V, strides and bases 4-aligned)
   int B;    // k_aggc_bwd: samples (stride of the dD partials)
+  // k_aggc / k_aggc_bwd, spatial: the a's (frames) of one (sample, channel
+  // chunk) split over asplit workgroups of apg frames each (their slab is a
+  // contiguous [apg * V] run of every channel row); 1 / A: one workgroup
+  int asplit, apg;
 };
 constexpr int kAggMaxC = 64, kAggMaxNN = 64;
 
@@ -890,15 +894,19 @@ __global__ __launch_bounds__(kAggcThreads) void k_aggc(AggArgs g) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
   const int C = g.C, NN = g.NN, V = g.V, TV = g.TV, TVP = g.QP, P = g.P, RK = g.RK;
   const int cch = cdiv(C, 16);
-  const int n = blockIdx.x / cch, c0 = (blockIdx.x - n * cch) * 16;
+  const int blk = blockIdx.x / g.asplit, ag = blockIdx.x - blk * g.asplit;
+  const int n = blk / cch, c0 = (blk - n * cch) * 16;
   const int cv = min(16, C - c0);
+  // this workgroup's a's [a_lo, a_hi) and their slab: W floats from sb of every channel row
+  const int a_lo = TEMP ? 0 : ag * g.apg, a_hi = TEMP ? g.A : min(g.A, a_lo + g.apg);
+  const int W = TEMP ? TV : (a_hi - a_lo) * V, sb = TEMP ? 0 : a_lo * V;
   float* S = agg_sm;  // [16][TVP]
   float* Dl = agg_sm + 16 * TVP + wave * RK * P;
-  const float* In = g.X + n * g.xs + (long long)c0 * TV;
-  float* Out = g.O + n * g.os + (long long)c0 * TV;
+  const float* In = g.X + n * g.xs + (long long)c0 * TV + sb;
+  float* Out = g.O + n * g.os + (long long)c0 * TV + sb;
   const int NN2 = NN * NN;
   const FastDiv div_nn(NN);
-  auto off = [&](int a, int i) __attribute__((always_inline)) { return TEMP ? i * V + a : a * V + i; };
+  auto off = [&](int a, int i) __attribute__((always_inline)) { return TEMP ? i * V + a : (a - a_lo) * V + i; };
 
   // first D tile of this wave into registers (its latency overlaps the slab)
   float dv[DR];
@@ -907,51 +915,59 @@ __global__ __launch_bounds__(kAggcThreads) void k_aggc(AggArgs g) {
 #pragma unroll
     for (int r = 0; r < DR; ++r) dv[r] = Da[min(lane + 64 * r, NN2 - 1)];
   };
-  if (wave < g.A) load_d(wave);
-  // the 16 channel rows are contiguous in memory
+  if (a_lo + wave < a_hi) load_d(a_lo + wave);
+  // the 16 channel rows: runs of W floats, TV apart
   if (g.vec) {
     constexpr int U = 8;
-    const int tv4 = TV >> 2, tot4 = cv * tv4;
-    const FastDiv div_tv4(tv4);
+    const int w4 = W >> 2, tv4 = TV >> 2, tot4 = cv * w4;
+    const FastDiv div_w4(w4);
     const f32x4* In4 = reinterpret_cast<const f32x4*>(In);
     for (int e0 = tid; e0 < tot4; e0 += U * kAggcThreads) {
       f32x4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = In4[min(e0 + u * kAggcThreads, tot4 - 1)];  // (clamped: no branch)
+      for (int u = 0; u < U; ++u) {  // (clamped: no branch)
+        const int e = min(e0 + u * kAggcThreads, tot4 - 1);
+        const int c = div_w4(e);
+        v[u] = In4[c * tv4 + e - c * w4];
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {  // (a clamped element is rewritten with its own value)
         const int e = min(e0 + u * kAggcThreads, tot4 - 1);
-        const int c = div_tv4(e), q = e - c * tv4;
+        const int c = div_w4(e), q = e - c * w4;
         *reinterpret_cast<f32x4*>(S + c * TVP + 4 * q) = v[u];
       }
     }
   } else {
     constexpr int U = 16;
-    const int tot = cv * TV;
-    const FastDiv div_tv(TV);
+    const int tot = cv * W;
+    const FastDiv div_w(W);
     for (int e0 = tid; e0 < tot; e0 += U * kAggcThreads) {
       float v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = In[min(e0 + u * kAggcThreads, tot - 1)];
+      for (int u = 0; u < U; ++u) {
+        const int e = min(e0 + u * kAggcThreads, tot - 1);
+        const int c = div_w(e);
+        v[u] = In[c * TV + e - c * W];
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = min(e0 + u * kAggcThreads, tot - 1);
-        const int c = div_tv(e);
-        S[c * TVP + e - c * TV] = v[u];
+        const int c = div_w(e);
+        S[c * TVP + e - c * W] = v[u];
       }
     }
   }
   for (int e = lane; e < (RK - NN) * P; e += 64) Dl[NN * P + e] = 0.f;  // K-tail rows
   __syncthreads();
 
-  for (int a = wave; a < g.A; a += NW) {
+  for (int a = a_lo + wave; a < a_hi; a += NW) {
 #pragma unroll
     for (int r = 0; r < DR; ++r) {  // D[a] -> Dl[i][j] (fwd) / Dl[j][i] (dF)
       const int e = min(lane + 64 * r, NN2 - 1);
       const int i = div_nn(e), j = e - i * NN;
       Dl[TRANS ? j * P + i : i * P + j] = dv[r];
     }
-    if (a + NW < g.A) load_d(a + NW);
+    if (a + NW < a_hi) load_d(a + NW);
     __builtin_amdgcn_wave_barrier();
     f32x4 acc[JF];
 #pragma unroll
@@ -982,23 +998,23 @@ __global__ __launch_bounds__(kAggcThreads) void k_aggc(AggArgs g) {
   __syncthreads();
   const bool acc_out = g.beta != 0.f;
   if (g.vec) {
-    const int tv4 = TV >> 2, tot4 = cv * tv4;
-    const FastDiv div_tv4(tv4);
+    const int w4 = W >> 2, tv4 = TV >> 2, tot4 = cv * w4;
+    const FastDiv div_w4(w4);
     f32x4* Out4 = reinterpret_cast<f32x4*>(Out);
     for (int e = tid; e < tot4; e += kAggcThreads) {
-      const int c = div_tv4(e), q = e - c * tv4;
+      const int c = div_w4(e), q = e - c * w4;
       f32x4 v = *reinterpret_cast<const f32x4*>(S + c * TVP + 4 * q);
-      if (acc_out) v += g.beta * Out4[e];
-      Out4[e] = v;
+      if (acc_out) v += g.beta * Out4[c * tv4 + q];
+      Out4[c * tv4 + q] = v;
     }
   } else {
-    const int tot = cv * TV;
-    const FastDiv div_tv(TV);
+    const int tot = cv * W;
+    const FastDiv div_w(W);
     for (int e = tid; e < tot; e += kAggcThreads) {
-      const int c = div_tv(e);
-      float v = S[c * TVP + e - c * TV];
-      if (acc_out) v = fmaf(g.beta, Out[e], v);
-      Out[e] = v;
+      const int c = div_w(e), q = e - c * W;
+      float v = S[c * TVP + q];
+      if (acc_out) v = fmaf(g.beta, Out[c * TV + q], v);
+      Out[c * TV + q] = v;
     }
   }
 }
@@ -1020,17 +1036,21 @@ __global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
   const int C = g.C, NN = g.NN, V = g.V, TV = g.TV, TVP = g.QP, P = g.P, RK = g.RK;
   const int cch = cdiv(C, 16);
-  const int n = blockIdx.x / cch, p = blockIdx.x - n * cch, c0 = p * 16;
+  const int blk = blockIdx.x / g.asplit, ag = blockIdx.x - blk * g.asplit;
+  const int n = blk / cch, p = blk - n * cch, c0 = p * 16;
   const int cv = min(16, C - c0);
+  // this workgroup's a's [a_lo, a_hi) and their slab: W floats from sb of every channel row
+  const int a_lo = TEMP ? 0 : ag * g.apg, a_hi = TEMP ? g.A : min(g.A, a_lo + g.apg);
+  const int W = TEMP ? TV : (a_hi - a_lo) * V, sb = TEMP ? 0 : a_lo * V;
   float* SY = agg_sm;              // [16][TVP] dy, then dF
   float* SF = agg_sm + 16 * TVP;   // [16][TVP] F
   float* Dl = agg_sm + 32 * TVP + wave * RK * P;
-  const float* Yn = g.Y0 + n * g.y0s + (long long)c0 * TV;
-  const float* Fn = g.X + n * g.xs + (long long)c0 * TV;
-  float* Out = g.O + n * g.os + (long long)c0 * TV;
+  const float* Yn = g.Y0 + n * g.y0s + (long long)c0 * TV + sb;
+  const float* Fn = g.X + n * g.xs + (long long)c0 * TV + sb;
+  float* Out = g.O + n * g.os + (long long)c0 * TV + sb;
   const int NN2 = NN * NN;
   const FastDiv div_nn(NN);
-  auto off = [&](int a, int i) __attribute__((always_inline)) { return TEMP ? i * V + a : a * V + i; };
+  auto off = [&](int a, int i) __attribute__((always_inline)) { return TEMP ? i * V + a : (a - a_lo) * V + i; };
 
   float dv[DR];
   auto load_d = [&](int a) __attribute__((always_inline)) {
@@ -1038,11 +1058,11 @@ __global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
 #pragma unroll
     for (int r = 0; r < DR; ++r) dv[r] = Da[min(lane + 64 * r, NN2 - 1)];
   };
-  if (wave < g.A) load_d(wave);
+  if (a_lo + wave < a_hi) load_d(a_lo + wave);
   if (g.vec) {
     constexpr int U = 8;
-    const int tv4 = TV >> 2, tot4 = cv * tv4;
-    const FastDiv div_tv4(tv4);
+    const int w4 = W >> 2, tv4 = TV >> 2, tot4 = cv * w4;
+    const FastDiv div_w4(w4);
     const f32x4* Y4 = reinterpret_cast<const f32x4*>(Yn);
     const f32x4* F4 = reinterpret_cast<const f32x4*>(Fn);
     for (int e0 = tid; e0 < tot4; e0 += U * kAggcbThreads) {
@@ -1050,33 +1070,35 @@ __global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = min(e0 + u * kAggcbThreads, tot4 - 1);
-        vy[u] = Y4[e];
-        vf[u] = F4[e];
+        const int c = div_w4(e), gi = c * tv4 + e - c * w4;
+        vy[u] = Y4[gi];
+        vf[u] = F4[gi];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {  // (a clamped element is rewritten with its own value)
         const int e = min(e0 + u * kAggcbThreads, tot4 - 1);
-        const int c = div_tv4(e), q = c * TVP + 4 * (e - c * tv4);
+        const int c = div_w4(e), q = c * TVP + 4 * (e - c * w4);
         *reinterpret_cast<f32x4*>(SY + q) = vy[u];
         *reinterpret_cast<f32x4*>(SF + q) = vf[u];
       }
     }
   } else {
     constexpr int U = 8;
-    const int tot = cv * TV;
-    const FastDiv div_tv(TV);
+    const int tot = cv * W;
+    const FastDiv div_w(W);
     for (int e0 = tid; e0 < tot; e0 += U * kAggcbThreads) {
       float vy[U], vf[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = min(e0 + u * kAggcbThreads, tot - 1);
-        vy[u] = Yn[e];
-        vf[u] = Fn[e];
+        const int c = div_w(e), gi = c * TV + e - c * W;
+        vy[u] = Yn[gi];
+        vf[u] = Fn[gi];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = min(e0 + u * kAggcbThreads, tot - 1);
-        const int c = div_tv(e), q = c * TVP + e - c * TV;
+        const int c = div_w(e), q = c * TVP + e - c * W;
         SY[q] = vy[u];
         SF[q] = vf[u];
       }
@@ -1086,7 +1108,7 @@ __global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
   __syncthreads();
 
   float* dDp = g.dD + (long long)p * g.B * g.A * NN2;
-  for (int a = wave; a < g.A; a += NW) {
+  for (int a = a_lo + wave; a < a_hi; a += NW) {
     {  // partial dD[a] over the chunk's channels: rows i, columns j, K = c
       f32x4 acc[JF][JF];
 #pragma unroll
@@ -1127,7 +1149,7 @@ __global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
       const int i = div_nn(e), j = e - i * NN;
       Dl[j * P + i] = dv[r];
     }
-    if (a + NW < g.A) load_d(a + NW);
+    if (a + NW < a_hi) load_d(a + NW);
     __builtin_amdgcn_wave_barrier();
     f32x4 acc[JF];
 #pragma unroll
@@ -1157,19 +1179,19 @@ __global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
   }
   __syncthreads();
   if (g.vec) {
-    const int tv4 = TV >> 2, tot4 = cv * tv4;
-    const FastDiv div_tv4(tv4);
+    const int w4 = W >> 2, tv4 = TV >> 2, tot4 = cv * w4;
+    const FastDiv div_w4(w4);
     f32x4* Out4 = reinterpret_cast<f32x4*>(Out);
     for (int e = tid; e < tot4; e += kAggcbThreads) {
-      const int c = div_tv4(e);
-      Out4[e] = *reinterpret_cast<const f32x4*>(SY + c * TVP + 4 * (e - c * tv4));
+      const int c = div_w4(e), q = e - c * w4;
+      Out4[c * tv4 + q] = *reinterpret_cast<const f32x4*>(SY + c * TVP + 4 * q);
     }
   } else {
-    const int tot = cv * TV;
-    const FastDiv div_tv(TV);
+    const int tot = cv * W;
+    const FastDiv div_w(W);
     for (int e = tid; e < tot; e += kAggcbThreads) {
-      const int c = div_tv(e);
-      Out[e] = SY[c * TVP + e - c * TV];
+      const int c = div_w(e), q = e - c * W;
+      Out[c * TV + q] = SY[c * TVP + q];
     }
   }
 }
@@ -2433,6 +2455,37 @@ void agg_go(K kern, dim3 grid, dim3 block, size_t lds, const AggArgs& g, hipStre
 bool agg_ok(const AggArgs& g) {
   return g.C > 0 && g.C <= kAggMaxC && g.NN > 0 && g.NN <= kAggMaxNN && g.A > 0;
 }
+int agg_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+// Channel-chunk kernels, spatial: below DSTD_AGG_SPLIT_WG (sample, chunk)
+// workgroups per CU, the frames of each are split over several workgroups of
+// apg frames (apg * V a multiple of 4: 16-byte runs stay aligned), so the
+// config-5 batch (64 samples x 4 chunks: one workgroup and 4 waves per CU)
+// gets ~DSTD_AGG_SPLIT_WG workgroups per CU (2: B=32 step 4.72 -> 4.67 ms,
+// profiles/r05n_train_anchor_aggsplit.txt); sets g.asplit / g.apg and returns the
+// widest slab (floats per channel row)
+#ifndef DSTD_AGG_SPLIT_WG  // (experiments: 0 = no split)
+#define DSTD_AGG_SPLIT_WG 2
+#endif
+int agg_split(AggArgs& g, int B, bool temporal) {
+  g.asplit = 1;
+  g.apg = g.A;
+  const int wgs = B * cdiv(g.C, 16), cus = agg_cus();
+  if (temporal || DSTD_AGG_SPLIT_WG <= 0 || wgs >= DSTD_AGG_SPLIT_WG * cus) return g.TV;
+  const int m = (g.V % 4 == 0) ? 1 : (g.V % 2 == 0) ? 2 : 4;
+  const int want = std::min(g.A, cdiv(DSTD_AGG_SPLIT_WG * cus, wgs));
+  g.apg = std::min(g.A, rup(cdiv(g.A, want), m));
+  g.asplit = cdiv(g.A, g.apg);
+  return g.apg * g.V;
+}
 // a-chunk kernel: fwd, bwd dD + dF (df) or bwd dD only
 hipError_t agg_launch_a(bool bwd, bool df, AggArgs g, int B, int temporal, hipStream_t s) {
   if (!agg_ok(g)) return hipErrorNotSupported;
@@ -2470,13 +2523,13 @@ hipError_t agg_launch_a(bool bwd, bool df, AggArgs g, int B, int temporal, hipSt
 hipError_t agg_launch_c(bool trans, AggArgs g, int B, int temporal, hipStream_t s) {
   if (!agg_ok(g)) return hipErrorNotSupported;
   agg_tile(g.NN, g.RK, g.P);
-  g.QP = g.TV;
+  g.QP = agg_split(g, B, temporal);
   while ((g.QP & 63) != 4) ++g.QP;
   const size_t lds = sizeof(float) * ((size_t)16 * g.QP + (size_t)(kAggcThreads / 64) * g.RK * g.P);
   if (lds > 160 * 1024) return hipErrorNotSupported;
   g.vec = (g.TV % 4 == 0 && g.xs % 4 == 0 && g.os % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
            ((uintptr_t)g.O & 15) == 0);
-  const dim3 grid(B * cdiv(g.C, 16)), block(kAggcThreads);
+  const dim3 grid(B * cdiv(g.C, 16) * g.asplit), block(kAggcThreads);
   const int jf = cdiv(g.NN, 16);
   auto pick = [&](auto tb, auto rb) {
     constexpr bool T_ = decltype(tb)::value, R_ = decltype(rb)::value;
@@ -2527,13 +2580,13 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
     if (cch > 1) g.dD = dDpart, *nparts = cch;
     g.B = B;
     agg_tile(g.NN, g.RK, g.P);
-    g.QP = g.TV;
+    g.QP = agg_split(g, B, temporal);
     while ((g.QP & 63) != 4) ++g.QP;
     const size_t lds = sizeof(float) * ((size_t)32 * g.QP + (size_t)(kAggcbThreads / 64) * g.RK * g.P);
     if (lds <= 160 * 1024) {
       g.vec = (g.TV % 4 == 0 && g.xs % 4 == 0 && g.os % 4 == 0 && g.y0s % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
                ((uintptr_t)g.O & 15) == 0 && ((uintptr_t)g.Y0 & 15) == 0);
-      const dim3 grid(B * cch), block(kAggcbThreads);
+      const dim3 grid(B * cch * g.asplit), block(kAggcbThreads);
       const int jf = cdiv(g.NN, 16);
       auto pick = [&](auto tb) {
         constexpr bool T_ = decltype(tb)::value;

@@ -6,15 +6,17 @@ loss curve (train_grads.npz).
 Tolerances
   single DSTDGC op        : every output / gradient within 1e-4 of its max |ref|
   DSTDGCB (train-mode BN) : 2e-4 (BN backward subtracts two O(1) means)
-  whole model, one step   : err / noise per tensor, where noise is the larger
-                            fp32 error of two other fp32 implementations (the
-                            reference's g32err and the CPU oracle in fp32) --
-                            the 21-op stack is chaotic in fp32:
-                            median <= 1.5, 90th percentile <= 3; every
-                            tensor above 3x printed and required to be a
-                            global-sum gradient (GLOBAL_SUM: scalars and conv
-                            biases), those within 12x
-                            (scripts/grad_noise.py prints the table)
+  whole model, one step   : err / noise per tensor, where noise is the largest
+                            fp32 error of ten other fp32 runs (the oracle's
+                            fp32 step on the CPU, on the GPU and over 8 sample
+                            orders, plus the reference's g32err where the
+                            fixture holds it) -- the 21-op stack is chaotic in
+                            fp32: every tensor within 4x, median
+                            <= 1.5, 90th percentile <= 2 (fp32_noise /
+                            check_ratios; the per-block bisection behind it:
+                            test_model_step_gradient_tail_is_propagation)
+  eval-mode model backward: the former two-sample criterion (GLOBAL_SUM /
+                            check_tail, below)
   5-step loss curve       : within twice the reference's own fp32 deviation
                             from its fp64 curve
 """
@@ -482,6 +484,16 @@ def test_gradient_sink_paths_agree():
     TOL = 1e-4
     params = [p for p in m.parameters() if p.requires_grad]
     m._dstd_inplace_grads = True  # what engine.PredictionEngine.train opts into
+    # in-place mode: one anchor leaf stands in for the ~300 parameters as the
+    # Function's tensor inputs (x, anchor -- dstdgcn._anchor_of)
+    probe = m(inp.view(B, T, 23, 3))
+    assert len(probe.grad_fn.next_functions) == 2, len(probe.grad_fn.next_functions)
+    del probe
+    m._dstd_inplace_grads = False
+    probe = m(inp.view(B, T, 23, 3))
+    assert len(probe.grad_fn.next_functions) == 1 + len(list(m.parameters()))
+    del probe
+    m._dstd_inplace_grads = True
     step()  # direct: .grad were None
     g_direct = [p.grad.clone() for p in params]
     bases = {p.grad._base.data_ptr() for p in params}
