@@ -793,6 +793,15 @@ __global__ __launch_bounds__(spatial_nt()) __attribute__((amdgpu_waves_per_eu(DS
   __shared__ SpatialStage<V, CIN, COUT> st;
   stage_spatial<V, CIN, COUT, spatial_nt()>(a, st, threadIdx.x);
   __syncthreads();
+  // static VALU-arbitration priority 1 for the younger half (waves 4-7: the
+  // arbitration losers at equal priority; MI355X guide "two waves per SIMD"
+  // item 4, T5 static form): spatial GC -1.8%, forward -0.8% at H36M and
+  // -0.9% at 3DPW, B=32 neutral, bit-identical (profiles/r05o_setprio_ab.txt)
+#ifndef DSTD_SETPRIO_SP  // (0: off)
+#define DSTD_SETPRIO_SP 256
+#endif
+  if (DSTD_SETPRIO_SP > 0 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= DSTD_SETPRIO_SP)
+    __builtin_amdgcn_s_setprio(1);
   const int lane = threadIdx.x & 63, kl = lane >> 4, cl = lane & 15;
   const int T = a.T;
   constexpr uint32_t adj_bytes = 2 * V * SL * 2;  // one (n, g, t) adjacency: 2 planes of V x SL halves
@@ -1337,6 +1346,9 @@ __global__ __launch_bounds__((temporal_nt<T, C>())) __attribute__((amdgpu_waves_
   __shared__ TemporalStage<T, EPI, C, 32> st;
   stage_temporal<T, EPI, C, 32, temporal_nt<T, C>()>(a, st, threadIdx.x);
   __syncthreads();
+#ifdef DSTD_SETPRIO_TH  // (experiment: the younger waves' static priority, as k_spatial_hl)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= DSTD_SETPRIO_TH) __builtin_amdgcn_s_setprio(1);
+#endif
   int uend;
   const int u0 = unit_range(a.B * a.V, uend);
   const int cl = threadIdx.x & 15, kl = (threadIdx.x & 63) >> 4;
@@ -1545,6 +1557,9 @@ __global__ __launch_bounds__((AdjHLGeom<MODE, NROW, K, NA>::AT)) void k_adj_hl(A
   const int n = blockIdx.x / (nch * a.ngroups);
   if (n >= a.B) return;
   TLH(MODE, 0)
+#ifdef DSTD_SETPRIO_ADJ  // (experiment: the younger waves' static priority, as k_spatial_hl)
+  if (__builtin_amdgcn_readfirstlane(tid) >= DSTD_SETPRIO_ADJ) __builtin_amdgcn_s_setprio(1);
+#endif
 
   // ---- prologue: P/Q -> E/F rows, conv_rm fragments, A-stat, bias.  Every
   // global load is issued before the first LDS write (one memory round
@@ -2090,6 +2105,9 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   const int kg = lane >> 4, cl = lane & 15;
   const int n = blockIdx.x;  // one sample per workgroup
   if constexpr (C == 64) { TLH(3, 0) TLH(4, 0) }
+#ifdef DSTD_SETPRIO_TF  // (experiment, r05o: waves 4-11 +0.6%, 8-11 neutral at H36M -- off)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= DSTD_SETPRIO_TF) __builtin_amdgcn_s_setprio(1);
+#endif
 
   {
     for (int ch = 0; ch < Gm::NCHUNK; ++ch) {

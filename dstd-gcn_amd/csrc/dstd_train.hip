@@ -2469,19 +2469,23 @@ int agg_cus() {
 // workgroups per CU, the frames of each are split over several workgroups of
 // apg frames (apg * V a multiple of 4: 16-byte runs stay aligned), so the
 // config-5 batch (64 samples x 4 chunks: one workgroup and 4 waves per CU)
-// gets ~DSTD_AGG_SPLIT_WG workgroups per CU (2: B=32 step 4.72 -> 4.67 ms,
-// profiles/r05n_train_anchor_aggsplit.txt); sets g.asplit / g.apg and returns the
+// gets ~per_cu workgroups per CU (2 each way: B=32 step 4.725 -> 4.671 ms;
+// forward alone 4.698, backward alone 4.683, a forward target of 4: 4.739;
+// profiles/r05q_agg_split_ab.txt); sets g.asplit / g.apg and returns the
 // widest slab (floats per channel row)
-#ifndef DSTD_AGG_SPLIT_WG  // (experiments: 0 = no split)
+#ifndef DSTD_AGG_SPLIT_WG  // forward (k_aggc); experiments: 0 = no split
 #define DSTD_AGG_SPLIT_WG 2
 #endif
-int agg_split(AggArgs& g, int B, bool temporal) {
+#ifndef DSTD_AGGB_SPLIT_WG  // backward (k_aggc_bwd)
+#define DSTD_AGGB_SPLIT_WG 2
+#endif
+int agg_split(AggArgs& g, int B, bool temporal, int per_cu) {
   g.asplit = 1;
   g.apg = g.A;
   const int wgs = B * cdiv(g.C, 16), cus = agg_cus();
-  if (temporal || DSTD_AGG_SPLIT_WG <= 0 || wgs >= DSTD_AGG_SPLIT_WG * cus) return g.TV;
+  if (temporal || per_cu <= 0 || wgs >= per_cu * cus) return g.TV;
   const int m = (g.V % 4 == 0) ? 1 : (g.V % 2 == 0) ? 2 : 4;
-  const int want = std::min(g.A, cdiv(DSTD_AGG_SPLIT_WG * cus, wgs));
+  const int want = std::min(g.A, cdiv(per_cu * cus, wgs));
   g.apg = std::min(g.A, rup(cdiv(g.A, want), m));
   g.asplit = cdiv(g.A, g.apg);
   return g.apg * g.V;
@@ -2523,7 +2527,7 @@ hipError_t agg_launch_a(bool bwd, bool df, AggArgs g, int B, int temporal, hipSt
 hipError_t agg_launch_c(bool trans, AggArgs g, int B, int temporal, hipStream_t s) {
   if (!agg_ok(g)) return hipErrorNotSupported;
   agg_tile(g.NN, g.RK, g.P);
-  g.QP = agg_split(g, B, temporal);
+  g.QP = agg_split(g, B, temporal, DSTD_AGG_SPLIT_WG);
   while ((g.QP & 63) != 4) ++g.QP;
   const size_t lds = sizeof(float) * ((size_t)16 * g.QP + (size_t)(kAggcThreads / 64) * g.RK * g.P);
   if (lds > 160 * 1024) return hipErrorNotSupported;
@@ -2580,7 +2584,7 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
     if (cch > 1) g.dD = dDpart, *nparts = cch;
     g.B = B;
     agg_tile(g.NN, g.RK, g.P);
-    g.QP = agg_split(g, B, temporal);
+    g.QP = agg_split(g, B, temporal, DSTD_AGGB_SPLIT_WG);
     while ((g.QP & 63) != 4) ++g.QP;
     const size_t lds = sizeof(float) * ((size_t)32 * g.QP + (size_t)(kAggcbThreads / 64) * g.RK * g.P);
     if (lds <= 160 * 1024) {
