@@ -100,6 +100,14 @@ size_t adj_bwd_scratch_floats(int B, int A, int NN2);
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
                    float* dalpha, float* scratch, hipStream_t s, int assign_dA = 0, const float* dDpart = nullptr,
                    int nparts = 1, float* dW2 = nullptr, const float* Amul = nullptr);
+// The same in two launches the caller can put on different streams: the
+// part (dE in place, the partials in scratch) and the finish (dA, dbrm,
+// dalpha, dW2 from the partials -- parameter gradients only, which nothing
+// later in the backward reads).
+hipError_t adj_bwd_part(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* scratch,
+                        hipStream_t s, const float* dDpart, int nparts);
+hipError_t adj_bwd_finish(int B, int A, int NN2, float* dA, float* dbrm, float* dalpha, const float* scratch,
+                          hipStream_t s, int assign_dA, float* dW2, const float* Amul);
 
 // Batched strided 2-D copies in one launch: dst[r*dst_ld + c] (+)= src[r*src_ld + c].
 struct CopyJob {

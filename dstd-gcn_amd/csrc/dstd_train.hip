@@ -2645,23 +2645,52 @@ size_t adj_bwd_scratch_floats(int B, int A, int NN2) {
   return (size_t)nch * A * NN2 + 3 * (size_t)nch * A * cdiv(NN2, 256) + 64;  // pal: doubles
 }
 
+#ifndef DSTD_ADJ_SPLIT  // (r04u: B=256 step 27.9 -> 27.0 ms, B=32 neutral; 0 = one column block)
+#define DSTD_ADJ_SPLIT 1
+#endif
+namespace {
+// the partials' layout in scratch (256-byte aligned workspace carve): pal
+// (doubles), then pdA, then pbr
+struct AdjBwdScratch {
+  int nch, nij;
+  double* pal;
+  float *pdA, *pbr;
+  AdjBwdScratch(float* scratch, int B, int A, int NN2)
+      : nch(adj_bwd_chunks(B, A)), nij(DSTD_ADJ_SPLIT ? cdiv(NN2, 256) : 1) {
+    pal = reinterpret_cast<double*>(scratch);
+    pdA = scratch + 2 * (size_t)nch * A * nij;
+    pbr = pdA + (size_t)nch * A * NN2;
+  }
+};
+}  // namespace
+
+hipError_t adj_bwd_part(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* scratch,
+                        hipStream_t s, const float* dDpart, int nparts) {
+  if (nparts > 1 && !dDpart) return hipErrorInvalidValue;
+  if (A > 256) return hipErrorInvalidValue;  // (k_adj_bwd_finish: S threads per row, A * S <= 256)
+  const AdjBwdScratch P(scratch, B, A, NN2);
+  k_adj_bwd_part<<<dim3(A, P.nch, P.nij), 256, 0, s>>>(dD, E, alpha, B, A, NN2, P.nch, P.pdA, P.pbr, P.pal, dDpart,
+                                                       nparts);
+  return hipGetLastError();
+}
+
+hipError_t adj_bwd_finish(int B, int A, int NN2, float* dA, float* dbrm, float* dalpha, const float* scratch,
+                          hipStream_t s, int assign_dA, float* dW2, const float* Amul) {
+  if (dW2 && !Amul) return hipErrorInvalidValue;
+  if (A > 256) return hipErrorInvalidValue;
+  const AdjBwdScratch P(const_cast<float*>(scratch), B, A, NN2);
+  k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(P.pdA, P.pbr, P.pal, A, NN2, P.nch, dA, dbrm, dalpha, assign_dA,
+                                                      dW2, Amul, P.nij);
+  return hipGetLastError();
+}
+
 hipError_t adj_bwd(float* dD, const float* E, const float* alpha, int B, int A, int NN2, float* dA, float* dbrm,
                    float* dalpha, float* scratch, hipStream_t s, int assign_dA, const float* dDpart, int nparts,
                    float* dW2, const float* Amul) {
   if (dW2 && !Amul) return hipErrorInvalidValue;
-  if (nparts > 1 && !dDpart) return hipErrorInvalidValue;
-  if (A > 256) return hipErrorInvalidValue;  // (k_adj_bwd_finish: S threads per row, A * S <= 256)
-#ifndef DSTD_ADJ_SPLIT  // (r04u: B=256 step 27.9 -> 27.0 ms, B=32 neutral; 0 = one column block)
-#define DSTD_ADJ_SPLIT 1
-#endif
-  const int nch = adj_bwd_chunks(B, A), nij = DSTD_ADJ_SPLIT ? cdiv(NN2, 256) : 1;
-  double* pal = reinterpret_cast<double*>(scratch);  // (scratch: 256-byte aligned workspace carve)
-  float* pdA = scratch + 2 * (size_t)nch * A * nij;
-  float* pbr = pdA + (size_t)nch * A * NN2;
-  k_adj_bwd_part<<<dim3(A, nch, nij), 256, 0, s>>>(dD, E, alpha, B, A, NN2, nch, pdA, pbr, pal, dDpart, nparts);
-  k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(pdA, pbr, pal, A, NN2, nch, dA, dbrm, dalpha, assign_dA, dW2,
-                                                      Amul, nij);
-  return hipGetLastError();
+  const hipError_t e = adj_bwd_part(dD, E, alpha, B, A, NN2, scratch, s, dDpart, nparts);
+  if (e != hipSuccess) return e;
+  return adj_bwd_finish(B, A, NN2, dA, dbrm, dalpha, scratch, s, assign_dA, dW2, Amul);
 }
 
 hipError_t copy_jobs(const CopyJobs& js, hipStream_t s) {

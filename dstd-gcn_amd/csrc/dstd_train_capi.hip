@@ -142,8 +142,10 @@ struct OpWs {
   float* dDp;  // channel-chunk partials of dD (agg_bwd), null when one chunk suffices
   // the second dG / dD set and the GEMM scratch of the weight-gradient stream
   // (WgradStream): consecutive ops alternate sets so that an op's weight
-  // gradients can still read its dE / dG while the next op runs
+  // gradients can still read its dE / dG while the next op runs; adjp: the
+  // adjacency backward's partials per set (its finish runs on that stream)
   float *dG2, *dD2, *gs2;
+  float* adjp[2];
 };
 
 // ---------------------------------------------------------------------------
@@ -264,8 +266,9 @@ size_t red_floats(const OpGeom& g) {
 // Sized for the largest of the given op geometries (one workspace serves every
 // op of a block / model in turn).
 void carve_op_ws(Carver& cv, OpWs& w, const std::vector<OpGeom>& gl) {
-  size_t nG = 0, nD = 0, nM = 0, nW = 0, nmn = 0, nred = 0, nDp = 0;
+  size_t nG = 0, nD = 0, nM = 0, nW = 0, nmn = 0, nred = 0, nDp = 0, nadj = 0;
   for (const OpGeom& g : gl) {
+    nadj = std::max(nadj, adj_bwd_scratch_floats(g.B, g.A, g.NN2));
     nG = std::max(nG, (size_t)g.B * g.CG() * g.TV);
     nD = std::max(nD, (size_t)g.B * g.A * g.NN2);
     if (agg_parts(g.cout) > 1) nDp = std::max(nDp, (size_t)agg_parts(g.cout) * g.B * g.A * g.NN2);
@@ -285,6 +288,8 @@ void carve_op_ws(Carver& cv, OpWs& w, const std::vector<OpGeom>& gl) {
   w.dG2 = cv.take(nG);
   w.dD2 = cv.take(nD);
   w.gs2 = cv.take(gemm_scratch_floats((int)nmn, 1));
+  w.adjp[0] = cv.take(nadj);
+  w.adjp[1] = cv.take(nadj);
 }
 
 // 1x1 conv as GEMMs over NCTV (W [cout][cin]).
@@ -406,9 +411,19 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
     DSTD_TRYH(gemm(d, nullptr, s));
     nparts = 1;
   }
-  // Adj = alpha * (conv_rm(M)) + A:  dalpha, dA, d b_rm, and dE = alpha dD in place
-  DSTD_TRYH(adj_bwd(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, dA, gr->brm, dalpha, ws.red, s, assign_dA, ws.dDp, nparts,
-                    dW2, Amul));
+  // Adj = alpha * (conv_rm(M)) + A:  dE = alpha dD in place (main stream);
+  // dalpha, dA, d b_rm from the partials -- parameter gradients only, so on
+  // the weight-gradient stream when there is one (B=32 step: 21 finishes off
+  // the critical path), with the partials in the op's set
+#ifndef DSTD_ADJ_FINISH_MAIN  // (A/B: 1 = the finish on the caller's stream, before the fork)
+#define DSTD_ADJ_FINISH_MAIN 0
+#endif
+  float* const adjs = wg->res ? ws0.adjp[slot] : ws.red;
+  DSTD_TRYH(adj_bwd_part(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, adjs, s, ws.dDp, nparts));
+  if (DSTD_ADJ_FINISH_MAIN) DSTD_TRYH(adj_bwd_finish(g.B, g.A, g.NN2, dA, gr->brm, dalpha, adjs, s, assign_dA, dW2, Amul));
+  if (wg->res) DSTD_TRYH(wg->fork());
+  if (!DSTD_ADJ_FINISH_MAIN)
+    DSTD_TRYH(adj_bwd_finish(g.B, g.A, g.NN2, dA, gr->brm, dalpha, adjs, ws_s, assign_dA, dW2, Amul));
   const float* dE = ws.dD;
   Gemm wr;  // dWrm[a][k] = sum_{n,ij} dE[n][a][ij] M[n][k][ij]
   wr.M = g.A, wr.N = g.R * g.A, wr.K = g.NN2, wr.nb1 = g.B, wr.reduce = 1;
@@ -416,7 +431,6 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   wr.B = sv.M, wr.b_b1 = (long long)g.R * g.A * g.NN2, wr.b_k = 1, wr.b_n = g.NN2;
   wr.C = gr->wrm, wr.c_m = g.R * g.A, wr.c_n = 1;
   wr.beta = 1.f;
-  if (wg->res) DSTD_TRYH(wg->fork());
   DSTD_TRYH(gemm(wr, ws_gs, ws_s));
   Gemm dm;  // dM[n][k][ij] = sum_a Wrm[a][k] dE[n][a][ij]
   dm.M = g.R * g.A, dm.N = g.NN2, dm.K = g.A, dm.nb1 = g.B;
