@@ -340,8 +340,12 @@ hipError_t conv_bwd(const float* W, const float* X, const float* dY, float* dX, 
 // y (beta_y: 0 '=' / 1 '+=') = DSTDGC(x, Acomb, alpha); fills sv.  The packed
 // weights sv.Wp / sv.bp must already hold the op's conv weights (pack_jobs).
 // Acomb = A0 (* W0) (+ R0), formed by the conv_rm GEMM's epilogue (W0, R0 may be null).
-hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* A0, const float* W0,
-                  const float* R0, const float* alpha, float* y, float beta_y, const OpSaved& sv, hipStream_t s) {
+// op_fwd in two parts: op_fwd_adj (the packed conv, M, E and D: everything up
+// to the adjacency) and op_fwd_agg (the aggregation into y), so that a
+// block's second spatial op can build its adjacency on another stream while
+// the first runs (block_fwd)
+hipError_t op_fwd_adj(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* A0, const float* W0,
+                      const float* R0, const float* alpha, const OpSaved& sv, hipStream_t s) {
   // conv_f, conv_m1, conv_m2 in one GEMM                         :81-82
   DSTD_TRYH(gemm(conv_fwd(sv.Wp, sv.bp, x, sv.G, g.B, g.cin, g.CG(), g.TV), nullptr, s));
   const float* P = sv.G + (size_t)g.cout * g.TV;
@@ -358,7 +362,9 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   e.d_A = A0;
   e.d_W = W0;
   e.d_R = R0;
-  DSTD_TRYH(gemm(e, nullptr, s));
+  return gemm(e, nullptr, s);
+}
+hipError_t op_fwd_agg(const OpGeom& g, float* y, float beta_y, const OpSaved& sv, hipStream_t s) {
   {  // y[c][(a,j)] = sum_i F[c][(a,i)] D[a][i][j]     :87 / :93
     const hipError_t e = agg_fwd(sv.G, (long long)g.CG() * g.TV, sv.D, y, (long long)g.cout * g.TV, beta_y, g.B,
                                  g.cout, g.T, g.V, g.temporal, s);
@@ -371,6 +377,11 @@ hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   a.C = y, a.c_b1 = (long long)g.cout * g.TV, a.c_b2 = g.ps_a, a.c_m = g.TV, a.c_n = g.ps_i;
   a.beta = beta_y;
   return gemm(a, nullptr, s);
+}
+hipError_t op_fwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, const float* A0, const float* W0,
+                  const float* R0, const float* alpha, float* y, float beta_y, const OpSaved& sv, hipStream_t s) {
+  DSTD_TRYH(op_fwd_adj(g, x, w, A0, W0, R0, alpha, sv, s));
+  return op_fwd_agg(g, y, beta_y, sv, s);
 }
 
 // dx_beta 0: dx (=) instead of (+=); assign_dA: dA likewise (block-internal
@@ -529,9 +540,13 @@ void pack_block(CopyJobs& js, const dstd_block_params* p, const BlockSaved& S, i
 
 // packed: the caller already packed the block's weights (the model forward
 // packs all blocks in two launches)
+// side (optional): a second stream of the device (the backward's weight-
+// gradient stream set): the second spatial op builds its adjacency there while
+// the first runs on s; its aggregation then adds into y on s after the
+// first's, so the result is bit-identical to the one-stream order.
 hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum, float* y,
                      const BlockSaved& S, hipStream_t s, int run = 0, const dstd_bn_sync* sync = nullptr,
-                     bool packed = false) {
+                     bool packed = false, Wgrad* side = nullptr) {
   const int cin = p->cin, cout = p->cout, TV = T * V;
   const bool res = cin != cout;
   const OpGeom gs(DSTD_MODE_SPATIAL, B, cin, cout, T, V);
@@ -541,9 +556,20 @@ hipError_t block_fwd(const dstd_block_params* p, const float* x, int B, int T, i
     pack_block(js, p, S, B, T, V);
     DSTD_TRYH(copy_jobs(js, s));
   }
-  for (int i = 0; i < 2; ++i)  // :145-150, A_s*W_s + R_s (:146-149)
-    DSTD_TRYH(op_fwd(gs, x, &p->conv_s[i], p->A_s + i * V * V, p->W_s + i * V * V, p->R_s + i * V * V, p->alpha_sm,
-                     S.ysp, i ? 1.f : 0.f, S.op[i], s));
+  // :145-150, A_s*W_s + R_s (:146-149)
+  if (side && side->res) {
+    side->main = s;
+    DSTD_TRYH(side->fork());
+    DSTD_TRYH(op_fwd_adj(gs, x, &p->conv_s[1], p->A_s + V * V, p->W_s + V * V, p->R_s + V * V, p->alpha_sm, S.op[1],
+                         side->res->st));
+    DSTD_TRYH(op_fwd(gs, x, &p->conv_s[0], p->A_s, p->W_s, p->R_s, p->alpha_sm, S.ysp, 0.f, S.op[0], s));
+    DSTD_TRYH(side->join());
+    DSTD_TRYH(op_fwd_agg(gs, S.ysp, 1.f, S.op[1], s));
+  } else {
+    for (int i = 0; i < 2; ++i)
+      DSTD_TRYH(op_fwd(gs, x, &p->conv_s[i], p->A_s + i * V * V, p->W_s + i * V * V, p->R_s + i * V * V,
+                       p->alpha_sm, S.ysp, i ? 1.f : 0.f, S.op[i], s));
+  }
   const float* r = x;
   if (res) {  // residual Conv1x1 + BatchNorm (:117-121)
     DSTD_TRYH(gemm(conv_fwd(p->res_w, p->res_b, x, S.rc, B, cin, cout, TV), nullptr, s));
@@ -896,6 +922,13 @@ int dstd_model_train_fwd_sync(const dstd_model_params* p, const float* x, int B,
   ModelSaved S;
   carve_model_saved(cv, S, B, T, V, C, L);
   const size_t act = (size_t)B * C * T * V;
+  // the blocks' second spatial ops build their adjacency on a second stream
+  // (block_fwd); joined at each block and by the destructor on any return
+#ifndef DSTD_FWD_SIDE  // (A/B: 0 = the forward on the caller's stream only)
+#define DSTD_FWD_SIDE 1
+#endif
+  Wgrad side((flags & DSTD_TRAIN_ONE_STREAM) || !DSTD_FWD_SIDE ? nullptr : wgrad_acquire());
+  side.main = s;
   DSTD_TRY(prep_nctv(x, B, T, V, 3, S.X0, s));                                   // :298-303
   {  // every block's packed conv weights, kMaxCopyJobs per launch
     CopyJobs js;
@@ -912,7 +945,7 @@ int dstd_model_train_fwd_sync(const dstd_model_params* p, const float* x, int B,
     DSTD_TRY(add(&p->st_out, S.st_out));
     DSTD_TRY(copy_jobs(js, s));
   }
-  DSTD_TRY(block_fwd(&p->st_in, S.X0, B, T, V, momentum, S.y0, S.st_in, s, run, sync, true));  // :305
+  DSTD_TRY(block_fwd(&p->st_in, S.X0, B, T, V, momentum, S.y0, S.st_in, s, run, sync, true, &side));  // :305
   BnFwd b0;                                                                      // :306-308
   b0.x = S.y0;
   b0.gamma = p->bn_in.weight;
@@ -932,7 +965,7 @@ int dstd_model_train_fwd_sync(const dstd_model_params* p, const float* x, int B,
   DSTD_TRY(bn_train_fwd(b0, B, C, T, V, S.red, s));
   if (dropout_p > 0.f) DSTD_TRY(dropout(S.hp0, S.h[0], act, dropout_p, seed, s, (flags & DSTD_TRAIN_SEED_DEVICE) != 0));  // do_in
   for (int i = 0; i < L; ++i) {                                                  // :310-311
-    DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s, run, sync, true));
+    DSTD_TRY(block_fwd(&p->enc[i], S.h[i], B, T, V, momentum, S.yb[i], S.enc[i], s, run, sync, true, &side));
     BnFwd be;  // BN(block(h) + h) -> PReLU  (:278-285, Identity residual :247-248)
     be.x = S.yb[i];
     be.x2 = S.h[i];
@@ -952,7 +985,7 @@ int dstd_model_train_fwd_sync(const dstd_model_params* p, const float* x, int B,
     be.sync = sync;
     DSTD_TRY(bn_train_fwd(be, B, C, T, V, S.red, s));
   }
-  DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s, run, sync, true));  // :313
+  DSTD_TRY(block_fwd(&p->st_out, S.h[L], B, T, V, momentum, S.o, S.st_out, s, run, sync, true, &side));  // :313
   DSTD_TRY(out_ntvc(S.o, x, B, T, V, 3, y, s));                                       // :314-315
   return DSTD_OK;
 }

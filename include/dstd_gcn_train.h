@@ -132,11 +132,13 @@ int dstd_block_train_bwd(const dstd_block_params* p, const float* x, int B, int 
  * draws a fresh one per replay).  Pass the same flags and address to the
  * backward before the value changes. */
 #define DSTD_TRAIN_SEED_DEVICE 4u
-/* DSTD_TRAIN_ONE_STREAM (model train bwd only): every launch on the caller's
- * stream.  By default the backward runs each DSTDGC's weight-gradient
- * reductions on a second stream of the device, forked from and joined back
- * into the caller's stream by events (also inside a HIP graph capture);
- * both orders give bit-identical results. */
+/* DSTD_TRAIN_ONE_STREAM (model train fwd / bwd only): every launch on the
+ * caller's stream.  By default the backward runs each DSTDGC's weight-gradient
+ * reductions (and its adjacency-gradient finish) on a second stream of the
+ * device, and the forward builds each block's second spatial adjacency there
+ * while the first spatial op runs, forked from and joined back into the
+ * caller's stream by events (also inside a HIP graph capture); both orders
+ * give bit-identical results. */
 #define DSTD_TRAIN_ONE_STREAM 8u
 int dstd_block_train_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float momentum,
                             float* y, void* saved, size_t saved_bytes, void* stream, unsigned flags);
