@@ -12,7 +12,7 @@ G=gpurun_out/$T
 [ -f $G/kt/run_kernel_stats.csv ] && cp $G/kt/run_kernel_stats.csv profiles/${T}_kernel_stats.csv
 [ -f $G/kt32/run_kernel_stats.csv ] && cp $G/kt32/run_kernel_stats.csv profiles/${T}_kernel_stats_b32.csv
 if [ -f $G/train_trace_summary.txt ]; then
-  { echo "# round 4 ($T): kernel trace of the B=32 3DPW training step (scripts/bench_train.py), last 3 steady-state steps"; cat $G/train_trace_summary.txt; } > profiles/${T}_train_trace_summary.txt
+  { echo "# ($T): kernel trace of the B=32 3DPW training step (scripts/bench_train.py), last 3 steady-state steps"; cat $G/train_trace_summary.txt; } > profiles/${T}_train_trace_summary.txt
 fi
 if [ -d $G/pmc1 ] && [ -d $G/pmc2 ]; then
   python3 scripts/pmc_traffic.py $G profiles/${T}
