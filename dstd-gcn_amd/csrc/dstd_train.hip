@@ -1027,9 +1027,14 @@ __global__ __launch_bounds__(kAggcThreads) void k_aggc(AggArgs g) {
 // partial dD (K = 16 channels), then dF (D[a]^T through its LDS tile) in
 // place of the a's dy slots.  The cdiv(C, 16) partials are summed in a fixed
 // order by adj_bwd (deterministic).
-constexpr int kAggcbThreads = 256;
+#ifndef DSTD_AGGCB_THREADS  // (experiments: waves per workgroup x 64)
+#define DSTD_AGGCB_THREADS 512  // (spatial: 8 waves, B=32 step -1.3%, profiles/r05z_aggcb_waves_ab.txt)
+#endif
+// (the temporal instantiations keep 4 waves: at 8, JF = 3 spills)
+__host__ __device__ constexpr int aggcb_threads(bool temporal) { return temporal ? 256 : DSTD_AGGCB_THREADS; }
 template <bool TEMP, int JF>
-__global__ __launch_bounds__(kAggcbThreads) void k_aggc_bwd(AggArgs g) {
+__global__ __launch_bounds__(aggcb_threads(TEMP)) void k_aggc_bwd(AggArgs g) {
+  constexpr int kAggcbThreads = aggcb_threads(TEMP);
   extern __shared__ float agg_sm[];
   constexpr int DR = JF * JF * 4;  // >= ceil(NN^2 / 64): D values per lane
   constexpr int NW = kAggcbThreads / 64;
@@ -1527,7 +1532,10 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 // Rows are visited RB at a time with all RB loads issued before the first
 // use (a row-at-a-time loop pays one memory latency per row, ~8 per chunk at
 // the config-5 batch); the accumulation order is unchanged.
-constexpr int kBnRB = 8;
+#ifndef DSTD_BN_RB  // (experiments)
+#define DSTD_BN_RB 8
+#endif
+constexpr int kBnRB = DSTD_BN_RB;
 struct BnRows {  // the rows row0, row0 + S, ... of one batch as (n, t)
   int n[kBnRB], t[kBnRB];
   bool ok[kBnRB];
@@ -2586,11 +2594,12 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
     agg_tile(g.NN, g.RK, g.P);
     g.QP = agg_split(g, B, temporal, DSTD_AGGB_SPLIT_WG);
     while ((g.QP & 63) != 4) ++g.QP;
-    const size_t lds = sizeof(float) * ((size_t)32 * g.QP + (size_t)(kAggcbThreads / 64) * g.RK * g.P);
+    const int nth = aggcb_threads(temporal);
+    const size_t lds = sizeof(float) * ((size_t)32 * g.QP + (size_t)(nth / 64) * g.RK * g.P);
     if (lds <= 160 * 1024) {
       g.vec = (g.TV % 4 == 0 && g.xs % 4 == 0 && g.os % 4 == 0 && g.y0s % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
                ((uintptr_t)g.O & 15) == 0 && ((uintptr_t)g.Y0 & 15) == 0);
-      const dim3 grid(B * cch * g.asplit), block(kAggcbThreads);
+      const dim3 grid(B * cch * g.asplit), block(nth);
       const int jf = cdiv(g.NN, 16);
       auto pick = [&](auto tb) {
         constexpr bool T_ = decltype(tb)::value;
