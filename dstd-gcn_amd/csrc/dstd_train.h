@@ -56,7 +56,14 @@ struct Gemm {
 
 // Scratch (floats) a reduce-GEMM may need for its split-over-batches partials.
 size_t gemm_scratch_floats(int M, int N);
-hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s);
+// A reduce GEMM's split-K finish handed back instead of launched (gemm's
+// defer argument; nsplit 0: the GEMM needed none), for finish_set.
+struct GemmFinish {
+  Gemm g;
+  int nsplit = 0;
+  const float* part = nullptr;
+};
+hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s, GemmFinish* defer = nullptr);
 
 // The DSTDGC aggregation products per sample n (model/dstdgcn.py:87 / :93),
 // NCTV operands with channel stride T*V and per-sample strides fs / ys / dys /
@@ -108,6 +115,13 @@ hipError_t adj_bwd_part(float* dD, const float* E, const float* alpha, int B, in
                         hipStream_t s, const float* dDpart, int nparts);
 hipError_t adj_bwd_finish(int B, int A, int NN2, float* dA, float* dbrm, float* dalpha, const float* scratch,
                           hipStream_t s, int assign_dA, float* dW2, const float* Amul);
+// One launch for an op's weight-gradient finishes (the model backward's
+// second stream): the adjacency-backward finish above and up to two deferred
+// split-K GEMM finishes (f0 / f1: null or nsplit 0 for none), each with the
+// arithmetic of its own launch.
+hipError_t finish_set(int B, int A, int NN2, float* dA, float* dbrm, float* dalpha, const float* adj_scratch,
+                      int assign_dA, float* dW2, const float* Amul, const GemmFinish* f0, const GemmFinish* f1,
+                      hipStream_t s);
 
 // Batched strided 2-D copies in one launch: dst[r*dst_ld + c] (+)= src[r*src_ld + c].
 struct CopyJob {

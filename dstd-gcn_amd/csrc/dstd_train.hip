@@ -256,10 +256,10 @@ __global__ __launch_bounds__(256) void k_gemm(Gemm g, int nsplit, int kch, int k
 // C = alpha * sum_z partial[z] + bias + beta * C.  Workgroup = 16 outputs x
 // 16 partial slices (slice s sums z = s, s + 16, ...), slices combined in LDS
 // in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void k_gemm_finish(Gemm g, int nsplit, const float* partial) {
+__device__ __forceinline__ void gemm_finish_block(int blk, const Gemm& g, int nsplit, const float* partial) {
   __shared__ float red[16][17];
   const int el = threadIdx.x & 15, sl = threadIdx.x >> 4;
-  const int idx = blockIdx.x * 16 + el;
+  const int idx = blk * 16 + el;
   const int MN = g.M * g.N;
   float s = 0.f;
   if (idx < MN)
@@ -274,6 +274,9 @@ __global__ __launch_bounds__(256) void k_gemm_finish(Gemm g, int nsplit, const f
   float v = g.alpha * t;
   if (g.bias_m) v += g.bias_m[m];
   gemm_store(g, g.C, g.d_out, m, n, v);
+}
+__global__ __launch_bounds__(256) void k_gemm_finish(Gemm g, int nsplit, const float* partial) {
+  gemm_finish_block(blockIdx.x, g, nsplit, partial);
 }
 
 constexpr int kMaxSplit = 128;
@@ -1327,17 +1330,35 @@ __global__ __launch_bounds__(256) void k_adj_bwd_part(float* __restrict__ dD, co
 // A*nch partial rows); the last block finishes dbrm and dalpha.
 // dW2 (optional): also dW2[ij] += dA-contribution * Amul[ij] (the spatial
 // adjacency A_s * W_s + R_s: dR_s = dA as dA itself, dW_s = dA * A_s)
-__global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict__ pdA, const float* __restrict__ pbr,
-                                                        const double* __restrict__ pal, int A, int NN2, int nch,
-                                                        float* __restrict__ dA, float* __restrict__ dbrm,
-                                                        float* __restrict__ dalpha, int assign_dA, float* __restrict__ dW2,
-                                                        const float* __restrict__ Amul, int nij) {
+struct AdjFinishArgs {
+  const float* pdA;
+  const float* pbr;
+  const double* pal;
+  int A, NN2, nch;
+  float* dA;
+  float* dbrm;
+  float* dalpha;
+  int assign_dA;
+  float* dW2;
+  const float* Amul;
+  int nij;
+};
+__device__ __forceinline__ void adj_finish_block(int blk, const AdjFinishArgs& f) {
+  const float* __restrict__ pdA = f.pdA;
+  const float* __restrict__ pbr = f.pbr;
+  const double* __restrict__ pal = f.pal;
+  const int A = f.A, NN2 = f.NN2, nch = f.nch, assign_dA = f.assign_dA, nij = f.nij;
+  float* __restrict__ dA = f.dA;
+  float* __restrict__ dbrm = f.dbrm;
+  float* __restrict__ dalpha = f.dalpha;
+  float* __restrict__ dW2 = f.dW2;
+  const float* __restrict__ Amul = f.Amul;
   __shared__ float lds[16][17];
   __shared__ double redd[4];
   const int nblk = (NN2 + 15) / 16;
-  if ((int)blockIdx.x < nblk) {
+  if (blk < nblk) {
     const int el = threadIdx.x & 15, sl = threadIdx.x >> 4;
-    const int ij = blockIdx.x * 16 + el;
+    const int ij = blk * 16 + el;
     float s = 0.f;
     if (ij < NN2)
 #pragma unroll 8
@@ -1377,6 +1398,29 @@ __global__ __launch_bounds__(256) void k_adj_bwd_finish(const float* __restrict_
   for (int i = threadIdx.x; i < A * nch * nij; i += blockDim.x) t += pal[i];
   t = block_sum(t, redd);
   if (threadIdx.x == 0) dalpha[0] += (float)t;
+}
+__global__ __launch_bounds__(256) void k_adj_bwd_finish(AdjFinishArgs f) { adj_finish_block(blockIdx.x, f); }
+// finish_set: blocks [0, na) the adjacency finish, then each GEMM finish's
+struct FinishSetArgs {
+  AdjFinishArgs adj;
+  int na;
+  Gemm g[2];
+  int nsplit[2], nb[2];
+  const float* part[2];
+};
+__global__ __launch_bounds__(256) void k_finish_set(FinishSetArgs a) {
+  int b = blockIdx.x;  // (block-uniform branches: the finishes' barriers are safe)
+  if (b < a.na) {
+    adj_finish_block(b, a.adj);
+    return;
+  }
+  b -= a.na;
+  if (b < a.nb[0]) {
+    gemm_finish_block(b, a.g[0], a.nsplit[0], a.part[0]);
+    return;
+  }
+  b -= a.nb[0];
+  if (b < a.nb[1]) gemm_finish_block(b, a.g[1], a.nsplit[1], a.part[1]);
 }
 
 __global__ void k_copy_jobs(CopyJobs js) {
@@ -2387,7 +2431,8 @@ hipError_t gemm_skinny(const Gemm& g, float* scratch, hipStream_t s) {
 }
 }  // namespace
 
-hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
+hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s, GemmFinish* defer) {
+  if (defer) defer->nsplit = 0;
   if (g.M <= 0 || g.N <= 0) return hipSuccess;
   if (g.d_out && (g.reduce || !g.d_A || !g.d_alpha)) return hipErrorInvalidValue;
   {
@@ -2433,6 +2478,12 @@ hipError_t gemm(const Gemm& g, float* scratch, hipStream_t s) {
 #undef DSTD_GEMM_GO
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nsplit == 1) return e;
+  if (defer) {  // the caller launches the finish (finish_set)
+    defer->g = g;
+    defer->nsplit = nsplit;
+    defer->part = part;
+    return hipSuccess;
+  }
   k_gemm_finish<<<cdiv(g.M * g.N, 16), 256, 0, s>>>(g, nsplit, part);
   return hipGetLastError();
 }
@@ -2688,8 +2739,29 @@ hipError_t adj_bwd_finish(int B, int A, int NN2, float* dA, float* dbrm, float* 
   if (dW2 && !Amul) return hipErrorInvalidValue;
   if (A > 256) return hipErrorInvalidValue;
   const AdjBwdScratch P(const_cast<float*>(scratch), B, A, NN2);
-  k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(P.pdA, P.pbr, P.pal, A, NN2, P.nch, dA, dbrm, dalpha, assign_dA,
-                                                      dW2, Amul, P.nij);
+  const AdjFinishArgs f{P.pdA, P.pbr, P.pal, A, NN2, P.nch, dA, dbrm, dalpha, assign_dA, dW2, Amul, P.nij};
+  k_adj_bwd_finish<<<cdiv(NN2, 16) + 1, 256, 0, s>>>(f);
+  return hipGetLastError();
+}
+
+hipError_t finish_set(int B, int A, int NN2, float* dA, float* dbrm, float* dalpha, const float* adj_scratch,
+                      int assign_dA, float* dW2, const float* Amul, const GemmFinish* f0, const GemmFinish* f1,
+                      hipStream_t s) {
+  if (dW2 && !Amul) return hipErrorInvalidValue;
+  if (A > 256) return hipErrorInvalidValue;
+  const AdjBwdScratch P(const_cast<float*>(adj_scratch), B, A, NN2);
+  FinishSetArgs a{};
+  a.adj = AdjFinishArgs{P.pdA, P.pbr, P.pal, A, NN2, P.nch, dA, dbrm, dalpha, assign_dA, dW2, Amul, P.nij};
+  a.na = cdiv(NN2, 16) + 1;
+  const GemmFinish* f[2] = {f0, f1};
+  for (int i = 0; i < 2; ++i) {
+    const bool on = f[i] && f[i]->nsplit > 1;
+    if (on) a.g[i] = f[i]->g;
+    a.nsplit[i] = on ? f[i]->nsplit : 0;
+    a.part[i] = on ? f[i]->part : nullptr;
+    a.nb[i] = on ? cdiv(f[i]->g.M * f[i]->g.N, 16) : 0;
+  }
+  k_finish_set<<<a.na + a.nb[0] + a.nb[1], 256, 0, s>>>(a);
   return hipGetLastError();
 }
 

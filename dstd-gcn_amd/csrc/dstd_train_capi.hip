@@ -146,6 +146,7 @@ struct OpWs {
   // adjacency backward's partials per set (its finish runs on that stream)
   float *dG2, *dD2, *gs2;
   float* adjp[2];
+  float* gs3;  // the dW_rm reduction's partials (its finish waits for dWp's: finish_set)
 };
 
 // ---------------------------------------------------------------------------
@@ -290,6 +291,7 @@ void carve_op_ws(Carver& cv, OpWs& w, const std::vector<OpGeom>& gl) {
   w.gs2 = cv.take(gemm_scratch_floats((int)nmn, 1));
   w.adjp[0] = cv.take(nadj);
   w.adjp[1] = cv.take(nadj);
+  w.gs3 = cv.take(gemm_scratch_floats((int)nmn, 1));
 }
 
 // 1x1 conv as GEMMs over NCTV (W [cout][cin]).
@@ -429,11 +431,20 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
 #ifndef DSTD_ADJ_FINISH_MAIN  // (A/B: 1 = the finish on the caller's stream, before the fork)
 #define DSTD_ADJ_FINISH_MAIN 0
 #endif
+  // With the weight-gradient stream, this finish and the two reductions'
+  // split-K finishes below run as ONE launch after dWp's reduction
+  // (finish_set: 2 launches per op fewer; dW_rm's partials in gs3)
   float* const adjs = wg->res ? ws0.adjp[slot] : ws.red;
   DSTD_TRYH(adj_bwd_part(ws.dD, sv.E, alpha, g.B, g.A, g.NN2, adjs, s, ws.dDp, nparts));
-  if (DSTD_ADJ_FINISH_MAIN) DSTD_TRYH(adj_bwd_finish(g.B, g.A, g.NN2, dA, gr->brm, dalpha, adjs, s, assign_dA, dW2, Amul));
+  if (DSTD_ADJ_FINISH_MAIN || !wg->res)
+    DSTD_TRYH(adj_bwd_finish(g.B, g.A, g.NN2, dA, gr->brm, dalpha, adjs, s, assign_dA, dW2, Amul));
   if (wg->res) DSTD_TRYH(wg->fork());
-  if (!DSTD_ADJ_FINISH_MAIN)
+#ifndef DSTD_FINISH_SET  // (A/B: 0 = the three finishes as launches of their own on the side stream)
+#define DSTD_FINISH_SET 1
+#endif
+  GemmFinish wrf, gwf;
+  const bool fset = wg->res && !DSTD_ADJ_FINISH_MAIN && DSTD_FINISH_SET;
+  if (wg->res && !DSTD_ADJ_FINISH_MAIN && !fset)
     DSTD_TRYH(adj_bwd_finish(g.B, g.A, g.NN2, dA, gr->brm, dalpha, adjs, ws_s, assign_dA, dW2, Amul));
   const float* dE = ws.dD;
   Gemm wr;  // dWrm[a][k] = sum_{n,ij} dE[n][a][ij] M[n][k][ij]
@@ -442,7 +453,7 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   wr.B = sv.M, wr.b_b1 = (long long)g.R * g.A * g.NN2, wr.b_k = 1, wr.b_n = g.NN2;
   wr.C = gr->wrm, wr.c_m = g.R * g.A, wr.c_n = 1;
   wr.beta = 1.f;
-  DSTD_TRYH(gemm(wr, ws_gs, ws_s));
+  DSTD_TRYH(gemm(wr, fset ? ws.gs3 : ws_gs, ws_s, fset ? &wrf : nullptr));
   Gemm dm;  // dM[n][k][ij] = sum_a Wrm[a][k] dE[n][a][ij]
   dm.M = g.R * g.A, dm.N = g.NN2, dm.K = g.A, dm.nb1 = g.B;
   dm.A = w->wrm, dm.a_m = 1, dm.a_k = g.R * g.A;
@@ -463,7 +474,9 @@ hipError_t op_bwd(const OpGeom& g, const float* x, const dstd_gc_weights* w, con
   gw.seg[2] = Gemm::Seg{g.cout + g.R, g.R, gr->wm2, gr->bm2};
   if (wg->res) {  // queued before dx, which then runs beside it
     DSTD_TRYH(wg->fork());
-    DSTD_TRYH(gemm(gw, ws_gs, ws_s));
+    DSTD_TRYH(gemm(gw, ws_gs, ws_s, fset ? &gwf : nullptr));
+    if (fset)
+      DSTD_TRYH(finish_set(g.B, g.A, g.NN2, dA, gr->brm, dalpha, adjs, assign_dA, dW2, Amul, &wrf, &gwf, ws_s));
     DSTD_TRYH(wg->release(slot));
   }
   // the three 1x1 convs at once: dx += Wp^T dG;  [dWp | dbp] = sum dG [x; 1]^T
