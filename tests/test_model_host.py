@@ -92,3 +92,28 @@ def test_fast_variant_schema_and_derivation_cpu():
         assert not any(k.startswith("_shadow") for k in m.state_dict())
         c = copy.deepcopy(m)
         assert c.__dict__["_shadow"] is None
+
+
+def test_anchor_of_selects_the_parameter_inputs():
+    """The training Function's parameter inputs (model/dstdgcn.py:_anchor_of):
+    one empty leaf requiring grad only in the opted-in in-place gradient mode
+    (engine.PredictionEngine.train) with grad enabled, a plain tensor and no
+    parameter hooks -- otherwise the parameters themselves, so hooks, DDP and
+    torch.autograd.grad keep ordinary autograd gradients."""
+    from model.dstdgcn import _anchor_of
+    m = get_model("dstdgcn", dstdgcn=OPTS)
+    params = m._tree.get(m)[0]
+    x = torch.zeros(2, 35, 22, 3)
+    assert _anchor_of(m, x, params) is params  # default: not opted in
+    m._dstd_inplace_grads = True
+    a = _anchor_of(m, x, params)
+    assert len(a) == 1 and a[0].requires_grad and a[0].numel() == 0 and a[0].is_leaf
+    assert _anchor_of(m, x, params)[0] is a[0]  # one leaf per model
+    with torch.no_grad():
+        assert _anchor_of(m, x, params) is params
+    h = next(p for p in params if p.requires_grad).register_hook(lambda g: g)
+    assert _anchor_of(m, x, params) is params  # a hook: parameter inputs
+    h.remove()
+    assert _anchor_of(m, x, params)[0] is a[0]
+    frozen = [p.detach() for p in params]  # nothing requires grad: parameter inputs
+    assert _anchor_of(m, x, frozen) is frozen
