@@ -2534,9 +2534,14 @@ hipError_t adj_hl_run(const AdjHLArgs& a, hipStream_t s) {
     // column tiles over more workgroups -- each repeats the prologue, but the
     // launch is its prologue plus 1/nch of the tiles -- keeping at least half
     // the waves of a workgroup busy
+#ifndef DSTD_ADJ_CHUNK_PCT  // (experiments: workgroups aimed at, % of the CUs / the busy-wave floor's divisor)
+#define DSTD_ADJ_CHUNK_PCT 100
+#define DSTD_ADJ_CHUNK_DIV 2
+#endif
     const int sets = a.B * a.ngroups, cus = hl_num_cus();
     b.nchunk = Gm::NCHUNK;
-    if (sets * Gm::NCHUNK < cus) b.nchunk = max(Gm::NCHUNK, min(cdiv(cus, sets), cdiv(Gm::NCT, cdiv(Gm::AW, 2))));
+    if (sets * Gm::NCHUNK < cus)
+      b.nchunk = max(Gm::NCHUNK, min(cdiv(DSTD_ADJ_CHUNK_PCT * cus, 100 * sets), cdiv(Gm::NCT, cdiv(Gm::AW, DSTD_ADJ_CHUNK_DIV))));
   }
   const int grid = a.B * a.ngroups * b.nchunk;
   hipLaunchKernelGGL((k_adj_hl<MODE, NROW, K, NA>), dim3(grid), dim3(Gm::AT), 0, s, b);
