@@ -1028,31 +1028,33 @@ __global__ __launch_bounds__(kAggcThreads) void k_aggc(AggArgs g) {
 // Workgroup = (sample, 16-channel chunk p) over all a, dy and F slabs of the
 // chunk in LDS (16-byte loads); per a, the wave first forms the chunk's
 // partial dD (K = 16 channels), then dF (D[a]^T through its LDS tile) in
-// place of the a's dy slots.  The cdiv(C, 16) partials are summed in a fixed
-// order by adj_bwd (deterministic).
+// place of the a's dy slots.  The cdiv(C, CW) partials are summed in a fixed
+// order by adj_bwd (deterministic).  CW = 16 MF channels: 16 (temporal), 64
+// (spatial, MF = 4 row tiles of dF per a).
 #ifndef DSTD_AGGCB_THREADS  // (experiments: waves per workgroup x 64)
 #define DSTD_AGGCB_THREADS 512  // (spatial: 8 waves, B=32 step -1.3%, profiles/r05z_aggcb_waves_ab.txt)
 #endif
 // (the temporal instantiations keep 4 waves: at 8, JF = 3 spills)
 __host__ __device__ constexpr int aggcb_threads(bool temporal) { return temporal ? 256 : DSTD_AGGCB_THREADS; }
-template <bool TEMP, int JF>
+template <bool TEMP, int JF, int MF>
 __global__ __launch_bounds__(aggcb_threads(TEMP)) void k_aggc_bwd(AggArgs g) {
   constexpr int kAggcbThreads = aggcb_threads(TEMP);
   extern __shared__ float agg_sm[];
   constexpr int DR = JF * JF * 4;  // >= ceil(NN^2 / 64): D values per lane
   constexpr int NW = kAggcbThreads / 64;
+  constexpr int CW = 16 * MF;  // channels per chunk (MF row tiles of dF)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
   const int C = g.C, NN = g.NN, V = g.V, TV = g.TV, TVP = g.QP, P = g.P, RK = g.RK;
-  const int cch = cdiv(C, 16);
+  const int cch = cdiv(C, CW);
   const int blk = blockIdx.x / g.asplit, ag = blockIdx.x - blk * g.asplit;
-  const int n = blk / cch, p = blk - n * cch, c0 = p * 16;
-  const int cv = min(16, C - c0);
+  const int n = blk / cch, p = blk - n * cch, c0 = p * CW;
+  const int cv = min(CW, C - c0);
   // this workgroup's a's [a_lo, a_hi) and their slab: W floats from sb of every channel row
   const int a_lo = TEMP ? 0 : ag * g.apg, a_hi = TEMP ? g.A : min(g.A, a_lo + g.apg);
   const int W = TEMP ? TV : (a_hi - a_lo) * V, sb = TEMP ? 0 : a_lo * V;
-  float* SY = agg_sm;              // [16][TVP] dy, then dF
-  float* SF = agg_sm + 16 * TVP;   // [16][TVP] F
-  float* Dl = agg_sm + 32 * TVP + wave * RK * P;
+  float* SY = agg_sm;              // [CW][TVP] dy, then dF
+  float* SF = agg_sm + CW * TVP;   // [CW][TVP] F
+  float* Dl = agg_sm + 2 * CW * TVP + wave * RK * P;
   const float* Yn = g.Y0 + n * g.y0s + (long long)c0 * TV + sb;
   const float* Fn = g.X + n * g.xs + (long long)c0 * TV + sb;
   float* Out = g.O + n * g.os + (long long)c0 * TV + sb;
@@ -1124,7 +1126,7 @@ __global__ __launch_bounds__(aggcb_threads(TEMP)) void k_aggc_bwd(AggArgs g) {
 #pragma unroll
         for (int y = 0; y < JF; ++y) acc[x][y] = zero4();
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
+      for (int ks = 0; ks < 4 * MF; ++ks) {
         const int c = ks * 4 + lk;
         float av[JF], bv[JF];
 #pragma unroll
@@ -1159,17 +1161,25 @@ __global__ __launch_bounds__(aggcb_threads(TEMP)) void k_aggc_bwd(AggArgs g) {
     }
     if (a + NW < a_hi) load_d(a + NW);
     __builtin_amdgcn_wave_barrier();
-    f32x4 acc[JF];
+    f32x4 acc[MF][JF];
 #pragma unroll
-    for (int y = 0; y < JF; ++y) acc[y] = zero4();
+    for (int m = 0; m < MF; ++m)
+#pragma unroll
+      for (int y = 0; y < JF; ++y) acc[m][y] = zero4();
     auto kstep = [&](int k, bool tail) __attribute__((always_inline)) {
-      float av = SY[lr * TVP + off(a, k)];
-      if (tail) av = k < NN ? av : 0.f;
+      float av[MF];
+#pragma unroll
+      for (int m = 0; m < MF; ++m) {
+        av[m] = SY[(m * 16 + lr) * TVP + off(a, k)];
+        if (tail) av[m] = k < NN ? av[m] : 0.f;
+      }
       float bv[JF];
 #pragma unroll
       for (int y = 0; y < JF; ++y) bv[y] = Dl[k * P + y * 16 + lr];
 #pragma unroll
-      for (int y = 0; y < JF; ++y) acc[y] = mfma16x16x4(av, bv[y], acc[y]);
+      for (int m = 0; m < MF; ++m)
+#pragma unroll
+        for (int y = 0; y < JF; ++y) acc[m][y] = mfma16x16x4(av[m], bv[y], acc[m][y]);
     };
     int k = lk;
     for (; k < (NN & ~3); k += 4) kstep(k, false);
@@ -1180,7 +1190,9 @@ __global__ __launch_bounds__(aggcb_threads(TEMP)) void k_aggc_bwd(AggArgs g) {
       if (i < NN) {
         const int q = off(a, i);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) SY[(lk * 4 + r) * TVP + q] = acc[y][r];
+        for (int m = 0; m < MF; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) SY[(m * 16 + lk * 4 + r) * TVP + q] = acc[m][y][r];
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -2538,10 +2550,10 @@ int agg_cus() {
 #ifndef DSTD_AGGB_SPLIT_WG  // backward (k_aggc_bwd)
 #define DSTD_AGGB_SPLIT_WG 2
 #endif
-int agg_split(AggArgs& g, int B, bool temporal, int per_cu) {
+int agg_split(AggArgs& g, int B, bool temporal, int per_cu, int cw = 16) {
   g.asplit = 1;
   g.apg = g.A;
-  const int wgs = B * cdiv(g.C, 16), cus = agg_cus();
+  const int wgs = B * cdiv(g.C, cw), cus = agg_cus();
   if (temporal || per_cu <= 0 || wgs >= per_cu * cus) return g.TV;
   const int m = (g.V % 4 == 0) ? 1 : (g.V % 2 == 0) ? 2 : 4;
   const int want = std::min(g.A, cdiv(per_cu * cus, wgs));
@@ -2637,31 +2649,46 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
   // dF on the channel-chunk backward kernel, dD as its per-chunk partials
   // (dDpart; one chunk: dD itself); else dF on the channel-chunk kernel and
   // dD on the a-chunk kernel
-  const int cch = cdiv(C, 16);
+  // channels per chunk: 16 (temporal); spatial DSTD_AGGB_CW_SP: one chunk
+  // of all 64 channels reads D once and leaves one dD (no partials for
+  // adj_bwd_part to sum): B=32 step -1.3%, profiles/r05gg_aggb_cw_ab.txt
+#ifndef DSTD_AGGB_CW_SP
+#define DSTD_AGGB_CW_SP 64
+#endif
+  const int mfc = temporal ? 1 : std::min(DSTD_AGGB_CW_SP / 16, cdiv(C, 16)), cw = 16 * mfc;
+  const int cch = cdiv(C, cw);
   *nparts = 1;
   if (cch == 1 || dDpart) {
     if (cch > 1) g.dD = dDpart, *nparts = cch;
     g.B = B;
     agg_tile(g.NN, g.RK, g.P);
-    g.QP = agg_split(g, B, temporal, DSTD_AGGB_SPLIT_WG);
+    g.QP = agg_split(g, B, temporal, DSTD_AGGB_SPLIT_WG, cw);
     while ((g.QP & 63) != 4) ++g.QP;
     const int nth = aggcb_threads(temporal);
-    const size_t lds = sizeof(float) * ((size_t)32 * g.QP + (size_t)(nth / 64) * g.RK * g.P);
+    const size_t lds = sizeof(float) * ((size_t)2 * cw * g.QP + (size_t)(nth / 64) * g.RK * g.P);
     if (lds <= 160 * 1024) {
       g.vec = (g.TV % 4 == 0 && g.xs % 4 == 0 && g.os % 4 == 0 && g.y0s % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
                ((uintptr_t)g.O & 15) == 0 && ((uintptr_t)g.Y0 & 15) == 0);
       const dim3 grid(B * cch * g.asplit), block(nth);
       const int jf = cdiv(g.NN, 16);
-      auto pick = [&](auto tb) {
+      auto pick = [&](auto tb, auto mb) {
         constexpr bool T_ = decltype(tb)::value;
+        constexpr int M_ = decltype(mb)::value;
         switch (jf) {
-          case 1: agg_go(k_aggc_bwd<T_, 1>, grid, block, lds, g, s); break;
-          case 2: agg_go(k_aggc_bwd<T_, 2>, grid, block, lds, g, s); break;
-          case 3: agg_go(k_aggc_bwd<T_, 3>, grid, block, lds, g, s); break;
-          default: agg_go(k_aggc_bwd<T_, 4>, grid, block, lds, g, s); break;
+          case 1: agg_go(k_aggc_bwd<T_, 1, M_>, grid, block, lds, g, s); break;
+          case 2: agg_go(k_aggc_bwd<T_, 2, M_>, grid, block, lds, g, s); break;
+          case 3: agg_go(k_aggc_bwd<T_, 3, M_>, grid, block, lds, g, s); break;
+          default: agg_go(k_aggc_bwd<T_, 4, M_>, grid, block, lds, g, s); break;
         }
       };
-      temporal ? pick(std::true_type()) : pick(std::false_type());
+      if (temporal) pick(std::true_type(), std::integral_constant<int, 1>());
+      else if (mfc == 1) pick(std::false_type(), std::integral_constant<int, 1>());
+#if DSTD_AGGB_CW_SP >= 32
+      else if (mfc == 2) pick(std::false_type(), std::integral_constant<int, 2>());
+#endif
+#if DSTD_AGGB_CW_SP >= 64
+      else pick(std::false_type(), std::integral_constant<int, 4>());
+#endif
       return hipGetLastError();
     }
     *nparts = 1;

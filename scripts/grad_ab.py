@@ -42,13 +42,14 @@ def dump(path, B=32):
 
 def compare(a, b):
     A, Bz = np.load(a), np.load(b)
-    worst, nid = 0.0, 0
+    rel, nid = {}, 0
     for k in A.files:
-        x, y = A[k], Bz[k]
-        d = float(np.abs(x - y).max() / max(np.abs(x).max(), 1e-30))
-        nid += int(np.array_equal(x, y))
-        worst = max(worst, d)
-    print(f"{os.path.basename(b)} vs {os.path.basename(a)}: {nid}/{len(A.files)} tensors identical, max rel {worst:.3e}")
+        x, y = A[k].astype(np.float64), Bz[k].astype(np.float64)
+        rel[k] = float(np.linalg.norm(x - y) / max(np.linalg.norm(x), 1e-30))  # (norm-relative: near-zero
+        nid += int(np.array_equal(A[k], Bz[k]))                                #  noise tensors do not dominate)
+    w = sorted(rel, key=rel.get)[-3:]
+    print(f"{os.path.basename(b)} vs {os.path.basename(a)}: {nid}/{len(A.files)} tensors identical, "
+          f"median |d|/|g| {np.median(list(rel.values())):.2e}, worst " + ", ".join(f"{k} {rel[k]:.2e}" for k in w))
 
 
 if __name__ == "__main__":
