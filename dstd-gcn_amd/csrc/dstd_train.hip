@@ -889,22 +889,23 @@ __global__ __launch_bounds__(256) void k_agg(AggArgs g) {
 // = 4 mod 64 so the 16 rows x 4 k of an A fragment hit distinct banks for
 // both k strides (1: spatial, V: temporal).
 constexpr int kAggcThreads = 512;
-template <bool TEMP, bool TRANS, int JF>
+template <bool TEMP, bool TRANS, int JF, int MF>
 __global__ __launch_bounds__(kAggcThreads) void k_aggc(AggArgs g) {
   extern __shared__ float agg_sm[];
   constexpr int DR = JF * JF * 4;  // >= ceil(NN^2 / 64): D values per lane
   constexpr int NW = kAggcThreads / 64;
+  constexpr int CW = 16 * MF;  // channels per chunk (MF row tiles)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lk = lane >> 4;
   const int C = g.C, NN = g.NN, V = g.V, TV = g.TV, TVP = g.QP, P = g.P, RK = g.RK;
-  const int cch = cdiv(C, 16);
+  const int cch = cdiv(C, CW);
   const int blk = blockIdx.x / g.asplit, ag = blockIdx.x - blk * g.asplit;
-  const int n = blk / cch, c0 = (blk - n * cch) * 16;
-  const int cv = min(16, C - c0);
+  const int n = blk / cch, c0 = (blk - n * cch) * CW;
+  const int cv = min(CW, C - c0);
   // this workgroup's a's [a_lo, a_hi) and their slab: W floats from sb of every channel row
   const int a_lo = TEMP ? 0 : ag * g.apg, a_hi = TEMP ? g.A : min(g.A, a_lo + g.apg);
   const int W = TEMP ? TV : (a_hi - a_lo) * V, sb = TEMP ? 0 : a_lo * V;
-  float* S = agg_sm;  // [16][TVP]
-  float* Dl = agg_sm + 16 * TVP + wave * RK * P;
+  float* S = agg_sm;  // [CW][TVP]
+  float* Dl = agg_sm + CW * TVP + wave * RK * P;
   const float* In = g.X + n * g.xs + (long long)c0 * TV + sb;
   float* Out = g.O + n * g.os + (long long)c0 * TV + sb;
   const int NN2 = NN * NN;
@@ -972,17 +973,25 @@ __global__ __launch_bounds__(kAggcThreads) void k_aggc(AggArgs g) {
     }
     if (a + NW < a_hi) load_d(a + NW);
     __builtin_amdgcn_wave_barrier();
-    f32x4 acc[JF];
+    f32x4 acc[MF][JF];
 #pragma unroll
-    for (int y = 0; y < JF; ++y) acc[y] = zero4();
+    for (int m = 0; m < MF; ++m)
+#pragma unroll
+      for (int y = 0; y < JF; ++y) acc[m][y] = zero4();
     auto kstep = [&](int k, bool tail) __attribute__((always_inline)) {
-      float av = S[lr * TVP + off(a, k)];
-      if (tail) av = k < NN ? av : 0.f;
+      float av[MF];
+#pragma unroll
+      for (int m = 0; m < MF; ++m) {
+        av[m] = S[(m * 16 + lr) * TVP + off(a, k)];
+        if (tail) av[m] = k < NN ? av[m] : 0.f;
+      }
       float bv[JF];
 #pragma unroll
       for (int y = 0; y < JF; ++y) bv[y] = Dl[k * P + y * 16 + lr];
 #pragma unroll
-      for (int y = 0; y < JF; ++y) acc[y] = mfma16x16x4(av, bv[y], acc[y]);
+      for (int m = 0; m < MF; ++m)
+#pragma unroll
+        for (int y = 0; y < JF; ++y) acc[m][y] = mfma16x16x4(av[m], bv[y], acc[m][y]);
     };
     int k = lk;
     for (; k < (NN & ~3); k += 4) kstep(k, false);
@@ -993,7 +1002,9 @@ __global__ __launch_bounds__(kAggcThreads) void k_aggc(AggArgs g) {
       if (j < NN) {
         const int q = off(a, j);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) S[(lk * 4 + r) * TVP + q] = acc[y][r];
+        for (int m = 0; m < MF; ++m)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) S[(m * 16 + lk * 4 + r) * TVP + q] = acc[m][y][r];
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -2597,28 +2608,42 @@ hipError_t agg_launch_a(bool bwd, bool df, AggArgs g, int B, int temporal, hipSt
 // channel-chunk kernel: fwd (trans 0) or dF (trans 1)
 hipError_t agg_launch_c(bool trans, AggArgs g, int B, int temporal, hipStream_t s) {
   if (!agg_ok(g)) return hipErrorNotSupported;
+  // channels per chunk: 16; the spatial forward DSTD_AGG_CW_SP (16 or 64: a
+  // wider chunk reads D once per chunk, but 64 measured +0.7% at B=32, +1.7%
+  // at B=256 -- half its waves idle over 4 frames; profiles/r05jj_agg_cw_ab.txt)
+#ifndef DSTD_AGG_CW_SP
+#define DSTD_AGG_CW_SP 16
+#endif
+  // (row tiles 1 or 4: 2 and 3 run as 4, cv masking the rest)
+  const int mfc = temporal || trans || DSTD_AGG_CW_SP < 64 || g.C <= 16 ? 1 : 4, cw = 16 * mfc;
   agg_tile(g.NN, g.RK, g.P);
-  g.QP = agg_split(g, B, temporal, DSTD_AGG_SPLIT_WG);
+  g.QP = agg_split(g, B, temporal, DSTD_AGG_SPLIT_WG, cw);
   while ((g.QP & 63) != 4) ++g.QP;
-  const size_t lds = sizeof(float) * ((size_t)16 * g.QP + (size_t)(kAggcThreads / 64) * g.RK * g.P);
+  const size_t lds = sizeof(float) * ((size_t)cw * g.QP + (size_t)(kAggcThreads / 64) * g.RK * g.P);
   if (lds > 160 * 1024) return hipErrorNotSupported;
   g.vec = (g.TV % 4 == 0 && g.xs % 4 == 0 && g.os % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
            ((uintptr_t)g.O & 15) == 0);
-  const dim3 grid(B * cdiv(g.C, 16) * g.asplit), block(kAggcThreads);
+  const dim3 grid(B * cdiv(g.C, cw) * g.asplit), block(kAggcThreads);
   const int jf = cdiv(g.NN, 16);
-  auto pick = [&](auto tb, auto rb) {
+  auto pick = [&](auto tb, auto rb, auto mb) {
     constexpr bool T_ = decltype(tb)::value, R_ = decltype(rb)::value;
+    constexpr int M_ = decltype(mb)::value;
     switch (jf) {
-      case 1: agg_go(k_aggc<T_, R_, 1>, grid, block, lds, g, s); break;
-      case 2: agg_go(k_aggc<T_, R_, 2>, grid, block, lds, g, s); break;
-      case 3: agg_go(k_aggc<T_, R_, 3>, grid, block, lds, g, s); break;
-      default: agg_go(k_aggc<T_, R_, 4>, grid, block, lds, g, s); break;
+      case 1: agg_go(k_aggc<T_, R_, 1, M_>, grid, block, lds, g, s); break;
+      case 2: agg_go(k_aggc<T_, R_, 2, M_>, grid, block, lds, g, s); break;
+      case 3: agg_go(k_aggc<T_, R_, 3, M_>, grid, block, lds, g, s); break;
+      default: agg_go(k_aggc<T_, R_, 4, M_>, grid, block, lds, g, s); break;
     }
   };
   using T1 = std::true_type;
   using F0 = std::false_type;
-  if (temporal) trans ? pick(T1(), T1()) : pick(T1(), F0());
-  else trans ? pick(F0(), T1()) : pick(F0(), F0());
+  using M1 = std::integral_constant<int, 1>;
+  if (temporal) trans ? pick(T1(), T1(), M1()) : pick(T1(), F0(), M1());
+  else if (trans) pick(F0(), T1(), M1());
+  else if (mfc == 1) pick(F0(), F0(), M1());
+#if DSTD_AGG_CW_SP >= 64
+  else pick(F0(), F0(), std::integral_constant<int, 4>());
+#endif
   return hipGetLastError();
 }
 AggArgs agg_geom(int C, int T, int V, int temporal) {
@@ -2655,7 +2680,8 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
 #ifndef DSTD_AGGB_CW_SP
 #define DSTD_AGGB_CW_SP 64
 #endif
-  const int mfc = temporal ? 1 : std::min(DSTD_AGGB_CW_SP / 16, cdiv(C, 16)), cw = 16 * mfc;
+  // (row tiles 1, 2 or 4: 3 runs as 4, cv masking the fourth)
+  const int mf0 = temporal ? 1 : std::min(DSTD_AGGB_CW_SP / 16, cdiv(C, 16)), mfc = mf0 == 3 ? 4 : mf0, cw = 16 * mfc;
   const int cch = cdiv(C, cw);
   *nparts = 1;
   if (cch == 1 || dDpart) {
