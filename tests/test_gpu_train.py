@@ -97,6 +97,31 @@ def test_dstdgc_op_backward(mode, cin, cout, T, V):
         assert rel(p.grad, sd64[name].grad) < 1e-4, name
 
 
+def test_dstdgc_op_backward_partial_row_tiles():
+    """Spatial op with 40 output channels at B=128: the backward aggregation
+    runs its 4-row-tile (64-channel) kernel over 40 channels with every wave
+    busy (12 frames per workgroup), so its LDS must be sized for 64 rows
+    (reference model/dstdgcn.py:80-87 under autograd, fp64 oracle)."""
+    mode, cin, cout, T, V, B = "spatial", 32, 40, 40, 23, 128
+    torch.manual_seed(5)
+    op = DSTDGC(cin, cout, T, V, mode=mode)
+    randomise(op, 77)
+    x = torch.randn(B, cin, T, V)
+    A = 0.3 * torch.randn(1, V, V)
+    alpha = torch.tensor([0.7])
+    w = torch.randn(B, cout, T, V)
+    sd64 = {k: v.detach().double().requires_grad_(True) for k, v in op.state_dict().items()}
+    x64, A64, a64 = (t.double().requires_grad_(True) for t in (x, A, alpha))
+    (O.dstdgc(x64, sd64, A64, a64.reshape(()), mode) * w.double()).sum().backward()
+    op = op.to(DEV)
+    xg, Ag, ag = (t.to(DEV).requires_grad_(True) for t in (x, A, alpha))
+    (op(xg, Ag, ag) * w.to(DEV)).sum().backward()
+    assert rel(xg.grad, x64.grad) < 1e-4
+    assert rel(Ag.grad, A64.grad) < 1e-4
+    for name, p in op.named_parameters():
+        assert rel(p.grad, sd64[name].grad) < 1e-4, name
+
+
 @pytest.mark.parametrize("mode", ["spatial", "temporal"])
 @pytest.mark.parametrize("red", [1, 3, 8])
 def test_dstdgc_op_red_channels(mode, red):
