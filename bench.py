@@ -185,6 +185,19 @@ def model_block_bytes(opts, split_on):
     return phase3_moves(out, opts, split_on)
 
 
+def merge_blocks(blocks, fused_t):
+    """Each block as ONE launch (k_block_fused, the default wherever the fused
+    temporal kernel runs): its spatial GC, its temporal adjacency (built in
+    LDS) and its temporal GC (with phase 3) are one family, KIND_BLOCK."""
+    out = []
+    for b in blocks:
+        b = dict(b)
+        b[native.KIND_BLOCK] = b.pop(native.KIND_SPATIAL) + b.pop(native.KIND_TEMPORAL) + \
+            (b.pop(native.KIND_ADJ_T) if fused_t else 0)
+        out.append(b)
+    return out
+
+
 def model_block_flops(opts, split_on=False):
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V, C, L = opts["joints_to_consider"], opts["num_feature"], opts["num_layers"]
@@ -245,6 +258,7 @@ def split_instance(kind, T, V):
     """Kernel instantiation of DSTDGCB 1 (an encoder) for kind."""
     temporal = f"k_temporal_fused<{T}, {V}, 1, 64>" if (T, V) in FUSED_TEMPORAL else f"k_temporal_hl<{T}, 1, 64>"
     return {native.KIND_SPATIAL: f"k_spatial_hl<{V}, 64, 64>", native.KIND_TEMPORAL: temporal,
+            native.KIND_BLOCK: f"k_block_fused<{T}, {V}, 64, 64, 1>",
             native.KIND_ADJ_S: f"k_adj_hl<0, {T}, {2 * T}, {V}>", native.KIND_ADJ_T: f"k_adj_hl<1, {V}, {2 * V}, {T}>"}.get(kind)
 
 
@@ -298,22 +312,29 @@ def cpu_model():
     return None
 
 
-def config_leg(config, B, device, steps, warmup):
+def config_leg(config, B, device, steps, warmup, cpu_seconds=None):
     """Side measurement at N=1 (not `value`): the eval forward of another
     BASELINE.json config through the drop-in call model(x), fixture weights of
     that layout.  "h36m75": BASELINE.json's metric names "22J x 50T" while the
     shipped yaml (dstdgcn_h36m.yaml:137-138) runs 10 + 25 frames, so the
     '50 in / 25 out' T=75 variant is on the line too; "cmu" / "3dpw": configs
-    3 and the 3DPW shape at B=256."""
-    model, opts, _ = load_model(config, device)
+    3 and the 3DPW shape at B=256.  cpu_seconds: the leg's own CPU baseline
+    (the fp32 oracle on this host, same batch, same thread sweep as the main
+    line's, BASELINE.md "Official CPU-baseline plan") and the GPU/CPU ratio."""
+    model, opts, sd = load_model(config, device)
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V = opts["joints_to_consider"]
-    x = synth_input(B, T, V, opts["input_time_frame"], 1234).to(device)
+    x_cpu = synth_input(B, T, V, opts["input_time_frame"], 1234)
+    x = x_cpu.to(device)
     with torch.no_grad():
         ms, host = timed_calls(lambda: model(x), steps, max(warmup, 2))
-    return {"workload": CONFIGS[config][1] + f", B={B}, eval forward", "seq_len": T, "joints": V,
-            "value": round(B / ms * 1e3, 2), "unit": "seq/s", "ms_per_step": round(ms, 4),
-            "host_us_per_call": round(host, 2), "timed_call": "model(x)"}
+    out = {"workload": CONFIGS[config][1] + f", B={B}, eval forward", "seq_len": T, "joints": V,
+           "value": round(B / ms * 1e3, 2), "unit": "seq/s", "ms_per_step": round(ms, 4),
+           "host_us_per_call": round(host, 2), "timed_call": "model(x)"}
+    if cpu_seconds is not None:
+        out["cpu_baseline"] = cpu_baseline(opts, sd, x_cpu, cpu_seconds, 30.0)
+        out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
+    return out
 
 
 def timed_calls(fn, steps, warmup):
@@ -447,6 +468,8 @@ def main():
     ap.add_argument("--config", default="h36m", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--side-cpu-seconds", type=float, default=3.0,
+                    help="timed CPU oracle seconds (after the thread sweep) of each side config leg's own CPU baseline")
     ap.add_argument("--no-variant", action="store_true",
                     help="skip the side measurements of the other configs at N=1 (H36M '50 in / 25 out' T=75, "
                          "CMU and 3DPW at B=256)")
@@ -502,6 +525,11 @@ def main():
         for kind, _, ms in prof.elapsed():
             per_kind[kind] = per_kind.get(kind, 0.0) + ms
         prof.close()
+        split_on = model.gc_arithmetic == "split"
+        fused_t = split_on and (T, V) in FUSED_TEMPORAL
+        fused_b = native.KIND_BLOCK in per_kind  # the blocks ran as single launches (k_block_fused)
+        if fused_b:
+            fl = merge_blocks(fl, fused_t)
         dominant = max((k for k in per_kind if k in fl[0]), key=lambda k: per_kind[k])
 
         # timed region: exactly K steps; in one of every P steps two events
@@ -516,8 +544,8 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
-            # the drop-in call itself (DSTDGCN.forward -> torch.ops.dstd.dstdgcn_forward);
-            # a probed step carries the event brackets through the module
+            # the drop-in call itself (DSTDGCN.forward -> _forward_native -> the C
+            # ABI); a probed step carries the event brackets through the module
             if i % every == 0:
                 model._dstd_profile = probe
             h0 = time.perf_counter()
@@ -538,8 +566,9 @@ def main():
         # partials (the forward itself has no exchange)
         D.reduce_partials(y.double().abs().sum().reshape(1), torch.tensor([B], device=device))
 
-    split_on = model.gc_arithmetic == "split"
     bb = model_block_bytes(opts, split_on)
+    if fused_b:
+        bb = merge_blocks(bb, fused_t)
     kernel_ms = sum(ms for _, _, ms in launches)
     avg_launch_s = kernel_ms * 1e-3 / max(len(launches), 1)
     C = opts["num_feature"]
@@ -554,7 +583,6 @@ def main():
     # algorithmic FLOPs of the probed launch (the fused temporal launch also
     # builds its own adjacency and, phase 3, the next block's spatial one:
     # those families' FLOPs count to it -- phase3_moves did the latter)
-    fused_t = split_on and (T, V) in FUSED_TEMPORAL
     launch_flop = fl[1][dominant] + (fl[1][native.KIND_ADJ_T] if fused_t and dominant == native.KIND_TEMPORAL else 0)
     flops = launch_flop * B / avg_launch_s / 1e12 if kernel_ms > 0 else 0.0
     whole_bytes = model_compulsory_bytes(opts) * G * args.steps / elapsed / 1e9
@@ -584,8 +612,10 @@ def main():
                          "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "compulsory_bytes_per_launch": comp,
-                         "compulsory_basis": f"SURVEY §8(d): {op_compulsory_bytes(C, C, T, V)} B/seq (one 64->64 "
-                                             f"DSTDGC: input read + output written once) x {B} seq",
+                         "compulsory_basis": f"SURVEY §8(d): {op_compulsory_bytes(C, C, T, V)} B/seq (" +
+                                             ("one 64->64 DSTDGCB, the launch's whole block" if fused_b else
+                                              "one 64->64 DSTDGC") +
+                                             f": input read + output written once) x {B} seq",
                          "layout_bytes_per_launch": int(bb[1][dominant] * B) if launches else None,
                          "launches": len(launches), "probe_every": every,
                          "avg_launch_us": round(avg_launch_s * 1e6, 2),
@@ -603,18 +633,22 @@ def main():
             "kernel_ms_per_step_event_bracketed": {native.KIND_NAMES[k]: round(v / args.steps, 4)
                                                    for k, v in sorted(per_kind.items())},
             "host_us_per_call": round(host_s / args.steps * 1e6, 2),
-            "timed_call": "model(x): DSTDGCN.forward -> torch.ops.dstd.dstdgcn_forward (the drop-in path)",
+            "timed_call": "model(x): DSTDGCN.forward (the drop-in path) -> eager: DSTDGCN._forward_native -> "
+                          "dstd_model_fwd_ex, the implementation of torch.ops.dstd.dstdgcn_forward without the "
+                          "dispatcher's boxing (the op itself runs under tracing / torch.compile)",
         }
+        side_cpu = None if args.no_cpu_baseline else args.side_cpu_seconds
         if world == 1 and args.config == "h36m" and not args.no_variant:
-            out["variant_t75"] = config_leg("h36m75", B, device, args.steps, args.warmup)
-            out["cmu_b256"] = config_leg("cmu", B, device, args.steps, args.warmup)
-            out["3dpw_b256"] = config_leg("3dpw", B, device, args.steps, args.warmup)
+            out["variant_t75"] = config_leg("h36m75", B, device, args.steps, args.warmup, side_cpu)
+            out["cmu_b256"] = config_leg("cmu", B, device, args.steps, args.warmup, side_cpu)
+            out["3dpw_b256"] = config_leg("3dpw", B, device, args.steps, args.warmup, side_cpu)
         if world == 1 and not args.no_side:
             out["exact_fp32"] = arithmetic_leg(model, x, "fp32", args.steps, args.warmup)
             out["eval_b32"] = small_batch_leg(model, x, 32, max(args.steps, 100), args.warmup)
             out["train_b32"] = train_leg(device, 32, 20, 5)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(opts, sd, x_cpu, args.cpu_seconds, 30.0)
+            out["vs_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 1)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

@@ -111,6 +111,7 @@ struct BlockFold {
 struct BlockHL {
   bool s, t, tf;
   bool s_pre = false;  // the spatial adjacency planes were built by the previous block's temporal launch
+  bool bf = false;     // spatial + fused temporal GC in one launch (k_block_fused)
 };
 
 struct BlockScratch {
@@ -290,6 +291,9 @@ BlockHL block_hl(const dstd_block_params* p, const BlockTail& tail, int B, int T
   r.tf = r.t && temporal_fused_supported(T, V) &&
          ((B >= hl_device_cus() && temporal_fused_default(T, V)) || (flags & DSTD_FWD_FUSED_TEMPORAL));
 #endif
+  // the whole block as one launch wherever both GCs run split and the
+  // temporal one fused (one workgroup per sample either way)
+  r.bf = r.s && r.tf && !(flags & DSTD_FWD_SEPARATE_BLOCK) && block_fused_supported(T, V, p->cin, p->cout, tail.epi);
   return r;
 }
 
@@ -435,8 +439,8 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   if (e != hipSuccess) return e;
 
   // (2) spatial GC + bn + residual + prelu, P_t/Q_t of h
+  SpatialHLArgs ha{};
   if (hl.s) {
-    SpatialHLArgs ha{};
     ha.x = from_model ? xmodel : x;
     ha.xmodel = from_model ? 1 : 0;
     ha.B = B;
@@ -467,10 +471,12 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     ha.pqb[0] = p->conv_t.bm1;
     ha.pqb[1] = p->conv_t.bm2;
     ha.pq = sc.pq_t;
-    pf.begin(DSTD_KIND_SPATIAL, s);
-    e = launch_spatial_hl(ha, s);
-    pf.end(s);
-    if (e != hipSuccess) return e;
+    if (!hl.bf) {  // (k_block_fused runs it with the temporal GC, step 4)
+      pf.begin(DSTD_KIND_SPATIAL, s);
+      e = launch_spatial_hl(ha, s);
+      pf.end(s);
+      if (e != hipSuccess) return e;
+    }
   } else {
   SpatialArgs sa{};
   sa.x = x;
@@ -613,6 +619,12 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
       sn.out = reinterpret_cast<uint16_t*>(sc.adj_s);
       sn.out_sG = 2L * T * ncol;  // halves
       sn.out_sN = 2 * sn.out_sG;
+    }
+    if (hl.bf) {
+      pf.begin(DSTD_KIND_BLOCK, s);
+      e = launch_block_fused(ha, ht, aht, tail.next_adj ? &sn : nullptr, s);
+      pf.end(s);
+      return e;
     }
     pf.begin(DSTD_KIND_TEMPORAL, s);
     e = hl.tf ? launch_temporal_fused(ht, aht, tail.next_adj ? &sn : nullptr, s) : launch_temporal_hl(ht, s);
@@ -880,7 +892,7 @@ int dstd_block_fwd(const dstd_block_params* p, const float* x, int B, int T, int
 int dstd_block_fwd_ex(const dstd_block_params* p, const float* x, int B, int T, int V, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags) {
   StreamDeviceGuard dev_guard_(stream, x);
-  if (flags & ~(DSTD_FWD_EXACT_FP32 | DSTD_FWD_FUSED_TEMPORAL)) return DSTD_EINVAL;
+  if (flags & ~(DSTD_FWD_EXACT_FP32 | DSTD_FWD_FUSED_TEMPORAL | DSTD_FWD_SEPARATE_BLOCK)) return DSTD_EINVAL;
   if (!x || !y || !workspace || !block_ok(p) || !shape_ok(B, T, V)) return DSTD_EINVAL;
   if (!limits_ok(T, V, p->cin, p->cout)) return DSTD_ELIMIT;
   if (workspace_bytes < dstd_block_workspace_bytes(B, p->cin, p->cout, T, V)) return DSTD_EWORKSPACE;
@@ -918,7 +930,8 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
                       size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof) {
   StreamDeviceGuard dev_guard_(stream, x);
   const bool reuse = (flags & DSTD_FWD_REUSE_CONSTANTS) != 0;
-  if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32 | DSTD_FWD_SEPARATE_ADJ | DSTD_FWD_FUSED_TEMPORAL))
+  if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32 | DSTD_FWD_SEPARATE_ADJ | DSTD_FWD_FUSED_TEMPORAL |
+                DSTD_FWD_SEPARATE_BLOCK))
     return DSTD_EINVAL;
   if (!p || !x || !y || !workspace) return DSTD_EINVAL;
   if (prof && (prof->capacity < 0 || (prof->capacity > 0 && (!prof->events || !prof->kinds)))) return DSTD_EINVAL;

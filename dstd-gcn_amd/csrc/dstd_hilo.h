@@ -385,5 +385,13 @@ hipError_t launch_temporal_fused(const TemporalHLArgs& g, const AdjHLArgs& j, co
 bool temporal_fused_supported(int T, int V);
 bool temporal_fused_phase3(int T, int V);  // the next block's spatial adjacency in the same launch
 bool temporal_fused_default(int T, int V);  // fused at full batch without DSTD_FWD_FUSED_TEMPORAL
+// a whole DSTDGCB per sample (k_block_fused): the spatial GC of launch_spatial_hl
+// (sa) then the fused temporal GC of launch_temporal_fused (g, j, sn) in one
+// launch, one workgroup per sample; sa.y must be g.h and sa.pq j.pq.  The
+// block kinds of the model (6 -> 64 IN, 64 -> 64 ENC, 64 -> 3 OUT) at the
+// fused temporal kernel's shapes (not T = 75); hipErrorNotSupported elsewhere
+bool block_fused_supported(int T, int V, int cin, int cout, int epi);
+hipError_t launch_block_fused(const SpatialHLArgs& sa, const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn,
+                              hipStream_t s);
 
 }  // namespace dstd

@@ -44,8 +44,9 @@ extern "C" int dstd_debug_w(unsigned* host) {
 #ifdef DSTD_STAMPS
 // modes: 0 k_adj_hl<0>, 1 k_adj_hl<1>, 2 k_temporal_fused phase 3 (start,
 // E/F ready, tiles issued, stores drained), 3 k_temporal_fused C = 64 (entry,
-// chunk 0 phase 1 done, units done, exit)
-__device__ unsigned long long g_tl_hl[5][2048][4];
+// chunk 0 phase 1 done, units done, exit), 5 k_block_fused 64 -> 64 (entry,
+// spatial units done, after the barrier, exit)
+__device__ unsigned long long g_tl_hl[6][2048][4];
 #define TLH(m, i) \
   if (threadIdx.x == 0 && blockIdx.x < 2048) g_tl_hl[m][blockIdx.x][i] = __builtin_amdgcn_s_memrealtime();
 #else
@@ -138,12 +139,13 @@ __device__ __forceinline__ uint4 bldu4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 #ifndef DSTD_ADJ_ST_AUX
 #define DSTD_ADJ_ST_AUX 0
 #endif
+template <int AUX = DSTD_GC_ST_AUX>
 __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
 #ifdef DSTD_ABL_STORE
   if (v.x == 12345.f) off = 0;  // keep the value alive; store only lanes with nothing to store
   else off = OOB;
 #endif
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, DSTD_GC_ST_AUX);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, AUX);
 }
 
 // ---- range scaling helpers (dstd_hilo.h "range scaling") ----
@@ -471,7 +473,7 @@ __device__ __forceinline__ void stage_spatial(const SpatialHLArgs& a, SpatialSta
 // The spatial GC units u, u + ustep, ... < uend (unit = (sample, frame) =
 // n * T + t); load_adj_g(u, g, ab[NWT][2]) fetches the unit's graph-g
 // adjacency B fragments (hi, lo planes) for its two w tiles.
-template <int V, int CIN, int COUT, typename AdjLoad>
+template <int V, int CIN, int COUT, typename AdjLoad, bool LATE_RES = kSpLateRes, int ST_AUX = DSTD_GC_ST_AUX>
 __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const SpatialStage<V, CIN, COUT>& st, int u,
                                               int uend, int ustep, AdjLoad load_adj_g) {
   using SM = SlotMap<V, true>;
@@ -537,7 +539,7 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
       for (int wt = 0; wt < NWT; ++wt)
 #pragma unroll
         for (int ks = 0; ks < KSI; ++ks) row8(rx, rxl, 16 * wt + cl, 32 * ks + 8 * kl, xw[wt][ks][0], xw[wt][ks][1]);
-    } else if constexpr (!kSpLateRes) {
+    } else if constexpr (!LATE_RES) {
       load_res();
     }
     // this unit's graph-0 adjacency now, graph 1 after the first conv (a
@@ -647,7 +649,7 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
     // the identity residual after the aggregations (kSpLateRes: its 32
     // registers are not live through the convs; the frame was just read, so
     // the rows come from the cache)
-    if constexpr (!RES && kSpLateRes) {
+    if constexpr (!RES && LATE_RES) {
       __builtin_amdgcn_sched_barrier(0);
       load_res();
       __builtin_amdgcn_sched_barrier(0);
@@ -724,7 +726,7 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
         o[2] = prelu_m(fmaf(o[2], sc.z, sh.z) + r[2], pw, pc);
         o[3] = prelu_m(fmaf(o[3], sc.w, sh.w) + r[3], pw, pc);
         if constexpr (COUT % 4 == 0) {
-          bst4(ry, (uint32_t)((16 * wt + cl) * COUT + 16 * ct + 4 * kl) * 4, make_float4(o[0], o[1], o[2], o[3]));
+          bst4<ST_AUX>(ry, (uint32_t)((16 * wt + cl) * COUT + 16 * ct + 4 * kl) * 4, make_float4(o[0], o[1], o[2], o[3]));
         } else {
           static_assert(COUT == 3, "thin output: 3 channels");
           const uint32_t off = kl == 0 ? (uint32_t)(16 * wt + cl) * 12 : OOB;
@@ -777,7 +779,7 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
       const auto rp = rsrc(a.pq + (size_t)u * V * 4, V * 16);
 #pragma unroll
       for (int wt = 0; wt < NWT; ++wt)
-        bst4(rp, wpq0 + wt * 256,
+        bst4<ST_AUX>(rp, wpq0 + wt * 256,
              make_float4(fmaf(acc[wt][0], s, st.bql[0]), fmaf(acc[wt][1], s, st.bql[1]), fmaf(acc[wt][2], s, st.bql[2]),
                          fmaf(acc[wt][3], s, st.bql[3])));
     }
@@ -2073,8 +2075,12 @@ constexpr bool tf_phase3() {
 #endif
 template <int T, int V>
 constexpr int tf_waves() { return T == 35 && V == 22 ? DSTD_TF_NW_H36M : 8; }
+
+// The body of k_temporal_fused for sample n on the workgroup's dynamic LDS
+// dsm (TFusedGeom::LDS bytes): the kernel below runs it once, k_block_fused
+// after the sample's spatial GC.
 template <int T, int V, int EPI, int C>
-__global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_waves_per_eu((tf_waves<T, V>() / 4), (tf_waves<T, V>() / 4)))) void k_temporal_fused(TemporalFusedArgs fa) {
+__device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const int n, unsigned char* dsm) {
   using Gm = TFusedGeom<T, V, EPI, C>;
   using SM = typename Gm::SM;
   using EF = typename Gm::EF;
@@ -2084,7 +2090,6 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   constexpr float C2 = 2.8853900817779268f;       // 2*log2(e)
   const TemporalHLArgs& a = fa.g;
   const AdjHLArgs& j = fa.j;
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   _Float16* planes = reinterpret_cast<_Float16*>(dsm);
   unsigned char* un = dsm + Gm::PLANES;  // phase-1 scratch / phase-2 stage (union)
   float* El = reinterpret_cast<float*>(un);
@@ -2103,7 +2108,6 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   // VGPRs more and spilled)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = lane >> 4, cl = lane & 15;
-  const int n = blockIdx.x;  // one sample per workgroup
   if constexpr (C == 64) { TLH(3, 0) TLH(4, 0) }
 #ifdef DSTD_SETPRIO_TF  // (experiment, r05o: waves 4-11 +0.6%, 8-11 neutral at H36M -- off)
   if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= DSTD_SETPRIO_TF) __builtin_amdgcn_s_setprio(1);
@@ -2449,6 +2453,80 @@ __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_wave
   }
 }
 
+template <int T, int V, int EPI, int C>
+__global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_waves_per_eu((tf_waves<T, V>() / 4), (tf_waves<T, V>() / 4)))) void k_temporal_fused(TemporalFusedArgs fa) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  tfused_body<T, V, EPI, C>(fa, blockIdx.x, dsm);  // one sample per workgroup
+}
+
+// ===========================================================================
+// One whole DSTDGCB per sample (model/dstdgcn.py:141-163): the workgroup of
+// k_temporal_fused first runs the sample's spatial GC units (the T (sample,
+// frame) units of k_spatial_hl, its waves striding the frames), then, after a
+// barrier, the fused temporal GC of the same sample (tfused_body: temporal
+// adjacency in LDS, the joint units, the next block's spatial planes).  h and
+// the temporal P/Q of the sample pass between the phases through the CU's own
+// L1 / L2 (same workgroup: the barrier's workgroup-scope fence orders them, as
+// phase 3's P/Q reads); the spatial launch, its kernel boundary and its
+// grid-wide unit imbalance (T B units over the chip's waves) are gone.
+// ===========================================================================
+struct BlockFusedArgs {
+  SpatialHLArgs s;
+  TemporalFusedArgs t;
+};
+
+template <int T, int V, int CIN, int COUT, int EPI>
+struct BlockFusedGeom {
+  static constexpr size_t SP = sizeof(SpatialStage<V, CIN, COUT>);
+  static constexpr size_t TF = TFusedGeom<T, V, EPI, COUT>::LDS;
+  static constexpr size_t LDS = SP > TF ? SP : TF;
+  static_assert(LDS <= kLdsBudget, "LDS");
+};
+
+template <int T, int V, int CIN, int COUT, int EPI>
+__global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_waves_per_eu((tf_waves<T, V>() / 4), (tf_waves<T, V>() / 4)))) void k_block_fused(BlockFusedArgs ba) {
+  constexpr int NW = tf_waves<T, V>(), NT = 64 * NW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
+  const int n = blockIdx.x;  // one sample per workgroup
+  if constexpr (CIN == 64 && COUT == 64) { TLH(5, 0) }
+  {
+    using SM = SlotMap<V, true>;
+    constexpr int SL = SM::SL, NG = SM::NG, NWT = cdiv(V, 16);
+    auto& st = *reinterpret_cast<SpatialStage<V, CIN, COUT>*>(dsm);
+    stage_spatial<V, CIN, COUT, NT>(ba.s, st, threadIdx.x);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, kl = lane >> 4, cl = lane & 15;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const SpatialHLArgs& a = ba.s;
+    constexpr uint32_t adj_bytes = 2 * V * SL * 2;  // one (n, g, t) adjacency: 2 planes of V x SL halves
+    const uint32_t wadj0 = kl < NG ? (uint32_t)(cl * SL + 8 * kl) * 2 : OOB;
+    auto load_adj_g = [&](int uu, int g, uint4 (&ab)[NWT][2]) {
+      const int t = uu - n * T;
+      const uint16_t* base = a.adj + ((size_t)(n * 2 + g) * T + t) * (adj_bytes / 2);
+      const auto rh = rsrc(base, adj_bytes / 2), rl = rsrc(base + V * SL, adj_bytes / 2);
+#pragma unroll
+      for (int wt = 0; wt < NWT; ++wt) {
+        ab[wt][0] = bldu4(rh, wadj0 + wt * 32 * SL);
+        ab[wt][1] = bldu4(rl, wadj0 + wt * 32 * SL);
+      }
+    };
+    // (three waves per SIMD: the identity residual loaded after the
+    // aggregations, as DSTD_HL_WPE=3 builds of k_spatial_hl do, or it spills)
+    // (h and the temporal P/Q: DSTD_BF_ST_AUX, the cache policy of their
+    // stores -- the same CU reads them back right after the barrier)
+#ifndef DSTD_BF_ST_AUX
+#define DSTD_BF_ST_AUX DSTD_GC_ST_AUX
+#endif
+    spatial_units<V, CIN, COUT, decltype(load_adj_g), (NW > 8), DSTD_BF_ST_AUX>(a, st, n * T + wave, (n + 1) * T, NW,
+                                                                                 load_adj_g);
+  }
+  if constexpr (CIN == 64 && COUT == 64) { TLH(5, 1) }
+  __syncthreads();  // h and the temporal P/Q of sample n written; the spatial stage is dead
+  if constexpr (CIN == 64 && COUT == 64) { TLH(5, 2) }
+  tfused_body<T, V, EPI, COUT>(ba.t, n, dsm);
+  if constexpr (CIN == 64 && COUT == 64) { TLH(5, 3) }
+}
+
 // ===========================================================================
 // dispatch
 // ===========================================================================
@@ -2615,6 +2693,53 @@ hipError_t tfused_tv(const TemporalFusedArgs& a, hipStream_t s) {
   }
 }
 
+template <int T, int V, int CIN, int COUT, int EPI>
+hipError_t bfused_run(const BlockFusedArgs& a, hipStream_t s) {
+  using Gm = BlockFusedGeom<T, V, CIN, COUT, EPI>;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)k_block_fused<T, V, CIN, COUT, EPI>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::LDS);
+  if (attr != hipSuccess) return attr;
+  hipLaunchKernelGGL((k_block_fused<T, V, CIN, COUT, EPI>), dim3(a.t.g.B), dim3(64 * tf_waves<T, V>()), Gm::LDS, s, a);
+  return hipGetLastError();
+}
+
+// the model's three block kinds: conv_st_in (6 -> 64, IN tail), encoders
+// (64 -> 64, ENC tail), conv_st_out (64 -> 3, OUT tail)
+template <int T, int V>
+hipError_t bfused_tv(const BlockFusedArgs& a, hipStream_t s) {
+  const int cin = a.s.Cin, cout = a.s.Cout, epi = a.t.g.epi;
+  if (cin == 64 && cout == 64 && epi == TEPI_ENC) return bfused_run<T, V, 64, 64, TEPI_ENC>(a, s);
+  if (cin == 6 && cout == 64 && epi == TEPI_IN) return bfused_run<T, V, 6, 64, TEPI_IN>(a, s);
+  if (cin == 64 && cout == 3 && epi == TEPI_OUT) return bfused_run<T, V, 64, 3, TEPI_OUT>(a, s);
+  return hipErrorNotSupported;
+}
+
+bool block_fused_supported(int T, int V, int cin, int cout, int epi) {
+#ifdef DSTD_NO_BFUSED
+  return false;
+#endif
+  const bool shape = (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23);
+  return shape && ((cin == 64 && cout == 64 && epi == TEPI_ENC) || (cin == 6 && cout == 64 && epi == TEPI_IN) ||
+                   (cin == 64 && cout == 3 && epi == TEPI_OUT));
+}
+
+hipError_t launch_block_fused(const SpatialHLArgs& sa, const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn,
+                              hipStream_t s) {
+  if (!block_fused_supported(g.T, g.V, sa.Cin, sa.Cout, g.epi) || sa.T != g.T || sa.V != g.V || sa.B != g.B ||
+      sa.Cout != g.C || sa.y != g.h || sa.pq != j.pq || g.V != (int)(j.pql.st / 4) || j.pql.sch != 1 || j.pql.sv != 4 ||
+      ((uintptr_t)j.pq & 15))
+    return hipErrorNotSupported;
+  if (sn && (!temporal_fused_phase3(g.T, g.V) || g.C != 64 || !g.pq || sn->pq != g.pq || sn->ngroups != 2 || sn->xin ||
+             sn->pql.sch != 1 || (sn->pql.st & 3) || (sn->pql.sv & 3) || (sn->pql.sn & 3) || (sn->p_ch[0] & 3) ||
+             (sn->p_ch[1] & 3) || !sn->out))
+    return hipErrorNotSupported;
+  const BlockFusedArgs a{sa, TemporalFusedArgs{g, j, sn ? *sn : AdjHLArgs{}}};
+  if (g.T == 35 && g.V == 22) return bfused_tv<35, 22>(a, s);
+  if (g.T == 35 && g.V == 25) return bfused_tv<35, 25>(a, s);
+  if (g.T == 40 && g.V == 23) return bfused_tv<40, 23>(a, s);
+  return hipErrorNotSupported;
+}
+
 bool temporal_fused_supported(int T, int V) {
   return (T == 35 && (V == 22 || V == 25)) || (T == 40 && V == 23) || (T == 75 && V == 22);
 }
@@ -2666,7 +2791,7 @@ hipError_t launch_temporal_hl(const TemporalHLArgs& a, hipStream_t s) {
 
 #ifdef DSTD_STAMPS
 extern "C" int dstd_debug_timeline_hl(int mode, unsigned long long* host, int n) {
-  if (mode < 0 || mode > 4 || n > 2048 * 4) return 1;
+  if (mode < 0 || mode > 5 || n > 2048 * 4) return 1;
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tl_hl), n * sizeof(unsigned long long),
                                   mode * 2048 * 4 * sizeof(unsigned long long));
 }

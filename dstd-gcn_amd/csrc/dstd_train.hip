@@ -2,6 +2,7 @@
 // strides and small: the config-5 training batch is 32 sequences per GPU, so
 // these kernels favour simple, deterministic reductions (fixed-order partials,
 // no float atomics) over the hand-scheduled pipelines of the inference path.
+#include <atomic>
 #include "dstd_common.h"
 #include "dstd_train.h"
 
@@ -2664,6 +2665,10 @@ hipError_t agg_fwd(const float* F, long long fs, const float* D, float* y, long 
   return agg_launch_c(false, g, B, temporal, s);
 }
 
+// which kernel the last agg_bwd dispatched (dstd_debug_aggb_last): the
+// channel-chunk kernel's chunk width, or 0 for the two-launch path
+static std::atomic<int> g_aggb_last{-1};
+
 hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys, const float* D, float* dF,
                    long long dfs, float* dD, int B, int C, int T, int V, int temporal, hipStream_t s, float* dDpart,
                    int* nparts) {
@@ -2680,46 +2685,54 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
 #ifndef DSTD_AGGB_CW_SP
 #define DSTD_AGGB_CW_SP 64
 #endif
-  // (row tiles 1, 2 or 4: 3 runs as 4, cv masking the fourth)
-  const int mf0 = temporal ? 1 : std::min(DSTD_AGGB_CW_SP / 16, cdiv(C, 16)), mfc = mf0 == 3 ? 4 : mf0, cw = 16 * mfc;
-  const int cch = cdiv(C, cw);
-  *nparts = 1;
-  if (cch == 1 || dDpart) {
-    if (cch > 1) g.dD = dDpart, *nparts = cch;
+  // (row tiles 1, 2 or 4: 3 runs as 4, cv masking the fourth).  When the
+  // preferred chunk's slab does not fit LDS (large batches split fewer frames
+  // per workgroup: H36M / 3DPW at B=256 need 231-264 KB at 64 channels) the
+  // 16-channel chunk is tried before the two-launch path (dF kernel + dD
+  // a-chunk kernel)
+  const int mf_pref = temporal ? 1 : std::min(DSTD_AGGB_CW_SP / 16, cdiv(C, 16));
+  const int tries[2] = {mf_pref == 3 ? 4 : mf_pref, 1};
+  for (int ti = 0; ti < (tries[0] == 1 ? 1 : 2); ++ti) {
+    const int mfc = tries[ti], cw = 16 * mfc;
+    const int cch = cdiv(C, cw);
+    if (!(cch == 1 || dDpart)) continue;
+    g.dD = cch > 1 ? dDpart : dD;
     g.B = B;
     agg_tile(g.NN, g.RK, g.P);
     g.QP = agg_split(g, B, temporal, DSTD_AGGB_SPLIT_WG, cw);
     while ((g.QP & 63) != 4) ++g.QP;
     const int nth = aggcb_threads(temporal);
     const size_t lds = sizeof(float) * ((size_t)2 * cw * g.QP + (size_t)(nth / 64) * g.RK * g.P);
-    if (lds <= 160 * 1024) {
-      g.vec = (g.TV % 4 == 0 && g.xs % 4 == 0 && g.os % 4 == 0 && g.y0s % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
-               ((uintptr_t)g.O & 15) == 0 && ((uintptr_t)g.Y0 & 15) == 0);
-      const dim3 grid(B * cch * g.asplit), block(nth);
-      const int jf = cdiv(g.NN, 16);
-      auto pick = [&](auto tb, auto mb) {
-        constexpr bool T_ = decltype(tb)::value;
-        constexpr int M_ = decltype(mb)::value;
-        switch (jf) {
-          case 1: agg_go(k_aggc_bwd<T_, 1, M_>, grid, block, lds, g, s); break;
-          case 2: agg_go(k_aggc_bwd<T_, 2, M_>, grid, block, lds, g, s); break;
-          case 3: agg_go(k_aggc_bwd<T_, 3, M_>, grid, block, lds, g, s); break;
-          default: agg_go(k_aggc_bwd<T_, 4, M_>, grid, block, lds, g, s); break;
-        }
-      };
-      if (temporal) pick(std::true_type(), std::integral_constant<int, 1>());
-      else if (mfc == 1) pick(std::false_type(), std::integral_constant<int, 1>());
+    if (lds > 160 * 1024) continue;
+    *nparts = cch;
+    g_aggb_last.store(cw, std::memory_order_relaxed);
+    g.vec = (g.TV % 4 == 0 && g.xs % 4 == 0 && g.os % 4 == 0 && g.y0s % 4 == 0 && ((uintptr_t)g.X & 15) == 0 &&
+             ((uintptr_t)g.O & 15) == 0 && ((uintptr_t)g.Y0 & 15) == 0);
+    const dim3 grid(B * cch * g.asplit), block(nth);
+    const int jf = cdiv(g.NN, 16);
+    auto pick = [&](auto tb, auto mb) {
+      constexpr bool T_ = decltype(tb)::value;
+      constexpr int M_ = decltype(mb)::value;
+      switch (jf) {
+        case 1: agg_go(k_aggc_bwd<T_, 1, M_>, grid, block, lds, g, s); break;
+        case 2: agg_go(k_aggc_bwd<T_, 2, M_>, grid, block, lds, g, s); break;
+        case 3: agg_go(k_aggc_bwd<T_, 3, M_>, grid, block, lds, g, s); break;
+        default: agg_go(k_aggc_bwd<T_, 4, M_>, grid, block, lds, g, s); break;
+      }
+    };
+    if (temporal) pick(std::true_type(), std::integral_constant<int, 1>());
+    else if (mfc == 1) pick(std::false_type(), std::integral_constant<int, 1>());
 #if DSTD_AGGB_CW_SP >= 32
-      else if (mfc == 2) pick(std::false_type(), std::integral_constant<int, 2>());
+    else if (mfc == 2) pick(std::false_type(), std::integral_constant<int, 2>());
 #endif
 #if DSTD_AGGB_CW_SP >= 64
-      else pick(std::false_type(), std::integral_constant<int, 4>());
+    else pick(std::false_type(), std::integral_constant<int, 4>());
 #endif
-      return hipGetLastError();
-    }
-    *nparts = 1;
-    g.dD = dD;
+    return hipGetLastError();
   }
+  *nparts = 1;
+  g.dD = dD;
+  g_aggb_last.store(0, std::memory_order_relaxed);
   AggArgs c = agg_geom(C, T, V, temporal);  // dF = dy . D^T per a
   c.X = dy, c.xs = dys, c.Dm = D, c.O = dF, c.os = dfs;
   const hipError_t e = agg_launch_c(true, c, B, temporal, s);
@@ -2733,6 +2746,14 @@ hipError_t agg_bwd(const float* F, long long fs, const float* dy, long long dys,
 }
 
 
+
+}  // namespace train
+}  // namespace dstd
+
+extern "C" int dstd_debug_aggb_last(void) { return dstd::train::g_aggb_last.load(std::memory_order_relaxed); }
+
+namespace dstd {
+namespace train {
 
 hipError_t tanh_outer_fwd(const float* P, const float* Q, PQView v, int B, int R, int A, int NN, float* M,
                           hipStream_t s) {

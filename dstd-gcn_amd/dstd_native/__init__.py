@@ -92,8 +92,9 @@ FWD_REUSE_CONSTANTS = 1  # include/dstd_gcn.h DSTD_FWD_REUSE_CONSTANTS
 FWD_EXACT_FP32 = 2  # include/dstd_gcn.h DSTD_FWD_EXACT_FP32
 FWD_SEPARATE_ADJ = 4  # include/dstd_gcn.h DSTD_FWD_SEPARATE_ADJ
 FWD_FUSED_TEMPORAL = 8  # include/dstd_gcn.h DSTD_FWD_FUSED_TEMPORAL
-KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL = range(6)
-KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temporal_gc")
+FWD_SEPARATE_BLOCK = 16  # include/dstd_gcn.h DSTD_FWD_SEPARATE_BLOCK
+KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL, KIND_BLOCK = range(7)
+KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temporal_gc", "block")
 
 _lib = None
 
@@ -249,7 +250,8 @@ TRAIN_EXPORTS = ("dstd_dstdgc_train_saved_bytes", "dstd_dstdgc_train_workspace_b
                  "dstd_block_train_fwd_ex", "dstd_block_train_bwd_ex", "dstd_model_train_fwd_ex",
                  "dstd_model_train_bwd_ex", "dstd_dstdgc_train_saved_bytes_r",
                  "dstd_dstdgc_train_workspace_bytes_r", "dstd_dstdgc_train_fwd_r", "dstd_dstdgc_train_bwd_r",
-                 "dstd_bn_sync_buffer_floats", "dstd_model_train_fwd_sync", "dstd_model_train_bwd_sync")
+                 "dstd_bn_sync_buffer_floats", "dstd_model_train_fwd_sync", "dstd_model_train_bwd_sync",
+                 "dstd_debug_aggb_last")
 AUX_EXPORTS = ("dstd_ctg_workspace_bytes", "dstd_ctg_fwd", "dstd_ctg_bwd", "dstd_conv2d_workspace_bytes",
                "dstd_conv2d_fwd", "dstd_conv2d_bwd")
 

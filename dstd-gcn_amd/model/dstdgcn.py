@@ -407,14 +407,22 @@ class _BlockTrain(torch.autograd.Function):
 
 
 @torch._dynamo.disable
-def _host_seed():
+def _host_seed(model):
     """A dropout seed for the op branch of _ModelTrain: an integer drawn on
     the host at run time (under torch.compile this is a graph break, not a
     traced random value -- dynamo would turn one into a tensor, which the ops'
-    integer `seed` cannot take).  Drawn from torch's CPU generator, so
-    torch.manual_seed makes compiled training with dropout reproducible like
-    the eager path."""
-    return int(torch.randint(0, 2 ** 62, (1,)).item())
+    integer `seed` cannot take).  Taken from the model device's generator --
+    the one the eager branch draws its device seed from -- as its (seed,
+    philox offset) pair, whose offset it then advances as one device draw
+    would: torch.manual_seed makes compiled training with dropout
+    reproducible, compiled and eager steps consume the same stream, and the
+    global CPU stream (samplers, DataLoader base seeds) is not touched
+    (ADVICE r05)."""
+    dev = next(model.parameters()).device
+    g = torch.cuda.default_generators[dev.index if dev.index is not None else torch.cuda.current_device()]
+    seed, off = g.initial_seed(), g.get_offset()
+    g.set_offset(off + 4)
+    return (seed * 0x9E3779B97F4A7C15 + (off + 1) * 0xBF58476D1CE4E5B9) % (2 ** 62)
 
 
 class _ModelTrain(torch.autograd.Function):
@@ -450,7 +458,7 @@ class _ModelTrain(torch.autograd.Function):
             # (and a FakeTensor has no data pointer).  Drawn outside the traced
             # region (_host_seed), so it stays an integer and every compiled call
             # gets a new mask
-            seed = _host_seed()
+            seed = _host_seed(model)
         buffers = model._tree.get(model)[1]
         if eager:
             # eager: the op's implementation without the dispatcher's boxing

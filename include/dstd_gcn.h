@@ -134,14 +134,16 @@ int dstd_model_fwd(const dstd_model_params* p, const float* x, int B, float* y, 
 /* ---- measurement hooks (bench.py) ---------------------------------------
  * Kernel families of one forward, in launch order per DSTDGCB:
  *   ADJ_S (tanh GEMM, both graphs), SPATIAL (spatial GC + mid epilogue),
- *   ADJ_T (tanh GEMM), TEMPORAL (temporal GC + tail epilogue). */
+ *   ADJ_T (tanh GEMM), TEMPORAL (temporal GC + tail epilogue); BLOCK: the
+ *   whole DSTDGCB in one launch (spatial + temporal GC, DSTD_FWD_SEPARATE_BLOCK). */
 #define DSTD_KIND_FOLD 0
 #define DSTD_KIND_PREP 1
 #define DSTD_KIND_ADJ_S 2
 #define DSTD_KIND_SPATIAL 3
 #define DSTD_KIND_ADJ_T 4
 #define DSTD_KIND_TEMPORAL 5
-#define DSTD_KIND_COUNT 6
+#define DSTD_KIND_BLOCK 6
+#define DSTD_KIND_COUNT 7
 
 /* Every launch whose family bit is set in kind_mask is bracketed by a
  * (start, stop) pair of hipEvents taken from events[2*i], events[2*i+1];
@@ -192,6 +194,13 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
  * is faster.  Same results either way; for testing and A/B.  Also accepted by
  * dstd_block_fwd_ex. */
 #define DSTD_FWD_FUSED_TEMPORAL 8u
+/* Launch schedule: the spatial and the temporal graph convolution of a block
+ * in two launches (k_spatial_hl, then k_temporal_fused) instead of one
+ * (k_block_fused: one workgroup per sample runs the sample's spatial GC, then
+ * its fused temporal GC; the default wherever the fused temporal kernel runs
+ * and the block is one of the model's three kinds).  Same results bit for
+ * bit; for testing and A/B.  Also accepted by dstd_block_fwd_ex. */
+#define DSTD_FWD_SEPARATE_BLOCK 16u
 int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof);
 int dstd_events_create(int n, void** events);

@@ -223,6 +223,12 @@ int dstd_frame_mpjpe(const float* all_seqs, const float* outputs, int B, int T, 
                      const int* used_pos, int n_used, const int* joint_src, const int* frames, int n_frames,
                      float* sums, void* stream);
 
+/* Diagnostics: which kernel the last spatial/temporal aggregation backward of
+ * this process dispatched -- the channel-chunk kernel's chunk width (16, 32 or
+ * 64 channels per workgroup) or 0 for the two-launch path (dF kernel + dD
+ * a-chunk kernel); -1 before the first.  Host-side record for tests. */
+int dstd_debug_aggb_last(void);
+
 #ifdef __cplusplus
 }
 #endif

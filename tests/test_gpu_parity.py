@@ -288,6 +288,32 @@ def test_fused_temporal_schedule_bit_identical(tag):
         assert torch.equal(y0, y1), (tag, x.shape[0], float((y0 - y1).abs().max()))
 
 
+@pytest.mark.parametrize("tag", ["h36m", "cmu", "3dpw"])
+def test_block_fused_schedule_bit_identical(tag):
+    """Wherever the fused temporal kernel runs (B >= the CU count by default,
+    any B with DSTD_FWD_FUSED_TEMPORAL) each of the model's blocks is ONE
+    launch (k_block_fused: a sample's spatial GC units, then its fused
+    temporal GC); DSTD_FWD_SEPARATE_BLOCK runs the two GCs as two launches
+    (k_spatial_hl, k_temporal_fused).  The same unit code in the same order:
+    bit-identical at the bench batch (B=256, the default schedule), at a ragged
+    small batch and for inputs x1000 (range-scaled operands)."""
+    import dstd_native as native
+    m, d, _, opts = load_model(tag)
+    T = opts["input_time_frame"] + opts["output_time_frame"]
+    V = opts["joints_to_consider"]
+    cases = [(synth(256, T, V, opts["input_time_frame"], 5).to(DEV), 0),
+             (synth(7, T, V, opts["input_time_frame"], 6).to(DEV), native.FWD_FUSED_TEMPORAL),
+             ((synth(16, T, V, opts["input_time_frame"], 8) * 1000.0).to(DEV), native.FWD_FUSED_TEMPORAL)]
+    for x, fl in cases:
+        y0, y1 = torch.empty_like(x), torch.empty_like(x)
+        with torch.no_grad():
+            m._forward_native(x, y0, arith=fl)
+            m._forward_native(x, y1, arith=fl | native.FWD_SEPARATE_BLOCK)
+        torch.cuda.synchronize()
+        assert torch.isfinite(y0).all()
+        assert torch.equal(y0, y1), (tag, x.shape[0], float((y0 - y1).abs().max()))
+
+
 @pytest.mark.parametrize("cin,cout", [(64, 64), (6, 64), (64, 3)])
 def test_fused_temporal_schedule_bit_identical_block(cin, cout):
     """The same at block level (dstd_block_fwd_ex), with a large adjacency
@@ -729,6 +755,17 @@ def test_torch_library_ops_opcheck_and_compile():
     yc.square().sum().backward()
     assert torch.isfinite(yc).all() and xg.grad is not None and torch.isfinite(xg.grad).all()
     assert m.conv_st_out.stgcn[0][0].conv_t[0].conv_f.weight.grad is not None
+    # its dropout seed comes from the model's own generator (seeded from
+    # torch.initial_seed()): reproducible under torch.manual_seed, and the
+    # global CPU stream is not advanced
+    with torch.no_grad():
+        torch.manual_seed(3)
+        rng = torch.get_rng_state()
+        y1 = mc(x)
+        assert torch.equal(torch.get_rng_state(), rng)
+        torch.manual_seed(3)
+        y2 = mc(x)
+    assert torch.equal(y1, y2)
     m.do_in.p = 0.0
     m.zero_grad(set_to_none=True)
     blk = m.encoders[0][0].stgcn[0][0]

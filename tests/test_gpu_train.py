@@ -28,6 +28,7 @@ import numpy as np
 import pytest
 import torch
 
+import dstd_native as native
 from conftest import group, load_npz
 from model import DSTDGC, DSTDGCB, get_model
 from oracle import dstdgcn_oracle as O
@@ -98,11 +99,14 @@ def test_dstdgc_op_backward(mode, cin, cout, T, V):
 
 
 def test_dstdgc_op_backward_partial_row_tiles():
-    """Spatial op with 40 output channels at B=128: the backward aggregation
+    """Spatial op with 40 output channels at B=64: the backward aggregation
     runs its 4-row-tile (64-channel) kernel over 40 channels with every wave
-    busy (12 frames per workgroup), so its LDS must be sized for 64 rows
+    busy (8 frames per workgroup on a 256-CU device: slab 196 floats per
+    channel row, 100 KB of LDS sized for 64 rows), and the test checks that
+    this kernel is the one that ran (dstd_debug_aggb_last); at B=128 the
+    64-row slab would not fit and the dispatch takes the 16-channel kernel
     (reference model/dstdgcn.py:80-87 under autograd, fp64 oracle)."""
-    mode, cin, cout, T, V, B = "spatial", 32, 40, 40, 23, 128
+    mode, cin, cout, T, V, B = "spatial", 32, 40, 40, 23, 64
     torch.manual_seed(5)
     op = DSTDGC(cin, cout, T, V, mode=mode)
     randomise(op, 77)
@@ -116,6 +120,37 @@ def test_dstdgc_op_backward_partial_row_tiles():
     op = op.to(DEV)
     xg, Ag, ag = (t.to(DEV).requires_grad_(True) for t in (x, A, alpha))
     (op(xg, Ag, ag) * w.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    if torch.cuda.get_device_properties(0).multi_processor_count == 256:
+        assert native.lib().dstd_debug_aggb_last() == 64
+    assert rel(xg.grad, x64.grad) < 1e-4
+    assert rel(Ag.grad, A64.grad) < 1e-4
+    for name, p in op.named_parameters():
+        assert rel(p.grad, sd64[name].grad) < 1e-4, name
+
+
+def test_aggb_dispatch_falls_back_to_16_channel_chunks():
+    """Where the 64-channel slab of the spatial aggregation backward does not
+    fit LDS (B=128 above; the model's H36M / 3DPW ops at B=256) the dispatch
+    retries the 16-channel kernel before the two-launch path:
+    the backward runs it and meets the same fp64 bar."""
+    mode, cin, cout, T, V, B = "spatial", 32, 40, 40, 23, 128
+    torch.manual_seed(6)
+    op = DSTDGC(cin, cout, T, V, mode=mode)
+    randomise(op, 78)
+    x = torch.randn(B, cin, T, V)
+    A = 0.3 * torch.randn(1, V, V)
+    alpha = torch.tensor([0.7])
+    w = torch.randn(B, cout, T, V)
+    sd64 = {k: v.detach().double().requires_grad_(True) for k, v in op.state_dict().items()}
+    x64, A64, a64 = (t.double().requires_grad_(True) for t in (x, A, alpha))
+    (O.dstdgc(x64, sd64, A64, a64.reshape(()), mode) * w.double()).sum().backward()
+    op = op.to(DEV)
+    xg, Ag, ag = (t.to(DEV).requires_grad_(True) for t in (x, A, alpha))
+    (op(xg, Ag, ag) * w.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    if torch.cuda.get_device_properties(0).multi_processor_count == 256:
+        assert native.lib().dstd_debug_aggb_last() == 16
     assert rel(xg.grad, x64.grad) < 1e-4
     assert rel(Ag.grad, A64.grad) < 1e-4
     for name, p in op.named_parameters():
