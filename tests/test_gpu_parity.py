@@ -291,12 +291,13 @@ def test_fused_temporal_schedule_bit_identical(tag):
 @pytest.mark.parametrize("tag", ["h36m", "cmu", "3dpw"])
 def test_block_fused_schedule_bit_identical(tag):
     """Wherever the fused temporal kernel runs (B >= the CU count by default,
-    any B with DSTD_FWD_FUSED_TEMPORAL) each of the model's blocks is ONE
-    launch (k_block_fused: a sample's spatial GC units, then its fused
-    temporal GC); DSTD_FWD_SEPARATE_BLOCK runs the two GCs as two launches
-    (k_spatial_hl, k_temporal_fused).  The same unit code in the same order:
-    bit-identical at the bench batch (B=256, the default schedule), at a ragged
-    small batch and for inputs x1000 (range-scaled operands)."""
+    any B with DSTD_FWD_FUSED_TEMPORAL) each block is ONE launch
+    (k_block_fused: a sample's spatial GC units, then its fused temporal GC);
+    DSTD_FWD_SEPARATE_BLOCK runs two per block (k_spatial_hl,
+    k_temporal_fused).
+    The same unit code in the same order: bit-identical at the bench batch
+    (B=256, the default schedule), at a ragged small batch and for inputs
+    x1000 (range-scaled operands)."""
     import dstd_native as native
     m, d, _, opts = load_model(tag)
     T = opts["input_time_frame"] + opts["output_time_frame"]
