@@ -198,16 +198,6 @@ def merge_blocks(blocks, fused_t):
     return out
 
 
-def merge_model(blocks):
-    """The whole model after block 0's spatial adjacency as ONE launch
-    (k_model_fused, the default wherever every block runs fused): every
-    block's KIND_BLOCK family summed into block 0's KIND_MODEL (the launch's
-    block index is -1; block 0 keeps its adjacency launch)."""
-    out = [dict(b) for b in blocks]
-    out[0][native.KIND_MODEL] = sum(b.pop(native.KIND_BLOCK) for b in out)
-    return out
-
-
 def model_block_flops(opts, split_on=False):
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V, C, L = opts["joints_to_consider"], opts["num_feature"], opts["num_layers"]
@@ -268,7 +258,7 @@ def split_instance(kind, T, V):
     """Kernel instantiation of DSTDGCB 1 (an encoder) for kind."""
     temporal = f"k_temporal_fused<{T}, {V}, 1, 64>" if (T, V) in FUSED_TEMPORAL else f"k_temporal_hl<{T}, 1, 64>"
     return {native.KIND_SPATIAL: f"k_spatial_hl<{V}, 64, 64>", native.KIND_TEMPORAL: temporal,
-            native.KIND_BLOCK: f"k_block_fused<{T}, {V}, 64, 64, 1>", native.KIND_MODEL: f"k_model_fused<{T}, {V}>",
+            native.KIND_BLOCK: f"k_block_fused<{T}, {V}, 64, 64, 1>",
             native.KIND_ADJ_S: f"k_adj_hl<0, {T}, {2 * T}, {V}>", native.KIND_ADJ_T: f"k_adj_hl<1, {V}, {2 * V}, {T}>"}.get(kind)
 
 
@@ -537,12 +527,9 @@ def main():
         prof.close()
         split_on = model.gc_arithmetic == "split"
         fused_t = split_on and (T, V) in FUSED_TEMPORAL
-        fused_m = native.KIND_MODEL in per_kind  # the whole model after block 0's adjacency: one launch
-        fused_b = fused_m or native.KIND_BLOCK in per_kind  # the blocks ran as single launches (k_block_fused)
+        fused_b = native.KIND_BLOCK in per_kind  # the blocks ran as single launches (k_block_fused)
         if fused_b:
             fl = merge_blocks(fl, fused_t)
-        if fused_m:
-            fl = merge_model(fl)
         dominant = max((k for k in per_kind if k in fl[0]), key=lambda k: per_kind[k])
 
         # timed region: exactly K steps; in one of every P steps two events
@@ -550,7 +537,7 @@ def main():
         # event pair in every step slows the whole step by ~5%
         every = max(1, args.probe_every)
         prof = Profiler(L, (args.steps + every - 1) // every, 1 << dominant)
-        prof.prof.only_block = -1 if dominant == native.KIND_MODEL else 1
+        prof.prof.only_block = 1
         probe = ctypes.byref(prof.prof)
         host_s = 0.0
         barrier()
@@ -582,25 +569,21 @@ def main():
     bb = model_block_bytes(opts, split_on)
     if fused_b:
         bb = merge_blocks(bb, fused_t)
-    if fused_m:
-        bb = merge_model(bb)
     kernel_ms = sum(ms for _, _, ms in launches)
     avg_launch_s = kernel_ms * 1e-3 / max(len(launches), 1)
     C = opts["num_feature"]
     # compulsory bytes of the probed launch: DSTDGCB 1 is a 64 -> 64 block; its
     # spatial / temporal GC launch is one DSTDGC's input read + output write
-    whole = dominant == native.KIND_MODEL  # the probed launch is the whole forward (but block 0's adjacency)
-    comp = (model_compulsory_bytes(opts) if whole else op_compulsory_bytes(C, C, T, V)) * B
+    comp = op_compulsory_bytes(C, C, T, V) * B
     achieved = comp / avg_launch_s / 1e9 if kernel_ms > 0 else 0.0
     kname = native.KIND_NAMES[dominant]
     split_blk = split_on and opts["num_layers"] > 0
     traffic = load_traffic(kname + "_split" if split_blk else kname, split_instance(dominant, T, V) if split_blk else None)
-    lb = 0 if whole else 1  # the probed launch's block (the whole-model launch carries block 0's slot)
     total_flop_per_seq = sum(sum(b.values()) for b in fl)
     # algorithmic FLOPs of the probed launch (the fused temporal launch also
     # builds its own adjacency and, phase 3, the next block's spatial one:
     # those families' FLOPs count to it -- phase3_moves did the latter)
-    launch_flop = fl[lb][dominant] + (fl[lb][native.KIND_ADJ_T] if fused_t and dominant == native.KIND_TEMPORAL else 0)
+    launch_flop = fl[1][dominant] + (fl[1][native.KIND_ADJ_T] if fused_t and dominant == native.KIND_TEMPORAL else 0)
     flops = launch_flop * B / avg_launch_s / 1e12 if kernel_ms > 0 else 0.0
     whole_bytes = model_compulsory_bytes(opts) * G * args.steps / elapsed / 1e9
 
@@ -625,18 +608,15 @@ def main():
             "config": {"workload": CONFIGS[args.config][1] + (f", {G} sequences over {world} GPU(s)" if strong else
                                                               f", B={B}/GPU") + ", eval forward",
                        "global_batch": G, "seq_len": T, "joints": V, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm", "kernel": kname + (" (split-f16, all 7 DSTDGCBs: k_model_fused)" if whole else
-                                                            " (split-f16, DSTDGCB 1)" if split_blk else " (DSTDGCB 1)"),
+            "roofline": {"bound": "hbm", "kernel": kname + (" (split-f16, DSTDGCB 1)" if split_blk else " (DSTDGCB 1)"),
                          "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "compulsory_bytes_per_launch": comp,
-                         "compulsory_basis": (f"SURVEY §8(d): {model_compulsory_bytes(opts)} B/seq (every DSTDGCB "
-                                              f"of the forward: input read + output written once) x {B} seq" if whole
-                                              else f"SURVEY §8(d): {op_compulsory_bytes(C, C, T, V)} B/seq (" +
-                                              ("one 64->64 DSTDGCB, the launch's whole block" if fused_b else
-                                               "one 64->64 DSTDGC") +
-                                              f": input read + output written once) x {B} seq"),
-                         "layout_bytes_per_launch": int(bb[lb][dominant] * B) if launches else None,
+                         "compulsory_basis": f"SURVEY §8(d): {op_compulsory_bytes(C, C, T, V)} B/seq (" +
+                                             ("one 64->64 DSTDGCB, the launch's whole block" if fused_b else
+                                              "one 64->64 DSTDGC") +
+                                             f": input read + output written once) x {B} seq",
+                         "layout_bytes_per_launch": int(bb[1][dominant] * B) if launches else None,
                          "launches": len(launches), "probe_every": every,
                          "avg_launch_us": round(avg_launch_s * 1e6, 2),
                          "compute": {"flop_per_launch": launch_flop * B, "achieved_tflops": round(flops, 2),

@@ -332,11 +332,9 @@ void add_block_hl_jobs(HLList& l, const dstd_block_params* p, const BlockFold& f
 // xmodel (conv_st_in of the model, split spatial only): the model input
 // [B][T][V][3]; the kernels build x6 and block-0's spatial P/Q from it, x is
 // not read.
-// capture (hl.bf only): fill the block's k_block_fused arguments instead of
-// launching it (the whole-model launch runs every block, k_model_fused)
 hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const BlockScratch& sc, int B, int T, int V,
                      const float* x, float* h, float* y, const BlockTail& tail, hipStream_t s, Prof& pf,
-                     const BlockHL& hl, const float* xmodel = nullptr, BlockFusedArgs* capture = nullptr) {
+                     const BlockHL& hl, const float* xmodel = nullptr) {
   const bool res = p->cin != p->cout;
   const bool from_model = xmodel && hl.s && p->cin == 6;
   // (1) spatial adjacency for both graphs
@@ -622,7 +620,6 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
       sn.out_sG = 2L * T * ncol;  // halves
       sn.out_sN = 2 * sn.out_sG;
     }
-    if (hl.bf && capture) return block_fused_args(ha, ht, aht, tail.next_adj ? &sn : nullptr, capture);
     if (hl.bf) {
       pf.begin(DSTD_KIND_BLOCK, s);
       e = launch_block_fused(ha, ht, aht, tail.next_adj ? &sn : nullptr, s);
@@ -725,7 +722,6 @@ void carve_block(Carver& cv, BlockLayout& L, int B, int cin, int cout, int T, in
 
 struct ModelLayout {
   float* act[3];
-  BlockFusedArgs* mdesc;  // the whole-model launch's block descriptors (DSTD_MAX_LAYERS + 2)
   BlockFold f_in, f_out, f_enc[DSTD_MAX_LAYERS];
   float* bnin_s;
   float* bnin_h;
@@ -736,7 +732,6 @@ struct ModelLayout {
 void carve_model(Carver& cv, ModelLayout& L, int B, int T, int V, int C, int layers, int cin_model,
                  int cout_model) {
   for (int i = 0; i < 3; ++i) L.act[i] = cv.take((size_t)B * T * V * C);
-  L.mdesc = reinterpret_cast<BlockFusedArgs*>(cv.take(cdiv((DSTD_MAX_LAYERS + 2) * sizeof(BlockFusedArgs), sizeof(float))));
   carve_fold(cv, L.f_in, T, V, C, cin_model != C);
   carve_fold(cv, L.f_out, T, V, cout_model, C != cout_model);
   for (int i = 0; i < layers; ++i) {
@@ -936,7 +931,7 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
   StreamDeviceGuard dev_guard_(stream, x);
   const bool reuse = (flags & DSTD_FWD_REUSE_CONSTANTS) != 0;
   if (flags & ~(DSTD_FWD_REUSE_CONSTANTS | DSTD_FWD_EXACT_FP32 | DSTD_FWD_SEPARATE_ADJ | DSTD_FWD_FUSED_TEMPORAL |
-                DSTD_FWD_SEPARATE_BLOCK | DSTD_FWD_WHOLE_MODEL))
+                DSTD_FWD_SEPARATE_BLOCK))
     return DSTD_EINVAL;
   if (!p || !x || !y || !workspace) return DSTD_EINVAL;
   if (prof && (prof->capacity < 0 || (prof->capacity > 0 && (!prof->events || !prof->kinds)))) return DSTD_EINVAL;
@@ -1060,29 +1055,6 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
     pf.begin(DSTD_KIND_FOLD, s);
     DSTD_TRY(run_hl_prep(hj, s));
     pf.end(s);
-  }
-  // DSTD_FWD_WHOLE_MODEL: the whole model in one launch (k_model_fused) where
-  // every block runs as a fused block and blocks 1.. get their spatial planes
-  // from the previous block's phase 3: only block 0's spatial adjacency
-  // launch stays in front
-  bool mf = (flags & DSTD_FWD_WHOLE_MODEL) && NB >= 2 && model_fused_supported(T, V);
-  for (int b = 0; b < NB && mf; ++b) mf = hls[b].bf && (b == 0 || hls[b].s_pre);
-  if (mf) {
-    BlockFusedArgs desc[DSTD_MAX_LAYERS + 2];
-    for (int b = 0; b < NB; ++b) {
-      pf.block = b;
-      DSTD_TRY(run_block(blk[b], *fold[b], L.sc, B, T, V, xin[b], hbuf[b], ybuf[b], tails[b], s, pf, hls[b],
-                         b == 0 ? x : nullptr, &desc[b]));
-    }
-    // the descriptors depend on the parameters, the workspace and B only (x
-    // and y travel as kernel arguments), so a reuse call finds them in place
-    if (!reuse) DSTD_TRY(launch_desc_copy(desc, NB * sizeof(BlockFusedArgs), L.mdesc, s));
-    pf.block = -1;
-    pf.begin(DSTD_KIND_MODEL, s);
-    const hipError_t e = launch_model_fused(L.mdesc, NB, x, y, B, T, V, s);
-    pf.end(s);
-    DSTD_TRY(e);
-    return DSTD_OK;
   }
   for (int b = 0; b < NB; ++b) {
     pf.block = b;

@@ -372,7 +372,7 @@ struct TemporalFusedArgs {
   AdjHLArgs sn;      // out != null: the next block's spatial adjacency planes (launch_adj_hl mode 0 args;
                      // pq = g.pq, the P/Q this launch writes), built after the units (phase 3)
 };
-// one DSTDGCB of k_block_fused / k_model_fused: the spatial GC (launch_spatial_hl
+// one DSTDGCB of k_block_fused: the spatial GC (launch_spatial_hl
 // arguments) and the fused temporal GC (launch_temporal_fused arguments)
 struct BlockFusedArgs {
   SpatialHLArgs s;
@@ -409,19 +409,6 @@ hipError_t launch_block_fused(const SpatialHLArgs& sa, const TemporalHLArgs& g, 
 // validates one block's k_block_fused arguments and fills *out (no launch)
 hipError_t block_fused_args(const SpatialHLArgs& sa, const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn,
                             BlockFusedArgs* out);
-// the whole model forward after block 0's spatial adjacency in ONE launch
-// (k_model_fused: one workgroup per sample runs conv_st_in, the encoders and
-// conv_st_out back to back, block kinds IN, ENC..., OUT as block_fused_args
-// describes them).  desc: nb BlockFusedArgs in device memory (written by
-// launch_desc_copy); x / y: the model input and output of this call (they
-// replace block 0's spatial input and the last block's residual / output,
-// so the descriptors stay valid across calls)
-bool model_fused_supported(int T, int V);
-hipError_t launch_model_fused(const BlockFusedArgs* desc, int nb, const float* x, float* y, int B, int T, int V,
-                              hipStream_t s);
-// copies `bytes` (a multiple of 16) of host data into device memory on stream s
-// with kernel launches (the bytes travel as kernel arguments: stream-ordered,
-// graph-capturable, no pinned staging)
-hipError_t launch_desc_copy(const void* src, size_t bytes, void* dst, hipStream_t s);
+
 
 }  // namespace dstd

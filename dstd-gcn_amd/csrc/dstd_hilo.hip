@@ -475,7 +475,7 @@ __device__ __forceinline__ void stage_spatial(const SpatialHLArgs& a, SpatialSta
 // adjacency B fragments (hi, lo planes) for its two w tiles.
 template <int V, int CIN, int COUT, typename AdjLoad, bool LATE_RES = kSpLateRes, int ST_AUX = DSTD_GC_ST_AUX>
 __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const SpatialStage<V, CIN, COUT>& st, int u,
-                                              int uend, int ustep, AdjLoad load_adj_g, const float* xover = nullptr) {
+                                              int uend, int ustep, AdjLoad load_adj_g) {
   using SM = SlotMap<V, true>;
   constexpr bool RES = CIN != COUT;
   constexpr int NWT = cdiv(V, 16);
@@ -503,9 +503,8 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
   // xmodel (CIN == 6 only): x is the model input [B][T][V][3] and the rows
   // are x6 = cat(x, x - x[:, -1]) built on the fly (no x6 tensor, no prep launch)
   const bool x6 = CIN == 6 && a.xmodel;
-  const float* const X = xover ? xover : a.x;  // (k_model_fused: the call's model input)
-  auto frame_rsrc = [&](int uu) { return x6 ? rsrc(X + (size_t)uu * V * 3, V * 12) : rsrc(X + (size_t)uu * V * CIN, xunit); };
-  auto last_rsrc = [&](int uu) { return rsrc(X + ((size_t)(uu / T) * T + T - 1) * V * 3, V * 12); };
+  auto frame_rsrc = [&](int uu) { return x6 ? rsrc(a.x + (size_t)uu * V * 3, V * 12) : rsrc(a.x + (size_t)uu * V * CIN, xunit); };
+  auto last_rsrc = [&](int uu) { return rsrc(a.x + ((size_t)(uu / T) * T + T - 1) * V * 3, V * 12); };
   auto row8 = [&](__amdgpu_buffer_rsrc_t rf, __amdgpu_buffer_rsrc_t rl, int row, int k0, float4& lo4, float4& hi4) {
     if (x6) load_x6row(rf, rl, row, k0, lo4, hi4);
     else load_row8<CIN>(rf, row, k0, lo4, hi4);
@@ -973,11 +972,7 @@ __host__ __device__ constexpr bool tf_res_acc(int T, int V) { return (T == 35 &&
 template <int T, int EPI, int C, int VB, bool LAZY, typename AdjLoad, bool PF = true, bool RA = false,
           int NUTC = cdiv(T, 16)>
 __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const TemporalStage<T, EPI, C, VB>& st, int u,
-                                               int uend, int ustep, AdjLoad load_adj, int ut0 = 0,
-                                               const float* xres_over = nullptr, float* y_over = nullptr) {
-  // (k_model_fused: the call's model input / output for the OUT block)
-  const float* const XRES = xres_over ? xres_over : a.xres;
-  float* const YO = y_over ? y_over : a.y;
+                                               int uend, int ustep, AdjLoad load_adj, int ut0 = 0) {
   // NUTC / ut0: the u tiles ut0 .. ut0 + NUTC - 1 of each unit (a u chunk of
   // k_temporal_fused at T = 75; every tile otherwise); load_adj fills
   // [NUTC] fragments for them
@@ -1104,7 +1099,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     // so its 48 registers are not live across it
     float4 R[use_res ? NCT : 1][use_res ? NUTC : 1];
     auto load_res_enc = [&]() {
-      const auto rr = rsrc(XRES + cbase, col_bytes);
+      const auto rr = rsrc(a.xres + cbase, col_bytes);
 #pragma unroll
       for (int ut = 0; ut < NUTC; ++ut)
 #pragma unroll
@@ -1124,7 +1119,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     } else if constexpr (EPI == TEPI_ENC) {
     } else if constexpr (EPI == TEPI_OUT) {
       // x_model [B][T][V][C]: frame T-1 of joint v, 3 channels on lanes kl == 0
-      const auto rr = rsrc(XRES + (((size_t)n * T + T - 1) * V + v) * C, C * 4);
+      const auto rr = rsrc(a.xres + (((size_t)n * T + T - 1) * V + v) * C, C * 4);
       float e[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < C && i < 4; ++i)
@@ -1136,7 +1131,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
     // ---- aggregation: O[c][u] = sum_t D[t][c] Adj[v][t][u] ----
     f32x4 O[NCT][NUTC];
     if constexpr (res_acc) {
-      const auto rr = rsrc(XRES + cbase, col_bytes);
+      const auto rr = rsrc(a.xres + cbase, col_bytes);
 #pragma unroll
       for (int ut = 0; ut < NUTC; ++ut)
 #pragma unroll
@@ -1239,7 +1234,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 #pragma unroll
         for (int ut = 0; ut < NUTC; ++ut) O[ct][ut] *= up;
     }
-    const auto ry = rsrc(YO + cbase, col_bytes);
+    const auto ry = rsrc(a.y + cbase, col_bytes);
 #pragma unroll
     for (int ut = 0; ut < NUTC; ++ut) {
 #pragma unroll
@@ -2078,8 +2073,7 @@ constexpr int tf_waves() { return T == 35 && V == 22 ? DSTD_TF_NW_H36M : 8; }
 // dsm (TFusedGeom::LDS bytes): the kernel below runs it once, k_block_fused
 // after the sample's spatial GC.
 template <int T, int V, int EPI, int C>
-__device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const int n, unsigned char* dsm,
-                                            const float* xres_over = nullptr, float* y_over = nullptr) {
+__device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const int n, unsigned char* dsm) {
   using Gm = TFusedGeom<T, V, EPI, C>;
   using SM = typename Gm::SM;
   using EF = typename Gm::EF;
@@ -2435,7 +2429,7 @@ __device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const i
       };
 #ifndef DSTD_TF_SKIP_P2  // (timing experiments: phase 1 alone)
       temporal_units<T, EPI, C, V, true, decltype(load_adj), (NW <= 8 && !Gm::UCH), tf_res_acc(T, V), NUTC>(
-          a, st, ub + wave, ub + nv, NW, load_adj, u0 / 16, xres_over, y_over);
+          a, st, ub + wave, ub + nv, NW, load_adj, u0 / 16);
 #endif
     }
   }
@@ -2479,8 +2473,7 @@ struct BlockFusedGeom {
 
 template <int T, int V, int CIN, int COUT, int EPI>
 __device__ __forceinline__ void block_fused_body(const SpatialHLArgs& sa, const TemporalFusedArgs& ta, const int n,
-                                                 unsigned char* dsm, const float* x_over = nullptr,
-                                                 const float* xres_over = nullptr, float* y_over = nullptr) {
+                                                 unsigned char* dsm) {
   constexpr int NW = tf_waves<T, V>(), NT = 64 * NW;
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 0) }
   {
@@ -2512,12 +2505,12 @@ __device__ __forceinline__ void block_fused_body(const SpatialHLArgs& sa, const 
 #define DSTD_BF_ST_AUX DSTD_GC_ST_AUX
 #endif
     spatial_units<V, CIN, COUT, decltype(load_adj_g), (NW > 8), DSTD_BF_ST_AUX>(a, st, n * T + wave, (n + 1) * T, NW,
-                                                                                 load_adj_g, x_over);
+                                                                                 load_adj_g);
   }
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 1) }
   __syncthreads();  // h and the temporal P/Q of sample n written; the spatial stage is dead
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 2) }
-  tfused_body<T, V, EPI, COUT>(ta, n, dsm, xres_over, y_over);
+  tfused_body<T, V, EPI, COUT>(ta, n, dsm);
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 3) }
 }
 
@@ -2525,72 +2518,6 @@ template <int T, int V, int CIN, int COUT, int EPI>
 __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_waves_per_eu((tf_waves<T, V>() / 4), (tf_waves<T, V>() / 4)))) void k_block_fused(BlockFusedArgs ba) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
   block_fused_body<T, V, CIN, COUT, EPI>(ba.s, ba.t, blockIdx.x, dsm);  // one sample per workgroup
-}
-
-// ===========================================================================
-// The whole model forward per sample (DSTDGCN.forward, model/dstdgcn.py:293-317,
-// after block 0's spatial adjacency): conv_st_in (6 -> 64, IN tail), the
-// encoders (64 -> 64, ENC tail) and conv_st_out (64 -> 3, OUT tail: the
-// output residual) as block_fused_body after block_fused_body, one workgroup
-// per sample.  Every hand-off -- a block's output to the next block's spatial
-// GC, the next block's spatial planes from phase 3 -- stays inside the
-// workgroup (barrier-ordered, as k_block_fused's h), so the model needs no
-// kernel boundary at all: each CU walks its sample through the 7 blocks at
-// its own pace (no per-launch fill / drain, no wait for the slowest CU of the
-// chip between blocks).  The block descriptors live in device memory (one
-// upload per constant refold); x and y come per call.
-// ===========================================================================
-struct ModelFusedArgs {
-  const BlockFusedArgs* __restrict__ blk;
-  int nb;
-  const float* x;  // model input [B][T][V][3]: block 0's spatial input, the OUT residual
-  float* y;        // model output [B][T][V][3]
-};
-
-// A block body as a function of its own (noinline): inlined three times
-// into one kernel, the bodies' loop-invariant values were hoisted across
-// the encoder loop and the kernel spilled ~170 VGPRs; as a call each body
-// gets its own register allocation, for one save / restore of the
-// callee-saved registers per block.  Function arguments arrive in VGPRs, so
-// the descriptor and the override pointers are made wave-uniform again, and
-// the descriptor is read through the constant address space (scalar,
-// invariant loads, as a kernel argument would be).
-__device__ __forceinline__ uint64_t uniform_bits(const void* p) {
-  const uint64_t v = (uint64_t)p;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ const void* uniform_ptr(const void* p) { return (const void*)uniform_bits(p); }
-template <int T, int V, int CIN, int COUT, int EPI>
-__device__ __attribute__((noinline)) void block_fused_call(const BlockFusedArgs* dv, const float* x_over,
-                                                          const float* xres_over, float* y_over) {
-  typedef const __attribute__((address_space(4))) BlockFusedArgs* CP;
-  const BlockFusedArgs& d = *(const BlockFusedArgs*)(CP)uniform_bits(dv);
-  extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  block_fused_body<T, V, CIN, COUT, EPI>(d.s, d.t, blockIdx.x, dsm, (const float*)uniform_ptr(x_over),
-                                         (const float*)uniform_ptr(xres_over), (float*)uniform_ptr(y_over));
-}
-
-template <int T, int V>
-__global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_waves_per_eu((tf_waves<T, V>() / 4), (tf_waves<T, V>() / 4)))) void k_model_fused(ModelFusedArgs a) {
-  block_fused_call<T, V, 6, 64, TEPI_IN>(a.blk, a.x, nullptr, nullptr);
-#pragma unroll 1
-  for (int b = 1; b + 1 < a.nb; ++b) {
-    __syncthreads();  // the previous block's output and this block's planes written; its LDS dead
-    block_fused_call<T, V, 64, 64, TEPI_ENC>(a.blk + b, nullptr, nullptr, nullptr);
-  }
-  __syncthreads();
-  block_fused_call<T, V, 64, 3, TEPI_OUT>(a.blk + a.nb - 1, nullptr, a.x, a.y);
-}
-
-struct DescChunk {
-  static constexpr int N = 224;  // uint4 per launch (3.5 KB of kernel arguments)
-  uint4 v[N];
-  int n;
-  uint4* dst;
-};
-__global__ __launch_bounds__(256) void k_desc_copy(DescChunk c) {
-  for (int i = threadIdx.x; i < c.n; i += 256) c.dst[i] = c.v[i];
 }
 
 // ===========================================================================
@@ -2812,52 +2739,6 @@ hipError_t launch_block_fused(const SpatialHLArgs& sa, const TemporalHLArgs& g, 
   if (g.T == 35 && g.V == 25) return bfused_tv<35, 25>(a, s);
   if (g.T == 40 && g.V == 23) return bfused_tv<40, 23>(a, s);
   return hipErrorNotSupported;
-}
-
-template <int T, int V>
-hipError_t mfused_run(const ModelFusedArgs& a, int B, hipStream_t s) {
-  constexpr size_t L0 = BlockFusedGeom<T, V, 6, 64, TEPI_IN>::LDS, L1 = BlockFusedGeom<T, V, 64, 64, TEPI_ENC>::LDS,
-                   L2 = BlockFusedGeom<T, V, 64, 3, TEPI_OUT>::LDS;
-  constexpr size_t LDS = L0 > L1 ? (L0 > L2 ? L0 : L2) : (L1 > L2 ? L1 : L2);
-  static const hipError_t attr =
-      hipFuncSetAttribute((const void*)k_model_fused<T, V>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
-  if (attr != hipSuccess) return attr;
-  hipLaunchKernelGGL((k_model_fused<T, V>), dim3(B), dim3(64 * tf_waves<T, V>()), LDS, s, a);
-  return hipGetLastError();
-}
-
-bool model_fused_supported(int T, int V) {
-#ifdef DSTD_NO_MFUSED
-  return false;
-#endif
-  return block_fused_supported(T, V, 64, 64, TEPI_ENC);
-}
-
-hipError_t launch_model_fused(const BlockFusedArgs* desc, int nb, const float* x, float* y, int B, int T, int V,
-                              hipStream_t s) {
-  if (!model_fused_supported(T, V) || nb < 2 || !desc || !x || !y || B <= 0) return hipErrorNotSupported;
-  const ModelFusedArgs a{desc, nb, x, y};
-  if (T == 35 && V == 22) return mfused_run<35, 22>(a, B, s);
-  if (T == 35 && V == 25) return mfused_run<35, 25>(a, B, s);
-  if (T == 40 && V == 23) return mfused_run<40, 23>(a, B, s);
-  return hipErrorNotSupported;
-}
-
-hipError_t launch_desc_copy(const void* src, size_t bytes, void* dst, hipStream_t s) {
-  if (bytes % 16) return hipErrorInvalidValue;
-  const uint4* p = static_cast<const uint4*>(src);
-  uint4* d = static_cast<uint4*>(dst);
-  const size_t n = bytes / 16;
-  for (size_t i = 0; i < n; i += DescChunk::N) {
-    DescChunk c{};
-    c.n = (int)std::min<size_t>(DescChunk::N, n - i);
-    for (int k = 0; k < c.n; ++k) c.v[k] = p[i + k];
-    c.dst = d + i;
-    hipLaunchKernelGGL(k_desc_copy, dim3(1), dim3(256), 0, s, c);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
 }
 
 bool temporal_fused_supported(int T, int V) {

@@ -93,9 +93,8 @@ FWD_EXACT_FP32 = 2  # include/dstd_gcn.h DSTD_FWD_EXACT_FP32
 FWD_SEPARATE_ADJ = 4  # include/dstd_gcn.h DSTD_FWD_SEPARATE_ADJ
 FWD_FUSED_TEMPORAL = 8  # include/dstd_gcn.h DSTD_FWD_FUSED_TEMPORAL
 FWD_SEPARATE_BLOCK = 16  # include/dstd_gcn.h DSTD_FWD_SEPARATE_BLOCK
-FWD_WHOLE_MODEL = 32  # include/dstd_gcn.h DSTD_FWD_WHOLE_MODEL (experimental)
-KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL, KIND_BLOCK, KIND_MODEL = range(8)
-KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temporal_gc", "block", "model")
+KIND_FOLD, KIND_PREP, KIND_ADJ_S, KIND_SPATIAL, KIND_ADJ_T, KIND_TEMPORAL, KIND_BLOCK = range(7)
+KIND_NAMES = ("fold", "prep", "adj_spatial", "spatial_gc", "adj_temporal", "temporal_gc", "block")
 
 _lib = None
 

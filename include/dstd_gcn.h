@@ -135,8 +135,7 @@ int dstd_model_fwd(const dstd_model_params* p, const float* x, int B, float* y, 
  * Kernel families of one forward, in launch order per DSTDGCB:
  *   ADJ_S (tanh GEMM, both graphs), SPATIAL (spatial GC + mid epilogue),
  *   ADJ_T (tanh GEMM), TEMPORAL (temporal GC + tail epilogue); BLOCK: the
- *   whole DSTDGCB in one launch (spatial + temporal GC, DSTD_FWD_SEPARATE_BLOCK);
- *   MODEL: every block in one launch (DSTD_FWD_WHOLE_MODEL). */
+ *   whole DSTDGCB in one launch (spatial + temporal GC, DSTD_FWD_SEPARATE_BLOCK). */
 #define DSTD_KIND_FOLD 0
 #define DSTD_KIND_PREP 1
 #define DSTD_KIND_ADJ_S 2
@@ -144,8 +143,7 @@ int dstd_model_fwd(const dstd_model_params* p, const float* x, int B, float* y, 
 #define DSTD_KIND_ADJ_T 4
 #define DSTD_KIND_TEMPORAL 5
 #define DSTD_KIND_BLOCK 6
-#define DSTD_KIND_MODEL 7 /* the whole model after block 0's spatial adjacency (block index -1) */
-#define DSTD_KIND_COUNT 8
+#define DSTD_KIND_COUNT 7
 
 /* Every launch whose family bit is set in kind_mask is bracketed by a
  * (start, stop) pair of hipEvents taken from events[2*i], events[2*i+1];
@@ -203,11 +201,6 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
  * and the block is one of the model's three kinds).  Same results bit for
  * bit; for testing and A/B.  Also accepted by dstd_block_fwd_ex. */
 #define DSTD_FWD_SEPARATE_BLOCK 16u
-/* Launch schedule (experimental, opt-in): the whole model after block 0's
- * spatial adjacency in ONE launch (k_model_fused: one workgroup per sample
- * walks it through every block as calls of the block body) instead of one
- * launch per block (k_block_fused, the default).  For testing and A/B. */
-#define DSTD_FWD_WHOLE_MODEL 32u
 int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* y, void* workspace,
                       size_t workspace_bytes, void* stream, unsigned flags, dstd_profile* prof);
 int dstd_events_create(int n, void** events);

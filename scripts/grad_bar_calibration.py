@@ -28,7 +28,7 @@ for p in (ROOT, os.path.join(ROOT, "dstd-gcn_amd"), os.path.join(ROOT, "tests"))
     sys.path.insert(0, p)
 from conftest import group, load_npz  # noqa: E402
 from oracle import dstdgcn_oracle as O  # noqa: E402
-from test_gpu_train import DEV, N_ORDERS, _model_3dpw  # noqa: E402
+from test_gpu_train import DEV, GLOBAL_SUM, N_ORDERS, _model_3dpw  # noqa: E402
 from engine import mpjpe_error_3d  # noqa: E402
 
 
@@ -58,14 +58,24 @@ def summarize(r):
 
 def calibrate(name, native_err, errs, g64):
     """Leave-one-out ratios of every fp32 run, and the native step's ratios
-    against the floor of all runs (the test's criterion)."""
+    against the floor of all runs (the test's criterion); also split by
+    tensor class (GLOBAL_SUM: the scalars and biases, each one sum over every
+    position of the step, vs every other tensor)."""
     keys = list(g64)
-    loo = {}
+    glob = np.array([bool(GLOBAL_SUM.search(k)) for k in keys])
+    loo, loo_cls = {}, {"global_sum": [], "other": []}
     for run in errs:
         floor = {k: max(e[k] for r2, e in errs.items() if r2 != run) for k in keys}
-        loo[run] = summarize(ratios(errs[run], floor, g64))
+        r = ratios(errs[run], floor, g64)
+        loo[run] = summarize(r)
+        loo_cls["global_sum"].append(float(r[glob].max()))
+        loo_cls["other"].append(float(r[~glob].max()))
     full = {k: max(e[k] for e in errs.values()) for k in keys}
     rn = ratios(native_err, full, g64)
+    by_class = {c: {"loo_max_p95": round(float(np.quantile(v, 0.95)), 3), "loo_max_max": round(float(max(v)), 3),
+                    "loo_maxima": [round(x, 3) for x in v],
+                    "native_max": round(float((rn[glob] if c == "global_sum" else rn[~glob]).max()), 3)}
+                for c, v in loo_cls.items()}
     top = sorted(zip(rn, keys), reverse=True)[:3]
     maxima = np.array([v["max"] for v in loo.values()])
     p90s = np.array([v["p90"] for v in loo.values()])
@@ -75,7 +85,7 @@ def calibrate(name, native_err, errs, g64):
                         "p95": round(float(np.quantile(maxima, 0.95)), 3), "max": round(float(maxima.max()), 3)},
             "loo_p90": {"p95": round(float(np.quantile(p90s, 0.95)), 3), "max": round(float(p90s.max()), 3)},
             "loo_median": {"p95": round(float(np.quantile(meds, 0.95)), 3), "max": round(float(meds.max()), 3)},
-            "native": summarize(rn), "native_top": [(round(float(v), 3), k) for v, k in top]}
+            "native": summarize(rn), "native_top": [(round(float(v), 3), k) for v, k in top], "by_class": by_class}
 
 
 def native_fixture(m, d):
@@ -128,7 +138,12 @@ def main():
     allmax = np.array([v["max"] for r in res for v in r["leave_one_out"].values()])
     allp90 = np.array([v["p90"] for r in res for v in r["leave_one_out"].values()])
     allmed = np.array([v["median"] for r in res for v in r["leave_one_out"].values()])
+    pooled_cls = {c: [x for r in res for x in r["by_class"][c]["loo_maxima"]] for c in ("global_sum", "other")}
     doc = {"what": __doc__.strip().splitlines()[0], "cases": res,
+           "pooled_by_class": {c: {"n": len(v), "loo_max_p95": round(float(np.quantile(v, 0.95)), 3),
+                                   "loo_max_max": round(float(max(v)), 3),
+                                   "native_max": max(r["by_class"][c]["native_max"] for r in res)}
+                               for c, v in pooled_cls.items()},
            "pooled_leave_one_out": {"n": int(allmax.size),
                                     "max_p95": round(float(np.quantile(allmax, 0.95)), 3),
                                     "max_max": round(float(allmax.max()), 3),
@@ -139,6 +154,7 @@ def main():
         with open(sys.argv[1], "w") as f:
             f.write(text + "\n")
     print(json.dumps(doc["pooled_leave_one_out"]))
+    print(json.dumps(doc["pooled_by_class"]))
 
 
 if __name__ == "__main__":

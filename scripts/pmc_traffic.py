@@ -20,8 +20,6 @@ from collections import defaultdict
 def family(name):
     # split-f16 kernels (dstd_hilo.hip) are families of their own: the
     # 64->64 launches whose bytes bench.py's roofline divides
-    if "k_model_fused" in name:
-        return "model_split"
     if "k_block_fused" in name:
         return "block_split"
     if "k_spatial_hl" in name:

@@ -11,7 +11,10 @@ Tolerances
                             fp32 step on the CPU, on the GPU and over 8 sample
                             orders, plus the reference's g32err where the
                             fixture holds it) -- the 21-op stack is chaotic in
-                            fp32: every tensor within 4x, median
+                            fp32: every tensor within 3x, the
+                            global sums within 4x (bars calibrated by
+                            leave-one-out over those runs,
+                            profiles/r06g_grad_bar_calibration.json), median
                             <= 1.5, 90th percentile <= 2 (fp32_noise /
                             check_ratios; the per-block bisection behind it:
                             test_model_step_gradient_tail_is_propagation)
@@ -292,13 +295,27 @@ def _bn_of(module, key):
 # N_ORDERS sample orders of the batch (the loss and train-mode BatchNorm are
 # order-invariant, so each order is only another rounding sequence), plus the
 # reference's own fp32 run where the fixture holds it -- and every tensor of
-# the native step must be within 4x that floor (median <= 1.5, 90th
-# percentile <= 2).  Before round 5 the floor was the max of two samples,
-# and a tail exemption (12x for global sums) covered its undershoot.  (The
-# native step is one more draw from the same heavy-tailed distribution: at
-# B=32 its largest ratio was 3.16, on a PReLU slope -- a sum over 3.8M
-# positions -- against 8 samples, r05f.)
+# the native step must be within MAX_RATIO of that floor (median <= 1.5,
+# 90th percentile <= 2).  Before round 5 the floor was the max of two
+# samples, and a tail exemption (12x for global sums) covered its undershoot.
+# The largest-ratio bars are calibrated, not chosen (round 6,
+# scripts/grad_bar_calibration.py, profiles/r06g_grad_bar_calibration.json):
+# each fp32 run measured the way the native step is -- against the floor of
+# the OTHER runs -- on the fixture step, B=32 and B=256 (31 leave-one-out
+# runs), split by tensor class:
+#  * every tensor but the global sums: largest ratio p95 2.22, max 2.71 ->
+#    MAX_RATIO 3.0 (the native steps: at most 1.22);
+#  * GLOBAL_SUM tensors (scalars and biases: ONE sum over every position of
+#    both passes): p95 2.66, max 2.96.  The native step exceeds that on one
+#    tensor per step at most -- B=32 3.17 (a block PReLU slope), the world-2
+#    SyncBN step 3.40 (a conv_rm bias) -- which the per-block bisection
+#    (test_model_step_gradient_tail_is_propagation, r05f) places in the
+#    propagation through the 21-op chain, not in a kernel's summation (the
+#    slope's partials carried in fp64 changed nothing, r06f) -> their bar
+#    stays MAX_RATIO_GLOBAL 4.0, 1.35x the calibrated maximum.
 N_ORDERS = 8
+MAX_RATIO = 3.0
+MAX_RATIO_GLOBAL = 4.0
 
 
 def fp32_noise(sd0, batch, g64, extra=None, n_orders=N_ORDERS):
@@ -337,7 +354,9 @@ def check_ratios(ratios, what=""):
           f"max {r[0]:.2f}", [(round(v, 2), k) for v, k in top[:3]])
     assert np.median(r) <= 1.5, (what, np.median(r), top)
     assert np.quantile(r, 0.9) <= 2.0, (what, np.quantile(r, 0.9), top)
-    assert r[0] <= 4.0, (what, top)
+    other = [(v, k) for v, k in ratios if not GLOBAL_SUM.search(k)]
+    assert max(other)[0] <= MAX_RATIO, (what, sorted(other, reverse=True)[:3])
+    assert r[0] <= MAX_RATIO_GLOBAL, (what, top)
 
 
 # The eval-mode backward tests (tests/test_gpu_parity.py, test_gpu_fast.py;
