@@ -473,9 +473,16 @@ __device__ __forceinline__ void stage_spatial(const SpatialHLArgs& a, SpatialSta
 // The spatial GC units u, u + ustep, ... < uend (unit = (sample, frame) =
 // n * T + t); load_adj_g(u, g, ab[NWT][2]) fetches the unit's graph-g
 // adjacency B fragments (hi, lo planes) for its two w tiles.
-template <int V, int CIN, int COUT, typename AdjLoad, bool LATE_RES = kSpLateRes, int ST_AUX = DSTD_GC_ST_AUX>
-__device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const SpatialStage<V, CIN, COUT>& st, int u,
-                                              int uend, int ustep, AdjLoad load_adj_g) {
+// (k_block_fused: a sink that also receives every unit's temporal P/Q -- the
+// values it stores -- and returns the range flag of phase 1's prologue)
+struct NoPQSink {
+  __device__ int operator()(int, int, float, float, float, float) const { return 0; }
+};
+template <int V, int CIN, int COUT, typename AdjLoad, bool LATE_RES = kSpLateRes, int ST_AUX = DSTD_GC_ST_AUX,
+          typename PQSink = NoPQSink>
+__device__ __forceinline__ int spatial_units(const SpatialHLArgs& a, const SpatialStage<V, CIN, COUT>& st, int u,
+                                             int uend, int ustep, AdjLoad load_adj_g, PQSink pq_sink = {}) {
+  int bad = 0;
   using SM = SlotMap<V, true>;
   constexpr bool RES = CIN != COUT;
   constexpr int NWT = cdiv(V, 16);
@@ -778,13 +785,18 @@ __device__ __forceinline__ void spatial_units(const SpatialHLArgs& a, const Spat
       const float s = st.scl[2] * pow2f(sh);
       const auto rp = rsrc(a.pq + (size_t)u * V * 4, V * 16);
 #pragma unroll
-      for (int wt = 0; wt < NWT; ++wt)
-        bst4<ST_AUX>(rp, wpq0 + wt * 256,
-             make_float4(fmaf(acc[wt][0], s, st.bql[0]), fmaf(acc[wt][1], s, st.bql[1]), fmaf(acc[wt][2], s, st.bql[2]),
-                         fmaf(acc[wt][3], s, st.bql[3])));
+      for (int wt = 0; wt < NWT; ++wt) {
+        const float4 pq4 = make_float4(fmaf(acc[wt][0], s, st.bql[0]), fmaf(acc[wt][1], s, st.bql[1]),
+                                       fmaf(acc[wt][2], s, st.bql[2]), fmaf(acc[wt][3], s, st.bql[3]));
+        bst4<ST_AUX>(rp, wpq0 + wt * 256, pq4);
+        if constexpr (!std::is_same<PQSink, NoPQSink>::value) {
+          if (kl == 0 && 16 * wt + cl < V) bad |= pq_sink(u, 16 * wt + cl, pq4.x, pq4.y, pq4.z, pq4.w);
+        }
+      }
     }
     u = un;
   }
+  return bad;
 }
 
 template <int V, int CIN, int COUT>
@@ -2072,8 +2084,78 @@ constexpr int tf_waves() { return T == 35 && V == 22 ? DSTD_TF_NW_H36M : 8; }
 // The body of k_temporal_fused for sample n on the workgroup's dynamic LDS
 // dsm (TFusedGeom::LDS bytes): the kernel below runs it once, k_block_fused
 // after the sample's spatial GC.
+// k_block_fused, before the barrier that ends the spatial GC: the part of
+// chunk 0's phase-1 prologue that does not depend on the spatial GC's output
+// -- E / F pads, the chunk's conv_rm rows, the Astat / alpha tables, the bias
+// -- into the phase-1 scratch (past the planes region, where the spatial
+// stage lives), each wave right after its last spatial unit.  The same values
+// and places as tfused_body's own prologue writes.
 template <int T, int V, int EPI, int C>
-__device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const int n, unsigned char* dsm) {
+__device__ __forceinline__ void tfused_pre(const TemporalFusedArgs& fa, unsigned char* dsm) {
+  using Gm = TFusedGeom<T, V, EPI, C>;
+  using SM = typename Gm::SM;
+  using EF = typename Gm::EF;
+  constexpr int NS = Gm::NS, TAIL = Gm::TAIL, KP = Gm::KP, K = Gm::K, SL = Gm::SL, NCOL = Gm::NCOL;
+  constexpr int RTC = Gm::RTC, WIMG = Gm::WIMG, NT = 64 * tf_waves<T, V>(), NFR = Gm::NFR;
+  const AdjHLArgs& j = fa.j;
+  float* El = reinterpret_cast<float*>(dsm + Gm::PLANES);
+  float* Fl = El + Gm::EFE;
+  uint4* wl = reinterpret_cast<uint4*>(Fl + Gm::EFF);
+  float* asq = reinterpret_cast<float*>(wl + WIMG);
+  float* alq = asq + Gm::ASQ;
+  float* bsl = alq + Gm::ASQ;
+  const int tid = threadIdx.x;
+  constexpr int FULL = NS * 2 * 64;
+  constexpr int NWF = cdiv(RTC * FULL, NT), NWT = TAIL ? cdiv(RTC * 64, NT) : 0, NAS = cdiv(Gm::ASQ, NT);
+  uint4 wf[NWF], wt[NWT > 0 ? NWT : 1];
+  float av[NAS];
+  int aok = 0;
+#pragma unroll
+  for (int it = 0; it < NWF; ++it) wf[it] = j.wimg[0][min(tid + it * NT, RTC * FULL - 1)];
+#pragma unroll
+  for (int it = 0; it < NWT; ++it) wt[it] = j.wimg[0][Gm::RTG * FULL + min(tid + it * NT, RTC * 64 - 1)];
+#pragma unroll
+  for (int it = 0; it < NAS; ++it) {
+    const int i = tid + it * NT, q = i / SL, pi = i < NCOL ? SM::slot_idx(i - q * SL) : T;
+    const bool ok = pi < T && q < T;
+    if (ok) aok |= 1 << it;
+    av[it] = j.astat[0][ok ? pi * T + q : 0];
+  }
+  const float dna = pow2f(-hl_range_shift(fexp_bits(__float_as_uint(j.wscale[0][HLS_BOUND]))));
+  const float alpha = *j.alpha * dna;
+  const float bv = tid < 16 * RTC && tid < V ? j.bias[0][tid] : 0.f;
+  for (int i = tid; i < (T + 1) * (KP - K); i += NT) {
+    const int r = i / (KP > K ? KP - K : 1), k = K + i % (KP > K ? KP - K : 1);
+    El[EF::row(r) + k] = 1.f;
+    if (r < NFR) Fl[EF::row(r) + k] = 1.f;
+  }
+  for (int i = tid; i < K; i += NT) {
+    El[EF::row(T) + i] = 1.f;
+    Fl[EF::row(NFR - 1) + i] = 1.f;
+  }
+#pragma unroll
+  for (int it = 0; it < NWF; ++it)
+    if (tid + it * NT < RTC * FULL) wl[tid + it * NT] = wf[it];
+#pragma unroll
+  for (int it = 0; it < NWT; ++it)
+    if (tid + it * NT < RTC * 64) wl[RTC * FULL + tid + it * NT] = wt[it];
+#pragma unroll
+  for (int it = 0; it < NAS; ++it)
+    if (tid + it * NT < Gm::ASQ) {
+      const bool ok = (aok >> it) & 1;
+      asq[tid + it * NT] = ok ? av[it] * dna : 0.f;
+      alq[tid + it * NT] = ok ? alpha : 0.f;
+    }
+  if (tid < 16 * RTC) bsl[tid] = bv;
+}
+
+// PRE (k_block_fused): chunk 0's phase-1 prologue is done already -- the E /
+// F rows by the spatial units (pq_sink), the pads, conv_rm rows, tables and
+// bias by tfused_pre before the workgroup barrier whose OR of the range flags
+// is sep_pre -- so phase 1 starts with its tiles
+template <int T, int V, int EPI, int C, bool PRE = false>
+__device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const int n, unsigned char* dsm,
+                                            const bool sep_pre = true) {
   using Gm = TFusedGeom<T, V, EPI, C>;
   using SM = typename Gm::SM;
   using EF = typename Gm::EF;
@@ -2127,6 +2209,13 @@ __device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const i
           Fl[EF::row(NFR - 1) + i] = val;
         }
       };
+      const float inv = j.wscale[0][HLS_INV];
+      bool sep;
+      if (PRE && ch == 0) {
+        // (the planes region held the spatial stage until the barrier: the pads now)
+        if (tid < Gm::jn(RC)) *reinterpret_cast<uint4*>(planes + tid * PJ + Gm::ZPAD) = make_uint4(0u, 0u, 0u, 0u);
+        sep = sep_pre;
+      } else {
       ef_pad(1.f);
       // every global load of the prologue is issued before the first LDS
       // write that needs one (one memory round trip, not one per loop trip)
@@ -2164,7 +2253,7 @@ __device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const i
       }
       // planes stored as 2^-sa Adj (dstd_hilo.h "range scaling")
       const float dna = pow2f(-hl_range_shift(fexp_bits(__float_as_uint(j.wscale[0][HLS_BOUND]))));
-      const float alpha = *j.alpha * dna, inv = j.wscale[0][HLS_INV];
+      const float alpha = *j.alpha * dna;
       const float bv = tid < 16 * RTC && 16 * rt0 + tid < V ? j.bias[0][16 * rt0 + tid] : 0.f;
       int bad = 0;
 #pragma unroll
@@ -2200,11 +2289,12 @@ __device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const i
         }
       if (tid < 16 * RTC) bsl[tid] = bv;
       if (tid < Gm::jn(RC)) *reinterpret_cast<uint4*>(planes + tid * PJ + Gm::ZPAD) = make_uint4(0u, 0u, 0u, 0u);
-      const bool sep = __syncthreads_or(bad) == 0;
+      sep = __syncthreads_or(bad) == 0;
       // (__syncthreads_or already orders the LDS writes above: __ockl_wgred_or_i32
       // waits lgkmcnt(0) before its first barrier, checked in the ISA; round
       // 2's "did not order" was the mixed-shape MFMA hazard)
       __syncthreads();
+      }  // (!PRE || ch)
       if (!sep) {  // direct path: E / F hold P / Q themselves (padding 0)
         for (int i = tid; i < T * V; i += NT) {
           const int t = i / V, v = i % V;
@@ -2476,10 +2566,13 @@ __device__ __forceinline__ void block_fused_body(const SpatialHLArgs& sa, const 
                                                  unsigned char* dsm) {
   constexpr int NW = tf_waves<T, V>(), NT = 64 * NW;
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 0) }
+  int bad = 0;
   {
     using SM = SlotMap<V, true>;
     constexpr int SL = SM::SL, NG = SM::NG, NWT = cdiv(V, 16);
     auto& st = *reinterpret_cast<SpatialStage<V, CIN, COUT>*>(dsm);
+    static_assert(sizeof(SpatialStage<V, CIN, COUT>) <= TFusedGeom<T, V, EPI, COUT>::PLANES,
+                  "the spatial stage must lie within the planes region (tfused_pre writes past it)");
     stage_spatial<V, CIN, COUT, NT>(sa, st, threadIdx.x);
     __syncthreads();
     const int lane = threadIdx.x & 63, kl = lane >> 4, cl = lane & 15;
@@ -2504,13 +2597,34 @@ __device__ __forceinline__ void block_fused_body(const SpatialHLArgs& sa, const 
 #ifndef DSTD_BF_ST_AUX
 #define DSTD_BF_ST_AUX DSTD_GC_ST_AUX
 #endif
-    spatial_units<V, CIN, COUT, decltype(load_adj_g), (NW > 8), DSTD_BF_ST_AUX>(a, st, n * T + wave, (n + 1) * T, NW,
-                                                                                 load_adj_g);
+    // every unit also writes its frame's E / F rows of phase 1 (the tanh
+    // GEMM's exp2 of its temporal P / Q -- the values it stores, the same
+    // float operations as phase 1's prologue) straight into the phase-1
+    // scratch, which lies past the planes region and so past the stage
+    using TG = TFusedGeom<T, V, EPI, COUT>;
+    using TEF = typename TG::EF;
+    float* El = reinterpret_cast<float*>(dsm + TG::PLANES);
+    float* Fl = El + TG::EFE;
+    auto pq_sink = [&](int uu, int w, float p0, float p1, float q0, float q1) -> int {
+      constexpr float C2 = 2.8853900817779268f;  // 2*log2(e)
+      const int t = uu - n * T;
+      const float ep0 = C2 * p0, ep1 = C2 * p1, eq0 = -C2 * q0, eq1 = -C2 * q1;
+      El[TEF::row(t) + w] = __builtin_amdgcn_exp2f(ep0);
+      El[TEF::row(t) + V + w] = __builtin_amdgcn_exp2f(ep1);
+      Fl[TEF::row(t) + w] = __builtin_amdgcn_exp2f(eq0);
+      Fl[TEF::row(t) + V + w] = __builtin_amdgcn_exp2f(eq1);
+      return !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
+    };
+    bad = spatial_units<V, CIN, COUT, decltype(load_adj_g), (NW > 8), DSTD_BF_ST_AUX, decltype(pq_sink)>(
+        a, st, n * T + wave, (n + 1) * T, NW, load_adj_g, pq_sink);
   }
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 1) }
-  __syncthreads();  // h and the temporal P/Q of sample n written; the spatial stage is dead
+  tfused_pre<T, V, EPI, COUT>(ta, dsm);
+  // h and the temporal P/Q of sample n written, chunk 0's E / F rows and
+  // tables in LDS, the range flags OR-ed; the spatial stage is dead
+  const bool sep = __syncthreads_or(bad) == 0;
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 2) }
-  tfused_body<T, V, EPI, COUT>(ta, n, dsm);
+  tfused_body<T, V, EPI, COUT, true>(ta, n, dsm, sep);
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 3) }
 }
 
