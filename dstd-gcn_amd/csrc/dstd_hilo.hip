@@ -898,66 +898,100 @@ struct TemporalStage {
   int rng[3];
 };
 
+// The stage's global loads (load) and its LDS writes (store) as two steps:
+// the fused temporal body issues the loads before the barrier that ends
+// phase 1 (the tile registers are dead by then) and writes once the phase-1
+// scratch is free, so the load latency hides in the barrier wait.
+#ifndef DSTD_TF_STAGE_EARLY
+#define DSTD_TF_STAGE_EARLY 1
+#endif
+template <int T, int EPI, int C, int VB, int NTH>
+struct TemporalStageLoad {
+  using S = TemporalStage<T, EPI, C, VB>;
+  static constexpr int NW = cdiv(S::WIMG, NTH), NP = cdiv(S::PIMG, NTH);
+  static constexpr int NB = S::use_bn ? cdiv(VB * 4 * S::NCT, NTH) : 0;
+  // (native vectors: a uint4 array copied from global memory is a memcpy
+  // that keeps the array in scratch)
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 wv[NW], pv[NP];
+  float4 bs[NB > 0 ? NB : 1], bh[NB > 0 ? NB : 1];
+  float bf, bq;
+  // (oz: an opaque zero from a caller that stages once per loop trip, so
+  // that these loop-invariant loads are not hoisted out of its loop)
+  __device__ __forceinline__ void load(const TemporalHLArgs& a, int tid, int oz = 0) {
+    const bool has_pq = a.pq != nullptr;
+#pragma unroll
+    for (int it = 0; it < NW; ++it)
+      wv[it] = *reinterpret_cast<const u32x4*>(a.wimg + min(tid + it * NTH + oz, S::WIMG - 1));
+#pragma unroll
+    for (int it = 0; it < NP; ++it)
+      pv[it] = has_pq ? *reinterpret_cast<const u32x4*>(a.pqimg + min(tid + it * NTH + oz, S::PIMG - 1)) : u32x4{0, 0, 0, 0};
+    const int nbn = a.V * 4 * S::NCT;
+    if constexpr (S::use_bn) {
+      static_assert(C % 4 == 0, "folded BN rows load as float4");
+      // folded BN vectors [V][C] -> [c/4][v]
+#pragma unroll
+      for (int it = 0; it < NB; ++it) {
+        const int i = min(tid + it * NTH + oz, nbn - 1);
+        const int v = i / (4 * S::NCT), c4 = i - v * (4 * S::NCT);
+        bs[it] = ld4(a.bn_s + v * C + 4 * c4);
+        bh[it] = ld4(a.bn_h + v * C + 4 * c4);
+      }
+    }
+    bf = tid < 16 * S::NCT && tid < C ? a.bf[tid] : 0.f;
+    // (the pointer by selects, not an indexed kernel-argument load: that load
+    // is dependent and its wait would hold wave 0 on every load above)
+    const float* p4[4] = {a.pqb[0], a.pqb[1], a.pqb[2], a.pqb[3]};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+s"(p4[i]));
+    const int g = (tid >> 1) & 3;
+    const float* pb = g == 0 ? p4[0] : g == 1 ? p4[1] : g == 2 ? p4[2] : p4[3];
+    typedef __attribute__((address_space(1))) const float gfloat;
+    bq = tid < 8 && has_pq ? ((gfloat*)pb)[tid & 1] : 0.f;
+  }
+  __device__ __forceinline__ void store(const TemporalHLArgs& a, S& st, int tid) const {
+    const bool has_pq = a.pq != nullptr;
+    const int nbn = a.V * 4 * S::NCT;
+#pragma unroll
+    for (int it = 0; it < NW; ++it)
+      if (tid + it * NTH < S::WIMG) *reinterpret_cast<u32x4*>(st.wl + tid + it * NTH) = wv[it];
+    if (has_pq) {
+#pragma unroll
+      for (int it = 0; it < NP; ++it)
+        if (tid + it * NTH < S::PIMG) *reinterpret_cast<u32x4*>(st.pql + tid + it * NTH) = pv[it];
+    }
+    if constexpr (S::use_bn) {
+#pragma unroll
+      for (int it = 0; it < NB; ++it) {
+        const int i = tid + it * NTH;
+        if (i < nbn) {
+          const int v = i / (4 * S::NCT), c4 = i - v * (4 * S::NCT);
+          st.bnl[0][c4 * a.V + v] = bs[it];
+          st.bnl[1][c4 * a.V + v] = bh[it];
+        }
+      }
+    }
+    if (tid < 16 * S::NCT) st.bfl[tid] = bf;
+    if (tid < 8) st.bql[tid] = bq;
+    if (tid == 0) {
+      st.scl[0] = *a.wscale;
+      st.scl[1] = has_pq ? *a.pqscale : 0.f;
+      // range: |W_f|_inf, max|b_f| and the planes' shift
+      st.rng[0] = fexp_bits(__float_as_uint(fmaxf(1.f, a.wscale[HLS_BOUND])));
+      st.rng[1] = fexp_bits(__float_as_uint(a.wscale[HLS_BMAX]));
+      st.rng[2] = hl_range_shift(fexp_bits(__float_as_uint(a.adjb[HLS_BOUND])));
+    }
+  }
+};
+
+// every global load is issued before the first LDS write (one memory round
+// trip instead of one per loop trip)
 template <int T, int EPI, int C, int VB, int NTH>
 __device__ __forceinline__ void stage_temporal(const TemporalHLArgs& a, TemporalStage<T, EPI, C, VB>& st, int tid,
                                                int oz = 0) {
-  using S = TemporalStage<T, EPI, C, VB>;
-  const bool has_pq = a.pq != nullptr;
-  // every global load is issued before the first LDS write (one memory
-  // round trip instead of one per loop trip)
-  constexpr int NW = cdiv(S::WIMG, NTH), NP = cdiv(S::PIMG, NTH);
-  constexpr int NB = S::use_bn ? cdiv(VB * 4 * S::NCT, NTH) : 0;
-  uint4 wv[NW], pv[NP];
-  float4 bs[NB > 0 ? NB : 1], bh[NB > 0 ? NB : 1];
-#pragma unroll
-  // (oz: an opaque zero from a caller that stages once per loop trip, so
-  // that these loop-invariant loads are not hoisted out of its loop)
-  for (int it = 0; it < NW; ++it) wv[it] = a.wimg[min(tid + it * NTH + oz, S::WIMG - 1)];
-#pragma unroll
-  for (int it = 0; it < NP; ++it) pv[it] = has_pq ? a.pqimg[min(tid + it * NTH + oz, S::PIMG - 1)] : make_uint4(0, 0, 0, 0);
-  const int nbn = a.V * 4 * S::NCT;
-  if constexpr (S::use_bn) {
-    static_assert(C % 4 == 0, "folded BN rows load as float4");
-    // folded BN vectors [V][C] -> [c/4][v]
-#pragma unroll
-    for (int it = 0; it < NB; ++it) {
-      const int i = min(tid + it * NTH + oz, nbn - 1);
-      const int v = i / (4 * S::NCT), c4 = i - v * (4 * S::NCT);
-      bs[it] = ld4(a.bn_s + v * C + 4 * c4);
-      bh[it] = ld4(a.bn_h + v * C + 4 * c4);
-    }
-  }
-  const float bf = tid < 16 * S::NCT && tid < C ? a.bf[tid] : 0.f;
-  const float bq = tid < 8 && has_pq ? a.pqb[tid >> 1][tid & 1] : 0.f;
-#pragma unroll
-  for (int it = 0; it < NW; ++it)
-    if (tid + it * NTH < S::WIMG) st.wl[tid + it * NTH] = wv[it];
-  if (has_pq) {
-#pragma unroll
-    for (int it = 0; it < NP; ++it)
-      if (tid + it * NTH < S::PIMG) st.pql[tid + it * NTH] = pv[it];
-  }
-  if constexpr (S::use_bn) {
-#pragma unroll
-    for (int it = 0; it < NB; ++it) {
-      const int i = tid + it * NTH;
-      if (i < nbn) {
-        const int v = i / (4 * S::NCT), c4 = i - v * (4 * S::NCT);
-        st.bnl[0][c4 * a.V + v] = bs[it];
-        st.bnl[1][c4 * a.V + v] = bh[it];
-      }
-    }
-  }
-  if (tid < 16 * S::NCT) st.bfl[tid] = bf;
-  if (tid < 8) st.bql[tid] = bq;
-  if (tid == 0) {
-    st.scl[0] = *a.wscale;
-    st.scl[1] = has_pq ? *a.pqscale : 0.f;
-    // range: |W_f|_inf, max|b_f| and the planes' shift
-    st.rng[0] = fexp_bits(__float_as_uint(fmaxf(1.f, a.wscale[HLS_BOUND])));
-    st.rng[1] = fexp_bits(__float_as_uint(a.wscale[HLS_BMAX]));
-    st.rng[2] = hl_range_shift(fexp_bits(__float_as_uint(a.adjb[HLS_BOUND])));
-  }
+  TemporalStageLoad<T, EPI, C, VB, NTH> sl;
+  sl.load(a, tid, oz);
+  sl.store(a, st, tid);
 }
 
 // The unit loop of the temporal GC over units u, u + ustep, ... < uend
@@ -1959,7 +1993,14 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
     }
   }
   // separable or direct tanh per graph, as k_adj_hl<0> decides per (sample, graph) workgroup
-  const bool sep0 = __syncthreads_or(bad[0]) == 0, sep1 = __syncthreads_or(bad[1]) == 0;
+  // (one reduction for both graphs in the common case; __syncthreads_or
+  // returns a boolean, not the OR of the bits, so a sample with a flag set
+  // asks per graph)
+  bool sep0 = true, sep1 = true;
+  if (__syncthreads_or(bad[0] | bad[1])) {
+    sep0 = __syncthreads_or(bad[0]) == 0;
+    sep1 = __syncthreads_or(bad[1]) == 0;
+  }
   if (!sep0 || !sep1) {  // direct path: E / F hold P / Q themselves (padding 0)
     __syncthreads();
     for (int g = 0; g < 2; ++g) {
@@ -1981,7 +2022,14 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
   const float inv0 = *j.wscale[0], inv1 = *j.wscale[1];
   TLH(2, 1)
 
-  {
+#ifndef DSTD_P3_TPI
+#define DSTD_P3_TPI 1
+#endif
+#ifndef DSTD_P3_NOSTORE  // (timing experiments only: the plane stores dropped, wrong output)
+#define DSTD_P3_NOSTORE 0
+#endif
+  constexpr int TPI = DSTD_P3_TPI;  // column tiles per iteration (independent dependency chains)
+  if constexpr (TPI == 1) {
     // one tile space over both graphs (2 NCTC column tiles): the waves split
     // it evenly instead of rounding up twice
     f16x8 wh[RT][NS], wo[RT][NS];  // the current graph's conv_rm rows as B fragments
@@ -2049,9 +2097,104 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
         split4(make_float4(vv[0], vv[1], vv[2], vv[3]), hi, lo);
         // frame t = 16 rt + cl: the hi plane at [t][0][col], lo at [t][1][col]
         const int t = 16 * rt + cl;
-        const uint32_t off = t < T && colb < NCOL ? 2u * (uint32_t)(t * 2 * NCOL + colb) : OOB;
+        const uint32_t off = t < T && colb < NCOL && !DSTD_P3_NOSTORE ? 2u * (uint32_t)(t * 2 * NCOL + colb) : OOB;
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hi), ro, off, 0, DSTD_ADJ_ST_AUX);
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lo), ro, off + 2u * NCOL, 0, DSTD_ADJ_ST_AUX);
+      }
+    }
+  } else {
+    // TPI column tiles of ONE graph per task (the W fragments stay per
+    // graph): tasks = (graph, tile group), the waves split them evenly; a
+    // wave interleaves its tiles' tanh -> split -> MFMA chains (round 6:
+    // phase 3 ran ~3x over its issue bound at one chain per wave)
+    constexpr int NGRP = cdiv(NCTC, TPI);
+    f16x8 wh[RT][NS], wo[RT][NS];
+    f16x4 wth[RT], wto[RT];
+    float b[RT];
+    int gcur = -1;
+#pragma unroll 1
+    for (int ti = wave; ti < 2 * NGRP; ti += NW) {
+      const int g = ti >= NGRP ? 1 : 0, ct0 = (ti - g * NGRP) * TPI;
+      if (g != gcur) {  // (wave-uniform: at most once per wave)
+        gcur = g;
+        const uint4* wg = wl + g * WIMG;
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) {
+#pragma unroll
+          for (int s = 0; s < NS; ++s) {
+            wh[rt][s] = as_h8(wg[((rt * NS + s) * 2 + 0) * 64 + lane]);
+            wo[rt][s] = as_h8(wg[((rt * NS + s) * 2 + 1) * 64 + lane]);
+          }
+          if constexpr (TAIL) {
+            const uint2* w16 = reinterpret_cast<const uint2*>(wg + RT * FULL);
+            wth[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 0) * 64 + lane]);
+            wto[rt] = __builtin_bit_cast(f16x4, w16[(rt * 2 + 1) * 64 + lane]);
+          }
+          b[rt] = bl[g * 16 * RT + 16 * rt + cl];
+        }
+      }
+      const float inv = g ? inv1 : inv0;
+      const float* El = Elg(g);
+      const float* Fl = El + EFN;
+      const float* as = asg(g);
+      const auto ro = rsrc(j.out + (size_t)n * j.out_sN + (size_t)g * j.out_sG, 2u * T * 2 * NCOL);
+      const bool sepg = g ? sep1 : sep0;
+      f16x8 bh[TPI][NS], bo[TPI][NS];
+      f16x4 th[TPI], to[TPI];
+      float asv[TPI][4], al[TPI][4];
+      int colb[TPI];
+#pragma unroll
+      for (int i = 0; i < TPI; ++i) {
+        const int ct = ct0 + i;  // (past NCTC: padding columns, their stores dropped)
+        const int col = ct * 16 + cl;
+        const int qa = col / SL, pa = SM::slot_idx(col - qa * SL);
+        const bool va = col < NCOL && pa < V;
+        const int pb = EF::row(va ? pa : V), qb = EF::row(col < NCOL ? qa : V);
+        if (sepg) tanh_frags<true, NS, TAIL>(El, Fl, pb, qb, kg, bh[i], bo[i], th[i], to[i]);
+        else tanh_frags<false, NS, TAIL>(El, Fl, pb, qb, kg, bh[i], bo[i], th[i], to[i]);
+        colb[i] = ct * 16 + 4 * kg;
+        const int cb = min(colb[i], Gm::ASQ - 4);  // (padding tiles: any in-range table entry)
+        const float4 as4 = ld4(as + cb), al4 = ld4(as + Gm::ASQ + cb);
+        asv[i][0] = as4.x, asv[i][1] = as4.y, asv[i][2] = as4.z, asv[i][3] = as4.w;
+        al[i][0] = al4.x, al[i][1] = al4.y, al[i][2] = al4.z, al[i][3] = al4.w;
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        f32x4 acc[TPI];
+#pragma unroll
+        for (int i = 0; i < TPI; ++i) acc[i] = zero4();
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+#pragma unroll
+          for (int i = 0; i < TPI; ++i) acc[i] = mfma32(bh[i][s], wo[rt][s], acc[i]);
+#pragma unroll
+          for (int i = 0; i < TPI; ++i) acc[i] = mfma32(bo[i][s], wh[rt][s], acc[i]);
+#pragma unroll
+          for (int i = 0; i < TPI; ++i) acc[i] = mfma32(bh[i][s], wh[rt][s], acc[i]);
+        }
+        if constexpr (TAIL) {  // on accumulators of their own (dstd_hilo.h: mixed-shape MFMA chains)
+          f32x4 tac[TPI];
+#pragma unroll
+          for (int i = 0; i < TPI; ++i) tac[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[i], wto[rt], zero4(), 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < TPI; ++i) tac[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(to[i], wth[rt], tac[i], 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < TPI; ++i) tac[i] = __builtin_amdgcn_mfma_f32_16x16x16f16(th[i], wth[rt], tac[i], 0, 0, 0);
+#pragma unroll
+          for (int i = 0; i < TPI; ++i) acc[i] += tac[i];
+        }
+        const int t = 16 * rt + cl;
+#pragma unroll
+        for (int i = 0; i < TPI; ++i) {
+          float vv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) vv[r] = fmaf(al[i][r], fmaf(acc[i][r], inv, b[rt]), asv[i][r]);
+          uint2 hi, lo;
+          split4(make_float4(vv[0], vv[1], vv[2], vv[3]), hi, lo);
+          const uint32_t off = t < T && colb[i] < NCOL ? 2u * (uint32_t)(t * 2 * NCOL + colb[i]) : OOB;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, hi), ro, off, 0, DSTD_ADJ_ST_AUX);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, lo), ro, off + 2u * NCOL, 0, DSTD_ADJ_ST_AUX);
+        }
       }
     }
   }
@@ -2482,7 +2625,12 @@ __device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const i
       if constexpr (C == 64) {
         if (ch == 0) { TLH(4, 2) }
       }
+      // the phase-2 stage's loads now, its LDS writes after the barrier
+      // (-DDSTD_TF_STAGE_EARLY=0: both after it, as before round 6)
+      TemporalStageLoad<T, EPI, C, V, NT> stl;
+      if constexpr (DSTD_TF_STAGE_EARLY) stl.load(a, tid, Gm::NCHUNK > 1 ? opaque_zero() : 0);
       __syncthreads();  // planes complete; the phase-1 scratch is free
+      if constexpr (!DSTD_TF_STAGE_EARLY) stl.load(a, tid, Gm::NCHUNK > 1 ? opaque_zero() : 0);
       if constexpr (C == 64) {
         if (ch == 0) { TLH(3, 1) }
       }
@@ -2494,7 +2642,7 @@ __device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const i
       }
 #endif
       // ---- phase 2: the stage, then the chunk's GC units ----
-      stage_temporal<T, EPI, C, V, NT>(a, st, tid, Gm::NCHUNK > 1 ? opaque_zero() : 0);
+      stl.store(a, st, tid);
       __syncthreads();
       if constexpr (C == 64) {
         if (ch == 0) { TLH(4, 3) }

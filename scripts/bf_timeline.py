@@ -55,6 +55,9 @@ def main():
               ("temporal phase 2 (stage + joint units)", e3[:, 2] - e3[:, 1]),
               ("phase 3 (next block's spatial planes)", e3[:, 3] - e3[:, 2]),
               ("phase 3 prologue (E/F ready)", e2[:, 1] - e2[:, 0]),
+              ("phase 3 wave 0: tiles issued", e2[:, 2] - e2[:, 1]),
+              ("phase 3 wave 0: its stores drained", e2[:, 3] - e2[:, 2]),
+              ("phase 3 wave 0 done -> workgroup exit", e5[:, 3] - e2[:, 3]),
               ("workgroup total", e5[:, 3] - e5[:, 0])]
     print(f"{cfg}: {ok.sum()} workgroups, launch span {e5[:, 3].max():.2f} us, entries {e5[:, 0].min():.2f}.."
           f"{e5[:, 0].max():.2f} us, exits {e5[:, 3].min():.2f}..{e5[:, 3].max():.2f} us")
