@@ -112,6 +112,7 @@ struct BlockHL {
   bool s, t, tf;
   bool s_pre = false;  // the spatial adjacency planes were built by the previous block's temporal launch
   bool bf = false;     // spatial + fused temporal GC in one launch (k_block_fused)
+  bool adj0 = false;   // (conv_st_in with bf) its spatial planes from the model input in that launch
 };
 
 struct BlockScratch {
@@ -372,7 +373,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
   }
   hipError_t e = hipSuccess;
   AdjHLArgs ah{};
-  const bool adj_launch = !hl.s_pre;
+  const bool adj_launch = !hl.s_pre && !(hl.adj0 && from_model);
   if (adj_launch) pf.begin(DSTD_KIND_ADJ_S, s);
   if (hl.s) {
     ah.pq = aa.pq;
@@ -622,7 +623,7 @@ hipError_t run_block(const dstd_block_params* p, const BlockFold& f, const Block
     }
     if (hl.bf) {
       pf.begin(DSTD_KIND_BLOCK, s);
-      e = launch_block_fused(ha, ht, aht, tail.next_adj ? &sn : nullptr, s);
+      e = launch_block_fused(ha, ht, aht, tail.next_adj ? &sn : nullptr, s, hl.adj0 && from_model ? &ah : nullptr);
       pf.end(s);
       return e;
     }
@@ -1023,6 +1024,10 @@ int dstd_model_fwd_ex(const dstd_model_params* p, const float* x, int B, float* 
       tails[b - 1].next_adj = true;
     }
 #endif
+  // block 0's spatial planes (from the model input) inside its block launch
+  // rather than a k_adj_hl<0> launch of their own
+  if (hls[0].bf && !(flags & DSTD_FWD_SEPARATE_ADJ) && blk[0]->cin == 6 && block_fused_adj0_supported(T, V))
+    hls[0].adj0 = true;
 
   // input prep: x6 = cat(x, x - x[:, -1]) and block-0 spatial P/Q (:298-305)
   PQArgs pa{};

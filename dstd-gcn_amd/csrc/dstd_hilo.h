@@ -377,6 +377,8 @@ struct TemporalFusedArgs {
 struct BlockFusedArgs {
   SpatialHLArgs s;
   TemporalFusedArgs t;
+  AdjHLArgs s0;  // out != null (conv_st_in only): this block's own spatial planes from the model
+                 // input (launch_adj_hl mode 0 args with xin), built before the spatial units
 };
 
 hipError_t launch_hl_prep(const HLPrepArgs& a, hipStream_t s);
@@ -402,13 +404,16 @@ bool temporal_fused_default(int T, int V);  // fused at full batch without DSTD_
 // (sa) then the fused temporal GC of launch_temporal_fused (g, j, sn) in one
 // launch, one workgroup per sample; sa.y must be g.h and sa.pq j.pq.  The
 // block kinds of the model (6 -> 64 IN, 64 -> 64 ENC, 64 -> 3 OUT) at the
-// fused temporal kernel's shapes (not T = 75); hipErrorNotSupported elsewhere
+// fused temporal kernel's shapes (not T = 75); hipErrorNotSupported elsewhere.
+// s0 (conv_st_in, block_fused_adj0_supported): the block's own spatial planes
+// from the model input in the same launch instead of a k_adj_hl<0> launch
 bool block_fused_supported(int T, int V, int cin, int cout, int epi);
+bool block_fused_adj0_supported(int T, int V);
 hipError_t launch_block_fused(const SpatialHLArgs& sa, const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn,
-                              hipStream_t s);
+                              hipStream_t s, const AdjHLArgs* s0 = nullptr);
 // validates one block's k_block_fused arguments and fills *out (no launch)
 hipError_t block_fused_args(const SpatialHLArgs& sa, const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn,
-                            BlockFusedArgs* out);
+                            BlockFusedArgs* out, const AdjHLArgs* s0 = nullptr);
 
 
 }  // namespace dstd

@@ -1893,7 +1893,9 @@ struct SAdjGeom {
   static constexpr size_t LDS = 2 * (EFB + AS + WB + BB);
 };
 
-template <int T, int V, int NT>
+// XIN: the P/Q from the model input (j.xin, conv_st_in's conv_m1/m2 rows
+// j.mw / j.mb, as k_adj_hl<0> forms them) instead of j.pq
+template <int T, int V, int NT, bool XIN = false>
 __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, unsigned char* dsm) {
   using Gm = SAdjGeom<T, V>;
   using SM = typename Gm::SM;
@@ -1918,10 +1920,43 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
     return ld4(j.pq + (size_t)n * L.sn + j.p_ch[g] + t * L.st + v * L.sv);
   };
   float4 q4[2][NPQ];
+  if constexpr (XIN) {
+    // conv_st_in (model/dstdgcn.py:298-305): P/Q of x6 = cat(x, x - x[:, -1]),
+    // the same fmaf chain as k_adj_hl<0>'s prologue (bit-identical planes)
+    const float* xn = j.xin + (size_t)n * T * V * 3;
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < 2; ++g) {
+      float wm[4][6], bm[4];
 #pragma unroll
-    for (int it = 0; it < NPQ; ++it) q4[g][it] = pq_at(g, min(tid + it * NT, T * V - 1));
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int c = 0; c < 6; ++c) wm[r][c] = j.mw[g][r >> 1][(r & 1) * 6 + c];
+        bm[r] = j.mb[g][r >> 1][r & 1];
+      }
+#pragma unroll
+      for (int it = 0; it < NPQ; ++it) {
+        const int i = min(tid + it * NT, T * V - 1);
+        const int t = i % T, v = i / T;
+        const float* xc = xn + (t * V + v) * 3;
+        const float* xl = xn + ((T - 1) * V + v) * 3;
+        const float x6v[6] = {xc[0], xc[1], xc[2], xc[0] - xl[0], xc[1] - xl[1], xc[2] - xl[2]};
+        float pq[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float acc = bm[r];
+#pragma unroll
+          for (int c = 0; c < 6; ++c) acc = fmaf(wm[r][c], x6v[c], acc);
+          pq[r] = acc;
+        }
+        q4[g][it] = make_float4(pq[0], pq[1], pq[2], pq[3]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int it = 0; it < NPQ; ++it) q4[g][it] = pq_at(g, min(tid + it * NT, T * V - 1));
+  }
   uint4 wv[NWI];
   float av[NAS];
 #pragma unroll
@@ -2008,13 +2043,28 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
       ef_pad(g, 0.f);
       float* El = Elg(g);
       float* Fl = El + EFN;
-      for (int i = tid; i < T * V; i += NT) {
-        const int t = i % T, v = i / T;
-        const float4 p4 = pq_at(g, i);
-        El[EF::row(v) + t] = p4.x;
-        El[EF::row(v) + T + t] = p4.y;
-        Fl[EF::row(v) + t] = p4.z;
-        Fl[EF::row(v) + T + t] = p4.w;
+      if constexpr (XIN) {  // (no P/Q in memory: the prologue's values)
+#pragma unroll
+        for (int it = 0; it < NPQ; ++it) {
+          const int i = tid + it * NT;
+          if (i < T * V) {
+            const int t = i % T, v = i / T;
+            const float4 p4 = g ? q4[1][it] : q4[0][it];
+            El[EF::row(v) + t] = p4.x;
+            El[EF::row(v) + T + t] = p4.y;
+            Fl[EF::row(v) + t] = p4.z;
+            Fl[EF::row(v) + T + t] = p4.w;
+          }
+        }
+      } else {
+        for (int i = tid; i < T * V; i += NT) {
+          const int t = i % T, v = i / T;
+          const float4 p4 = pq_at(g, i);
+          El[EF::row(v) + t] = p4.x;
+          El[EF::row(v) + T + t] = p4.y;
+          Fl[EF::row(v) + t] = p4.z;
+          Fl[EF::row(v) + T + t] = p4.w;
+        }
       }
     }
     __syncthreads();
@@ -2710,10 +2760,21 @@ struct BlockFusedGeom {
 };
 
 template <int T, int V, int CIN, int COUT, int EPI>
-__device__ __forceinline__ void block_fused_body(const SpatialHLArgs& sa, const TemporalFusedArgs& ta, const int n,
-                                                 unsigned char* dsm) {
+__device__ __forceinline__ void block_fused_body(const SpatialHLArgs& sa, const TemporalFusedArgs& ta, const AdjHLArgs& s0,
+                                                 const int n, unsigned char* dsm) {
   constexpr int NW = tf_waves<T, V>(), NT = 64 * NW;
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 0) }
+  if constexpr (CIN == 6 && tf_phase3<T, V>()) {
+    // conv_st_in: this block's own spatial planes from the model input (the
+    // k_adj_hl<0> launch of block 0), stored to HBM like phase 3's and read
+    // back by the units below on this CU; every wave's plane stores complete
+    // before the barrier (vmcnt 0), the units' loads come after it
+    if (s0.out) {
+      spatial_adj_sample<T, V, NT, true>(s0, n, dsm);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+  }
   int bad = 0;
   {
     using SM = SlotMap<V, true>;
@@ -2779,7 +2840,7 @@ __device__ __forceinline__ void block_fused_body(const SpatialHLArgs& sa, const 
 template <int T, int V, int CIN, int COUT, int EPI>
 __global__ __launch_bounds__((64 * tf_waves<T, V>())) __attribute__((amdgpu_waves_per_eu((tf_waves<T, V>() / 4), (tf_waves<T, V>() / 4)))) void k_block_fused(BlockFusedArgs ba) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dsm[];
-  block_fused_body<T, V, CIN, COUT, EPI>(ba.s, ba.t, blockIdx.x, dsm);  // one sample per workgroup
+  block_fused_body<T, V, CIN, COUT, EPI>(ba.s, ba.t, ba.s0, blockIdx.x, dsm);  // one sample per workgroup
 }
 
 // ===========================================================================
@@ -2978,8 +3039,15 @@ bool block_fused_supported(int T, int V, int cin, int cout, int epi) {
                    (cin == 64 && cout == 3 && epi == TEPI_OUT));
 }
 
+bool block_fused_adj0_supported(int T, int V) {
+#ifdef DSTD_NO_BF_ADJ0
+  return false;
+#endif
+  return block_fused_supported(T, V, 6, 64, TEPI_IN) && temporal_fused_phase3(T, V);
+}
+
 hipError_t block_fused_args(const SpatialHLArgs& sa, const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn,
-                            BlockFusedArgs* out) {
+                            BlockFusedArgs* out, const AdjHLArgs* s0) {
   if (!block_fused_supported(g.T, g.V, sa.Cin, sa.Cout, g.epi) || sa.T != g.T || sa.V != g.V || sa.B != g.B ||
       sa.Cout != g.C || sa.y != g.h || sa.pq != j.pq || g.V != (int)(j.pql.st / 4) || j.pql.sch != 1 || j.pql.sv != 4 ||
       ((uintptr_t)j.pq & 15))
@@ -2988,14 +3056,17 @@ hipError_t block_fused_args(const SpatialHLArgs& sa, const TemporalHLArgs& g, co
              sn->pql.sch != 1 || (sn->pql.st & 3) || (sn->pql.sv & 3) || (sn->pql.sn & 3) || (sn->p_ch[0] & 3) ||
              (sn->p_ch[1] & 3) || !sn->out))
     return hipErrorNotSupported;
-  *out = BlockFusedArgs{sa, TemporalFusedArgs{g, j, sn ? *sn : AdjHLArgs{}}};
+  if (s0 && (sa.Cin != 6 || !block_fused_adj0_supported(g.T, g.V) || !s0->xin || s0->ngroups != 2 || !s0->out ||
+             s0->B != g.B || !sa.xmodel || sa.adj != s0->out))
+    return hipErrorNotSupported;
+  *out = BlockFusedArgs{sa, TemporalFusedArgs{g, j, sn ? *sn : AdjHLArgs{}}, s0 ? *s0 : AdjHLArgs{}};
   return hipSuccess;
 }
 
 hipError_t launch_block_fused(const SpatialHLArgs& sa, const TemporalHLArgs& g, const AdjHLArgs& j, const AdjHLArgs* sn,
-                              hipStream_t s) {
+                              hipStream_t s, const AdjHLArgs* s0) {
   BlockFusedArgs a;
-  const hipError_t e = block_fused_args(sa, g, j, sn, &a);
+  const hipError_t e = block_fused_args(sa, g, j, sn, &a, s0);
   if (e != hipSuccess) return e;
   if (g.T == 35 && g.V == 22) return bfused_tv<35, 22>(a, s);
   if (g.T == 35 && g.V == 25) return bfused_tv<35, 25>(a, s);
