@@ -2715,10 +2715,15 @@ __device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const i
           bo[ut] = *reinterpret_cast<const uint4*>(base + (ok ? UF * SL + off : Gm::ZPAD));
         }
       };
+#ifndef DSTD_TF_P2PRIO  // (experiments: the younger waves' static priority in the joint units)
+#define DSTD_TF_P2PRIO 0
+#endif
+      if constexpr (DSTD_TF_P2PRIO) { if (wave >= 4) __builtin_amdgcn_s_setprio(1); }
 #ifndef DSTD_TF_SKIP_P2  // (timing experiments: phase 1 alone)
       temporal_units<T, EPI, C, V, true, decltype(load_adj), (NW <= 8 && !Gm::UCH), tf_res_acc(T, V), NUTC>(
           a, st, ub + wave, ub + nv, NW, load_adj, u0 / 16);
 #endif
+      if constexpr (DSTD_TF_P2PRIO) __builtin_amdgcn_s_setprio(0);
     }
   }
   // ---- phase 3: the next block's spatial adjacency planes of this sample
@@ -2728,7 +2733,12 @@ __device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const i
     if (fa.sn.out) {
       __syncthreads();  // every unit's P/Q written (one CU: the workgroup-scope fences of the barrier suffice)
       TLH(2, 0)
+#ifndef DSTD_TF_P3PRIO  // (experiments: the same in phase 3)
+#define DSTD_TF_P3PRIO 0
+#endif
+      if constexpr (DSTD_TF_P3PRIO) { if (wave >= 4) __builtin_amdgcn_s_setprio(1); }
       spatial_adj_sample<T, V, NT>(fa.sn, n, dsm);
+      if constexpr (DSTD_TF_P3PRIO) __builtin_amdgcn_s_setprio(0);
     }
     TLH(3, 3)
   }
@@ -2824,8 +2834,21 @@ __device__ __forceinline__ void block_fused_body(const SpatialHLArgs& sa, const 
       Fl[TEF::row(t) + V + w] = __builtin_amdgcn_exp2f(eq1);
       return !(fabsf(ep0) <= 120.f && fabsf(ep1) <= 120.f && fabsf(eq0) <= 120.f && fabsf(eq1) <= 120.f);
     };
+    // (experiments: static VALU priority for the younger waves during the
+    // spatial units -- 1: waves 4-11 at 1, 2: 4-7 at 1 and 8-11 at 2, 3:
+    // 8-11 at 1; back to 0 for the temporal phases)
+#ifndef DSTD_BF_SETPRIO
+#define DSTD_BF_SETPRIO 1
+#endif
+    if constexpr (DSTD_BF_SETPRIO == 1) { if (wave >= 4) __builtin_amdgcn_s_setprio(1); }
+    if constexpr (DSTD_BF_SETPRIO == 2) {
+      if (wave >= 8) __builtin_amdgcn_s_setprio(2);
+      else if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    }
+    if constexpr (DSTD_BF_SETPRIO == 3) { if (wave >= 8) __builtin_amdgcn_s_setprio(1); }
     bad = spatial_units<V, CIN, COUT, decltype(load_adj_g), (NW > 8), DSTD_BF_ST_AUX, decltype(pq_sink)>(
         a, st, n * T + wave, (n + 1) * T, NW, load_adj_g, pq_sink);
+    if constexpr (DSTD_BF_SETPRIO != 0) __builtin_amdgcn_s_setprio(0);
   }
   if constexpr (CIN == 64 && COUT == 64) { TLH(5, 1) }
   tfused_pre<T, V, EPI, COUT>(ta, dsm);
