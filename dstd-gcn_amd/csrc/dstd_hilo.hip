@@ -912,7 +912,6 @@ struct TemporalStageLoad {
   static constexpr int NB = S::use_bn ? cdiv(VB * 4 * S::NCT, NTH) : 0;
   // (native vectors: a uint4 array copied from global memory is a memcpy
   // that keeps the array in scratch)
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   u32x4 wv[NW], pv[NP];
   float4 bs[NB > 0 ? NB : 1], bh[NB > 0 ? NB : 1];
   float bf, bq;
@@ -1893,10 +1892,46 @@ struct SAdjGeom {
   static constexpr size_t LDS = 2 * (EFB + AS + WB + BB);
 };
 
+// The P/Q-independent global loads of spatial_adj_sample's prologue (both
+// conv_rm images, the Astat table entries, the conv_rm bias): issued by
+// phase 3's caller before the barrier that ends phase 2, so their latency
+// hides in the wait for the last joint units (the unit registers are dead)
+template <int T, int V, int NT>
+struct SAdjStatic {
+  using Gm = SAdjGeom<T, V>;
+  static constexpr int NWI = cdiv(2 * Gm::WIMG, NT), NAS = cdiv(2 * Gm::ASQ, NT);
+  u32x4 wv[NWI];
+  float av[NAS];
+  int aok;  // bit it: the table entry of iteration it is a valid (pi, q)
+  float bv;
+  __device__ __forceinline__ void load(const AdjHLArgs& j, int tid) {
+    using SM = typename Gm::SM;
+    constexpr int WIMG = Gm::WIMG, SL = Gm::SL, NCOL = Gm::NCOL, RT = Gm::RT;
+#pragma unroll
+    for (int it = 0; it < NWI; ++it) {
+      const int i = min(tid + it * NT, 2 * WIMG - 1);
+      wv[it] = *reinterpret_cast<const u32x4*>((i >= WIMG ? j.wimg[1] : j.wimg[0]) + (i >= WIMG ? i - WIMG : i));
+    }
+    aok = 0;
+#pragma unroll
+    for (int it = 0; it < NAS; ++it) {
+      const int i = tid + it * NT, g = i >= Gm::ASQ, col = i - g * Gm::ASQ, q = col / SL;
+      const int pi = col < NCOL ? SM::slot_idx(col - q * SL) : V;
+      const bool ok = pi < V && i < 2 * Gm::ASQ;
+      if (ok) aok |= 1 << it;
+      av[it] = (g ? j.astat[1] : j.astat[0])[ok ? pi * V + q : 0];
+    }
+    const int bg = tid >= 16 * RT, br = tid - bg * 16 * RT;
+    bv = tid < 2 * 16 * RT && br < T ? (bg ? j.bias[1] : j.bias[0])[br] : 0.f;
+  }
+};
+
 // XIN: the P/Q from the model input (j.xin, conv_st_in's conv_m1/m2 rows
-// j.mw / j.mb, as k_adj_hl<0> forms them) instead of j.pq
+// j.mw / j.mb, as k_adj_hl<0> forms them) instead of j.pq.  pre: the
+// prologue's static loads, already issued (SAdjStatic::load), or null
 template <int T, int V, int NT, bool XIN = false>
-__device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, unsigned char* dsm) {
+__device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, unsigned char* dsm,
+                                                   const SAdjStatic<T, V, NT>* pre = nullptr) {
   using Gm = SAdjGeom<T, V>;
   using SM = typename Gm::SM;
   using EF = typename Gm::EF;
@@ -1957,42 +1992,28 @@ __device__ __forceinline__ void spatial_adj_sample(const AdjHLArgs& j, int n, un
 #pragma unroll
       for (int it = 0; it < NPQ; ++it) q4[g][it] = pq_at(g, min(tid + it * NT, T * V - 1));
   }
-  uint4 wv[NWI];
-  float av[NAS];
-#pragma unroll
-  for (int it = 0; it < NWI; ++it) {
-    const int i = min(tid + it * NT, 2 * WIMG - 1);
-    wv[it] = (i >= WIMG ? j.wimg[1] : j.wimg[0])[i >= WIMG ? i - WIMG : i];
-  }
-  int aok = 0;  // bit it: the table entry of iteration it is a valid (pi, q)
-#pragma unroll
-  for (int it = 0; it < NAS; ++it) {
-    const int i = tid + it * NT, g = i >= Gm::ASQ, col = i - g * Gm::ASQ, q = col / SL;
-    const int pi = col < NCOL ? SM::slot_idx(col - q * SL) : V;
-    const bool ok = pi < V && i < 2 * Gm::ASQ;
-    if (ok) aok |= 1 << it;
-    av[it] = (g ? j.astat[1] : j.astat[0])[ok ? pi * V + q : 0];
-  }
+  static_assert(SAdjStatic<T, V, NT>::NWI == NWI && SAdjStatic<T, V, NT>::NAS == NAS, "prologue split");
+  SAdjStatic<T, V, NT> sl;
+  if (pre) sl = *pre;
+  else sl.load(j, tid);
   // planes stored as 2^-sa Adj, one sa for both graphs (dstd_hilo.h "range scaling")
   const float dna = pow2f(-hl_range_shift(
       fexp_bits(__float_as_uint(fmaxf(j.wscale[0][HLS_BOUND], j.wscale[1][HLS_BOUND])))));
   const float alpha = *j.alpha * dna;
-  const int bg = tid >= 16 * RT, br = tid - bg * 16 * RT;
-  const float bv = tid < 2 * 16 * RT && br < T ? (bg ? j.bias[1] : j.bias[0])[br] : 0.f;
 #pragma unroll
   for (int it = 0; it < NWI; ++it)
-    if (tid + it * NT < 2 * WIMG) wl[tid + it * NT] = wv[it];
+    if (tid + it * NT < 2 * WIMG) *reinterpret_cast<u32x4*>(wl + tid + it * NT) = sl.wv[it];
 #pragma unroll
   for (int it = 0; it < NAS; ++it) {
     const int i = tid + it * NT, g = i >= Gm::ASQ;
     if (i < 2 * Gm::ASQ) {
-      const bool ok = (aok >> it) & 1;
+      const bool ok = (sl.aok >> it) & 1;
       float* t = asg(g) + (i - g * Gm::ASQ);
-      t[0] = ok ? av[it] * dna : 0.f;
+      t[0] = ok ? sl.av[it] * dna : 0.f;
       t[Gm::ASQ] = ok ? alpha : 0.f;
     }
   }
-  if (tid < 2 * 16 * RT) bl[tid] = bv;
+  if (tid < 2 * 16 * RT) bl[tid] = sl.bv;
   auto ef_pad = [&](int g, float val) __attribute__((always_inline)) {  // padding k and the row p = q = V: tanh 0
     float* El = Elg(g);
     float* Fl = El + EFN;
@@ -2731,13 +2752,18 @@ __device__ __forceinline__ void tfused_body(const TemporalFusedArgs& fa, const i
   if constexpr (C == 64 && tf_phase3<T, V>()) {
     TLH(3, 2)
     if (fa.sn.out) {
+#ifndef DSTD_P3_PRELOAD  // (1: the static loads before the barrier -- r06q: 0.0% / -0.1% / +1.7%, off)
+#define DSTD_P3_PRELOAD 0
+#endif
+      SAdjStatic<T, V, NT> p3s;
+      if constexpr (DSTD_P3_PRELOAD) p3s.load(fa.sn, tid);
       __syncthreads();  // every unit's P/Q written (one CU: the workgroup-scope fences of the barrier suffice)
       TLH(2, 0)
 #ifndef DSTD_TF_P3PRIO  // (experiments: the same in phase 3)
 #define DSTD_TF_P3PRIO 0
 #endif
       if constexpr (DSTD_TF_P3PRIO) { if (wave >= 4) __builtin_amdgcn_s_setprio(1); }
-      spatial_adj_sample<T, V, NT>(fa.sn, n, dsm);
+      spatial_adj_sample<T, V, NT>(fa.sn, n, dsm, DSTD_P3_PRELOAD ? &p3s : nullptr);
       if constexpr (DSTD_TF_P3PRIO) __builtin_amdgcn_s_setprio(0);
     }
     TLH(3, 3)
