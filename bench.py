@@ -19,13 +19,15 @@ Timing: barrier + synchronize, t0, exactly K steps, synchronize, t1, barrier
 
 One JSON line on rank 0.  Besides the driver's fields it carries
   roofline     : the dominant kernel family (largest summed time per step in
-                 an untimed profiled pass) and its launch in DSTDGCB 1 (the
-                 first encoder, a 64->64 split-f16 launch), bracketed by two
-                 HIP events on the launch stream in one of every --probe-every
-                 timed steps.  achieved = the launch's COMPULSORY bytes (SURVEY
-                 §8(d): one 64->64 DSTDGC reads its input and writes its output
-                 once, 394,240 B per H36M sequence, x B sequences) / its average
-                 duration, against the 8 TB/s HBM3E peak.  layout_bytes: what the
+                 an untimed profiled pass; at B >= the CU count the block
+                 kernel, one launch per DSTDGCB) and its launch in DSTDGCB 1
+                 (the first encoder, a 64->64 split-f16 launch), bracketed by
+                 two HIP events on the launch stream in one of every
+                 --probe-every timed steps.  achieved = the launch's COMPULSORY
+                 bytes (the block -- or, in the two-launch
+                 schedule, each of its GCs -- reads its input and writes its
+                 output once, 394,240 B per H36M sequence, x B sequences) / its
+                 average duration, against the 8 TB/s HBM3E peak.  layout_bytes: what the
                  launch moves by design in this build's stored layouts (the
                  adjacency planes and P/Q it reads on top).  traffic: measured HBM
                  bytes per launch of that kernel (profiles/pmc_traffic.json,
