@@ -185,7 +185,9 @@ int dstd_model_fwd_profiled(const dstd_model_params* p, const float* x, int B, f
 /* Launch schedule, for A/B and the bit-identity test (same results either
  * way): every block's spatial adjacency planes in a launch of their own
  * (k_adj_hl<0>) instead of built by the previous block's fused temporal
- * launch after its units (k_temporal_fused phase 3, the default). */
+ * launch after its units (phase 3, the default) -- and block 0's, built from
+ * the model input, in its own launch instead of inside block 0's
+ * k_block_fused launch. */
 #define DSTD_FWD_SEPARATE_ADJ 4u
 /* Launch schedule: the temporal graph convolutions with their adjacency
  * built in LDS (k_temporal_fused, one workgroup per sample) at any batch
