@@ -486,16 +486,32 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    host_group = None  # the group of the steps before and around the timed region
     if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:  # any torch.distributed.run launch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # The default group is RCCL, its communicator created at its first
+        # collective: the elapsed-time MAX and the checksum exchange AFTER the
+        # timed region.  A live RCCL communicator makes this forward's kernels
+        # run 3-4% slower on this stack (gloo under torchrun does not;
+        # profiles/r06y_*, r06z_*), so the weight broadcast and
+        # the barriers around the timed region go over a gloo group (host-
+        # staged; the forward itself has no collective).  Diagnostics:
+        # DSTD_BENCH_RCCL_EARLY=1 (RCCL bound to the device at init and used
+        # for everything, as before round 6), DSTD_BENCH_BACKEND=gloo.
+        backend = os.environ.get("DSTD_BENCH_BACKEND", "nccl")
+        early = backend == "nccl" and os.environ.get("DSTD_BENCH_RCCL_EARLY", "0") == "1"
+        if early:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+            host_group = dist.new_group(backend="gloo") if backend == "nccl" else None
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
     model, opts, sd = load_model(args.config, device)
     if dist is not None:
-        D.broadcast_module(model, src=0)  # weights once, rank 0 -> all
+        D.broadcast_module(model, src=0, group=host_group)  # weights once, rank 0 -> all
     T = opts["input_time_frame"] + opts["output_time_frame"]
     V = opts["joints_to_consider"]
     strong = args.global_batch > 0
@@ -510,7 +526,7 @@ def main():
 
     def barrier():
         if dist is not None:
-            dist.barrier()
+            dist.barrier(group=host_group)
 
     with torch.no_grad():
         for _ in range(args.warmup):
