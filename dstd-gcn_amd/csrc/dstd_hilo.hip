@@ -1567,7 +1567,10 @@ struct AdjHLGeom {
   static constexpr int SL = SM::SL, NCOL = NA * SL, NCT = cdiv(NCOL, 16);
   // column chunks (one workgroup each) per (sample, graph) at full batch;
   // the launcher raises the count when B * ngroups * NCHUNK leaves CUs idle
-  static constexpr int NCHUNK = MODE == 0 ? 1 : 2;
+#ifndef DSTD_ADJ_T_NCHUNK  // (experiments: column chunks of the temporal adjacency per sample)
+#define DSTD_ADJ_T_NCHUNK 2
+#endif
+  static constexpr int NCHUNK = MODE == 0 ? 1 : DSTD_ADJ_T_NCHUNK;
   static constexpr int CPC = cdiv(NCT, NCHUNK);
   static constexpr int OS = 20;  // staging row stride (floats)
   static constexpr int T = MODE == 0 ? NROW : NA, V = MODE == 0 ? NA : NROW;
