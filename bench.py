@@ -464,6 +464,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--settle-ms", type=float, default=300.0,
+                    help="after the W warm-up steps, untimed forwards for this long so the timed region "
+                         "starts at the GPU's steady clocks (a fresh box's first process otherwise reads "
+                         "~1.5%% slow at K=20: profiles/r06ae_*); 0: off")
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch (weak scaling)")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="strong scaling: this many sequences in total, split over the ranks")
@@ -532,6 +536,13 @@ def main():
         for _ in range(args.warmup):
             model(x)
         torch.cuda.synchronize()
+        settle_steps = 0
+        t_settle = time.perf_counter()
+        while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+            for _ in range(10):
+                model(x)
+            torch.cuda.synchronize()
+            settle_steps += 10
 
         # untimed pass: per-family launch times -> dominant family
         nb = len(fl)
@@ -613,6 +624,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"ms": args.settle_ms, "steps": settle_steps,
+                       "note": "untimed forwards after the warm-up, before the timed region (steady clocks)"},
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
