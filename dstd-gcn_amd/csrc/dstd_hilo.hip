@@ -114,12 +114,13 @@ constexpr uint32_t OOB = 0x80000000u;
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
+template <int AUX = 0>
 __device__ __forceinline__ float4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 #ifdef DSTD_ABL_LOAD
   const float f = (float)(off & 255) * 1e-3f;
   return make_float4(f, f, f, f);
 #endif
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
 }
 __device__ __forceinline__ uint4 bldu4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 #ifdef DSTD_ABL_LOAD
@@ -138,6 +139,14 @@ __device__ __forceinline__ uint4 bldu4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 #endif
 #ifndef DSTD_ADJ_ST_AUX
 #define DSTD_ADJ_ST_AUX 0
+#endif
+// (experiments: cache policy of the temporal units' h-row loads and of the
+// encoder residual loads -- both the last read of those rows)
+#ifndef DSTD_TF_H_LD_AUX
+#define DSTD_TF_H_LD_AUX 0
+#endif
+#ifndef DSTD_TF_R_LD_AUX
+#define DSTD_TF_R_LD_AUX 0
 #endif
 template <int AUX = DSTD_GC_ST_AUX>
 __device__ __forceinline__ void bst4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
@@ -864,11 +873,11 @@ constexpr int temporal_nt() {
 
 // 8 channels k0 .. k0+7 of the row at byte offset `row_off` (C per row; zero
 // past C, and an out-of-range row_off reads zeros)
-template <int C>
+template <int C, int AUX = 0>
 __device__ __forceinline__ void load_row8_at(__amdgpu_buffer_rsrc_t r, uint32_t row_off, int k0, float4& lo4, float4& hi4) {
   if constexpr (C % 8 == 0) {
-    lo4 = bld4(r, row_off + 4 * k0);
-    hi4 = bld4(r, row_off + 4 * k0 + 16);
+    lo4 = bld4<AUX>(r, row_off + 4 * k0);
+    hi4 = bld4<AUX>(r, row_off + 4 * k0 + 16);
   } else {
     const uint32_t off = k0 == 0 ? row_off : OOB;
     float e[8];
@@ -1062,7 +1071,8 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int ks = 0; ks < KSI; ++ks) load_row8_at<C>(r, xoff[m], 32 * ks + 8 * kl, xr[m][ks][0], xr[m][ks][1]);
+      for (int ks = 0; ks < KSI; ++ks)
+        load_row8_at<C, DSTD_TF_H_LD_AUX>(r, xoff[m], 32 * ks + 8 * kl, xr[m][ks][0], xr[m][ks][1]);
   };
   if (PF && u < uend) load_x(u);
   while (u < uend) {
@@ -1148,7 +1158,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
 #pragma unroll
       for (int ut = 0; ut < NUTC; ++ut)
 #pragma unroll
-        for (int ct = 0; ct < NCT; ++ct) R[ct][ut] = bld4(rr, uoff[ut] + 64 * ct);
+        for (int ct = 0; ct < NCT; ++ct) R[ct][ut] = bld4<DSTD_TF_R_LD_AUX>(rr, uoff[ut] + 64 * ct);
     };
     constexpr bool late_res = LAZY && DSTD_TF_LATE_RES;
     // RES_ACC: the ENC residual is the aggregation accumulator's initial
@@ -1181,7 +1191,7 @@ __device__ __forceinline__ void temporal_units(const TemporalHLArgs& a, const Te
       for (int ut = 0; ut < NUTC; ++ut)
 #pragma unroll
         for (int ct = 0; ct < NCT; ++ct) {
-          const float4 r4 = bld4(rr, uoff[ut] + 64 * ct);
+          const float4 r4 = bld4<DSTD_TF_R_LD_AUX>(rr, uoff[ut] + 64 * ct);
           O[ct][ut] = f32x4{r4.x, r4.y, r4.z, r4.w};
         }
       if (const int su0 = min(sx + sa, 127)) {
