@@ -190,12 +190,15 @@ def model_block_bytes(opts, split_on):
 def merge_blocks(blocks, fused_t):
     """Each block as ONE launch (k_block_fused, the default wherever the fused
     temporal kernel runs): its spatial GC, its temporal adjacency (built in
-    LDS) and its temporal GC (with phase 3) are one family, KIND_BLOCK."""
+    LDS) and its temporal GC (with phase 3) are one family, KIND_BLOCK; block
+    0's spatial adjacency (built from the model input inside its launch,
+    phase 0) too -- the later blocks' moved into the previous launch
+    (phase3_moves) and are 0 here."""
     out = []
     for b in blocks:
         b = dict(b)
         b[native.KIND_BLOCK] = b.pop(native.KIND_SPATIAL) + b.pop(native.KIND_TEMPORAL) + \
-            (b.pop(native.KIND_ADJ_T) if fused_t else 0)
+            (b.pop(native.KIND_ADJ_T) if fused_t else 0) + b.pop(native.KIND_ADJ_S, 0)
         out.append(b)
     return out
 
